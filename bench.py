@@ -1,0 +1,300 @@
+#!/usr/bin/env python
+"""Benchmark: typed-CSR SpMM (GraphConv aggregation, robust_gcn.py:45-47) on
+MI355X -- BASELINE.json metric "aggregated edges/sec + SpMM HBM GB/s vs
+roofline, d=256, 1/2/4/8 GPU".
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
+
+Workload: per GPU a node-range shard of 1M nodes of a
+seeded Erdos-Renyi typed graph (avg total out-degree 32 over L=6 edge
+types, dedupe), d=256 fp32 features -- config C3 at N=1, the C4 shape
+(4M nodes) at N=4.  A step = one GraphConv aggregation forward over the
+rank's rows (N>1: preceded by the all-gather of node features that the
+node-range sharding needs).  Inputs are resident in HBM before timing.
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "graph-representation-learning_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "aggregated edges/sec + SpMM HBM GB/s vs roofline, d=256, 1/2/4/8 GPU"
+HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+F32_MFMA_PEAK_TFS = 157.3  # dense fp32 MFMA (v_mfma_f32_32x32x2_f32)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--nodes-per-gpu", type=int, default=1_000_000)
+    ap.add_argument("--avg-deg", type=float, default=32.0)
+    ap.add_argument("--types", type=int, default=6)
+    ap.add_argument("--dim", type=int, default=256)
+    ap.add_argument("--p", type=float, default=0.0, help="DropEdge rate inside the timed step (0 = eval)")
+    ap.add_argument("--graph", choices=["er", "rmat"], default="er")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 disables)")
+    ap.add_argument("--no-extras", action="store_true")
+    ap.add_argument("--only", choices=["fwd", "bwd", "linear", "layer"], default=None,
+                    help="profiling aid: run just that kernel K times (no JSON line)")
+    return ap.parse_args()
+
+
+def spmm_bytes(E, N, L, F, p, idx_bytes=4, ptr_bytes=4):
+    """Algorithmic HBM bytes of one unfused typed-SpMM forward."""
+    keep = 1.0 - p
+    return keep * E * F * 4 + idx_bytes * E + ptr_bytes * (N * L + 1) + keep * N * F * 4 + N * (L + 1) * F * 4
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    from grl import DropEdge, TypedGraph
+    from grl.ops import linear_fwd, typed_aggregate
+
+    L, F = args.types, args.dim
+    n_loc = args.nodes_per_gpu
+    N = n_loc * world
+    if args.graph == "rmat":
+        N = 1 << (N - 1).bit_length()
+        n_loc = N // world
+    rb, re = rank * n_loc, (rank + 1) * n_loc
+    t0 = time.time()
+    graph = TypedGraph.synthetic(N, args.avg_deg, L, kind=args.graph, seed=0, row_range=(rb, re), device=dev)
+    E_loc = graph.nnz
+    if world > 1:
+        t = torch.tensor([E_loc], dtype=torch.int64, device=dev)
+        allE = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(allE, t)
+        allE = [int(x.item()) for x in allE]
+        E_tot = sum(allE)
+        graph.edge_id_base = sum(allE[:rank])
+        graph.self_id_base = E_tot + rb
+    else:
+        E_tot = E_loc
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1 + rank)
+    X_loc = torch.randn(n_loc, F, generator=gen, device=dev, dtype=torch.float32)
+    X_full = torch.empty(N, F, device=dev) if world > 1 else X_loc
+    build_s = time.time() - t0
+
+    de = DropEdge(args.p, 2, 0, True) if args.p > 0 else None
+    g_step = graph.with_dropedge(de)
+    stream = torch.cuda.current_stream(dev)
+
+    def gather():
+        if world > 1:
+            dist.all_gather_into_tensor(X_full, X_loc)
+
+    def spmm():
+        return typed_aggregate(X_full, g_step)
+
+    if args.only is not None:
+        run_only(args, graph, X_full, gather, spmm, L, F)
+        return
+
+    for _ in range(args.warmup):
+        gather()
+        spmm()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for i in range(args.steps):
+        gather()
+        ev[i][0].record(stream)
+        Z = spmm()
+        ev[i][1].record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t_start
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    if world > 1:
+        tt = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        wall, kern_ms = float(tt[0]), float(tt[1])
+    ms_step = wall / args.steps * 1e3
+    value = E_tot / (wall / args.steps)
+
+    bytes_launch = spmm_bytes(E_loc, n_loc, L, F, args.p)
+    achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
+    traffic = load_traffic(args, n_loc, world)
+    out = {
+        "metric": METRIC, "value": value, "unit": "edges/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32",
+        "data": f"synthetic: seeded {'Erdos-Renyi' if args.graph == 'er' else 'R-MAT'} typed graph (graph seed 0), "
+                "X ~ N(0,1) fp32 (seed 1+rank)",
+        "config": {"workload": ("C3" if world == 1 else "C4-shape") + f": {args.graph.upper()} typed graph, "
+                   f"{n_loc} nodes/GPU, avg_deg {args.avg_deg:g} over L={L} edge types, d={F}, typed-SpMM "
+                   f"forward (GraphConv aggregation){' + DropEdge p=%g' % args.p if args.p else ''}",
+                   "nodes_total": N, "edges_total": E_tot, "nodes_per_gpu": n_loc, "avg_deg": args.avg_deg,
+                   "num_types": L, "d": F, "dropedge_p": args.p, "graph": args.graph,
+                   "parallelism": "single GPU" if world == 1 else f"node-range shards x{world}, all-gather of X"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "spmm_kernel<4,1,8,false,false> (grl_typed_spmm_fwd)",
+                     "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": bytes_launch},
+        "build_s": build_s,
+    }
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        out["cpu_baseline"], out["parity"] = cpu_baseline(args, graph, X_loc, Z, L, F)
+    if not args.no_extras:
+        out["extras"] = extras(args, graph, X_full, gather, L, F, dev, E_loc, n_loc)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def load_traffic(args, n_loc, world):
+    """HBM bytes per launch from a committed rocprofv3 PMC summary of the same
+    workload (profiles/pmc_traffic.json, written by tools/pmc_traffic.py),
+    or None."""
+    path = os.path.join(HERE, "profiles", "pmc_traffic.json")
+    if not os.path.exists(path):
+        return None
+    try:
+        d = json.load(open(path))
+        key = f"{args.graph}_n{n_loc}_deg{args.avg_deg:g}_L{args.types}_d{args.dim}_p{args.p:g}"
+        return d.get(key, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def cpu_baseline(args, graph, X, Z, L, F):
+    """Oracle (grl_oracle.c, OpenMP) on a bounded row sample of the SAME
+    graph and features; also checks the GPU rows of that sample bitwise."""
+    from oracle import c_oracle
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
+    rows = min(graph.num_rows, 100_000)
+    rowptr = graph.rowptr[: rows * L + 1].cpu().numpy()
+    colidx = graph.colidx[: int(rowptr[-1])].cpu().numpy()
+    Xh = X.cpu().numpy()
+    E = int(rowptr[-1])
+    t0 = time.perf_counter()
+    passes = 0
+    while True:
+        Zc = c_oracle.spmm_fwd(rowptr, colidx, Xh, L, True, nthreads=threads, self_base=graph.self_id_base)
+        passes += 1
+        if time.perf_counter() - t0 >= args.cpu_seconds:
+            break
+    dt = time.perf_counter() - t0
+    Zg = Z[:rows].cpu().numpy()
+    diff = float(np.abs(Zg.astype(np.float64) - Zc).max())
+    cpu = {"value": E * passes / dt, "unit": "edges/s", "cores": threads, "kind": "port",
+           "sample": f"first {rows} nodes ({E} typed edges) of the same graph and X, {passes} passes in {dt:.1f}s; "
+                     f"oracle/grl_oracle.c OpenMP typed-CSR SpMM"}
+    parity = {"rows_checked": rows, "max_abs_diff": diff, "bitwise_equal": bool(np.array_equal(Zg, Zc)),
+              "tolerance": 1e-4}
+    return cpu, parity
+
+
+def _time(fn, iters):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters
+
+
+def extras(args, graph, X_full, gather, L, F, dev, E_loc, n_loc):
+    """Secondary numbers (not the headline): fused DropEdge forward, backward
+    (transposed gather), MFMA linear, full GraphConv layer fwd+bwd."""
+    from grl import DropEdge
+    from grl.ops import graph_linear, linear_fwd, typed_aggregate
+
+    res = {}
+    iters = max(3, min(10, args.steps))
+    gd = graph.with_dropedge(DropEdge(0.3, 2, 0, True))
+    ms = _time(lambda: typed_aggregate(X_full, gd), iters)
+    res["spmm_fwd_dropedge_p0.3"] = {"ms": ms, "edges_per_s": E_loc / (ms * 1e-3),
+                                     "alg_GBps": spmm_bytes(E_loc, n_loc, L, F, 0.3) / (ms * 1e-3) / 1e9}
+    Xg = X_full.detach().clone().requires_grad_(True)
+    Z = typed_aggregate(Xg, graph)
+    dZ = torch.randn_like(Z)
+    graph.csc()  # one-time CSC build (cached per graph), not part of the step
+    ms = _time(lambda: torch.autograd.grad(Z, Xg, dZ, retain_graph=True), iters)
+    bwd_bytes = E_loc * F * 4 + 8 * E_loc + 4 * (graph.num_cols + 1) + graph.num_cols * F * 4 * 2
+    res["spmm_bwd"] = {"ms": ms, "edges_per_s": E_loc / (ms * 1e-3), "alg_GBps": bwd_bytes / (ms * 1e-3) / 1e9}
+    torch.manual_seed(3)
+    W = torch.randn((L + 1) * F, F, device=dev) / np.sqrt((L + 1) * F)
+    b = torch.randn(F, device=dev)
+    Zd = Z.detach()
+    ms = _time(lambda: linear_fwd(Zd, W, b, True), iters)
+    flops = 2.0 * Zd.shape[0] * Zd.shape[1] * F
+    res["linear_mfma_fwd"] = {"ms": ms, "TFLOPs": flops / (ms * 1e-3) / 1e12,
+                              "frac_of_f32_mfma_peak": flops / (ms * 1e-3) / 1e12 / F32_MFMA_PEAK_TFS}
+    Wp = W.clone().requires_grad_(True)
+    bp = b.clone().requires_grad_(True)
+    Xl = X_full.detach()[: graph.num_cols].clone().requires_grad_(True)
+    gl = graph.with_dropedge(DropEdge(0.3, 2, 1, True))
+
+    def layer():
+        out = graph_linear(typed_aggregate(Xl, gl), Wp, bp, relu=True)
+        out.sum().backward()
+
+    res["graphconv_layer_fwd_bwd_p0.3"] = {"ms": _time(layer, max(2, iters // 2))}
+    del Z, dZ, Zd
+    return res
+
+
+def run_only(args, graph, X_full, gather, spmm, L, F):
+    """Kernel-isolated loop for rocprofv3 (kernel trace / PMC passes)."""
+    from grl.ops import linear_fwd, typed_aggregate
+
+    if args.only == "fwd":
+        fn = spmm
+    elif args.only == "bwd":
+        Xg = X_full.detach().clone().requires_grad_(True)
+        Z = typed_aggregate(Xg, graph)
+        dZ = torch.randn_like(Z)
+        graph.csc()
+        fn = lambda: torch.autograd.grad(Z, Xg, dZ, retain_graph=True)  # noqa: E731
+    elif args.only == "linear":
+        Z = typed_aggregate(X_full, graph)
+        W = torch.randn((L + 1) * F, F, device=X_full.device) / np.sqrt((L + 1) * F)
+        fn = lambda: linear_fwd(Z, W, None, False)  # noqa: E731
+    else:
+        from grl.ops import graph_linear
+
+        Xl = X_full.detach().clone().requires_grad_(True)
+        W = (torch.randn((L + 1) * F, F, device=X_full.device) / np.sqrt((L + 1) * F)).requires_grad_(True)
+        fn = lambda: graph_linear(typed_aggregate(Xl, graph), W, None, True).sum().backward()  # noqa: E731
+    for _ in range(args.warmup):
+        fn()
+    torch.cuda.synchronize()
+    for _ in range(args.steps):
+        fn()
+    torch.cuda.synchronize()
+
+
+if __name__ == "__main__":
+    main()

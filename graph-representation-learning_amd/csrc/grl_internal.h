@@ -1,0 +1,104 @@
+// Internal helpers shared by the gfx950 translation units of libgrl.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <cstdarg>
+#include <cstdio>
+
+#include "grl.h"
+
+namespace grl {
+
+// ---- thread-local error string (grl_last_error) --------------------------
+void set_error(const char* fmt, ...);
+
+#define GRL_FAIL(code, ...)          \
+  do {                               \
+    ::grl::set_error(__VA_ARGS__);   \
+    return (code);                   \
+  } while (0)
+
+#define GRL_CHECK_ARG(cond, ...)                         \
+  do {                                                   \
+    if (!(cond)) GRL_FAIL(GRL_E_INVALID, __VA_ARGS__);   \
+  } while (0)
+
+#define GRL_HIP(call)                                                        \
+  do {                                                                       \
+    hipError_t _e = (call);                                                  \
+    if (_e != hipSuccess)                                                    \
+      GRL_FAIL(GRL_E_HIP, "%s failed: %s (%s:%d)", #call,                    \
+               hipGetErrorString(_e), __FILE__, __LINE__);                   \
+  } while (0)
+
+// Launch-error check after <<<>>> (no device sync: stream-ordered API).
+#define GRL_LAUNCH_CHECK() GRL_HIP(hipGetLastError())
+
+inline hipStream_t as_stream(grl_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+// ---- DropEdge counter hash -------------------------------------------------
+// splitmix64 finalizer (Steele, Lea, Flood 2014).  The same function is
+// restated independently in oracle/grl_oracle.c and oracle/hash.py.
+__host__ __device__ __forceinline__ uint64_t mix64(uint64_t x) {
+  x ^= x >> 30;
+  x *= 0xBF58476D1CE4E5B9ull;
+  x ^= x >> 27;
+  x *= 0x94D049BB133111EBull;
+  x ^= x >> 31;
+  return x;
+}
+
+__host__ __device__ __forceinline__ uint64_t dropedge_key(uint64_t seed, uint64_t call) {
+  return mix64(mix64(seed ^ 0x6A09E667F3BCC909ull) + call * 0x9E3779B97F4A7C15ull);
+}
+
+__host__ __device__ __forceinline__ uint32_t dropedge_bits(uint64_t key, uint64_t id) {
+  return static_cast<uint32_t>(mix64(key ^ (id * 0xD1B54A32D192ED03ull)) >> 32);
+}
+
+// Synthetic-graph candidate hash: 64 random bits for (seed, candidate, lane).
+__host__ __device__ __forceinline__ uint64_t synth_bits(uint64_t seed, uint64_t k, uint32_t lane) {
+  return mix64(mix64(seed + 0x243F6A8885A308D3ull * (uint64_t)(lane + 1)) ^ (k * 0x9E3779B97F4A7C15ull));
+}
+
+// Plain-data copy of GrlDropEdge passed by value to kernels.
+struct DropDev {
+  uint64_t key;
+  uint32_t threshold;
+  float scale;
+  int32_t active;
+  int32_t drop_self;
+};
+
+inline DropDev to_dev(const GrlDropEdge* de) {
+  DropDev d{0, 0, 1.0f, 0, 0};
+  if (de && de->active) {
+    d.key = de->key;
+    d.threshold = de->threshold;
+    d.scale = de->scale;
+    d.active = 1;
+    d.drop_self = de->drop_self;
+  }
+  return d;
+}
+
+// weight of an entry with value v and global id `id` under DropEdge d
+__device__ __forceinline__ float dropedge_weight(const DropDev& d, float v, uint64_t id) {
+  if (!d.active) return v;
+  return dropedge_bits(d.key, id) >= d.threshold ? v * d.scale : 0.0f;
+}
+
+__device__ __forceinline__ int readlane_i(int v, int lane) { return __builtin_amdgcn_readlane(v, lane); }
+__device__ __forceinline__ float readlane_f(float v, int lane) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+__device__ __forceinline__ int uniform_i(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// Number of CUs of the current device (cached per process).
+int device_cu_count();
+
+}  // namespace grl

@@ -1,0 +1,323 @@
+// Typed-CSR SpMM with fused DropEdge for gfx950 (MI355X).
+//
+// Replaces the dense aggregation of the reference GraphConv,
+//   new_V = torch.matmul(A_pre, V)       gnn/models/networks/robust_gcn.py:45-47
+// with the edge_dropout applied to A_pre right before each call
+//   (gnn/models/networks/drop_robust_gcn.py:38,76,80,85),
+// and its autograd backward dV = A_drop^T dZ (BmmBackward0).
+//
+// Design (HBM-bound gather):
+//  * one wavefront owns one destination row (node) at a time, grid-stride
+//    over rows; each lane owns VEC*NV contiguous feature columns, so every
+//    gathered neighbour row is read as one coalesced 16 B/lane sweep
+//    (1 KiB per wave-instruction at F = 256);
+//  * 64 edge indices are loaded per wave-instruction, the DropEdge weights
+//    are computed for all 64 in parallel from the counter hash, and a
+//    ballot keeps only surviving edges: dropped edges cost no gather bytes;
+//  * surviving edges are issued U at a time (U independent row loads in
+//    flight per wave) and accumulated with one fmaf per edge in CSR order,
+//    so results are deterministic and equal the oracle's fmaf chain;
+//  * type-segment boundaries are wave-uniform scalar compares, so a node's
+//    edges of all types stream through one loop (no per-type round trip).
+#include "grl_internal.h"
+
+namespace grl {
+namespace {
+
+template <int VEC>
+struct VecT;
+template <>
+struct VecT<4> {
+  using type = float4;
+};
+template <>
+struct VecT<1> {
+  using type = float;
+};
+
+__device__ __forceinline__ float4 vzero4() { return make_float4(0.f, 0.f, 0.f, 0.f); }
+__device__ __forceinline__ void vzero(float4& a) { a = vzero4(); }
+__device__ __forceinline__ void vzero(float& a) { a = 0.f; }
+__device__ __forceinline__ void vfma(float4& acc, float w, const float4& x) {
+  acc.x = __builtin_fmaf(w, x.x, acc.x);
+  acc.y = __builtin_fmaf(w, x.y, acc.y);
+  acc.z = __builtin_fmaf(w, x.z, acc.z);
+  acc.w = __builtin_fmaf(w, x.w, acc.w);
+}
+__device__ __forceinline__ void vfma(float& acc, float w, const float& x) { acc = __builtin_fmaf(w, x, acc); }
+__device__ __forceinline__ float4 vmul(float w, const float4& x) {
+  return make_float4(w * x.x, w * x.y, w * x.z, w * x.w);
+}
+__device__ __forceinline__ float vmul(float w, const float& x) { return w * x; }
+
+// BWD = false: forward, rows are destination nodes with S typed segments,
+//               sources are X rows (index = colidx), ids = edge_base + e.
+// BWD = true : backward, rows are source nodes with one segment (CSC column),
+//               sources are dZ rows (index = zrow), ids = edge_base + eid[e].
+template <int VEC, int NV, int U, bool VALS, bool BWD>
+__global__ __launch_bounds__(256) void spmm_kernel(
+    int64_t num_rows, int64_t self_rows, int S, int hs,
+    const int32_t* __restrict__ ptr,    // fwd: rowptr [rows*S+1]; bwd: colptr [rows+1]
+    const int32_t* __restrict__ idx,    // fwd: colidx; bwd: zrow
+    const int32_t* __restrict__ eidv,   // bwd: eid (CSR positions); fwd: unused
+    const float* __restrict__ vals, uint64_t edge_base, uint64_t self_base,
+    const float* __restrict__ src, int64_t lds,  // gathered matrix + row stride
+    int F, float* __restrict__ out, int64_t ldo, DropDev de) {
+  using vec_t = typename VecT<VEC>::type;
+  const int lane = threadIdx.x & 63;
+  const int cbase = blockIdx.y * (64 * VEC * NV);
+  int coff[NV];
+  bool cval[NV];
+#pragma unroll
+  for (int k = 0; k < NV; ++k) {
+    coff[k] = cbase + (k * 64 + lane) * VEC;
+    cval[k] = coff[k] < F;
+  }
+  const int nseg = BWD ? 1 : S;
+  const int64_t zstride = (int64_t)(S + hs) * F;  // dZ row stride (bwd self term)
+
+  const int64_t wave0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + uniform_i(threadIdx.x >> 6);
+  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+
+  for (int64_t n = wave0; n < num_rows; n += nwaves) {
+    float* orow = out + n * ldo;
+    vec_t acc[NV];
+#pragma unroll
+    for (int k = 0; k < NV; ++k) vzero(acc[k]);
+
+    // ---- self term (identity block of A_pre, robust_gcn.py:58-65) ------
+    if (hs && (!BWD || n < self_rows)) {
+      float w = 1.0f;
+      if (de.active && de.drop_self) w = dropedge_weight(de, 1.0f, self_base + (uint64_t)n);
+      const float* srow = BWD ? (src + n * zstride) : (src + n * lds);
+      if (w != 0.0f) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k) {
+          if (cval[k]) {
+            vec_t x = *reinterpret_cast<const vec_t*>(srow + coff[k]);
+            if (BWD)
+              acc[k] = vmul(w, x);
+            else
+              *reinterpret_cast<vec_t*>(orow + coff[k]) = vmul(w, x);
+          }
+        }
+      } else if (!BWD) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k)
+          if (cval[k]) {
+            vec_t z;
+            vzero(z);
+            *reinterpret_cast<vec_t*>(orow + coff[k]) = z;
+          }
+      }
+    }
+
+    // ---- segment pointers: lanes 0..nseg hold ptr[n*nseg + lane] --------
+    const int pv = lane <= nseg ? ptr[n * nseg + lane] : 0;
+    const int e_begin = readlane_i(pv, 0);
+    const int e_end = readlane_i(pv, nseg);
+    int t = 0;
+    int seg_end = readlane_i(pv, 1);
+    float* obase = BWD ? orow : orow + hs * F;
+
+    for (int c0 = e_begin; c0 < e_end; c0 += 64) {
+      const int cnt = min(64, e_end - c0);
+      int sidx = 0;
+      float w = 0.0f;
+      if (lane < cnt) {
+        sidx = idx[c0 + lane];
+        const float v = VALS ? vals[c0 + lane] : 1.0f;
+        const uint64_t id = BWD ? edge_base + (uint64_t)(uint32_t)eidv[c0 + lane]
+                                : edge_base + (uint64_t)(c0 + lane);
+        w = dropedge_weight(de, v, id);
+      }
+      uint64_t kept = __ballot(w != 0.0f);
+      while (kept) {
+        int jj[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (kept) {
+            jj[u] = __builtin_ctzll(kept);
+            kept &= kept - 1;
+          } else {
+            jj[u] = -1;
+          }
+        }
+        vec_t xv[U][NV];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (jj[u] >= 0) {
+            const int r = readlane_i(sidx, jj[u]);
+            const float* srow = src + (int64_t)r * lds;
+#pragma unroll
+            for (int k = 0; k < NV; ++k) {
+              if (cval[k])
+                xv[u][k] = *reinterpret_cast<const vec_t*>(srow + coff[k]);
+              else
+                vzero(xv[u][k]);
+            }
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (jj[u] >= 0) {
+            if (!BWD) {
+              const int e = c0 + jj[u];
+              while (e >= seg_end) {  // flush finished segments (wave-uniform)
+#pragma unroll
+                for (int k = 0; k < NV; ++k) {
+                  if (cval[k]) *reinterpret_cast<vec_t*>(obase + t * F + coff[k]) = acc[k];
+                  vzero(acc[k]);
+                }
+                ++t;
+                seg_end = readlane_i(pv, t + 1);
+              }
+            }
+            const float wj = readlane_f(w, jj[u]);
+#pragma unroll
+            for (int k = 0; k < NV; ++k) vfma(acc[k], wj, xv[u][k]);
+          }
+        }
+      }
+    }
+    // ---- flush the remaining (possibly empty) segments -----------------
+    for (; t < nseg; ++t) {
+#pragma unroll
+      for (int k = 0; k < NV; ++k) {
+        if (cval[k]) *reinterpret_cast<vec_t*>(obase + t * F + coff[k]) = acc[k];
+        vzero(acc[k]);
+      }
+    }
+  }
+}
+
+__global__ void mask_kernel(DropDev de, uint64_t id_base, int64_t count, uint8_t* __restrict__ keep) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    keep[i] = dropedge_weight(de, 1.0f, id_base + (uint64_t)i) != 0.0f ? 1 : 0;
+  }
+}
+
+struct LaunchShape {
+  int vec, nv, ycols;
+};
+
+LaunchShape pick_shape(const float* a, const float* b, int64_t lda, int64_t ldb, int F) {
+  const bool al = (reinterpret_cast<uintptr_t>(a) % 16 == 0) && (reinterpret_cast<uintptr_t>(b) % 16 == 0) &&
+                  (lda % 4 == 0) && (ldb % 4 == 0) && (F % 4 == 0);
+  if (al) {
+    const int nv = F <= 256 ? 1 : 2;
+    return {4, nv, 64 * 4 * nv};
+  }
+  const int nv = F <= 64 ? 1 : (F <= 128 ? 2 : 4);
+  return {1, nv, 64 * nv};
+}
+
+template <bool BWD>
+int launch_spmm(int64_t num_rows, int64_t self_rows, int S, int hs, const int32_t* ptr, const int32_t* idx,
+                const int32_t* eid, const float* vals, uint64_t edge_base, uint64_t self_base,
+                const float* src, int64_t lds, int F, float* out, int64_t ldo, const DropDev& de,
+                hipStream_t stream, const float* align_probe) {
+  if (num_rows == 0) return GRL_OK;
+  const LaunchShape sh = pick_shape(src, align_probe, lds, ldo, F);
+  const int64_t waves_needed = num_rows;
+  const int64_t cap = (int64_t)device_cu_count() * 16;  // 16 x 4-wave blocks per CU in flight
+  const int64_t gx = std::min<int64_t>(ceil_div(waves_needed, 4), cap);
+  const dim3 grid((unsigned)gx, (unsigned)ceil_div(F, sh.ycols));
+  const dim3 block(256);
+  const bool v = vals != nullptr;
+#define GRL_SPMM_LAUNCH(VEC, NV, U, VALS)                                                             \
+  hipLaunchKernelGGL((spmm_kernel<VEC, NV, U, VALS, BWD>), grid, block, 0, stream, num_rows, self_rows, \
+                     S, hs, ptr, idx, eid, vals, edge_base, self_base, src, lds, F, out, ldo, de)
+  if (sh.vec == 4) {
+    if (sh.nv == 1) {
+      if (v) GRL_SPMM_LAUNCH(4, 1, 8, true); else GRL_SPMM_LAUNCH(4, 1, 8, false);
+    } else {
+      if (v) GRL_SPMM_LAUNCH(4, 2, 4, true); else GRL_SPMM_LAUNCH(4, 2, 4, false);
+    }
+  } else {
+    if (sh.nv == 1) {
+      if (v) GRL_SPMM_LAUNCH(1, 1, 8, true); else GRL_SPMM_LAUNCH(1, 1, 8, false);
+    } else if (sh.nv == 2) {
+      if (v) GRL_SPMM_LAUNCH(1, 2, 8, true); else GRL_SPMM_LAUNCH(1, 2, 8, false);
+    } else {
+      if (v) GRL_SPMM_LAUNCH(1, 4, 8, true); else GRL_SPMM_LAUNCH(1, 4, 8, false);
+    }
+  }
+#undef GRL_SPMM_LAUNCH
+  GRL_LAUNCH_CHECK();
+  return GRL_OK;
+}
+
+}  // namespace
+}  // namespace grl
+
+using namespace grl;
+
+extern "C" int grl_dropedge_init(GrlDropEdge* de, float p, uint64_t seed, uint64_t call_id, int32_t drop_self) {
+  GRL_CHECK_ARG(de != nullptr, "grl_dropedge_init: de is NULL");
+  GRL_CHECK_ARG(p >= 0.0f && p == p, "grl_dropedge_init: p must be >= 0 (got %f)", (double)p);
+  de->key = dropedge_key(seed, call_id);
+  de->drop_self = drop_self ? 1 : 0;
+  if (p <= 0.0f) {
+    de->active = 0;
+    de->threshold = 0;
+    de->scale = 1.0f;
+    return GRL_OK;
+  }
+  de->active = 1;
+  if (p >= 1.0f) {  // torch: dropout(p=1) zeroes everything
+    de->threshold = 0xFFFFFFFFu;
+    de->scale = 0.0f;
+    return GRL_OK;
+  }
+  const double thr = std::floor((double)p * 4294967296.0);
+  de->threshold = thr >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)thr;
+  // torch native_dropout: scale = 1/(1-p) computed in double, applied as float.
+  de->scale = (float)(1.0 / (1.0 - (double)p));
+  return GRL_OK;
+}
+
+extern "C" int grl_dropedge_mask(const GrlDropEdge* de, uint64_t id_base, int64_t count, uint8_t* keep,
+                                 grl_stream_t stream) {
+  GRL_CHECK_ARG(count >= 0, "grl_dropedge_mask: negative count");
+  if (count == 0) return GRL_OK;
+  GRL_CHECK_ARG(keep != nullptr, "grl_dropedge_mask: keep is NULL");
+  const DropDev d = to_dev(de);
+  const int64_t blocks = std::min<int64_t>(ceil_div(count, 256), 65536);
+  hipLaunchKernelGGL(mask_kernel, dim3((unsigned)blocks), dim3(256), 0, as_stream(stream), d, id_base, count, keep);
+  GRL_LAUNCH_CHECK();
+  return GRL_OK;
+}
+
+extern "C" int grl_typed_spmm_fwd(const GrlTypedCsr* g, const float* X, int64_t ldx, int32_t F, float* Z,
+                                  const GrlDropEdge* de, grl_stream_t stream) {
+  GRL_CHECK_ARG(g != nullptr, "grl_typed_spmm_fwd: graph is NULL");
+  GRL_CHECK_ARG(g->num_rows >= 0 && g->num_types >= 1 && g->num_types <= 63,
+                "grl_typed_spmm_fwd: num_types must be in [1, 63] (got %d)", g->num_types);
+  GRL_CHECK_ARG(F > 0 && ldx >= F, "grl_typed_spmm_fwd: need F > 0 and ldx >= F (F=%d ldx=%lld)", F,
+                (long long)ldx);
+  if (g->num_rows == 0) return GRL_OK;
+  GRL_CHECK_ARG(X && Z && g->rowptr && (g->nnz == 0 || g->colidx), "grl_typed_spmm_fwd: NULL pointer");
+  GRL_CHECK_ARG(g->nnz < 2147483647LL, "grl_typed_spmm_fwd: nnz %lld exceeds int32", (long long)g->nnz);
+  const int hs = g->has_self ? 1 : 0;
+  const int64_t ldz = (int64_t)(g->num_types + hs) * F;
+  return launch_spmm<false>(g->num_rows, g->num_rows, g->num_types, hs, g->rowptr, g->colidx, nullptr,
+                            g->vals, g->edge_id_base, g->self_id_base, X, ldx, F, Z, ldz, to_dev(de),
+                            as_stream(stream), Z);
+}
+
+extern "C" int grl_typed_spmm_bwd(const GrlTypedCsc* g, const float* dZ, int32_t F, float* dX, int64_t lddx,
+                                  const GrlDropEdge* de, grl_stream_t stream) {
+  GRL_CHECK_ARG(g != nullptr, "grl_typed_spmm_bwd: graph is NULL");
+  GRL_CHECK_ARG(g->num_rows >= 0 && g->self_rows >= 0 && g->self_rows <= g->num_rows,
+                "grl_typed_spmm_bwd: bad num_rows/self_rows");
+  GRL_CHECK_ARG(g->num_types >= 1 && g->num_types <= 63, "grl_typed_spmm_bwd: num_types must be in [1, 63]");
+  GRL_CHECK_ARG(F > 0 && lddx >= F, "grl_typed_spmm_bwd: need F > 0 and lddx >= F");
+  if (g->num_rows == 0) return GRL_OK;
+  GRL_CHECK_ARG(dZ && dX && g->colptr && (g->nnz == 0 || (g->zrow && g->eid)), "grl_typed_spmm_bwd: NULL pointer");
+  const int hs = g->has_self ? 1 : 0;
+  return launch_spmm<true>(g->num_rows, g->self_rows, g->num_types, hs, g->colptr, g->zrow, g->eid, g->vals,
+                           g->edge_id_base, g->self_id_base, dZ, (int64_t)F, F, dX, lddx, to_dev(de),
+                           as_stream(stream), dX);
+}

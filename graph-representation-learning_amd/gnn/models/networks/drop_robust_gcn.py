@@ -1,0 +1,118 @@
+"""GraphCNNDropEdge on the MI355X engine (drop-in for
+gnn/models/networks/drop_robust_gcn.py).
+
+Forward (reference :61-103):
+    emb1 -> [edge_dropout -> GraphConv -> ReLU -> Dropout] x3 (skip concats)
+    -> emb2 -> NodeSelfAtten -> RanPAC random projection -> ReLU -> Dropout
+    -> classifier
+The adjacency is converted once to a TypedGraph (the reference preprocesses
+once in efficient_mode, :69); each edge_dropout call becomes a (p, seed,
+call) record that the aggregation kernels expand on the fly, so no dense
+A_pre and no dense mask exist.  Module names, parameter shapes and creation
+order match the reference (state_dict keys, shapes and init RNG identical).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+from torch import nn
+from torch.nn import functional as F
+
+from gnn.models.base_network import BaseNetwork
+from gnn.models.networks.robust_gcn import GraphConv, NodeSelfAtten, make_linear_relu
+from grl import DropEdge, TypedGraph
+
+RP_FACTOR = 10
+
+
+class RanPACLayer(nn.Module):
+    """Frozen Gaussian random projection (drop_robust_gcn.py:13-28)."""
+
+    def __init__(self, input_dim: int, output_dim: int):
+        super().__init__()
+        self.projection = nn.Linear(input_dim, output_dim, bias=False)
+        for p in self.projection.parameters():
+            p.requires_grad = False
+        nn.init.normal_(self.projection.weight, mean=0, std=1.0)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return self.projection(x)
+
+
+class EdgeDropout(nn.Dropout):
+    """nn.Dropout(p) over the preprocessed adjacency (drop_robust_gcn.py:38).
+
+    On a TypedGraph it returns the graph tagged with a fresh DropEdge draw
+    (training) or untagged (eval / p == 0): the mask is generated inside the
+    aggregation kernels from (seed, call, edge id).  `seed=None` draws each
+    call's seed from torch's default CPU generator, so torch.manual_seed
+    makes runs reproducible; a fixed `seed` numbers calls 0, 1, 2, ...
+    (reset_calls()) for parity tests.  Dense tensors get plain nn.Dropout.
+    """
+
+    def __init__(self, p: float = 0.5, seed: Optional[int] = None):
+        super().__init__(p=p)
+        self.seed = seed
+        self._calls = 0
+
+    def reset_calls(self) -> None:
+        self._calls = 0
+
+    def forward(self, A, drop_self: bool = True):
+        if not isinstance(A, TypedGraph):
+            return super().forward(A)
+        if not self.training or self.p == 0.0:
+            return A.with_dropedge(None)
+        if self.seed is None:
+            seed = int(torch.randint(0, 2**62, (1,)).item())
+            call = 0
+        else:
+            seed, call = self.seed, self._calls
+            self._calls += 1
+        return A.with_dropedge(DropEdge(p=float(self.p), seed=seed, call=call, drop_self=drop_self))
+
+
+class GraphCNNDropEdge(BaseNetwork):
+    def __init__(self, input_dim: int, output_dim: int, num_edges: int, net_size: int = 256,
+                 use_attention: bool = True, dropedge_seed: Optional[int] = None):
+        super().__init__()
+        self.output_dim = output_dim
+        self.net_size = net_size
+        self.emb1 = make_linear_relu(input_dim, self.net_size)
+        self.dropout = nn.Dropout(p=0.5)
+        self.edge_dropout = EdgeDropout(p=0.3, seed=dropedge_seed)
+        self.gcn1 = GraphConv(self.net_size, self.net_size, num_edges)
+        self.gcn2 = GraphConv(self.net_size, self.net_size, num_edges)
+        self.gcn3 = GraphConv(self.net_size * 2, self.net_size, num_edges)
+        half_net_size = self.net_size // 2
+        self.emb2 = make_linear_relu(self.net_size * 2, half_net_size)
+        self.use_attention = use_attention
+        if use_attention:
+            self.self_atten = NodeSelfAtten(half_net_size)
+        rp_size = half_net_size * RP_FACTOR
+        self.w_rand = RanPACLayer(half_net_size, rp_size)
+        self.classifier = nn.Linear(rp_size, output_dim)
+
+    def to_graph(self, A) -> TypedGraph:
+        """Collate-layout dense A (B, N, L, N) -> TypedGraph on the model's device."""
+        if isinstance(A, TypedGraph):
+            return A
+        dev = self.gcn1.h_weights.device
+        return TypedGraph.from_dense(A if A.device == dev else A.to(dev), layout="bnln")
+
+    def forward(self, inputs, efficient_mode: bool = True):
+        V, A = inputs
+        graph = self.to_graph(A)
+        embedding = self.dropout(self.emb1(V))
+        # efficient_mode=True: dropout covers the identity block of A_pre
+        # (:69,:76); False: dropout hits raw A, identity added after (:72-74).
+        ds = bool(efficient_mode)
+        g1 = self.dropout(self.gcn1.propagate(embedding, self.edge_dropout(graph, ds), relu=True))
+        g2 = self.dropout(self.gcn2.propagate(g1, self.edge_dropout(graph, ds), relu=True))
+        g3 = self.dropout(self.gcn3.propagate(torch.cat([g1, g2], dim=-1), self.edge_dropout(graph, ds), relu=True))
+        new_v = self.emb2(torch.cat([g1, g3], dim=-1))
+        if self.use_attention:
+            new_v = self.self_atten(new_v)
+        new_v = self.dropout(F.relu(self.w_rand(new_v)))
+        return self.classifier(new_v)

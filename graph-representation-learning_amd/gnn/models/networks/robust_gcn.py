@@ -1,0 +1,109 @@
+"""GraphConv on the MI355X engine (drop-in for gnn/models/networks/robust_gcn.py).
+
+Reference semantics (robust_gcn.py:14-75): for V (B, N, F) and the
+preprocessed adjacency A_pre (B, (L+1)N, N),
+    new_V = (A_pre @ V).view(B, N, (L+1)F)          # aggregation, :45-47
+    out   = new_V @ h_weights + bias                # dense linear, :50-51
+Here A_pre is a TypedGraph (typed CSR, identity block implicit) and the two
+steps are libgrl kernels: grl_typed_spmm_fwd (HBM-bound gather) and
+grl_linear_fwd (fp32 MFMA).  Parameters, their shapes, creation order and
+init RNG use are the reference's, so state_dicts load both ways and
+torch.manual_seed reproduces the reference's weights bit for bit.
+"""
+from __future__ import annotations
+
+from typing import Optional, Union
+
+import torch
+from torch import nn
+
+from grl import TypedGraph
+from grl.ops import graph_linear, typed_aggregate
+
+
+def make_linear_relu(input_dim: int, output_dim: int) -> nn.Sequential:
+    """Linear + ReLU block (robust_gcn.py:10-11); state_dict keys `0.weight`, `0.bias`."""
+    return nn.Sequential(nn.Linear(input_dim, output_dim), nn.ReLU())
+
+
+AdjLike = Union[TypedGraph, torch.Tensor]
+
+
+class GraphConv(nn.Module):
+    """Multi-edge-type graph convolution, `num_edges` (L) edge types plus the
+    identity block; h_weights rows are grouped by type: rows [l*F, (l+1)*F)
+    multiply segment l (l = 0 is the node itself)."""
+
+    def __init__(self, input_dim: int, output_dim: int, num_edges: int, with_bias: bool = True):
+        super().__init__()
+        self.C = output_dim
+        self.L = num_edges
+        self.F = input_dim
+        self.gpu = torch.cuda.is_available()
+        # Same allocation + init sequence as robust_gcn.py:22-30 (xavier_normal_
+        # on h_weights, then normal_(1e-4, 5e-5) on bias): identical RNG draws.
+        self.h_weights = nn.Parameter(torch.empty(self.F * (self.L + 1), self.C))
+        if with_bias:
+            self.bias = nn.Parameter(torch.empty(self.C))
+        else:
+            self.register_parameter("bias", None)
+        nn.init.xavier_normal_(self.h_weights)
+        if self.bias is not None:
+            nn.init.normal_(self.bias, mean=0.0001, std=0.00005)
+
+    # --------------------------------------------------------------- graph
+    def preprocess_adj(self, adj: AdjLike) -> TypedGraph:
+        """(B, N, N, L) adjacency -> TypedGraph (the sparse A_pre of
+        robust_gcn.py:53-72: identity block + typed segments)."""
+        if isinstance(adj, TypedGraph):
+            return adj
+        return TypedGraph.from_dense(self._on_device(adj), layout="bnnl")
+
+    def _on_device(self, t: torch.Tensor) -> torch.Tensor:
+        dev = self.h_weights.device
+        return t if t.device == dev else t.to(dev)
+
+    def _graph(self, A: AdjLike, preprocess_A: bool) -> TypedGraph:
+        if isinstance(A, TypedGraph):
+            return A
+        if preprocess_A:
+            return self.preprocess_adj(A)
+        return TypedGraph.from_dense(self._on_device(A), layout="pre")
+
+    # ------------------------------------------------------------- forward
+    def propagate(self, V: torch.Tensor, graph: TypedGraph, relu: bool = False) -> torch.Tensor:
+        """Aggregate + linear (+ fused ReLU) on a ready TypedGraph."""
+        B, N = V.shape[0], V.shape[1]
+        Z = typed_aggregate(V, graph)  # (B*N, (L+1)F), the reference's new_V
+        out = graph_linear(Z, self.h_weights, self.bias, relu=relu)
+        return out.view(B, N, self.C)
+
+    def forward(self, V: torch.Tensor, A: AdjLike, preprocess_A: bool = True) -> torch.Tensor:
+        """V: (B, N, F).  A: TypedGraph, or dense (B, N, N, L) when
+        preprocess_A, or dense A_pre (B, (L+1)N, N) when not."""
+        return self.propagate(V, self._graph(A, preprocess_A), relu=False)
+
+    def __repr__(self) -> str:
+        return f"GraphConv(in_dim={self.F}, out_dim={self.C}, num_edges={self.L}, bias={self.bias is not None})"
+
+
+class NodeSelfAtten(nn.Module):
+    """Dense node self-attention (robust_gcn.py:78-99): gamma * softmax(f g^T) h + V.
+    Runs on torch/hipBLASLt; a fused kernel is the §8(f) 'next' row."""
+
+    def __init__(self, input_dim: int):
+        super().__init__()
+        self.F = input_dim
+        self.f = make_linear_relu(input_dim, int(self.F // 8))
+        self.g = make_linear_relu(input_dim, int(self.F // 8))
+        self.h = make_linear_relu(input_dim, self.F)
+        self.softmax = nn.Softmax(-1)
+        self.gamma = nn.Parameter(torch.empty(input_dim))
+        nn.init.normal_(self.gamma)
+
+    def forward(self, V: torch.Tensor) -> torch.Tensor:
+        scores = torch.matmul(self.f(V), self.g(V).transpose(1, 2))  # B x N x N
+        return self.gamma * torch.matmul(self.softmax(scores), self.h(V)) + V
+
+    def __repr__(self) -> str:
+        return f"NodeSelfAttention(input_dim={self.F})"

@@ -1,0 +1,146 @@
+"""ctypes binding of libgrl.so (C ABI in include/grl.h).
+
+This is the whole Python <-> native boundary: plain pointers, sizes and a
+hipStream_t handle.  Tensors only appear in the callers (grl.graph,
+grl.ops), which pass ``tensor.data_ptr()`` and the current torch stream.
+
+There is deliberately no fallback: if libgrl.so is missing or a call fails,
+GrlError is raised (the reference raises Python exceptions for bad inputs,
+e.g. gnn/models/base_network.py:34-47; we keep that convention).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("GRL_LIB_PATH", os.path.join(_HERE, "libgrl.so"))
+
+
+class GrlError(RuntimeError):
+    """A libgrl call failed (negative GRL_E_* status)."""
+
+
+GRL_OK = 0
+GRL_E_INVALID = -1
+GRL_E_UNSUPPORTED = -2
+GRL_E_HIP = -3
+GRL_E_WORKSPACE = -4
+GRL_E_OVERFLOW = -5
+
+_c_i32 = ctypes.c_int32
+_c_i64 = ctypes.c_int64
+_c_u64 = ctypes.c_uint64
+_c_vp = ctypes.c_void_p
+_c_size = ctypes.c_size_t
+
+
+class GrlTypedCsr(ctypes.Structure):
+    _fields_ = [
+        ("num_rows", _c_i64),
+        ("num_types", _c_i32),
+        ("has_self", _c_i32),
+        ("rowptr", _c_vp),
+        ("colidx", _c_vp),
+        ("vals", _c_vp),
+        ("nnz", _c_i64),
+        ("edge_id_base", _c_u64),
+        ("self_id_base", _c_u64),
+    ]
+
+
+class GrlTypedCsc(ctypes.Structure):
+    _fields_ = [
+        ("num_rows", _c_i64),
+        ("self_rows", _c_i64),
+        ("num_types", _c_i32),
+        ("has_self", _c_i32),
+        ("colptr", _c_vp),
+        ("zrow", _c_vp),
+        ("eid", _c_vp),
+        ("vals", _c_vp),
+        ("nnz", _c_i64),
+        ("edge_id_base", _c_u64),
+        ("self_id_base", _c_u64),
+    ]
+
+
+class GrlDropEdge(ctypes.Structure):
+    _fields_ = [
+        ("key", _c_u64),
+        ("threshold", ctypes.c_uint32),
+        ("scale", ctypes.c_float),
+        ("active", _c_i32),
+        ("drop_self", _c_i32),
+    ]
+
+
+class GrlSynthSpec(ctypes.Structure):
+    _fields_ = [
+        ("kind", _c_i32),
+        ("num_types", _c_i32),
+        ("num_nodes", _c_i64),
+        ("num_candidates", _c_i64),
+        ("seed", _c_u64),
+        ("row_begin", _c_i64),
+        ("row_end", _c_i64),
+    ]
+
+
+_P = ctypes.POINTER
+# name -> (restype, argtypes); mirrors include/grl.h one for one.
+SIGNATURES = {
+    "grl_version": (ctypes.c_char_p, []),
+    "grl_last_error": (ctypes.c_char_p, []),
+    "grl_dropedge_init": (_c_i32, [_P(GrlDropEdge), ctypes.c_float, _c_u64, _c_u64, _c_i32]),
+    "grl_dropedge_mask": (_c_i32, [_P(GrlDropEdge), _c_u64, _c_i64, _c_vp, _c_vp]),
+    "grl_typed_spmm_fwd": (_c_i32, [_P(GrlTypedCsr), _c_vp, _c_i64, _c_i32, _c_vp, _P(GrlDropEdge), _c_vp]),
+    "grl_typed_spmm_bwd": (_c_i32, [_P(GrlTypedCsc), _c_vp, _c_i32, _c_vp, _c_i64, _P(GrlDropEdge), _c_vp]),
+    "grl_linear_fwd": (_c_i32, [_c_vp, _c_i64, _c_vp, _c_vp, _c_vp, _c_i64, _c_i32, _c_i32, _c_i32, _c_vp]),
+    "grl_dense_to_csr_workspace_size": (_c_size, [_c_i64]),
+    "grl_dense_to_csr_rowptr": (_c_i32, [_c_vp, _c_i64, _c_i64, _c_i32, _P(_c_i64), _c_vp, _c_vp, _c_size, _c_vp]),
+    "grl_dense_to_csr_fill": (_c_i32, [_c_vp, _c_i64, _c_i64, _c_i32, _P(_c_i64), _c_vp, _c_vp, _c_vp, _c_vp]),
+    "grl_csr_to_csc_workspace_size": (_c_size, [_c_i64, _c_i64]),
+    "grl_csr_to_csc": (_c_i32, [_P(GrlTypedCsr), _c_i64, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_size, _c_vp]),
+    "grl_synth_count": (_c_i32, [_P(GrlSynthSpec), _c_vp, _c_vp]),
+    "grl_synth_workspace_size": (_c_size, [_P(GrlSynthSpec), _c_i64]),
+    "grl_synth_build": (_c_i32, [_P(GrlSynthSpec), _c_i64, _c_vp, _c_vp, _c_vp, _c_vp, _c_size, _c_vp]),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libgrl.so once; raise GrlError (never fall back) if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise GrlError(
+                    f"libgrl.so not found at {LIB_PATH}; build it with "
+                    "`make -C graph-representation-learning_amd/csrc` or __graft_entry__.build()")
+            handle = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(handle, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = handle
+    return _lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != GRL_OK:
+        msg = lib().grl_last_error()
+        raise GrlError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+
+def call(name: str, *args) -> None:
+    check(getattr(lib(), name)(*args), name)
+
+
+def version() -> str:
+    return lib().grl_version().decode()

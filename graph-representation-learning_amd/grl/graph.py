@@ -1,0 +1,273 @@
+"""TypedGraph: the HBM-resident sparse stand-in for the reference's A_pre.
+
+The reference materialises A_pre = preprocess_adj(A) as a dense
+(B, (L+1)N, N) tensor (gnn/models/networks/robust_gcn.py:53-72) and draws a
+dense Bernoulli mask over it for every edge_dropout call
+(gnn/models/networks/drop_robust_gcn.py:76,80,85).  A TypedGraph holds the
+same operator as a typed CSR (rows = destination nodes, one segment per edge
+type, implicit identity block) plus, lazily, its CSC for the backward pass.
+DropEdge is a small (p, seed, call) record; the mask is regenerated inside
+the kernels and never stored.
+
+Layout in HBM (int32 indices, fp32 values):
+  rowptr [num_rows*L + 1]   colidx [nnz]   vals [nnz] or None (all ones)
+  colptr [num_cols + 1]     zrow [nnz]     eid [nnz]   cvals [nnz] (CSC)
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Optional, Tuple
+
+import torch
+
+from . import _lib
+from ._lib import GrlDropEdge, GrlSynthSpec, GrlTypedCsc, GrlTypedCsr, call
+
+
+def current_stream_handle(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _require_device(t: torch.Tensor, what: str) -> None:
+    if not t.is_cuda:
+        raise _lib.GrlError(
+            f"{what} must be a ROCm device tensor (got {t.device}); the MI355X engine has no CPU path")
+
+
+@dataclass(frozen=True)
+class DropEdge:
+    """One edge_dropout draw: nn.Dropout(p) over A_pre (drop_robust_gcn.py:38)."""
+
+    p: float
+    seed: int
+    call: int = 0
+    drop_self: bool = True  # efficient_mode=True masks the identity block too
+
+    def to_c(self) -> GrlDropEdge:
+        de = GrlDropEdge()
+        call("grl_dropedge_init", ctypes.byref(de), float(self.p), int(self.seed) & (2**64 - 1),
+             int(self.call) & (2**64 - 1), int(self.drop_self))
+        return de
+
+
+class TypedGraph:
+    """Typed CSR over `num_rows` destination nodes gathering from `num_cols`
+    source rows.  `batch_shape = (B, N)` records a block-diagonal batch of B
+    graphs of N (padded) nodes each, row id = b*N + n."""
+
+    def __init__(self, rowptr: torch.Tensor, colidx: torch.Tensor, num_types: int, *,
+                 vals: Optional[torch.Tensor] = None, has_self: bool = True, num_cols: Optional[int] = None,
+                 edge_id_base: int = 0, self_id_base: Optional[int] = None, self_rows: Optional[int] = None,
+                 batch_shape: Optional[Tuple[int, int]] = None, _shared: Optional[dict] = None):
+        _require_device(rowptr, "rowptr")
+        if rowptr.dtype != torch.int32 or colidx.dtype != torch.int32:
+            raise _lib.GrlError("rowptr/colidx must be int32")
+        if (rowptr.numel() - 1) % num_types:
+            raise _lib.GrlError(f"rowptr length {rowptr.numel()} is not num_rows*{num_types}+1")
+        self.rowptr = rowptr.contiguous()
+        self.colidx = colidx.contiguous()
+        self.vals = None if vals is None else vals.contiguous().float()
+        self.num_types = int(num_types)
+        self.has_self = bool(has_self)
+        self.num_rows = (rowptr.numel() - 1) // num_types
+        self.num_cols = self.num_rows if num_cols is None else int(num_cols)
+        self.nnz = int(colidx.numel())
+        self.edge_id_base = int(edge_id_base)
+        self.self_id_base = self.nnz if self_id_base is None else int(self_id_base)
+        self.self_rows = self.num_rows if self_rows is None else int(self_rows)
+        self.batch_shape = batch_shape
+        self.dropedge: Optional[DropEdge] = None
+        self._shared = {"csc": None} if _shared is None else _shared
+
+    # ------------------------------------------------------------------ views
+    @property
+    def device(self) -> torch.device:
+        return self.rowptr.device
+
+    @property
+    def segments(self) -> int:
+        """Output segments per row of Z: identity + typed (L+1 in the reference)."""
+        return self.num_types + (1 if self.has_self else 0)
+
+    def with_dropedge(self, de: Optional[DropEdge]) -> "TypedGraph":
+        """Shallow copy carrying a DropEdge draw (shares all device arrays and
+        the CSC cache), i.e. the reference's edge_dropout(A)."""
+        g = TypedGraph.__new__(TypedGraph)
+        g.__dict__.update(self.__dict__)
+        g.dropedge = de
+        return g
+
+    def __repr__(self) -> str:
+        return (f"TypedGraph(rows={self.num_rows}, cols={self.num_cols}, types={self.num_types}, "
+                f"nnz={self.nnz}, has_self={self.has_self}, vals={'yes' if self.vals is not None else 'ones'}, "
+                f"dropedge={self.dropedge})")
+
+    # ------------------------------------------------------------ C structs
+    def csr_c(self) -> GrlTypedCsr:
+        g = GrlTypedCsr()
+        g.num_rows = self.num_rows
+        g.num_types = self.num_types
+        g.has_self = int(self.has_self)
+        g.rowptr = self.rowptr.data_ptr()
+        g.colidx = self.colidx.data_ptr() if self.nnz else None
+        g.vals = self.vals.data_ptr() if self.vals is not None and self.nnz else None
+        g.nnz = self.nnz
+        g.edge_id_base = self.edge_id_base
+        g.self_id_base = self.self_id_base
+        return g
+
+    def csc(self) -> dict:
+        """CSC (colptr, zrow, eid, cvals), built once on the device and cached."""
+        c = self._shared.get("csc")
+        if c is not None:
+            return c
+        dev = self.device
+        ws_bytes = _lib.lib().grl_csr_to_csc_workspace_size(self.nnz, self.num_cols)
+        if ws_bytes == 0:
+            raise _lib.GrlError("grl_csr_to_csc_workspace_size failed")
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+        colptr = torch.empty(self.num_cols + 1, dtype=torch.int32, device=dev)
+        n = max(self.nnz, 1)
+        zrow = torch.empty(n, dtype=torch.int32, device=dev)
+        eid = torch.empty(n, dtype=torch.int32, device=dev)
+        cvals = torch.empty(n, dtype=torch.float32, device=dev) if self.vals is not None else None
+        csr = self.csr_c()
+        call("grl_csr_to_csc", ctypes.byref(csr), self.num_cols, colptr.data_ptr(), zrow.data_ptr(),
+             eid.data_ptr(), cvals.data_ptr() if cvals is not None else None, ws.data_ptr(), ws_bytes,
+             current_stream_handle(dev))
+        c = {"colptr": colptr, "zrow": zrow, "eid": eid, "cvals": cvals}
+        self._shared["csc"] = c
+        return c
+
+    def csc_c(self) -> GrlTypedCsc:
+        c = self.csc()
+        s = GrlTypedCsc()
+        s.num_rows = self.num_cols
+        s.self_rows = min(self.self_rows, self.num_cols)
+        s.num_types = self.num_types
+        s.has_self = int(self.has_self)
+        s.colptr = c["colptr"].data_ptr()
+        s.zrow = c["zrow"].data_ptr()
+        s.eid = c["eid"].data_ptr()
+        s.vals = c["cvals"].data_ptr() if c["cvals"] is not None else None
+        s.nnz = self.nnz
+        s.edge_id_base = self.edge_id_base
+        s.self_id_base = self.self_id_base
+        return s
+
+    # ----------------------------------------------------------- builders
+    @classmethod
+    def from_dense(cls, A: torch.Tensor, layout: str = "bnln", has_self: bool = True,
+                   keep_values: Optional[bool] = None) -> "TypedGraph":
+        """Dense adjacency -> TypedGraph on A's device.
+
+        layout "bnln": the collate layout (B, N, L, N) the dataset emits
+            (gnn/data_generator/data_process/graph_utils.py:782-834);
+        layout "bnnl": the permuted (B, N, N, L) view GraphConv.forward takes
+            (drop_robust_gcn.py:63, robust_gcn.py:32-37);
+        layout "pre":  an already preprocessed A_pre (B, (L+1)N, N)
+            (robust_gcn.py:71); its identity block becomes an ordinary typed
+            segment (has_self=False, L+1 types) so arbitrary values, e.g. a
+            dropout-scaled A_pre, are honoured exactly.
+        keep_values None: store vals only if some nonzero differs from 1.
+        """
+        _require_device(A, "adjacency")
+        if A.dtype != torch.float32:
+            A = A.float()
+        if layout == "bnln":
+            B, N, L, N2 = A.shape
+            sb, sn, st, sm = A.stride()
+        elif layout == "bnnl":
+            B, N, N2, L = A.shape
+            sb, sn, sm, st = A.stride()
+        elif layout == "pre":
+            B, R, N = A.shape
+            if R % N:
+                raise _lib.GrlError(f"A_pre rows {R} not a multiple of N={N}")
+            L = R // N
+            N2 = N
+            A = A.reshape(B, N, L, N)
+            sb, sn, st, sm = A.stride()
+            has_self = False
+        else:
+            raise _lib.GrlError(f"unknown adjacency layout {layout!r}")
+        if N != N2:
+            raise _lib.GrlError(f"adjacency is not square over nodes: {tuple(A.shape)}")
+        dev = A.device
+        stream = current_stream_handle(dev)
+        strides = (ctypes.c_int64 * 4)(sb, sn, st, sm)
+        rows = B * N * L
+        ws_bytes = _lib.lib().grl_dense_to_csr_workspace_size(rows)
+        ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=dev)
+        rowptr = torch.empty(rows + 1, dtype=torch.int32, device=dev)
+        call("grl_dense_to_csr_rowptr", A.data_ptr(), B, N, L, strides, rowptr.data_ptr(), ws.data_ptr(),
+             ws_bytes, stream)
+        nnz = int(rowptr[-1].item())
+        colidx = torch.empty(max(nnz, 1), dtype=torch.int32, device=dev)
+        vals = torch.empty(max(nnz, 1), dtype=torch.float32, device=dev)
+        call("grl_dense_to_csr_fill", A.data_ptr(), B, N, L, strides, rowptr.data_ptr(), colidx.data_ptr(),
+             vals.data_ptr(), stream)
+        colidx, vals = colidx[:nnz], vals[:nnz]
+        if keep_values is None:
+            keep_values = bool(nnz) and not bool((vals == 1.0).all().item())
+        return cls(rowptr, colidx, L, vals=vals if keep_values else None, has_self=has_self,
+                   num_cols=B * N, batch_shape=(B, N))
+
+    @classmethod
+    def from_csr_host(cls, rowptr, colidx, num_types: int, device, **kw) -> "TypedGraph":
+        """From host (numpy / CPU tensor) CSR arrays."""
+        rp = torch.as_tensor(rowptr, dtype=torch.int32).to(device)
+        ci = torch.as_tensor(colidx, dtype=torch.int32).to(device)
+        vals = kw.pop("vals", None)
+        if vals is not None:
+            vals = torch.as_tensor(vals, dtype=torch.float32).to(device)
+        return cls(rp, ci, num_types, vals=vals, **kw)
+
+    @classmethod
+    def synthetic(cls, num_nodes: int, avg_deg: float, num_types: int = 6, *, kind: str = "er", seed: int = 0,
+                  row_range: Optional[Tuple[int, int]] = None, device="cuda") -> "TypedGraph":
+        """Seeded synthetic typed graph: num_nodes*avg_deg
+        candidate edges (src, type, dst), deduped.  kind "er" (uniform) or
+        "rmat" (a,b,c,d = .57,.19,.19,.05, num_nodes = 2^scale).  row_range
+        selects the node-range shard [begin, end) this rank owns; colidx stay
+        global node ids."""
+        dev = torch.device(device)
+        rb, re = (0, num_nodes) if row_range is None else row_range
+        spec = GrlSynthSpec()
+        spec.kind = {"er": 0, "rmat": 1}[kind]
+        spec.num_types = num_types
+        spec.num_nodes = num_nodes
+        spec.num_candidates = int(round(num_nodes * avg_deg))
+        spec.seed = seed
+        spec.row_begin, spec.row_end = rb, re
+        stream = current_stream_handle(dev)
+        cnt_t = torch.zeros(1, dtype=torch.int64, device=dev)
+        call("grl_synth_count", ctypes.byref(spec), cnt_t.data_ptr(), stream)
+        count = int(cnt_t.item())
+        ws_bytes = _lib.lib().grl_synth_workspace_size(ctypes.byref(spec), count)
+        if ws_bytes == 0:
+            raise _lib.GrlError("grl_synth_workspace_size failed")
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+        rowptr = torch.empty((re - rb) * num_types + 1, dtype=torch.int32, device=dev)
+        colidx = torch.empty(max(count, 1), dtype=torch.int32, device=dev)
+        nnz_t = torch.zeros(1, dtype=torch.int64, device=dev)
+        call("grl_synth_build", ctypes.byref(spec), count, rowptr.data_ptr(), colidx.data_ptr(), nnz_t.data_ptr(),
+             ws.data_ptr(), ws_bytes, stream)
+        nnz = int(nnz_t.item())
+        colidx = colidx[:nnz].clone()
+        del ws
+        return cls(rowptr, colidx, num_types, has_self=True, num_cols=num_nodes)
+
+    # -------------------------------------------------------------- helpers
+    def to_host(self) -> dict:
+        """numpy copies of the CSR arrays (tests / CPU baseline)."""
+        return {"rowptr": self.rowptr.cpu().numpy(), "colidx": self.colidx.cpu().numpy(),
+                "vals": None if self.vals is None else self.vals.cpu().numpy()}
+
+    def dropedge_mask(self, de: DropEdge, id_base: int, count: int) -> torch.Tensor:
+        keep = torch.empty(max(count, 1), dtype=torch.uint8, device=self.device)
+        c = de.to_c()
+        call("grl_dropedge_mask", ctypes.byref(c), id_base, count, keep.data_ptr(),
+             current_stream_handle(self.device))
+        return keep[:count]

@@ -1,0 +1,107 @@
+"""Autograd ops over the libgrl kernels.
+
+  typed_aggregate(X, graph)   Z = A_drop X           robust_gcn.py:45-47
+                              (+ edge_dropout, drop_robust_gcn.py:76,80,85)
+  graph_linear(Z, W, b, relu) out = Z W + b [ReLU]    robust_gcn.py:50
+                              (+ F.relu, drop_robust_gcn.py:76,80,85)
+
+Both run on the current torch HIP stream; backward regenerates the DropEdge
+mask from the graph's (p, seed, call) record, exactly like forward.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import call
+from .graph import TypedGraph, _require_device, current_stream_handle
+
+
+def _rows_view(X: torch.Tensor) -> torch.Tensor:
+    """2-D row view with unit column stride (no copy when possible)."""
+    X2 = X.reshape(-1, X.shape[-1])
+    if X2.stride(-1) != 1:
+        X2 = X2.contiguous()
+    return X2
+
+
+class _TypedAggregate(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, X: torch.Tensor, graph: TypedGraph) -> torch.Tensor:
+        _require_device(X, "node features")
+        if X.dtype != torch.float32:
+            raise _lib.GrlError(f"node features must be float32 (got {X.dtype})")
+        X2 = _rows_view(X)
+        if X2.shape[0] != graph.num_cols:
+            raise _lib.GrlError(f"features have {X2.shape[0]} rows, graph gathers from {graph.num_cols}")
+        F = X2.shape[1]
+        Z = torch.empty(graph.num_rows, graph.segments * F, dtype=torch.float32, device=X.device)
+        csr = graph.csr_c()
+        de = graph.dropedge.to_c() if graph.dropedge is not None else None
+        call("grl_typed_spmm_fwd", ctypes.byref(csr), X2.data_ptr(), X2.stride(0), F, Z.data_ptr(),
+             ctypes.byref(de) if de is not None else None, current_stream_handle(X.device))
+        ctx.graph = graph
+        ctx.xshape = X.shape
+        return Z
+
+    @staticmethod
+    def backward(ctx, dZ: torch.Tensor):
+        graph: TypedGraph = ctx.graph
+        dZ = dZ.contiguous().float()
+        F = ctx.xshape[-1]
+        dX = torch.empty(graph.num_cols, F, dtype=torch.float32, device=dZ.device)
+        csc = graph.csc_c()
+        de = graph.dropedge.to_c() if graph.dropedge is not None else None
+        call("grl_typed_spmm_bwd", ctypes.byref(csc), dZ.data_ptr(), F, dX.data_ptr(), F,
+             ctypes.byref(de) if de is not None else None, current_stream_handle(dZ.device))
+        return dX.view(ctx.xshape), None
+
+
+def typed_aggregate(X: torch.Tensor, graph: TypedGraph) -> torch.Tensor:
+    """Z[n, s*F:(s+1)*F]: segment 0 = own row (identity block), segment 1+t =
+    sum over type-t neighbours; rows of X = graph.num_cols."""
+    return _TypedAggregate.apply(X, graph)
+
+
+def linear_fwd(Z2: torch.Tensor, W: torch.Tensor, b, relu: bool) -> torch.Tensor:
+    M, K = Z2.shape
+    C = W.shape[1]
+    out = torch.empty(M, C, dtype=torch.float32, device=Z2.device)
+    call("grl_linear_fwd", Z2.data_ptr(), Z2.stride(0), W.data_ptr(), b.data_ptr() if b is not None else None,
+         out.data_ptr(), M, K, C, int(relu), current_stream_handle(Z2.device))
+    return out
+
+
+class _GraphLinear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, Z: torch.Tensor, W: torch.Tensor, b, relu: bool):
+        Z2 = _rows_view(Z)
+        Wc = W.contiguous()
+        out = linear_fwd(Z2, Wc, b.contiguous() if b is not None else None, relu)
+        ctx.relu = relu
+        ctx.has_b = b is not None
+        ctx.save_for_backward(Z2, Wc, out if relu else None)
+        return out
+
+    @staticmethod
+    def backward(ctx, g: torch.Tensor):
+        Z2, W, out = ctx.saved_tensors
+        g = g.contiguous()
+        if ctx.relu:
+            g = g * (out > 0).to(g.dtype)
+        dZ = dW = db = None
+        if ctx.needs_input_grad[0]:
+            dZ = g @ W.t()
+        if ctx.needs_input_grad[1]:
+            dW = Z2.t() @ g
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            db = g.sum(0)
+        return dZ, dW, db, None
+
+
+def graph_linear(Z: torch.Tensor, W: torch.Tensor, b=None, relu: bool = False) -> torch.Tensor:
+    """out = Z W + b (optionally ReLU) on MFMA; Z rows x (L+1)F."""
+    _require_device(Z, "aggregated features")
+    return _GraphLinear.apply(Z, W, b, relu)

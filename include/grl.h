@@ -1,0 +1,225 @@
+/*
+ * grl.h — C ABI of the MI355X (gfx950) message-passing engine behind
+ * gnn.models.GraphCNNDropEdge / gnn.models.networks.robust_gcn.GraphConv.
+ *
+ * The reference (hoangthanh283/graph-representation-learning) is pure
+ * Python/PyTorch and has no FFI; every entry point below replaces one aten
+ * call (or one block of Python) on its GraphConv/DropEdge hot path.  The
+ * citation on each function names the reference code it stands in for
+ * (paths relative to the reference repository root).  A maintainer binds
+ * these with ctypes; nothing here mentions torch.
+ *
+ * Conventions
+ *  - Every pointer marked "device" is HBM memory owned by the caller (torch
+ *    caching allocator).  The library never allocates or frees persistent
+ *    memory; scratch comes from a caller workspace sized by *_workspace_size.
+ *  - Every call is stream-ordered on `stream` (a hipStream_t passed as void*,
+ *    NULL = default stream) and never synchronises the device, so calls can
+ *    be captured into a hipGraph.
+ *  - Return value 0 = success, negative GRL_E_* = failure; grl_last_error()
+ *    returns a thread-local message for the last failure on this thread.
+ *  - fp32 features, int32 indices.  Sums over a row's edges run in CSR order
+ *    with one fmaf per edge, so results are bitwise reproducible run to run
+ *    (no float atomics anywhere).
+ */
+#ifndef GRL_H_
+#define GRL_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* grl_stream_t; /* hipStream_t */
+
+enum {
+  GRL_OK = 0,
+  GRL_E_INVALID = -1,     /* bad shape / null pointer / inconsistent sizes   */
+  GRL_E_UNSUPPORTED = -2, /* well-formed request this build does not handle  */
+  GRL_E_HIP = -3,         /* a HIP runtime call failed                       */
+  GRL_E_WORKSPACE = -4,   /* workspace smaller than *_workspace_size()       */
+  GRL_E_OVERFLOW = -5     /* a count does not fit the int32 index type       */
+};
+
+/*
+ * Typed CSR: the sparse form of the reference's preprocessed adjacency
+ * A_pre[b, n*(L+1)+l, m] (gnn/models/networks/robust_gcn.py:53-72).
+ * Row segment (n, t) for t in [0, num_types) lists the source rows m whose
+ * features node n aggregates through edge type t, i.e. the nonzeros of
+ * A_in[b, n, t, m] in the collate layout (B, N, L, N).  With has_self = 1 the
+ * identity block l = 0 of A_pre is implicit (robust_gcn.py:58-65) and output
+ * segment 0 of row n is the node's own feature row.
+ *
+ * Z row n has (has_self + num_types) segments of F floats:
+ *   Z[n, has_self + t, :] = sum_{e in seg(n,t)} w_e * X[colidx[e], :]
+ *   Z[n, 0, :]            = w_self(n) * X[n, :]             (if has_self)
+ * which is exactly new_V of robust_gcn.py:45-47 for one graph of the batch.
+ */
+typedef struct GrlTypedCsr {
+  int64_t num_rows;      /* destination nodes (rows of Z)                     */
+  int32_t num_types;     /* typed segments per node (L, num_edges)            */
+  int32_t has_self;      /* 1: implicit identity segment 0                    */
+  const int32_t* rowptr; /* device [num_rows*num_types + 1], rowptr[0] == 0   */
+  const int32_t* colidx; /* device [nnz]: source row of X                     */
+  const float* vals;     /* device [nnz] edge values, or NULL for all-ones    */
+  int64_t nnz;
+  uint64_t edge_id_base; /* global DropEdge id of colidx[0] (node-range shard)*/
+  uint64_t self_id_base; /* global DropEdge id of row 0's self loop           */
+} GrlTypedCsr;
+
+/*
+ * Transposed typed CSR (CSC over source rows), used by the backward pass
+ * dX = A_drop^T dZ (the BmmBackward0 of robust_gcn.py:45).
+ *   dX[m, :] = w_self(m) * dZ[m, 0, :]  (m < self_rows, if has_self)
+ *            + sum_{i in col(m)} w_{eid[i]} * dZ_rows[zrow[i], :]
+ * where dZ_rows is dZ viewed as contiguous rows of F floats, so
+ * zrow = n*(has_self+num_types) + has_self + t for edge (n, t, m).
+ */
+typedef struct GrlTypedCsc {
+  int64_t num_rows;      /* rows of dX (local + halo rows in a shard)         */
+  int64_t self_rows;     /* rows that own a self loop (local rows)            */
+  int32_t num_types;
+  int32_t has_self;
+  const int32_t* colptr; /* device [num_rows + 1]                              */
+  const int32_t* zrow;   /* device [nnz]                                       */
+  const int32_t* eid;    /* device [nnz]: CSR position of the edge (local)     */
+  const float* vals;     /* device [nnz] values in CSC order, or NULL          */
+  int64_t nnz;
+  uint64_t edge_id_base; /* as in the matching GrlTypedCsr                     */
+  uint64_t self_id_base;
+} GrlTypedCsc;
+
+/*
+ * DropEdge: the reference's nn.Dropout(p) applied to A_pre
+ * (gnn/models/networks/drop_robust_gcn.py:38,76,80,85) as a fused,
+ * regenerable mask.  An entry with global id `id` is kept iff
+ *   grl_dropedge_bits(key, id) >= threshold,   weight = value * scale,
+ * with scale = float(1/(1-p)) as torch's native dropout computes it.
+ * Edge ids are CSR positions (+ edge_id_base); the self loop of global node g
+ * has id E_total + g.  No mask tensor ever exists.
+ */
+typedef struct GrlDropEdge {
+  uint64_t key;       /* grl_dropedge_key(seed, call_id)                       */
+  uint32_t threshold; /* floor(p * 2^32); 0 keeps everything                   */
+  float scale;        /* 1/(1-p) (0 when p >= 1); 1 when p == 0                */
+  int32_t active;     /* 0: identity (eval mode / p == 0)                      */
+  int32_t drop_self;  /* 1: the identity block is masked too (efficient_mode)  */
+} GrlDropEdge;
+
+/* Library identity / errors. */
+const char* grl_version(void);
+const char* grl_last_error(void);
+
+/* Fills *de for drop probability p, RNG stream (seed, call_id).
+ * drop_self = 1 reproduces efficient_mode=True (drop_robust_gcn.py:69,76):
+ * the mask covers the identity block; 0 reproduces efficient_mode=False,
+ * where dropout hits raw A before preprocess_adj adds the identity.
+ * Host-only, no device work.  Replaces nn.Dropout.__init__/bernoulli_ setup. */
+int grl_dropedge_init(GrlDropEdge* de, float p, uint64_t seed, uint64_t call_id,
+                      int32_t drop_self);
+
+/* keep[i] = 1 if id_base + i survives DropEdge `de`, else 0 (i < count).
+ * Exposes the fused mask for parity checks against the dense reference
+ * (the mask nn.Dropout would draw over A_pre, drop_robust_gcn.py:76).    */
+int grl_dropedge_mask(const GrlDropEdge* de, uint64_t id_base, int64_t count,
+                      uint8_t* keep /* device */, grl_stream_t stream);
+
+/* ---------------------------------------------------------------------- */
+/* Hot path                                                                */
+/* ---------------------------------------------------------------------- */
+
+/* Z = A_drop X in typed-CSR form.  Replaces
+ *   new_V = torch.matmul(A, V.view(-1, N, F)).view(-1, N, (L+1)*F)
+ * (gnn/models/networks/robust_gcn.py:45-47) together with the edge_dropout
+ * applied to A right before it (drop_robust_gcn.py:76,80,85).
+ * X: device, row stride ldx floats (>= F).  Z: device, contiguous
+ * [num_rows, (has_self+num_types)*F].  de may be NULL (eval).            */
+int grl_typed_spmm_fwd(const GrlTypedCsr* g, const float* X, int64_t ldx,
+                       int32_t F, float* Z, const GrlDropEdge* de,
+                       grl_stream_t stream);
+
+/* dX = A_drop^T dZ.  Replaces autograd's BmmBackward0 for robust_gcn.py:45
+ * (grad of V through the aggregation), with the same DropEdge mask as the
+ * forward call that used `de`.  dZ: contiguous [*, (has_self+num_types)*F];
+ * dX: device, row stride lddx, num_rows rows, fully overwritten.          */
+int grl_typed_spmm_bwd(const GrlTypedCsc* g, const float* dZ, int32_t F,
+                       float* dX, int64_t lddx, const GrlDropEdge* de,
+                       grl_stream_t stream);
+
+/* out = Z W + bias (optionally ReLU), fp32 on MFMA (v_mfma_f32_32x32x2_f32).
+ * Replaces torch.matmul(new_V, self.h_weights) + self.bias
+ * (robust_gcn.py:50) and, with relu = 1, the F.relu around the layer
+ * (drop_robust_gcn.py:76).  Z [M, K] row-major (ldz), W [K, C] row-major,
+ * bias [C] or NULL, out [M, C] contiguous.                                */
+int grl_linear_fwd(const float* Z, int64_t ldz, const float* W,
+                   const float* bias, float* out, int64_t M, int32_t K,
+                   int32_t C, int32_t relu, grl_stream_t stream);
+
+/* ---------------------------------------------------------------------- */
+/* Graph formats                                                           */
+/* ---------------------------------------------------------------------- */
+
+/* Dense adjacency -> typed CSR, block-diagonal over the batch.
+ * Replaces GraphConv.preprocess_adj (robust_gcn.py:53-72): instead of the
+ * dense (B, (L+1)N, N) A_pre, emit the nonzeros of A[b, n, t, m] addressed by
+ * element strides {sb, sn, st, sm} (the collate layout (B,N,L,N) has
+ * sm = 1; the permuted view GraphConv.forward receives, (B,N,N,L), is the
+ * same storage).  Global node id = b*N + n; global row = (b*N + n)*L + t.
+ * Two phases because nnz is data-dependent:
+ *   1) grl_dense_to_csr_rowptr writes rowptr[B*N*L + 1] (the caller reads
+ *      rowptr[B*N*L] to size colidx/vals);
+ *   2) grl_dense_to_csr_fill writes colidx (global source node b*N + m) and
+ *      vals (the A value; NULL to skip) in ascending m within each row.   */
+size_t grl_dense_to_csr_workspace_size(int64_t num_segments);
+int grl_dense_to_csr_rowptr(const float* A, int64_t B, int64_t N, int32_t L,
+                            const int64_t strides[4], int32_t* rowptr,
+                            void* workspace, size_t workspace_bytes,
+                            grl_stream_t stream);
+int grl_dense_to_csr_fill(const float* A, int64_t B, int64_t N, int32_t L,
+                          const int64_t strides[4], const int32_t* rowptr,
+                          int32_t* colidx, float* vals, grl_stream_t stream);
+
+/* Typed CSR -> CSC over source rows [0, num_cols) for the backward pass.
+ * Stable: within a column, entries keep CSR (edge id) order, so dX sums are
+ * deterministic.  colptr [num_cols+1], zrow/eid [nnz], vals_out [nnz] (only
+ * written when g->vals != NULL).                                          */
+size_t grl_csr_to_csc_workspace_size(int64_t nnz, int64_t num_cols);
+int grl_csr_to_csc(const GrlTypedCsr* g, int64_t num_cols, int32_t* colptr,
+                   int32_t* zrow, int32_t* eid, float* vals_out,
+                   void* workspace, size_t workspace_bytes,
+                   grl_stream_t stream);
+
+/* Synthetic graphs for the benchmark configs.
+ * Candidate edge k in [0, num_candidates) is (src, type, dst) drawn from a
+ * counter-based hash of (seed, k): Erdos-Renyi (kind 0: src, dst uniform in
+ * [0, N)) or R-MAT (kind 1: a,b,c,d = 0.57,0.19,0.19,0.05, N = 2^scale);
+ * type uniform in [0, L).  Node-range shard [row_begin, row_end) keeps the
+ * candidates whose src falls in it, dedupes (src, type, dst) and emits typed
+ * CSR rows for those nodes (global colidx).  Three phases:
+ *   grl_synth_count   -> *count (device int64) = candidates in the shard
+ *   grl_synth_build   -> rowptr [(row_end-row_begin)*L + 1], colidx, and
+ *                        *nnz (device int64) after dedupe
+ * Workspace from grl_synth_workspace_size(count).                         */
+typedef struct GrlSynthSpec {
+  int32_t kind;           /* 0 = Erdos-Renyi, 1 = R-MAT                     */
+  int32_t num_types;      /* L                                              */
+  int64_t num_nodes;      /* N                                              */
+  int64_t num_candidates; /* N * avg_deg before dedupe                      */
+  uint64_t seed;
+  int64_t row_begin, row_end;
+} GrlSynthSpec;
+int grl_synth_count(const GrlSynthSpec* spec, int64_t* count /* device */,
+                    grl_stream_t stream);
+size_t grl_synth_workspace_size(const GrlSynthSpec* spec, int64_t count);
+int grl_synth_build(const GrlSynthSpec* spec, int64_t count, int32_t* rowptr,
+                    int32_t* colidx, int64_t* nnz /* device */,
+                    void* workspace, size_t workspace_bytes,
+                    grl_stream_t stream);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* GRL_H_ */

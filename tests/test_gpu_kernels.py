@@ -1,0 +1,199 @@
+"""GPU parity: every libgrl kernel against the CPU oracle on identical inputs.
+
+The aggregation kernels sum each row in CSR order with one fmaf per edge,
+exactly like oracle/grl_oracle.c, so forward and backward are required to be
+BITWISE equal to the oracle (integer/index work: bitwise as well).  The fp32
+MFMA linear is checked against float64 numpy at 1e-5 relative (north_star
+tolerance is 1e-4) and bitwise on exact integer data (fragment-layout check).
+"""
+import numpy as np
+import pytest
+import torch
+
+from grl import DropEdge, TypedGraph, _lib
+from grl.graph import current_stream_handle
+from grl.ops import linear_fwd, typed_aggregate
+from oracle import c_oracle
+from oracle import hash as ohash
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def host_graph(N, L, deg, seed, hub=0, vals=False, empty_rows=True):
+    """ER typed CSR (oracle generator) + optional hub row with `hub` extra
+    edges spread over types, + optional float values."""
+    rowptr, colidx = ohash.synth_csr(0, L, N, int(N * deg), seed)
+    if hub:
+        rng = np.random.default_rng(seed + 1)
+        rows = [colidx[rowptr[s]:rowptr[s + 1]] for s in range(N * L)]
+        for t in range(L):
+            extra = rng.integers(0, N, size=hub // L + 1)
+            rows[t] = np.unique(np.concatenate([rows[t], extra])).astype(np.int32)
+        colidx = np.concatenate(rows).astype(np.int32)
+        rowptr = np.concatenate([[0], np.cumsum([r.size for r in rows])]).astype(np.int32)
+    v = np.random.default_rng(seed + 2).uniform(0.1, 2.0, colidx.size).astype(np.float32) if vals else None
+    return rowptr, colidx, v
+
+
+def to_dev(a, dtype=None):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV) if dtype is None else torch.as_tensor(
+        a, dtype=dtype).to(DEV)
+
+
+def assert_bitwise(gpu, ref, what):
+    gpu = np.asarray(gpu)
+    if not np.array_equal(gpu, ref):
+        d = np.abs(gpu.astype(np.float64) - ref.astype(np.float64))
+        raise AssertionError(f"{what}: not bitwise equal, max|d|={d.max():.3e} at {np.unravel_index(d.argmax(), d.shape)}")
+
+
+CASES = [
+    # N, L, deg, F, hub, vals, has_self
+    (300, 6, 16.0, 256, 0, False, True),
+    (300, 6, 16.0, 512, 0, True, True),
+    (257, 6, 4.0, 16, 0, False, True),
+    (129, 6, 8.0, 10, 0, True, True),     # F % 4 != 0 -> scalar-lane path
+    (200, 3, 12.0, 100, 0, False, False),  # VEC=1, NV=2; no identity block
+    (90, 6, 6.0, 1000, 0, False, True),    # 2 column blocks of 512
+    (500, 6, 2.0, 256, 700, False, True),  # hub row: > 64 edges in one segment
+    (64, 7, 0.0, 64, 0, False, True),      # no edges at all
+]
+DROPS = [None, DropEdge(0.3, 7, 1, True), DropEdge(0.2, 99, 4, False), DropEdge(1.0, 5, 0, True)]
+
+
+@pytest.mark.parametrize("case", CASES)
+@pytest.mark.parametrize("di", range(len(DROPS)))
+def test_spmm_fwd_bwd_bitwise(case, di):
+    N, L, deg, F, hub, vals, hs = case
+    de = DROPS[di]
+    rowptr, colidx, v = host_graph(N, L, deg, 1000 + N, hub, vals)
+    X = np.random.default_rng(N + F).standard_normal((N, F)).astype(np.float32)
+    ebase, sbase = 1234, 10 ** 9 + 7
+    g = TypedGraph.from_csr_host(rowptr, colidx, L, DEV, vals=v, has_self=hs, edge_id_base=ebase,
+                                 self_id_base=sbase).with_dropedge(de)
+    Xt = to_dev(X).requires_grad_(True)
+    Z = typed_aggregate(Xt, g)
+    d = None if de is None else c_oracle.drop(de.p, de.seed, de.call, de.drop_self)
+    Zref = c_oracle.spmm_fwd(rowptr, colidx, X, L, hs, vals=v, d=d, edge_base=ebase, self_base=sbase)
+    assert_bitwise(Z.detach().cpu().numpy(), Zref, "forward")
+    dZ = np.random.default_rng(N + F + 1).standard_normal(Zref.shape).astype(np.float32)
+    Z.backward(to_dev(dZ))
+    colptr, zrow, eid, cvals = c_oracle.csr_to_csc(rowptr, colidx, L, N, hs, v)
+    dXref = c_oracle.spmm_bwd(colptr, zrow, eid, dZ, L, F, N, hs, cvals, d=d, edge_base=ebase, self_base=sbase)
+    assert_bitwise(Xt.grad.cpu().numpy(), dXref, "backward")
+
+
+def test_spmm_strided_input_rows():
+    """X given as a column slice (ldx > F), as torch.cat views produce."""
+    N, L, F = 150, 6, 128
+    rowptr, colidx, _ = host_graph(N, L, 10.0, 5)
+    big = np.random.default_rng(0).standard_normal((N, 3 * F)).astype(np.float32)
+    g = TypedGraph.from_csr_host(rowptr, colidx, L, DEV)
+    Z = typed_aggregate(to_dev(big)[:, F:2 * F], g)
+    Zref = c_oracle.spmm_fwd(rowptr, colidx, big[:, F:2 * F].copy(), L, True)
+    assert_bitwise(Z.cpu().numpy(), Zref, "strided forward")
+
+
+def test_csc_matches_oracle():
+    N, L = 700, 6
+    rowptr, colidx, v = host_graph(N, L, 9.0, 77, hub=300, vals=True)
+    g = TypedGraph.from_csr_host(rowptr, colidx, L, DEV, vals=v)
+    c = g.csc()
+    colptr, zrow, eid, cvals = c_oracle.csr_to_csc(rowptr, colidx, L, N, True, v)
+    np.testing.assert_array_equal(c["colptr"].cpu().numpy(), colptr)
+    np.testing.assert_array_equal(c["zrow"].cpu().numpy()[:colidx.size], zrow)
+    np.testing.assert_array_equal(c["eid"].cpu().numpy()[:colidx.size], eid)
+    np.testing.assert_array_equal(c["cvals"].cpu().numpy()[:colidx.size], cvals)
+
+
+@pytest.mark.parametrize("layout", ["bnln", "bnnl", "pre"])
+@pytest.mark.parametrize("float_vals", [False, True])
+def test_dense_to_csr_matches_oracle(layout, float_vals):
+    import inputs as gi
+
+    B, N, L = 3, 37, 6
+    A = gi.random_adj_bnln(4, B, N, L, 5.0, float_vals=float_vals)
+    if layout == "bnln":
+        At = to_dev(A)
+        rp, ci, va = c_oracle.dense_to_csr(A, [N * L * N, L * N, N, 1], B, N, L)
+        Lx = L
+    elif layout == "bnnl":
+        At = to_dev(A).permute(0, 1, 3, 2)  # non-contiguous view, as GraphConv receives it
+        rp, ci, va = c_oracle.dense_to_csr(A, [N * L * N, L * N, N, 1], B, N, L)
+        Lx = L
+    else:
+        from oracle import dense_ref
+        pre = dense_ref.preprocess_adj(np.transpose(A, (0, 1, 3, 2))).astype(np.float32)
+        At = to_dev(pre)
+        Lx = L + 1
+        rp, ci, va = c_oracle.dense_to_csr(pre.reshape(B, N, Lx, N), [N * Lx * N, Lx * N, N, 1], B, N, Lx)
+    g = TypedGraph.from_dense(At, layout=layout)
+    assert g.num_types == Lx and g.has_self == (layout != "pre")
+    np.testing.assert_array_equal(g.rowptr.cpu().numpy(), rp)
+    np.testing.assert_array_equal(g.colidx.cpu().numpy(), ci)
+    if float_vals:
+        np.testing.assert_array_equal(g.vals.cpu().numpy(), va)
+    else:
+        assert g.vals is None
+
+
+@pytest.mark.parametrize("kind,N,deg,rng_", [(0, 5000, 16.0, None), (0, 3001, 7.0, (1000, 2500)),
+                                             (1, 1 << 13, 12.0, None), (1, 1 << 12, 20.0, (100, 3000))])
+def test_synth_matches_oracle(kind, N, deg, rng_):
+    rb, re = (0, N) if rng_ is None else rng_
+    g = TypedGraph.synthetic(N, deg, 6, kind=["er", "rmat"][kind], seed=11, row_range=rng_, device=DEV)
+    rp, ci = ohash.synth_csr(kind, 6, N, int(round(N * deg)), 11, rb, re)
+    np.testing.assert_array_equal(g.rowptr.cpu().numpy(), rp)
+    np.testing.assert_array_equal(g.colidx.cpu().numpy(), ci)
+
+
+@pytest.mark.parametrize("p", [0.0, 0.2, 0.3, 1.0])
+def test_dropedge_mask_matches_oracle(p):
+    g = TypedGraph.from_csr_host(np.zeros(7, np.int32), np.zeros(0, np.int32), 6, DEV)
+    de = DropEdge(p, 31337, 2)
+    keep = g.dropedge_mask(de, 2**33 + 5, 100_000).cpu().numpy()
+    ref = ohash.dropedge_keep(p, 31337, 2, np.arange(2**33 + 5, 2**33 + 5 + 100_000, dtype=np.uint64))
+    np.testing.assert_array_equal(keep.astype(bool), ref)
+
+
+@pytest.mark.parametrize("M,K,C", [(1, 8, 4), (74, 1792, 256), (300, 3584, 256), (129, 10, 5), (517, 36, 200),
+                                   (1000, 1792, 128)])
+@pytest.mark.parametrize("relu,bias", [(False, True), (True, True), (False, False)])
+def test_linear_matches_fp64(M, K, C, relu, bias):
+    rng = np.random.default_rng(M * 7 + K)
+    Z = rng.standard_normal((M, K)).astype(np.float32)
+    W = (rng.standard_normal((K, C)) / np.sqrt(K)).astype(np.float32)
+    b = rng.standard_normal(C).astype(np.float32) if bias else None
+    out = linear_fwd(to_dev(Z), to_dev(W), to_dev(b) if bias else None, relu).cpu().numpy()
+    ref = Z.astype(np.float64) @ W.astype(np.float64) + (b if bias else 0.0)
+    if relu:
+        ref = np.maximum(ref, 0)
+    scale = np.abs(Z).astype(np.float64) @ np.abs(W).astype(np.float64) + 1.0
+    assert np.all(np.abs(out - ref) <= 1e-5 * scale)
+
+
+def test_linear_fragment_layout_exact():
+    """Exact small-integer data: any row/col/k mapping error shows up bitwise.
+    B is asymmetric (guide: 'A=I-check with ASYMMETRIC B')."""
+    M, K, C = 160, 64, 136
+    I = np.zeros((M, K), np.float32)
+    I[np.arange(M), np.arange(M) % K] = 1.0
+    Wt = (np.arange(K * C).reshape(K, C) % 97 - 48).astype(np.float32)
+    out = linear_fwd(to_dev(I), to_dev(Wt), None, False).cpu().numpy()
+    np.testing.assert_array_equal(out, I @ Wt)
+    rng = np.random.default_rng(1)
+    Zi = rng.integers(-8, 9, (M, K)).astype(np.float32)
+    Wi = rng.integers(-8, 9, (K, C)).astype(np.float32)
+    bi = rng.integers(-8, 9, C).astype(np.float32)
+    out = linear_fwd(to_dev(Zi), to_dev(Wi), to_dev(bi), False).cpu().numpy()
+    np.testing.assert_array_equal(out, Zi @ Wi + bi)
+
+
+def test_errors_raise_not_fallback():
+    g = TypedGraph.from_csr_host(np.zeros(13, np.int32), np.zeros(0, np.int32), 6, DEV)
+    with pytest.raises(_lib.GrlError, match="rows"):
+        typed_aggregate(torch.zeros(3, 8, device=DEV), g)
+    with pytest.raises(_lib.GrlError, match="float32"):
+        typed_aggregate(torch.zeros(2, 8, device=DEV, dtype=torch.float16), g)
+    assert current_stream_handle(DEV) is not None
