@@ -38,7 +38,7 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--nodes-per-gpu", type=int, default=1_000_000)
     ap.add_argument("--avg-deg", type=float, default=32.0)
     ap.add_argument("--types", type=int, default=6)
@@ -46,7 +46,8 @@ def parse():
     ap.add_argument("--p", type=float, default=0.0, help="DropEdge rate inside the timed step (0 = eval)")
     ap.add_argument("--graph", choices=["er", "rmat"], default="er")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 disables)")
-    ap.add_argument("--no-extras", action="store_true")
+    ap.add_argument("--extras", action="store_true",
+                    help="also time fused-DropEdge fwd, backward, MFMA linear and a full layer (not the headline)")
     ap.add_argument("--only", choices=["fwd", "bwd", "linear", "layer"], default=None,
                     help="profiling aid: run just that kernel K times (no JSON line)")
     return ap.parse_args()
@@ -69,7 +70,7 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     from grl import DropEdge, TypedGraph
-    from grl.ops import linear_fwd, typed_aggregate
+    from grl.ops import spmm_forward
 
     L, F = args.types, args.dim
     n_loc = args.nodes_per_gpu
@@ -105,8 +106,10 @@ def main():
         if world > 1:
             dist.all_gather_into_tensor(X_full, X_loc)
 
+    Z = torch.empty(graph.num_rows, graph.segments * F, device=dev)  # preallocated: no allocation in the step
+
     def spmm():
-        return typed_aggregate(X_full, g_step)
+        return spmm_forward(X_full, g_step, out=Z)
 
     if args.only is not None:
         run_only(args, graph, X_full, gather, spmm, L, F)
@@ -123,13 +126,14 @@ def main():
     for i in range(args.steps):
         gather()
         ev[i][0].record(stream)
-        Z = spmm()
+        spmm()
         ev[i][1].record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t_start
-    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    per_step = [a.elapsed_time(b) for a, b in ev]
+    kern_ms = float(np.mean(per_step))
     if world > 1:
         tt = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -155,12 +159,13 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "spmm_kernel<4,1,8,false,false> (grl_typed_spmm_fwd)",
-                     "kernel_ms": kern_ms, "algorithmic_bytes_per_launch": bytes_launch},
+                     "kernel_ms": kern_ms, "kernel_ms_min_max": [min(per_step), max(per_step)],
+                     "algorithmic_bytes_per_launch": bytes_launch},
         "build_s": build_s,
     }
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         out["cpu_baseline"], out["parity"] = cpu_baseline(args, graph, X_loc, Z, L, F)
-    if not args.no_extras:
+    if args.extras:
         out["extras"] = extras(args, graph, X_full, gather, L, F, dev, E_loc, n_loc)
     if rank == 0:
         print(json.dumps(out), flush=True)

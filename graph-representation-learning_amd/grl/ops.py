@@ -27,21 +27,33 @@ def _rows_view(X: torch.Tensor) -> torch.Tensor:
     return X2
 
 
+def spmm_forward(X: torch.Tensor, graph: TypedGraph, out: torch.Tensor = None) -> torch.Tensor:
+    """Z = A_drop X without autograd bookkeeping, optionally into `out`
+    (contiguous [num_rows, segments*F] fp32): the inference / benchmark form."""
+    _require_device(X, "node features")
+    if X.dtype != torch.float32:
+        raise _lib.GrlError(f"node features must be float32 (got {X.dtype})")
+    X2 = _rows_view(X)
+    if X2.shape[0] != graph.num_cols:
+        raise _lib.GrlError(f"features have {X2.shape[0]} rows, graph gathers from {graph.num_cols}")
+    F = X2.shape[1]
+    shape = (graph.num_rows, graph.segments * F)
+    if out is None:
+        out = torch.empty(shape, dtype=torch.float32, device=X.device)
+    elif tuple(out.shape) != shape or out.dtype != torch.float32 or not out.is_contiguous() \
+            or out.device != X.device:
+        raise _lib.GrlError(f"out must be a contiguous float32 {shape} tensor on {X.device}")
+    csr = graph.csr_c()
+    de = graph.dropedge.to_c() if graph.dropedge is not None else None
+    call("grl_typed_spmm_fwd", ctypes.byref(csr), X2.data_ptr(), X2.stride(0), F, out.data_ptr(),
+         ctypes.byref(de) if de is not None else None, current_stream_handle(X.device))
+    return out
+
+
 class _TypedAggregate(torch.autograd.Function):
     @staticmethod
     def forward(ctx, X: torch.Tensor, graph: TypedGraph) -> torch.Tensor:
-        _require_device(X, "node features")
-        if X.dtype != torch.float32:
-            raise _lib.GrlError(f"node features must be float32 (got {X.dtype})")
-        X2 = _rows_view(X)
-        if X2.shape[0] != graph.num_cols:
-            raise _lib.GrlError(f"features have {X2.shape[0]} rows, graph gathers from {graph.num_cols}")
-        F = X2.shape[1]
-        Z = torch.empty(graph.num_rows, graph.segments * F, dtype=torch.float32, device=X.device)
-        csr = graph.csr_c()
-        de = graph.dropedge.to_c() if graph.dropedge is not None else None
-        call("grl_typed_spmm_fwd", ctypes.byref(csr), X2.data_ptr(), X2.stride(0), F, Z.data_ptr(),
-             ctypes.byref(de) if de is not None else None, current_stream_handle(X.device))
+        Z = spmm_forward(X, graph)
         ctx.graph = graph
         ctx.xshape = X.shape
         return Z

@@ -1,0 +1,47 @@
+#!/bin/bash
+# One GPU-box session: each GPU step runs under its own time limit; the
+# session stops at the first step that faults, aborts, segfaults or times
+# out (exit 124/134/137/139 or a signal).  Ordinary test failures (pytest
+# rc 1) do not stop later steps.  Usage: tools/gpu_session.sh STEP...
+#   steps: tests smoke bench bench_drop prof_fwd prof_bwd prof_linear pmc_fwd
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+export TMPDIR=/tmp
+OUT=gpurun_out
+mkdir -p "$OUT"
+
+fatal() { case "$1" in 124|134|137|139|13[0-9]|14[0-9]) return 0;; esac; [ "$1" -gt 128 ]; }
+
+run() {  # name seconds cmd...
+  local name=$1 secs=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"
+  tail -n 5 "$OUT/$name.log"
+  if fatal $rc; then echo "FATAL in $name (rc=$rc): stopping session"; exit $rc; fi
+  return 0
+}
+
+for step in "$@"; do
+  case $step in
+    tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -rf ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 600 python bench.py ;;
+    bench_extras) run bench_extras 600 python bench.py --extras --cpu-seconds 0 ;;
+    bench_drop) run bench_drop 600 python bench.py --p 0.3 --cpu-seconds 0 ;;
+    prof_bench) run prof_bench 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_bench" -o run --output-format csv \
+                  -- python bench.py ;;
+    prof_fwd) run prof_fwd 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_fwd" -o run --output-format csv \
+                  -- python bench.py --only fwd --steps 20 --warmup 3 ;;
+    prof_bwd) run prof_bwd 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_bwd" -o run --output-format csv \
+                  -- python bench.py --only bwd --steps 10 --warmup 2 ;;
+    prof_linear) run prof_linear 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_linear" -o run --output-format csv \
+                  -- python bench.py --only linear --steps 10 --warmup 2 ;;
+    pmc_fwd_fetch) run pmc_fwd_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fwd_fetch" -o run \
+                  --output-format csv -- python bench.py --only fwd --steps 5 --warmup 1 ;;
+    pmc_fwd_write) run pmc_fwd_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_fwd_write" -o run \
+                  --output-format csv -- python bench.py --only fwd --steps 5 --warmup 1 ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
+echo "=== session done"
