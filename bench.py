@@ -10,8 +10,8 @@ Workload: per GPU a node-range shard of 1M nodes of a
 seeded Erdos-Renyi typed graph (avg total out-degree 32 over L=6 edge
 types, dedupe), d=256 fp32 features -- config C3 at N=1, the C4 shape
 (4M nodes) at N=4.  A step = one GraphConv aggregation forward over the
-rank's rows (N>1: preceded by the all-gather of node features that the
-node-range sharding needs).  Inputs are resident in HBM before timing.
+rank's rows (N>1: preceded by the halo exchange -- RCCL all-to-all-v of the
+remote feature rows the shard's edges reference, grl/dist.py).  Inputs are resident in HBM before timing.
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
@@ -69,7 +69,8 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    from grl import DropEdge, TypedGraph
+    from grl import DropEdge
+    from grl.dist import ShardedGraph, halo_exchange_into
     from grl.ops import spmm_forward
 
     L, F = args.types, args.dim
@@ -78,35 +79,27 @@ def main():
     if args.graph == "rmat":
         N = 1 << (N - 1).bit_length()
         n_loc = N // world
-    rb, re = rank * n_loc, (rank + 1) * n_loc
     t0 = time.time()
-    graph = TypedGraph.synthetic(N, args.avg_deg, L, kind=args.graph, seed=0, row_range=(rb, re), device=dev)
-    E_loc = graph.nnz
-    if world > 1:
-        t = torch.tensor([E_loc], dtype=torch.int64, device=dev)
-        allE = [torch.zeros_like(t) for _ in range(world)]
-        dist.all_gather(allE, t)
-        allE = [int(x.item()) for x in allE]
-        E_tot = sum(allE)
-        graph.edge_id_base = sum(allE[:rank])
-        graph.self_id_base = E_tot + rb
-    else:
-        E_tot = E_loc
+    sg = ShardedGraph.synthetic(N, args.avg_deg, L, kind=args.graph, seed=0, device=dev)
+    graph, plan = sg.graph, sg.plan
+    n_loc = plan.n_loc
+    E_loc, E_tot = graph.nnz, plan.num_edges_total
     gen = torch.Generator(device=dev)
     gen.manual_seed(1 + rank)
-    X_loc = torch.randn(n_loc, F, generator=gen, device=dev, dtype=torch.float32)
-    X_full = torch.empty(N, F, device=dev) if world > 1 else X_loc
+    # [own rows | halo rows]: own rows are written once, halo rows by the exchange
+    X_full = torch.empty(plan.n_loc + plan.n_halo, F, device=dev)
+    X_loc = X_full[:n_loc]
+    X_loc.copy_(torch.randn(n_loc, F, generator=gen, device=dev, dtype=torch.float32))
+    send_buf = torch.empty(plan.send_index.numel(), F, device=dev)
     build_s = time.time() - t0
 
     de = DropEdge(args.p, 2, 0, True) if args.p > 0 else None
     g_step = graph.with_dropedge(de)
     stream = torch.cuda.current_stream(dev)
+    Z = torch.empty(graph.num_rows, graph.segments * F, device=dev)  # preallocated: no allocation in the step
 
     def gather():
-        if world > 1:
-            dist.all_gather_into_tensor(X_full, X_loc)
-
-    Z = torch.empty(graph.num_rows, graph.segments * F, device=dev)  # preallocated: no allocation in the step
+        halo_exchange_into(X_loc, X_full, send_buf, plan)
 
     def spmm():
         return spmm_forward(X_full, g_step, out=Z)
@@ -155,7 +148,8 @@ def main():
                    f"forward (GraphConv aggregation){' + DropEdge p=%g' % args.p if args.p else ''}",
                    "nodes_total": N, "edges_total": E_tot, "nodes_per_gpu": n_loc, "avg_deg": args.avg_deg,
                    "num_types": L, "d": F, "dropedge_p": args.p, "graph": args.graph,
-                   "parallelism": "single GPU" if world == 1 else f"node-range shards x{world}, all-gather of X"},
+                   "parallelism": "single GPU" if world == 1 else
+                   f"node-range shards x{world}, RCCL all-to-all-v halo ({plan.n_halo} halo rows on rank {rank})"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "spmm_kernel<4,1,8,false,false> (grl_typed_spmm_fwd)",

@@ -1,0 +1,175 @@
+"""Node-range sharding of the GraphConv aggregation over GPUs.
+
+One process per GPU (torch.distributed, backend "nccl" = RCCL over xGMI).
+Rank r owns node rows [row_begin_r, row_end_r): their feature rows, their
+typed-CSR rows (destination = owned node) and their output rows.  The only
+data-path exchange is the halo: before each aggregation every rank receives
+the feature rows of the remote sources its edges reference, via one
+all-to-all-v (`all_to_all_single` with per-peer split sizes); backward sends
+the halo-row gradients back the same way and the owner adds them in peer
+order (deterministic, no float atomics).
+
+The plan is static per graph and built once (two small all-to-alls of ids).
+Edge ids stay global (edge_id_base = nnz of lower ranks, self ids
+E_total + global node), so fused DropEdge masks are identical to the
+single-GPU run and the forward is bitwise identical to it.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+from .graph import DropEdge, TypedGraph
+from .ops import typed_aggregate
+
+
+def _world(group) -> int:
+    return dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
+
+
+def _rank(group) -> int:
+    return dist.get_rank(group) if dist.is_available() and dist.is_initialized() else 0
+
+
+@dataclass
+class HaloPlan:
+    row_begin: int
+    row_end: int
+    n_loc: int
+    n_halo: int
+    bounds: List[int]            # row ranges of all ranks: [b_0, b_1, ..., b_P]
+    send_index: torch.Tensor     # int64 local rows, concatenated per destination peer
+    send_counts: List[int]       # rows I send to each peer
+    recv_counts: List[int]       # halo rows I receive from each peer (owner order)
+    halo_ids: torch.Tensor       # int64 global ids of my halo rows, ascending
+    colidx_local: torch.Tensor   # int32: own -> id - row_begin, remote -> n_loc + halo slot
+    edge_id_base: int
+    num_edges_total: int
+
+
+def build_halo_plan(colidx: torch.Tensor, row_begin: int, row_end: int, group=None) -> HaloPlan:
+    """Collective: every rank of `group` calls it with its own shard."""
+    dev = colidx.device
+    world, rank = _world(group), _rank(group)
+    n_loc = row_end - row_begin
+    c = colidx.long()
+    if world > 1:
+        rr = torch.tensor([row_begin, row_end, colidx.numel()], dtype=torch.int64, device=dev)
+        allr = [torch.empty_like(rr) for _ in range(world)]
+        dist.all_gather(allr, rr, group=group)
+        allr = torch.stack(allr).cpu()
+        begins, ends, nnzs = allr[:, 0].tolist(), allr[:, 1].tolist(), allr[:, 2].tolist()
+        if begins != sorted(begins) or any(ends[i] != begins[i + 1] for i in range(world - 1)):
+            raise ValueError(f"node ranges must be contiguous in rank order: {list(zip(begins, ends))}")
+        bounds = begins + [ends[-1]]
+        edge_id_base = sum(nnzs[:rank])
+        num_edges_total = sum(nnzs)
+    else:
+        bounds = [row_begin, row_end]
+        edge_id_base, num_edges_total = 0, colidx.numel()
+    own = (c >= row_begin) & (c < row_end)
+    halo_ids = torch.unique(c[~own])  # sorted ascending => grouped by owner
+    if world > 1:
+        ends_t = torch.tensor(bounds[1:], dtype=torch.int64, device=dev)
+        owner = torch.searchsorted(ends_t, halo_ids, right=True)
+        need = torch.bincount(owner, minlength=world).to(torch.int64)
+        asked_counts = torch.empty_like(need)
+        dist.all_to_all_single(asked_counts, need, group=group)
+        recv_counts = need.cpu().tolist()
+        send_counts = asked_counts.cpu().tolist()
+        asked = torch.empty(sum(send_counts), dtype=torch.int64, device=dev)
+        dist.all_to_all_single(asked, halo_ids.contiguous(), send_counts, recv_counts, group=group)
+        send_index = asked - row_begin
+        if send_index.numel() and (int(send_index.min()) < 0 or int(send_index.max()) >= n_loc):
+            raise RuntimeError("halo plan: a peer asked for rows this rank does not own")
+    else:
+        if halo_ids.numel():
+            raise ValueError(f"single shard references {halo_ids.numel()} nodes outside [{row_begin}, {row_end})")
+        recv_counts, send_counts = [0], [0]
+        send_index = torch.zeros(0, dtype=torch.int64, device=dev)
+    slot = n_loc + torch.searchsorted(halo_ids, c)
+    colidx_local = torch.where(own, c - row_begin, slot).to(torch.int32)
+    return HaloPlan(row_begin, row_end, n_loc, int(halo_ids.numel()), bounds, send_index, send_counts, recv_counts,
+                    halo_ids, colidx_local, edge_id_base, num_edges_total)
+
+
+class _HaloExchange(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, X_loc: torch.Tensor, plan: HaloPlan, group):
+        F = X_loc.shape[1]
+        X_ext = X_loc.new_empty(plan.n_loc + plan.n_halo, F)
+        X_ext[: plan.n_loc].copy_(X_loc)
+        if _world(group) > 1:
+            send = X_loc.index_select(0, plan.send_index)
+            dist.all_to_all_single(X_ext[plan.n_loc:], send, plan.recv_counts, plan.send_counts, group=group)
+        ctx.plan, ctx.group = plan, group
+        return X_ext
+
+    @staticmethod
+    def backward(ctx, dX_ext: torch.Tensor):
+        plan, group = ctx.plan, ctx.group
+        dX_ext = dX_ext.contiguous()
+        dX_loc = dX_ext[: plan.n_loc].clone()
+        if _world(group) > 1:
+            back = dX_ext.new_empty(sum(plan.send_counts), dX_ext.shape[1])
+            dist.all_to_all_single(back, dX_ext[plan.n_loc:], plan.send_counts, plan.recv_counts, group=group)
+            off = 0
+            for cnt in plan.send_counts:  # peer order; indices unique within a peer -> deterministic
+                if cnt:
+                    dX_loc.index_add_(0, plan.send_index[off:off + cnt], back[off:off + cnt])
+                off += cnt
+        return dX_loc, None, None
+
+
+def halo_exchange(X_loc: torch.Tensor, plan: HaloPlan, group=None) -> torch.Tensor:
+    """[own rows; halo rows] feature matrix for the local aggregation."""
+    if plan.n_halo == 0 and _world(group) == 1:
+        return X_loc
+    return _HaloExchange.apply(X_loc, plan, group)
+
+
+def halo_exchange_into(X_loc: torch.Tensor, X_ext: torch.Tensor, send_buf: torch.Tensor, plan: HaloPlan,
+                       group=None) -> None:
+    """No-autograd, no-allocation form for inference / benchmarking:
+    X_ext[:n_loc] must already alias or hold X_loc; fills X_ext[n_loc:]."""
+    if _world(group) == 1:
+        return
+    torch.index_select(X_loc, 0, plan.send_index, out=send_buf)
+    dist.all_to_all_single(X_ext[plan.n_loc:], send_buf, plan.recv_counts, plan.send_counts, group=group)
+
+
+class ShardedGraph:
+    """This rank's node-range shard of a global typed graph, ready to aggregate."""
+
+    def __init__(self, rowptr: torch.Tensor, colidx_global: torch.Tensor, num_types: int, row_begin: int,
+                 row_end: int, *, vals: Optional[torch.Tensor] = None, group=None):
+        self.group = group
+        self.plan = build_halo_plan(colidx_global, row_begin, row_end, group)
+        p = self.plan
+        self.graph = TypedGraph(rowptr, p.colidx_local, num_types, vals=vals, has_self=True,
+                                num_cols=p.n_loc + p.n_halo, edge_id_base=p.edge_id_base,
+                                self_id_base=p.num_edges_total + row_begin, self_rows=p.n_loc)
+
+    @classmethod
+    def synthetic(cls, num_nodes: int, avg_deg: float, num_types: int = 6, *, kind: str = "er", seed: int = 0,
+                  device="cuda", group=None) -> "ShardedGraph":
+        world, rank = _world(group), _rank(group)
+        per = -(-num_nodes // world)
+        rb, re = min(num_nodes, rank * per), min(num_nodes, (rank + 1) * per)
+        g = TypedGraph.synthetic(num_nodes, avg_deg, num_types, kind=kind, seed=seed, row_range=(rb, re),
+                                 device=device)
+        return cls(g.rowptr, g.colidx, num_types, rb, re, group=group)
+
+    @property
+    def halo_rows(self) -> int:
+        return self.plan.n_halo
+
+    def exchange(self, X_loc: torch.Tensor) -> torch.Tensor:
+        return halo_exchange(X_loc, self.plan, self.group)
+
+    def aggregate(self, X_loc: torch.Tensor, dropedge: Optional[DropEdge] = None) -> torch.Tensor:
+        """Z rows of this shard: halo exchange + typed SpMM (autograd through both)."""
+        return typed_aggregate(self.exchange(X_loc), self.graph.with_dropedge(dropedge))
