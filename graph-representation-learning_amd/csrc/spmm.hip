@@ -6,19 +6,27 @@
 //   (gnn/models/networks/drop_robust_gcn.py:38,76,80,85),
 // and its autograd backward dV = A_drop^T dZ (BmmBackward0).
 //
-// Design (HBM-bound gather, see DESIGN.md §Kernels):
-//  * one wavefront owns one destination row (node) at a time, grid-stride
-//    over rows; each lane owns VEC*NV contiguous feature columns, so every
-//    gathered neighbour row is read as one coalesced 16 B/lane sweep
-//    (1 KiB per wave-instruction at F = 256);
-//  * 64 edge indices are loaded per wave-instruction, the DropEdge weights
-//    are computed for all 64 in parallel from the counter hash, and a
-//    ballot keeps only surviving edges: dropped edges cost no gather bytes;
-//  * surviving edges are issued U at a time (U independent row loads in
-//    flight per wave) and accumulated with one fmaf per edge in CSR order,
-//    so results are deterministic and equal the oracle's fmaf chain;
-//  * type-segment boundaries are wave-uniform scalar compares, so a node's
+// Design (HBM-bound gather, see DESIGN.md §4):
+//  * one wavefront owns one work item at a time (grid-stride): a destination
+//    row, or -- for rows heavier than the split threshold (power-law hubs) --
+//    one chunk of <= chunk_edges edges of one segment, summed into a partial
+//    row that a fixup pass adds in chunk order (deterministic, no atomics).
+//    Chunk items come first in the item space so hub work overlaps the rest;
+//  * each lane owns VEC*NV contiguous feature columns, so every gathered
+//    neighbour row is one coalesced 16 B/lane sweep (1 KiB per
+//    wave-instruction at F = 256);
+//  * 64 edge indices are loaded per wave-instruction, the DropEdge weights of
+//    all 64 are computed in parallel from the counter hash, and a ballot keeps
+//    only surviving edges: dropped edges cost no gather bytes;
+//  * surviving edges are issued U at a time (U independent row loads in flight
+//    per wave) and accumulated with one fmaf per edge in CSR order, so results
+//    are deterministic and equal the oracle's fmaf chain;
+//  * type-segment boundaries are wave-uniform scalar compares, so a row's
 //    edges of all types stream through one loop (no per-type round trip).
+#include <climits>
+
+#include <hipcub/hipcub.hpp>
+
 #include "grl_internal.h"
 
 namespace grl {
@@ -35,8 +43,7 @@ struct VecT<1> {
   using type = float;
 };
 
-__device__ __forceinline__ float4 vzero4() { return make_float4(0.f, 0.f, 0.f, 0.f); }
-__device__ __forceinline__ void vzero(float4& a) { a = vzero4(); }
+__device__ __forceinline__ void vzero(float4& a) { a = make_float4(0.f, 0.f, 0.f, 0.f); }
 __device__ __forceinline__ void vzero(float& a) { a = 0.f; }
 __device__ __forceinline__ void vfma(float4& acc, float w, const float4& x) {
   acc.x = __builtin_fmaf(w, x.x, acc.x);
@@ -49,6 +56,22 @@ __device__ __forceinline__ float4 vmul(float w, const float4& x) {
   return make_float4(w * x.x, w * x.y, w * x.z, w * x.w);
 }
 __device__ __forceinline__ float vmul(float w, const float& x) { return w * x; }
+__device__ __forceinline__ void vadd(float4& a, const float4& b) {
+  a.x += b.x;
+  a.y += b.y;
+  a.z += b.z;
+  a.w += b.w;
+}
+__device__ __forceinline__ void vadd(float& a, const float& b) { a += b; }
+
+// Device view of a split plan (all null / zero when the graph is not split).
+struct SplitDev {
+  int threshold;  // INT_MAX: nothing is heavy
+  int64_t num_chunks;
+  const int32_t* chunk_begin;
+  const int32_t* chunk_end;
+  float* partials;
+};
 
 // BWD = false: forward, rows are destination nodes with S typed segments,
 //               sources are X rows (index = colidx), ids = edge_base + e.
@@ -57,12 +80,12 @@ __device__ __forceinline__ float vmul(float w, const float& x) { return w * x; }
 template <int VEC, int NV, int U, bool VALS, bool BWD>
 __global__ __launch_bounds__(256) void spmm_kernel(
     int64_t num_rows, int64_t self_rows, int S, int hs,
-    const int32_t* __restrict__ ptr,    // fwd: rowptr [rows*S+1]; bwd: colptr [rows+1]
-    const int32_t* __restrict__ idx,    // fwd: colidx; bwd: zrow
-    const int32_t* __restrict__ eidv,   // bwd: eid (CSR positions); fwd: unused
+    const int32_t* __restrict__ ptr,   // fwd: rowptr [rows*S+1]; bwd: colptr [rows+1]
+    const int32_t* __restrict__ idx,   // fwd: colidx; bwd: zrow
+    const int32_t* __restrict__ eidv,  // bwd: eid (CSR positions); fwd: unused
     const float* __restrict__ vals, uint64_t edge_base, uint64_t self_base,
     const float* __restrict__ src, int64_t lds,  // gathered matrix + row stride
-    int F, float* __restrict__ out, int64_t ldo, DropDev de) {
+    int F, float* __restrict__ out, int64_t ldo, DropDev de, SplitDev sp) {
   using vec_t = typename VecT<VEC>::type;
   const int lane = threadIdx.x & 63;
   const int cbase = blockIdx.y * (64 * VEC * NV);
@@ -73,53 +96,60 @@ __global__ __launch_bounds__(256) void spmm_kernel(
     coff[k] = cbase + (k * 64 + lane) * VEC;
     cval[k] = coff[k] < F;
   }
-  const int nseg = BWD ? 1 : S;
+  const int nseg_row = BWD ? 1 : S;
   const int64_t zstride = (int64_t)(S + hs) * F;  // dZ row stride (bwd self term)
 
   const int64_t wave0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + uniform_i(threadIdx.x >> 6);
   const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const int64_t num_items = sp.num_chunks + num_rows;
 
-  for (int64_t n = wave0; n < num_rows; n += nwaves) {
-    float* orow = out + n * ldo;
+  for (int64_t item = wave0; item < num_items; item += nwaves) {
     vec_t acc[NV];
 #pragma unroll
     for (int k = 0; k < NV; ++k) vzero(acc[k]);
-
-    // ---- self term (identity block of A_pre, robust_gcn.py:58-65) ------
-    if (hs && (!BWD || n < self_rows)) {
-      float w = 1.0f;
-      if (de.active && de.drop_self) w = dropedge_weight(de, 1.0f, self_base + (uint64_t)n);
-      const float* srow = BWD ? (src + n * zstride) : (src + n * lds);
-      if (w != 0.0f) {
+    int pv, nseg;
+    float* obase;
+    if (item < sp.num_chunks) {
+      // ---- chunk of a heavy segment -> partial row --------------------------
+      const int64_t c = item;
+      pv = lane == 0 ? sp.chunk_begin[c] : (lane == 1 ? sp.chunk_end[c] : 0);
+      nseg = 1;
+      obase = sp.partials + c * F;
+    } else {
+      const int64_t n = item - sp.num_chunks;
+      float* orow = out + n * ldo;
+      pv = lane <= nseg_row ? ptr[n * nseg_row + lane] : 0;
+      nseg = nseg_row;
+      const bool heavy = readlane_i(pv, nseg) - readlane_i(pv, 0) > sp.threshold;
+      // ---- self term (identity block of A_pre, robust_gcn.py:58-65) ------
+      if (hs && (!BWD || (n < self_rows && !heavy))) {
+        float w = 1.0f;
+        if (de.active && de.drop_self) w = dropedge_weight(de, 1.0f, self_base + (uint64_t)n);
+        const float* srow = BWD ? (src + n * zstride) : (src + n * lds);
 #pragma unroll
         for (int k = 0; k < NV; ++k) {
           if (cval[k]) {
-            vec_t x = *reinterpret_cast<const vec_t*>(srow + coff[k]);
-            if (BWD)
-              acc[k] = vmul(w, x);
+            vec_t x;
+            if (w != 0.0f)
+              x = vmul(w, *reinterpret_cast<const vec_t*>(srow + coff[k]));
             else
-              *reinterpret_cast<vec_t*>(orow + coff[k]) = vmul(w, x);
+              vzero(x);
+            if (BWD)
+              acc[k] = x;
+            else
+              *reinterpret_cast<vec_t*>(orow + coff[k]) = x;
           }
         }
-      } else if (!BWD) {
-#pragma unroll
-        for (int k = 0; k < NV; ++k)
-          if (cval[k]) {
-            vec_t z;
-            vzero(z);
-            *reinterpret_cast<vec_t*>(orow + coff[k]) = z;
-          }
       }
+      if (heavy) continue;  // typed segments come from the chunk partials (fixup)
+      obase = BWD ? orow : orow + hs * F;
     }
 
-    // ---- segment pointers: lanes 0..nseg hold ptr[n*nseg + lane] --------
-    const int pv = lane <= nseg ? ptr[n * nseg + lane] : 0;
+    // ---- gather-accumulate over the item's edges ------------------------
     const int e_begin = readlane_i(pv, 0);
     const int e_end = readlane_i(pv, nseg);
     int t = 0;
     int seg_end = readlane_i(pv, 1);
-    float* obase = BWD ? orow : orow + hs * F;
-
     for (int c0 = e_begin; c0 < e_end; c0 += 64) {
       const int cnt = min(64, e_end - c0);
       int sidx = 0;
@@ -191,6 +221,42 @@ __global__ __launch_bounds__(256) void spmm_kernel(
   }
 }
 
+// Heavy segment h: out = [self term (bwd)] + sum of its chunk partials in
+// chunk order.  One wavefront per heavy segment.
+template <int VEC, int NV, bool BWD>
+__global__ __launch_bounds__(256) void spmm_fixup_kernel(
+    int64_t num_heavy, const int32_t* __restrict__ heavy_seg, const int32_t* __restrict__ heavy_cptr,
+    const float* __restrict__ partials, int nseg, int S, int hs, int64_t self_rows, uint64_t self_base,
+    const float* __restrict__ dZ, int F, float* __restrict__ out, int64_t ldo, DropDev de) {
+  using vec_t = typename VecT<VEC>::type;
+  const int lane = threadIdx.x & 63;
+  const int cbase = blockIdx.y * (64 * VEC * NV);
+  const int64_t zstride = (int64_t)(S + hs) * F;
+  const int64_t wave0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + uniform_i(threadIdx.x >> 6);
+  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  for (int64_t h = wave0; h < num_heavy; h += nwaves) {
+    const int64_t s = heavy_seg[h];
+    const int64_t n = s / nseg, t = s % nseg;
+    const int c_begin = heavy_cptr[h], c_end = heavy_cptr[h + 1];
+    float w_self = 0.0f;
+    if (BWD && hs && n < self_rows) {
+      w_self = 1.0f;
+      if (de.active && de.drop_self) w_self = dropedge_weight(de, 1.0f, self_base + (uint64_t)n);
+    }
+    float* orow = BWD ? out + n * ldo : out + n * ldo + (hs + t) * F;
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      const int col = cbase + (k * 64 + lane) * VEC;
+      if (col >= F) continue;
+      vec_t acc;
+      vzero(acc);
+      if (BWD && w_self != 0.0f) acc = vmul(w_self, *reinterpret_cast<const vec_t*>(dZ + n * zstride + col));
+      for (int c = c_begin; c < c_end; ++c) vadd(acc, *reinterpret_cast<const vec_t*>(partials + (int64_t)c * F + col));
+      *reinterpret_cast<vec_t*>(orow + col) = acc;
+    }
+  }
+}
+
 __global__ void mask_kernel(DropDev de, uint64_t id_base, int64_t count, uint8_t* __restrict__ keep) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -198,6 +264,84 @@ __global__ void mask_kernel(DropDev de, uint64_t id_base, int64_t count, uint8_t
   }
 }
 
+// ---------------------------------------------------------------------------
+// split plan construction
+// ---------------------------------------------------------------------------
+// per row: number of heavy segments (nseg or 0) and chunks
+__global__ void split_count_kernel(const int32_t* __restrict__ ptr, int64_t rows, int nseg, int threshold,
+                                   int chunk_edges, int64_t* __restrict__ hcnt, int64_t* __restrict__ ccnt) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t* p = ptr + r * nseg;
+    const bool heavy = p[nseg] - p[0] > threshold;
+    int64_t ch = 0;
+    if (heavy)
+      for (int t = 0; t < nseg; ++t) ch += (p[t + 1] - p[t] + chunk_edges - 1) / chunk_edges;
+    hcnt[r] = heavy ? nseg : 0;
+    ccnt[r] = ch;
+  }
+}
+
+__global__ void split_build_kernel(const int32_t* __restrict__ ptr, int64_t rows, int nseg, int threshold,
+                                   int chunk_edges, const int64_t* __restrict__ hoff, const int64_t* __restrict__ coff,
+                                   int32_t* __restrict__ heavy_seg, int32_t* __restrict__ heavy_cptr,
+                                   int32_t* __restrict__ chunk_begin, int32_t* __restrict__ chunk_end,
+                                   int64_t num_heavy, int64_t num_chunks) {
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < rows; r += (int64_t)gridDim.x * blockDim.x) {
+    const int32_t* p = ptr + r * nseg;
+    if (p[nseg] - p[0] <= threshold) continue;
+    int64_t h = hoff[r], c = coff[r];
+    for (int t = 0; t < nseg; ++t, ++h) {
+      heavy_seg[h] = (int32_t)(r * nseg + t);
+      heavy_cptr[h] = (int32_t)c;
+      for (int32_t e = p[t]; e < p[t + 1]; e += chunk_edges, ++c) {
+        chunk_begin[c] = e;
+        chunk_end[c] = min(e + chunk_edges, p[t + 1]);
+      }
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) heavy_cptr[num_heavy] = (int32_t)num_chunks;
+}
+
+__global__ void split_totals_kernel(const int64_t* __restrict__ hoff, const int64_t* __restrict__ coff, int64_t rows,
+                                    int64_t* __restrict__ counts) {
+  counts[0] = hoff[rows];
+  counts[1] = coff[rows];
+}
+
+__global__ void set_zero_i64(int64_t* p) { *p = 0; }
+
+size_t align_up(size_t x) { return (x + 255) & ~size_t(255); }
+
+// workspace: hcnt[rows+1], ccnt[rows+1], hoff[rows+1], coff[rows+1], cub temp
+int split_offsets(const int32_t* ptr, int64_t rows, int nseg, int threshold, int chunk_edges, void* ws,
+                  size_t ws_bytes, hipStream_t st, int64_t** hoff_out, int64_t** coff_out) {
+  const size_t a = align_up((size_t)(rows + 1) * 8);
+  char* w = static_cast<char*>(ws);
+  int64_t* hcnt = reinterpret_cast<int64_t*>(w);
+  int64_t* ccnt = reinterpret_cast<int64_t*>(w + a);
+  int64_t* hoff = reinterpret_cast<int64_t*>(w + 2 * a);
+  int64_t* coff = reinterpret_cast<int64_t*>(w + 3 * a);
+  void* temp = w + 4 * a;
+  size_t temp_bytes = ws_bytes - 4 * a;
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(rows, 256), 65536));
+  if (rows > 0) {
+    hipLaunchKernelGGL(split_count_kernel, dim3(grid), dim3(256), 0, st, ptr, rows, nseg, threshold, chunk_edges,
+                       hcnt, ccnt);
+    GRL_LAUNCH_CHECK();
+  }
+  hipLaunchKernelGGL(set_zero_i64, dim3(1), dim3(1), 0, st, hcnt + rows);
+  hipLaunchKernelGGL(set_zero_i64, dim3(1), dim3(1), 0, st, ccnt + rows);
+  GRL_LAUNCH_CHECK();
+  GRL_HIP(hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, hcnt, hoff, (int)(rows + 1), st));
+  GRL_HIP(hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, ccnt, coff, (int)(rows + 1), st));
+  *hoff_out = hoff;
+  *coff_out = coff;
+  return GRL_OK;
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
 struct LaunchShape {
   int vec, nv, ycols;
 };
@@ -213,22 +357,45 @@ LaunchShape pick_shape(const float* a, const float* b, int64_t lda, int64_t ldb,
   return {1, nv, 64 * nv};
 }
 
+int to_split_dev(const GrlSplitPlan* plan, int F, SplitDev& sp) {
+  sp = SplitDev{INT_MAX, 0, nullptr, nullptr, nullptr};
+  if (!plan) return GRL_OK;
+  GRL_CHECK_ARG(plan->threshold >= 0 && plan->chunk_edges > 0 && plan->num_heavy >= 0 && plan->num_chunks >= 0,
+                "split plan: bad threshold/chunk_edges/counts");
+  if (plan->num_chunks > 0) {
+    GRL_CHECK_ARG(plan->chunk_begin && plan->chunk_end && plan->partials, "split plan: NULL chunk arrays");
+    if (plan->partials_capacity < plan->num_chunks * (int64_t)F)
+      GRL_FAIL(GRL_E_WORKSPACE, "split plan: partials hold %lld floats, need %lld", (long long)plan->partials_capacity,
+               (long long)(plan->num_chunks * (int64_t)F));
+  }
+  GRL_CHECK_ARG(plan->num_heavy == 0 || (plan->heavy_seg && plan->heavy_cptr), "split plan: NULL heavy arrays");
+  sp.threshold = plan->threshold;
+  sp.num_chunks = plan->num_chunks;
+  sp.chunk_begin = plan->chunk_begin;
+  sp.chunk_end = plan->chunk_end;
+  sp.partials = plan->partials;
+  return GRL_OK;
+}
+
 template <bool BWD>
 int launch_spmm(int64_t num_rows, int64_t self_rows, int S, int hs, const int32_t* ptr, const int32_t* idx,
-                const int32_t* eid, const float* vals, uint64_t edge_base, uint64_t self_base,
-                const float* src, int64_t lds, int F, float* out, int64_t ldo, const DropDev& de,
+                const int32_t* eid, const float* vals, uint64_t edge_base, uint64_t self_base, const float* src,
+                int64_t lds, int F, float* out, int64_t ldo, const DropDev& de, const GrlSplitPlan* plan,
                 hipStream_t stream, const float* align_probe) {
   if (num_rows == 0) return GRL_OK;
+  SplitDev sp;
+  int rc = to_split_dev(plan, F, sp);
+  if (rc) return rc;
   const LaunchShape sh = pick_shape(src, align_probe, lds, ldo, F);
-  const int64_t waves_needed = num_rows;
+  const int64_t items = num_rows + sp.num_chunks;
   const int64_t cap = (int64_t)device_cu_count() * 16;  // 16 x 4-wave blocks per CU in flight
-  const int64_t gx = std::min<int64_t>(ceil_div(waves_needed, 4), cap);
+  const int64_t gx = std::min<int64_t>(ceil_div(items, 4), cap);
   const dim3 grid((unsigned)gx, (unsigned)ceil_div(F, sh.ycols));
   const dim3 block(256);
   const bool v = vals != nullptr;
-#define GRL_SPMM_LAUNCH(VEC, NV, U, VALS)                                                             \
-  hipLaunchKernelGGL((spmm_kernel<VEC, NV, U, VALS, BWD>), grid, block, 0, stream, num_rows, self_rows, \
-                     S, hs, ptr, idx, eid, vals, edge_base, self_base, src, lds, F, out, ldo, de)
+#define GRL_SPMM_LAUNCH(VEC, NV, U, VALS)                                                                  \
+  hipLaunchKernelGGL((spmm_kernel<VEC, NV, U, VALS, BWD>), grid, block, 0, stream, num_rows, self_rows, S, \
+                     hs, ptr, idx, eid, vals, edge_base, self_base, src, lds, F, out, ldo, de, sp)
   if (sh.vec == 4) {
     if (sh.nv == 1) {
       if (v) GRL_SPMM_LAUNCH(4, 1, 8, true); else GRL_SPMM_LAUNCH(4, 1, 8, false);
@@ -246,6 +413,21 @@ int launch_spmm(int64_t num_rows, int64_t self_rows, int S, int hs, const int32_
   }
 #undef GRL_SPMM_LAUNCH
   GRL_LAUNCH_CHECK();
+  if (plan && plan->num_heavy > 0) {
+    const dim3 fgrid((unsigned)std::min<int64_t>(ceil_div(plan->num_heavy, 4), cap), grid.y);
+    const int nseg = BWD ? 1 : S;
+#define GRL_FIXUP_LAUNCH(VEC, NV)                                                                            \
+  hipLaunchKernelGGL((spmm_fixup_kernel<VEC, NV, BWD>), fgrid, block, 0, stream, plan->num_heavy,            \
+                     plan->heavy_seg, plan->heavy_cptr, plan->partials, nseg, S, hs, self_rows, self_base, src, \
+                     F, out, ldo, de)
+    if (sh.vec == 4) {
+      if (sh.nv == 1) GRL_FIXUP_LAUNCH(4, 1); else GRL_FIXUP_LAUNCH(4, 2);
+    } else {
+      if (sh.nv == 1) GRL_FIXUP_LAUNCH(1, 1); else if (sh.nv == 2) GRL_FIXUP_LAUNCH(1, 2); else GRL_FIXUP_LAUNCH(1, 4);
+    }
+#undef GRL_FIXUP_LAUNCH
+    GRL_LAUNCH_CHECK();
+  }
   return GRL_OK;
 }
 
@@ -302,8 +484,8 @@ extern "C" int grl_typed_spmm_fwd(const GrlTypedCsr* g, const float* X, int64_t 
   GRL_CHECK_ARG(g->nnz < 2147483647LL, "grl_typed_spmm_fwd: nnz %lld exceeds int32", (long long)g->nnz);
   const int hs = g->has_self ? 1 : 0;
   const int64_t ldz = (int64_t)(g->num_types + hs) * F;
-  return launch_spmm<false>(g->num_rows, g->num_rows, g->num_types, hs, g->rowptr, g->colidx, nullptr,
-                            g->vals, g->edge_id_base, g->self_id_base, X, ldx, F, Z, ldz, to_dev(de),
+  return launch_spmm<false>(g->num_rows, g->num_rows, g->num_types, hs, g->rowptr, g->colidx, nullptr, g->vals,
+                            g->edge_id_base, g->self_id_base, X, ldx, F, Z, ldz, to_dev(de), g->split,
                             as_stream(stream), Z);
 }
 
@@ -318,6 +500,58 @@ extern "C" int grl_typed_spmm_bwd(const GrlTypedCsc* g, const float* dZ, int32_t
   GRL_CHECK_ARG(dZ && dX && g->colptr && (g->nnz == 0 || (g->zrow && g->eid)), "grl_typed_spmm_bwd: NULL pointer");
   const int hs = g->has_self ? 1 : 0;
   return launch_spmm<true>(g->num_rows, g->self_rows, g->num_types, hs, g->colptr, g->zrow, g->eid, g->vals,
-                           g->edge_id_base, g->self_id_base, dZ, (int64_t)F, F, dX, lddx, to_dev(de),
+                           g->edge_id_base, g->self_id_base, dZ, (int64_t)F, F, dX, lddx, to_dev(de), g->split,
                            as_stream(stream), dX);
+}
+
+extern "C" size_t grl_split_plan_workspace_size(int64_t rows) {
+  size_t temp = 0;
+  int64_t* d = nullptr;
+  if (hipcub::DeviceScan::ExclusiveSum(nullptr, temp, d, d, (int)std::max<int64_t>(rows + 1, 1)) != hipSuccess)
+    return 0;
+  return 4 * align_up((size_t)(rows + 1) * 8) + align_up(temp);
+}
+
+extern "C" int grl_split_plan_count(const int32_t* ptr, int64_t rows, int32_t nseg, int32_t threshold,
+                                    int32_t chunk_edges, int64_t* counts, void* workspace, size_t workspace_bytes,
+                                    grl_stream_t stream) {
+  GRL_CHECK_ARG(ptr && counts && rows >= 0 && nseg >= 1 && threshold >= 0 && chunk_edges > 0,
+                "grl_split_plan_count: bad arguments");
+  GRL_CHECK_ARG(rows < 2147483647LL, "grl_split_plan_count: too many rows");
+  const size_t need = grl_split_plan_workspace_size(rows);
+  if (!workspace || workspace_bytes < need)
+    GRL_FAIL(GRL_E_WORKSPACE, "grl_split_plan_count: workspace %zu < %zu", workspace_bytes, need);
+  hipStream_t st = as_stream(stream);
+  int64_t *hoff, *coff;
+  int rc = split_offsets(ptr, rows, nseg, threshold, chunk_edges, workspace, workspace_bytes, st, &hoff, &coff);
+  if (rc) return rc;
+  hipLaunchKernelGGL(split_totals_kernel, dim3(1), dim3(1), 0, st, hoff, coff, rows, counts);
+  GRL_LAUNCH_CHECK();
+  return GRL_OK;
+}
+
+extern "C" int grl_split_plan_build(const int32_t* ptr, int64_t rows, int32_t nseg, GrlSplitPlan* plan,
+                                    void* workspace, size_t workspace_bytes, grl_stream_t stream) {
+  GRL_CHECK_ARG(ptr && plan && rows >= 0 && nseg >= 1, "grl_split_plan_build: bad arguments");
+  GRL_CHECK_ARG(plan->threshold >= 0 && plan->chunk_edges > 0, "grl_split_plan_build: bad threshold/chunk_edges");
+  GRL_CHECK_ARG(plan->heavy_cptr != nullptr, "grl_split_plan_build: heavy_cptr is NULL");
+  GRL_CHECK_ARG(plan->num_heavy == 0 || plan->heavy_seg, "grl_split_plan_build: heavy_seg is NULL");
+  GRL_CHECK_ARG(plan->num_chunks == 0 || (plan->chunk_begin && plan->chunk_end),
+                "grl_split_plan_build: chunk arrays are NULL");
+  GRL_CHECK_ARG(plan->num_chunks < 2147483647LL, "grl_split_plan_build: too many chunks");
+  const size_t need = grl_split_plan_workspace_size(rows);
+  if (!workspace || workspace_bytes < need)
+    GRL_FAIL(GRL_E_WORKSPACE, "grl_split_plan_build: workspace %zu < %zu", workspace_bytes, need);
+  hipStream_t st = as_stream(stream);
+  int64_t *hoff, *coff;
+  int rc = split_offsets(ptr, rows, nseg, plan->threshold, plan->chunk_edges, workspace, workspace_bytes, st, &hoff,
+                         &coff);
+  if (rc) return rc;
+  const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(rows, 256), 65536));
+  hipLaunchKernelGGL(split_build_kernel, dim3(grid), dim3(256), 0, st, ptr, rows, nseg, plan->threshold,
+                     plan->chunk_edges, hoff, coff, const_cast<int32_t*>(plan->heavy_seg),
+                     const_cast<int32_t*>(plan->heavy_cptr), const_cast<int32_t*>(plan->chunk_begin),
+                     const_cast<int32_t*>(plan->chunk_end), plan->num_heavy, plan->num_chunks);
+  GRL_LAUNCH_CHECK();
+  return GRL_OK;
 }

@@ -36,6 +36,21 @@ _c_vp = ctypes.c_void_p
 _c_size = ctypes.c_size_t
 
 
+class GrlSplitPlan(ctypes.Structure):
+    _fields_ = [
+        ("threshold", _c_i32),
+        ("chunk_edges", _c_i32),
+        ("num_heavy", _c_i64),
+        ("num_chunks", _c_i64),
+        ("heavy_seg", _c_vp),
+        ("heavy_cptr", _c_vp),
+        ("chunk_begin", _c_vp),
+        ("chunk_end", _c_vp),
+        ("partials", _c_vp),
+        ("partials_capacity", _c_i64),
+    ]
+
+
 class GrlTypedCsr(ctypes.Structure):
     _fields_ = [
         ("num_rows", _c_i64),
@@ -47,6 +62,7 @@ class GrlTypedCsr(ctypes.Structure):
         ("nnz", _c_i64),
         ("edge_id_base", _c_u64),
         ("self_id_base", _c_u64),
+        ("split", ctypes.POINTER(GrlSplitPlan)),
     ]
 
 
@@ -63,6 +79,7 @@ class GrlTypedCsc(ctypes.Structure):
         ("nnz", _c_i64),
         ("edge_id_base", _c_u64),
         ("self_id_base", _c_u64),
+        ("split", ctypes.POINTER(GrlSplitPlan)),
     ]
 
 
@@ -103,6 +120,9 @@ SIGNATURES = {
     "grl_dense_to_csr_fill": (_c_i32, [_c_vp, _c_i64, _c_i64, _c_i32, _P(_c_i64), _c_vp, _c_vp, _c_vp, _c_vp]),
     "grl_csr_to_csc_workspace_size": (_c_size, [_c_i64, _c_i64]),
     "grl_csr_to_csc": (_c_i32, [_P(GrlTypedCsr), _c_i64, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_size, _c_vp]),
+    "grl_split_plan_workspace_size": (_c_size, [_c_i64]),
+    "grl_split_plan_count": (_c_i32, [_c_vp, _c_i64, _c_i32, _c_i32, _c_i32, _c_vp, _c_vp, _c_size, _c_vp]),
+    "grl_split_plan_build": (_c_i32, [_c_vp, _c_i64, _c_i32, _P(GrlSplitPlan), _c_vp, _c_size, _c_vp]),
     "grl_synth_count": (_c_i32, [_P(GrlSynthSpec), _c_vp, _c_vp]),
     "grl_synth_workspace_size": (_c_size, [_P(GrlSynthSpec), _c_i64]),
     "grl_synth_build": (_c_i32, [_P(GrlSynthSpec), _c_i64, _c_vp, _c_vp, _c_vp, _c_vp, _c_size, _c_vp]),

@@ -22,7 +22,12 @@ from typing import Optional, Tuple
 import torch
 
 from . import _lib
-from ._lib import GrlDropEdge, GrlSynthSpec, GrlTypedCsc, GrlTypedCsr, call
+from ._lib import GrlDropEdge, GrlSplitPlan, GrlSynthSpec, GrlTypedCsc, GrlTypedCsr, call
+
+# Heavy-row splitting (R-MAT hubs): rows with more edges than SPLIT_THRESHOLD
+# are summed in chunks of SPLIT_CHUNK edges by separate wavefronts.
+SPLIT_THRESHOLD = 2048
+SPLIT_CHUNK = 1024
 
 
 def current_stream_handle(device: torch.device) -> int:
@@ -78,6 +83,8 @@ class TypedGraph:
         self.self_rows = self.num_rows if self_rows is None else int(self_rows)
         self.batch_shape = batch_shape
         self.dropedge: Optional[DropEdge] = None
+        self.split_threshold = SPLIT_THRESHOLD
+        self.split_chunk = SPLIT_CHUNK
         self._shared = {"csc": None} if _shared is None else _shared
 
     # ------------------------------------------------------------------ views
@@ -103,8 +110,65 @@ class TypedGraph:
                 f"nnz={self.nnz}, has_self={self.has_self}, vals={'yes' if self.vals is not None else 'ones'}, "
                 f"dropedge={self.dropedge})")
 
+    # ----------------------------------------------------------- split plans
+    def _split(self, which: str, F: int):
+        """Cached heavy-row plan over rowptr ("csr") or colptr ("csc"), with
+        its partials scratch grown to F floats per chunk; None if no row is
+        heavier than the threshold."""
+        key = f"split_{which}"
+        if key not in self._shared:
+            self._shared[key] = self._build_split(which)
+        sp = self._shared[key]
+        if sp is None:
+            return None
+        need = sp["plan"].num_chunks * F
+        if sp["partials"] is None or sp["partials"].numel() < need:
+            sp["partials"] = torch.empty(max(need, 1), dtype=torch.float32, device=self.device)
+            sp["plan"].partials = sp["partials"].data_ptr()
+            sp["plan"].partials_capacity = sp["partials"].numel()
+        return sp["plan"]
+
+    def _build_split(self, which: str):
+        if self.nnz <= self.split_threshold:  # no row can be heavy: no device work, no sync
+            return None
+        if which == "csr":
+            ptr, rows, nseg = self.rowptr, self.num_rows, self.num_types
+        else:
+            ptr, rows, nseg = self.csc()["colptr"], self.num_cols, 1
+        dev = self.device
+        stream = current_stream_handle(dev)
+        ws_bytes = _lib.lib().grl_split_plan_workspace_size(rows)
+        if ws_bytes == 0:
+            raise _lib.GrlError("grl_split_plan_workspace_size failed")
+        ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+        counts = torch.zeros(2, dtype=torch.int64, device=dev)
+        call("grl_split_plan_count", ptr.data_ptr(), rows, nseg, self.split_threshold, self.split_chunk,
+             counts.data_ptr(), ws.data_ptr(), ws_bytes, stream)
+        num_heavy, num_chunks = (int(x) for x in counts.tolist())
+        if num_heavy == 0:
+            return None
+        t = {name: torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+             for name, n in (("heavy_seg", num_heavy), ("heavy_cptr", num_heavy + 1), ("chunk_begin", num_chunks),
+                             ("chunk_end", num_chunks))}
+        plan = GrlSplitPlan()
+        plan.threshold, plan.chunk_edges = self.split_threshold, self.split_chunk
+        plan.num_heavy, plan.num_chunks = num_heavy, num_chunks
+        for name, tensor in t.items():
+            setattr(plan, name, tensor.data_ptr())
+        call("grl_split_plan_build", ptr.data_ptr(), rows, nseg, ctypes.byref(plan), ws.data_ptr(), ws_bytes, stream)
+        return {"plan": plan, "tensors": t, "partials": None}
+
+    def split_stats(self) -> dict:
+        out = {}
+        for which in ("csr", "csc"):
+            self._split(which, 1)
+            sp = self._shared.get(f"split_{which}")
+            out[which] = {"heavy_segments": 0, "chunks": 0} if sp is None else {
+                "heavy_segments": sp["plan"].num_heavy, "chunks": sp["plan"].num_chunks}
+        return out
+
     # ------------------------------------------------------------ C structs
-    def csr_c(self) -> GrlTypedCsr:
+    def csr_c(self, F: Optional[int] = None) -> GrlTypedCsr:
         g = GrlTypedCsr()
         g.num_rows = self.num_rows
         g.num_types = self.num_types
@@ -115,6 +179,8 @@ class TypedGraph:
         g.nnz = self.nnz
         g.edge_id_base = self.edge_id_base
         g.self_id_base = self.self_id_base
+        plan = self._split("csr", F) if F is not None else None
+        g.split = ctypes.pointer(plan) if plan is not None else None
         return g
 
     def csc(self) -> dict:
@@ -140,7 +206,7 @@ class TypedGraph:
         self._shared["csc"] = c
         return c
 
-    def csc_c(self) -> GrlTypedCsc:
+    def csc_c(self, F: Optional[int] = None) -> GrlTypedCsc:
         c = self.csc()
         s = GrlTypedCsc()
         s.num_rows = self.num_cols
@@ -154,6 +220,8 @@ class TypedGraph:
         s.nnz = self.nnz
         s.edge_id_base = self.edge_id_base
         s.self_id_base = self.self_id_base
+        plan = self._split("csc", F) if F is not None else None
+        s.split = ctypes.pointer(plan) if plan is not None else None
         return s
 
     # ----------------------------------------------------------- builders

@@ -43,7 +43,7 @@ def spmm_forward(X: torch.Tensor, graph: TypedGraph, out: torch.Tensor = None) -
     elif tuple(out.shape) != shape or out.dtype != torch.float32 or not out.is_contiguous() \
             or out.device != X.device:
         raise _lib.GrlError(f"out must be a contiguous float32 {shape} tensor on {X.device}")
-    csr = graph.csr_c()
+    csr = graph.csr_c(F)
     de = graph.dropedge.to_c() if graph.dropedge is not None else None
     call("grl_typed_spmm_fwd", ctypes.byref(csr), X2.data_ptr(), X2.stride(0), F, out.data_ptr(),
          ctypes.byref(de) if de is not None else None, current_stream_handle(X.device))
@@ -64,7 +64,7 @@ class _TypedAggregate(torch.autograd.Function):
         dZ = dZ.contiguous().float()
         F = ctx.xshape[-1]
         dX = torch.empty(graph.num_cols, F, dtype=torch.float32, device=dZ.device)
-        csc = graph.csc_c()
+        csc = graph.csc_c(F)
         de = graph.dropedge.to_c() if graph.dropedge is not None else None
         call("grl_typed_spmm_bwd", ctypes.byref(csc), dZ.data_ptr(), F, dX.data_ptr(), F,
              ctypes.byref(de) if de is not None else None, current_stream_handle(dZ.device))

@@ -44,6 +44,29 @@ enum {
 };
 
 /*
+ * Heavy-row split plan (load balance for power-law graphs, e.g. R-MAT hubs).
+ * A row whose edge count exceeds `threshold` is not gathered by one
+ * wavefront: each of its segments is cut into chunks of at most
+ * `chunk_edges` edges, every chunk is summed by its own wavefront into
+ * `partials` (num_chunks x F floats), and a fixup pass adds a segment's
+ * chunk partials in chunk order (deterministic, no atomics).  Built once per
+ * graph by grl_split_plan_count / grl_split_plan_build; attach it to the
+ * GrlTypedCsr / GrlTypedCsc `split` field (NULL = no splitting).
+ */
+typedef struct GrlSplitPlan {
+  int32_t threshold;          /* rows with more edges than this are split   */
+  int32_t chunk_edges;        /* max edges per chunk                         */
+  int64_t num_heavy;          /* heavy segments (all segments of heavy rows) */
+  int64_t num_chunks;
+  const int32_t* heavy_seg;   /* device [num_heavy]: segment id row*nseg+t   */
+  const int32_t* heavy_cptr;  /* device [num_heavy+1]: chunk range per seg   */
+  const int32_t* chunk_begin; /* device [num_chunks]: first edge position    */
+  const int32_t* chunk_end;   /* device [num_chunks]: one past last edge     */
+  float* partials;            /* device scratch, >= num_chunks * F floats    */
+  int64_t partials_capacity;  /* floats available in `partials`              */
+} GrlSplitPlan;
+
+/*
  * Typed CSR: the sparse form of the reference's preprocessed adjacency
  * A_pre[b, n*(L+1)+l, m] (gnn/models/networks/robust_gcn.py:53-72).
  * Row segment (n, t) for t in [0, num_types) lists the source rows m whose
@@ -67,6 +90,7 @@ typedef struct GrlTypedCsr {
   int64_t nnz;
   uint64_t edge_id_base; /* global DropEdge id of colidx[0] (node-range shard)*/
   uint64_t self_id_base; /* global DropEdge id of row 0's self loop           */
+  const GrlSplitPlan* split; /* heavy-row plan over rowptr, or NULL           */
 } GrlTypedCsr;
 
 /*
@@ -89,6 +113,7 @@ typedef struct GrlTypedCsc {
   int64_t nnz;
   uint64_t edge_id_base; /* as in the matching GrlTypedCsr                     */
   uint64_t self_id_base;
+  const GrlSplitPlan* split; /* heavy-column plan over colptr, or NULL        */
 } GrlTypedCsc;
 
 /*
@@ -180,6 +205,21 @@ int grl_dense_to_csr_rowptr(const float* A, int64_t B, int64_t N, int32_t L,
 int grl_dense_to_csr_fill(const float* A, int64_t B, int64_t N, int32_t L,
                           const int64_t strides[4], const int32_t* rowptr,
                           int32_t* colidx, float* vals, grl_stream_t stream);
+
+/* Heavy-row plan over a segment pointer array ptr[rows*nseg + 1] (rowptr
+ * with nseg = L for the forward CSR, colptr with nseg = 1 for the CSC).
+ *   grl_split_plan_count -> counts[0] = heavy segments, counts[1] = chunks
+ *                           (device int64[2]; the caller reads them to size
+ *                           the plan arrays)
+ *   grl_split_plan_build -> fills plan->heavy_seg/heavy_cptr/chunk_begin/
+ *                           chunk_end (caller-allocated, sizes from count)
+ * Deterministic: segments and chunks are emitted in row, segment, edge order. */
+size_t grl_split_plan_workspace_size(int64_t rows);
+int grl_split_plan_count(const int32_t* ptr, int64_t rows, int32_t nseg, int32_t threshold,
+                         int32_t chunk_edges, int64_t* counts, void* workspace,
+                         size_t workspace_bytes, grl_stream_t stream);
+int grl_split_plan_build(const int32_t* ptr, int64_t rows, int32_t nseg, GrlSplitPlan* plan,
+                         void* workspace, size_t workspace_bytes, grl_stream_t stream);
 
 /* Typed CSR -> CSC over source rows [0, num_cols) for the backward pass.
  * Stable: within a column, entries keep CSR (edge id) order, so dX sums are

@@ -44,10 +44,10 @@ def lib():
         L.oracle_dropedge_mask.argtypes = [ctypes.POINTER(ODrop), _u64, _i64, _vp]
         L.oracle_spmm_fwd.restype = None
         L.oracle_spmm_fwd.argtypes = [_i64, _i32, _i32, _vp, _vp, _vp, _u64, _u64, _vp, _i64, _i32, _vp,
-                                      ctypes.POINTER(ODrop), _i32]
+                                      ctypes.POINTER(ODrop), _i32, _i32, _i32]
         L.oracle_spmm_bwd.restype = None
         L.oracle_spmm_bwd.argtypes = [_i64, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _u64, _u64, _vp, _i32, _vp, _i64,
-                                      ctypes.POINTER(ODrop), _i32]
+                                      ctypes.POINTER(ODrop), _i32, _i32, _i32]
         L.oracle_dense_to_csr.restype = _i64
         L.oracle_dense_to_csr.argtypes = [_vp, _i64, _i64, _i32, _vp, _vp, _vp, _vp]
         L.oracle_csr_to_csc.restype = None
@@ -79,7 +79,9 @@ def dropedge_mask(d: ODrop, id_base: int, count: int) -> np.ndarray:
 
 
 def spmm_fwd(rowptr, colidx, X, num_types, has_self=True, vals=None, d: ODrop | None = None, edge_base=0,
-             self_base=None, nthreads=0):
+             self_base=None, nthreads=0, split=None):
+    """split = (threshold, chunk_edges) reproduces the engine's chunked
+    summation order for rows heavier than threshold (GrlSplitPlan)."""
     rowptr = np.ascontiguousarray(rowptr, dtype=np.int32)
     colidx = np.ascontiguousarray(colidx, dtype=np.int32)
     X = np.ascontiguousarray(X, dtype=np.float32)
@@ -91,7 +93,8 @@ def spmm_fwd(rowptr, colidx, X, num_types, has_self=True, vals=None, d: ODrop | 
         self_base = int(rowptr[-1])
     Z = np.empty((rows, (num_types + hs) * F), dtype=np.float32)
     lib().oracle_spmm_fwd(rows, num_types, hs, _p(rowptr), _p(colidx), _p(vals), edge_base, self_base, _p(X), F, F,
-                          _p(Z), ctypes.byref(d) if d is not None else None, nthreads)
+                          _p(Z), ctypes.byref(d) if d is not None else None, nthreads,
+                          *(split if split is not None else (-1, 1)))
     return Z
 
 
@@ -111,7 +114,7 @@ def csr_to_csc(rowptr, colidx, num_types, ncols, has_self=True, vals=None):
 
 
 def spmm_bwd(colptr, zrow, eid, dZ, num_types, F, self_rows, has_self=True, cvals=None, d: ODrop | None = None,
-             edge_base=0, self_base=0, nthreads=0):
+             edge_base=0, self_base=0, nthreads=0, split=None):
     colptr = np.ascontiguousarray(colptr, dtype=np.int32)
     rows = colptr.size - 1
     dZ = np.ascontiguousarray(dZ, dtype=np.float32)
@@ -120,7 +123,8 @@ def spmm_bwd(colptr, zrow, eid, dZ, num_types, F, self_rows, has_self=True, cval
     lib().oracle_spmm_bwd(rows, self_rows, num_types, 1 if has_self else 0, _p(colptr),
                           _p(np.ascontiguousarray(zrow, dtype=np.int32)), _p(np.ascontiguousarray(eid, dtype=np.int32)),
                           _p(cvals), edge_base, self_base, _p(dZ), F, _p(dX), F,
-                          ctypes.byref(d) if d is not None else None, nthreads)
+                          ctypes.byref(d) if d is not None else None, nthreads,
+                          *(split if split is not None else (-1, 1)))
     return dX
 
 

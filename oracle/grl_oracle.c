@@ -90,64 +90,102 @@ void oracle_dropedge_mask(const ODrop* d, uint64_t id_base, int64_t count, uint8
 }
 
 /* ---------------- typed SpMM forward / backward ------------------------- */
+/* Sum of w_e * src[idx[e]] over edges [e0, e1) as one fmaf chain from 0 (the
+ * reference's bmm row restricted to nonzeros, in CSR/CSC order). */
+static void o_chain(float* acc, int32_t e0, int32_t e1, const int32_t* idx, const int32_t* eid, const float* vals,
+                    uint64_t edge_base, const float* src, int64_t lds, int32_t F, const ODrop* d) {
+  for (int32_t e = e0; e < e1; ++e) {
+    const float v = vals ? vals[e] : 1.0f;
+    const uint64_t id = edge_base + (eid ? (uint64_t)(uint32_t)eid[e] : (uint64_t)e);
+    const float w = o_weight(d, v, id);
+    if (w == 0.0f) continue;
+    const float* xr = src + (int64_t)idx[e] * lds;
+    for (int f = 0; f < F; ++f) acc[f] = fmaf(w, xr[f], acc[f]);
+  }
+}
+
+/* Segment [e0, e1) of a row: plain fmaf chain, or -- for rows the engine
+ * splits (row edges > split_threshold >= 0) -- chunks of split_chunk edges,
+ * each its own chain from 0, added in chunk order onto acc's initial value
+ * (the engine's load-balanced summation order; include/grl.h GrlSplitPlan). */
+static void o_segment(float* acc, float* tmp, int heavy, int32_t chunk, int32_t e0, int32_t e1, const int32_t* idx,
+                      const int32_t* eid, const float* vals, uint64_t edge_base, const float* src, int64_t lds,
+                      int32_t F, const ODrop* d) {
+  if (!heavy) {
+    o_chain(acc, e0, e1, idx, eid, vals, edge_base, src, lds, F, d);
+    return;
+  }
+  for (int32_t c = e0; c < e1; c += chunk) {
+    for (int f = 0; f < F; ++f) tmp[f] = 0.0f;
+    o_chain(tmp, c, c + chunk < e1 ? c + chunk : e1, idx, eid, vals, edge_base, src, lds, F, d);
+    for (int f = 0; f < F; ++f) acc[f] = acc[f] + tmp[f];
+  }
+}
+
 void oracle_spmm_fwd(int64_t rows, int32_t S, int32_t hs, const int32_t* rowptr, const int32_t* colidx,
                      const float* vals, uint64_t edge_base, uint64_t self_base, const float* X, int64_t ldx,
-                     int32_t F, float* Z, const ODrop* d, int32_t nthreads) {
+                     int32_t F, float* Z, const ODrop* d, int32_t nthreads, int32_t split_threshold,
+                     int32_t split_chunk) {
   const int64_t ldz = (int64_t)(S + hs) * F;
 #ifdef _OPENMP
   if (nthreads > 0) omp_set_num_threads(nthreads);
-#pragma omp parallel for schedule(dynamic, 256)
+#pragma omp parallel
 #endif
-  for (int64_t n = 0; n < rows; ++n) {
-    float* zr = Z + n * ldz;
-    if (hs) {
-      float w = 1.0f;
-      if (d && d->active && d->drop_self) w = o_weight(d, 1.0f, self_base + (uint64_t)n);
-      const float* xr = X + n * ldx;
-      for (int f = 0; f < F; ++f) zr[f] = w != 0.0f ? w * xr[f] : 0.0f;
-    }
-    for (int t = 0; t < S; ++t) {
-      float* acc = zr + (int64_t)(hs + t) * F;
-      for (int f = 0; f < F; ++f) acc[f] = 0.0f;
-      const int64_t s = n * S + t;
-      for (int32_t e = rowptr[s]; e < rowptr[s + 1]; ++e) {
-        const float v = vals ? vals[e] : 1.0f;
-        const float w = o_weight(d, v, edge_base + (uint64_t)e);
-        if (w == 0.0f) continue;
-        const float* xr = X + (int64_t)colidx[e] * ldx;
-        for (int f = 0; f < F; ++f) acc[f] = fmaf(w, xr[f], acc[f]);
+  {
+    float* tmp = (float*)malloc(sizeof(float) * (size_t)F);
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 256)
+#endif
+    for (int64_t n = 0; n < rows; ++n) {
+      float* zr = Z + n * ldz;
+      if (hs) {
+        float w = 1.0f;
+        if (d && d->active && d->drop_self) w = o_weight(d, 1.0f, self_base + (uint64_t)n);
+        const float* xr = X + n * ldx;
+        for (int f = 0; f < F; ++f) zr[f] = w != 0.0f ? w * xr[f] : 0.0f;
+      }
+      const int heavy = split_threshold >= 0 && rowptr[(n + 1) * S] - rowptr[n * S] > split_threshold;
+      for (int t = 0; t < S; ++t) {
+        float* acc = zr + (int64_t)(hs + t) * F;
+        for (int f = 0; f < F; ++f) acc[f] = 0.0f;
+        const int64_t s = n * S + t;
+        o_segment(acc, tmp, heavy, split_chunk, rowptr[s], rowptr[s + 1], colidx, NULL, vals, edge_base, X, ldx, F,
+                  d);
       }
     }
+    free(tmp);
   }
 }
 
 void oracle_spmm_bwd(int64_t rows, int64_t self_rows, int32_t S, int32_t hs, const int32_t* colptr,
                      const int32_t* zrow, const int32_t* eid, const float* cvals, uint64_t edge_base,
                      uint64_t self_base, const float* dZ, int32_t F, float* dX, int64_t lddx, const ODrop* d,
-                     int32_t nthreads) {
+                     int32_t nthreads, int32_t split_threshold, int32_t split_chunk) {
   const int64_t ldz = (int64_t)(S + hs) * F;
 #ifdef _OPENMP
   if (nthreads > 0) omp_set_num_threads(nthreads);
-#pragma omp parallel for schedule(dynamic, 256)
+#pragma omp parallel
 #endif
-  for (int64_t m = 0; m < rows; ++m) {
-    float* acc = dX + m * lddx;
-    for (int f = 0; f < F; ++f) acc[f] = 0.0f;
-    if (hs && m < self_rows) {
-      float w = 1.0f;
-      if (d && d->active && d->drop_self) w = o_weight(d, 1.0f, self_base + (uint64_t)m);
-      if (w != 0.0f) {
-        const float* zr = dZ + m * ldz;
-        for (int f = 0; f < F; ++f) acc[f] = w * zr[f];
+  {
+    float* tmp = (float*)malloc(sizeof(float) * (size_t)F);
+#ifdef _OPENMP
+#pragma omp for schedule(dynamic, 256)
+#endif
+    for (int64_t m = 0; m < rows; ++m) {
+      float* acc = dX + m * lddx;
+      for (int f = 0; f < F; ++f) acc[f] = 0.0f;
+      if (hs && m < self_rows) {
+        float w = 1.0f;
+        if (d && d->active && d->drop_self) w = o_weight(d, 1.0f, self_base + (uint64_t)m);
+        if (w != 0.0f) {
+          const float* zr = dZ + m * ldz;
+          for (int f = 0; f < F; ++f) acc[f] = w * zr[f];
+        }
       }
+      const int heavy = split_threshold >= 0 && colptr[m + 1] - colptr[m] > split_threshold;
+      o_segment(acc, tmp, heavy, split_chunk, colptr[m], colptr[m + 1], zrow, eid, cvals, edge_base, dZ, F, F, d);
     }
-    for (int32_t i = colptr[m]; i < colptr[m + 1]; ++i) {
-      const float v = cvals ? cvals[i] : 1.0f;
-      const float w = o_weight(d, v, edge_base + (uint64_t)(uint32_t)eid[i]);
-      if (w == 0.0f) continue;
-      const float* zr = dZ + (int64_t)zrow[i] * F;
-      for (int f = 0; f < F; ++f) acc[f] = fmaf(w, zr[f], acc[f]);
-    }
+    free(tmp);
   }
 }
 

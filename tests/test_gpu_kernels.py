@@ -197,3 +197,63 @@ def test_errors_raise_not_fallback():
     with pytest.raises(_lib.GrlError, match="float32"):
         typed_aggregate(torch.zeros(2, 8, device=DEV, dtype=torch.float16), g)
     assert current_stream_handle(DEV) is not None
+
+
+SPLITS = [(64, 24), (300, 128), (2048, 1024)]
+
+
+@pytest.mark.parametrize("split", SPLITS)
+@pytest.mark.parametrize("di", [0, 1])
+@pytest.mark.parametrize("F,vals", [(256, False), (512, True), (10, False)])
+def test_split_rows_bitwise_rmat(split, di, F, vals):
+    """Power-law (R-MAT) graph: rows/columns heavier than the threshold are
+    summed in chunks by separate wavefronts + an ordered fixup; must equal the
+    oracle restating that chunk order bitwise, forward and backward."""
+    N, L = 1 << 12, 6
+    rowptr, colidx = ohash.synth_csr(1, L, N, N * 40, 21)
+    deg = np.diff(rowptr[::L])
+    assert deg.max() > split[0] or split[0] == 2048  # the small thresholds really split rows
+    v = np.random.default_rng(3).uniform(0.1, 2.0, colidx.size).astype(np.float32) if vals else None
+    de = [None, DropEdge(0.3, 7, 1, True)][di]
+    g = TypedGraph.from_csr_host(rowptr, colidx, L, DEV, vals=v).with_dropedge(de)
+    g.split_threshold, g.split_chunk = split
+    X = np.random.default_rng(F).standard_normal((N, F)).astype(np.float32)
+    Xt = to_dev(X).requires_grad_(True)
+    Z = typed_aggregate(Xt, g)
+    d = None if de is None else c_oracle.drop(de.p, de.seed, de.call, de.drop_self)
+    Zref = c_oracle.spmm_fwd(rowptr, colidx, X, L, True, vals=v, d=d, split=split)
+    assert_bitwise(Z.detach().cpu().numpy(), Zref, "forward (split)")
+    dZ = np.random.default_rng(F + 1).standard_normal(Zref.shape).astype(np.float32)
+    Z.backward(to_dev(dZ))
+    colptr, zrow, eid, cvals = c_oracle.csr_to_csc(rowptr, colidx, L, N, True, v)
+    dXref = c_oracle.spmm_bwd(colptr, zrow, eid, dZ, L, F, N, True, cvals, d=d, self_base=int(rowptr[-1]),
+                              split=split)
+    assert_bitwise(Xt.grad.cpu().numpy(), dXref, "backward (split)")
+    st = g.split_stats()
+    if split[0] < 300:
+        assert st["csr"]["heavy_segments"] > 0 and st["csc"]["heavy_segments"] > 0
+    # and within fp32 tolerance of the unsplit summation order
+    Zplain = c_oracle.spmm_fwd(rowptr, colidx, X, L, True, vals=v, d=d)
+    assert np.allclose(Zref, Zplain, rtol=1e-5, atol=1e-4)
+
+
+def test_split_plan_matches_definition():
+    N, L = 1 << 11, 6
+    rowptr, colidx = ohash.synth_csr(1, L, N, N * 30, 4)
+    g = TypedGraph.from_csr_host(rowptr, colidx, L, DEV)
+    g.split_threshold, g.split_chunk = 100, 40
+    g._split("csr", 8)
+    sp = g._shared["split_csr"]
+    heavy_rows = np.nonzero(np.diff(rowptr[::L]) > 100)[0]
+    exp_seg = (heavy_rows[:, None] * L + np.arange(L)[None]).ravel()
+    np.testing.assert_array_equal(sp["tensors"]["heavy_seg"].cpu().numpy()[:exp_seg.size], exp_seg)
+    begins, ends, cptr = [], [], [0]
+    for s in exp_seg:
+        for e in range(rowptr[s], rowptr[s + 1], 40):
+            begins.append(e)
+            ends.append(min(e + 40, rowptr[s + 1]))
+        cptr.append(len(begins))
+    assert sp["plan"].num_chunks == len(begins)
+    np.testing.assert_array_equal(sp["tensors"]["chunk_begin"].cpu().numpy()[:len(begins)], begins)
+    np.testing.assert_array_equal(sp["tensors"]["chunk_end"].cpu().numpy()[:len(ends)], ends)
+    np.testing.assert_array_equal(sp["tensors"]["heavy_cptr"].cpu().numpy()[:len(cptr)], cptr)
