@@ -143,7 +143,7 @@ def main():
         "vs_baseline": None, "dtype": "f32",
         "data": f"synthetic: seeded {'Erdos-Renyi' if args.graph == 'er' else 'R-MAT'} typed graph (graph seed 0), "
                 "X ~ N(0,1) fp32 (seed 1+rank)",
-        "config": {"workload": ("C3" if world == 1 else "C4-shape") + f": {args.graph.upper()} typed graph, "
+        "config": {"workload": workload_name(args, world, n_loc) + f": {args.graph.upper()} typed graph, "
                    f"{n_loc} nodes/GPU, avg_deg {args.avg_deg:g} over L={L} edge types, d={F}, typed-SpMM "
                    f"forward (GraphConv aggregation){' + DropEdge p=%g' % args.p if args.p else ''}",
                    "nodes_total": N, "edges_total": E_tot, "nodes_per_gpu": n_loc, "avg_deg": args.avg_deg,
@@ -157,8 +157,11 @@ def main():
                      "algorithmic_bytes_per_launch": bytes_launch},
         "build_s": build_s,
     }
+    if args.graph == "rmat":
+        out["config"]["split"] = graph.split_stats()
+        out["config"]["max_row_edges"] = int((graph.rowptr[L::L] - graph.rowptr[:-1:L]).max())
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        out["cpu_baseline"], out["parity"] = cpu_baseline(args, graph, X_loc, Z, L, F)
+        out["cpu_baseline"], out["parity"] = cpu_baseline(args, g_step, X_loc, Z, L, F)
     if args.extras:
         out["extras"] = extras(args, graph, X_full, gather, L, F, dev, E_loc, n_loc)
     if rank == 0:
@@ -166,6 +169,17 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def workload_name(args, world, n_loc):
+    """Which SURVEY.md §8(d) config this run is (or is shaped like)."""
+    if args.graph == "rmat":
+        return "C5" if (n_loc * world == 1 << 23 and args.dim == 512) else "C5-shape"
+    if args.dim == 256 and args.avg_deg == 32 and n_loc == 1_000_000:
+        return {1: "C3", 4: "C4"}.get(world, "C4-shape (1M nodes/GPU)")
+    if args.dim == 256 and args.avg_deg == 16 and n_loc * world == 100_000:
+        return "C2"
+    return "custom"
 
 
 def load_traffic(args, n_loc, world):
@@ -189,23 +203,34 @@ def cpu_baseline(args, graph, X, Z, L, F):
     from oracle import c_oracle
 
     threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    rows = min(graph.num_rows, 100_000)
-    rowptr = graph.rowptr[: rows * L + 1].cpu().numpy()
-    colidx = graph.colidx[: int(rowptr[-1])].cpu().numpy()
+    # a contiguous row range from the middle of the graph holding ~3.2M edges
+    # (= 100k rows of C3; on R-MAT the bulk of rows, not the hub head)
+    node_ptr = graph.rowptr[::L].contiguous()
+    r0 = graph.num_rows // 2
+    target = torch.tensor([int(node_ptr[r0]) + 3_200_000], dtype=torch.int32, device=node_ptr.device)
+    r1 = max(r0 + 1, min(graph.num_rows, int(torch.searchsorted(node_ptr, target))))
+    rows = r1 - r0
+    e0 = int(node_ptr[r0])
+    rowptr = (graph.rowptr[r0 * L: r1 * L + 1] - e0).cpu().numpy()
+    colidx = graph.colidx[e0: e0 + int(rowptr[-1])].cpu().numpy()
     Xh = X.cpu().numpy()
     E = int(rowptr[-1])
+    d = None if args.p <= 0 else c_oracle.drop(args.p, 2, 0, True)  # the timed step's DropEdge stream
+    split = (graph.split_threshold, graph.split_chunk)  # the engine's chunked order on heavy rows
     t0 = time.perf_counter()
     passes = 0
     while True:
-        Zc = c_oracle.spmm_fwd(rowptr, colidx, Xh, L, True, nthreads=threads, self_base=graph.self_id_base)
+        Zc = c_oracle.spmm_fwd(rowptr, colidx, Xh, L, True, d=d, nthreads=threads, split=split,
+                               edge_base=graph.edge_id_base + e0, self_base=graph.self_id_base + r0,
+                               X_self=Xh[r0:])
         passes += 1
         if time.perf_counter() - t0 >= args.cpu_seconds:
             break
     dt = time.perf_counter() - t0
-    Zg = Z[:rows].cpu().numpy()
+    Zg = Z[r0:r1].cpu().numpy()
     diff = float(np.abs(Zg.astype(np.float64) - Zc).max())
     cpu = {"value": E * passes / dt, "unit": "edges/s", "cores": threads, "kind": "port",
-           "sample": f"first {rows} nodes ({E} typed edges) of the same graph and X, {passes} passes in {dt:.1f}s; "
+           "sample": f"nodes [{r0}, {r1}) ({E} typed edges) of the same graph and X, {passes} passes in {dt:.1f}s; "
                      f"oracle/grl_oracle.c OpenMP typed-CSR SpMM"}
     parity = {"rows_checked": rows, "max_abs_diff": diff, "bitwise_equal": bool(np.array_equal(Zg, Zc)),
               "tolerance": 1e-4}

@@ -193,6 +193,15 @@ __global__ __launch_bounds__(256) void synth_emit_kernel(SynthDev s, unsigned lo
   }
 }
 
+__global__ __launch_bounds__(256) void synth_degree_kernel(SynthDev s, int32_t* __restrict__ deg) {
+  for (int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; k < s.C; k += (int64_t)gridDim.x * blockDim.x) {
+    int64_t src, dst;
+    int t;
+    synth_edge(s, (uint64_t)k, src, dst, t);
+    if (src >= s.rb && src < s.re) atomicAdd(deg + (src - s.rb), 1);  // integer: order-independent
+  }
+}
+
 __global__ void synth_split_kernel(const uint64_t* __restrict__ ukeys, const int64_t* __restrict__ nnz_p, int64_t N,
                                    int32_t* __restrict__ colidx) {
   const int64_t nnz = *nnz_p;
@@ -360,6 +369,17 @@ extern "C" int grl_synth_count(const GrlSynthSpec* spec, int64_t* count, grl_str
                        reinterpret_cast<unsigned long long*>(count));
     GRL_LAUNCH_CHECK();
   }
+  return GRL_OK;
+}
+
+extern "C" int grl_synth_degrees(const GrlSynthSpec* spec, int32_t* deg, grl_stream_t stream) {
+  SynthDev s;
+  int rc = synth_validate(spec, s);
+  if (rc) return rc;
+  if (s.C == 0 || s.re == s.rb) return GRL_OK;
+  GRL_CHECK_ARG(deg != nullptr, "grl_synth_degrees: deg is NULL");
+  hipLaunchKernelGGL(synth_degree_kernel, dim3(grid_for(s.C, 256, 16384)), dim3(256), 0, as_stream(stream), s, deg);
+  GRL_LAUNCH_CHECK();
   return GRL_OK;
 }
 

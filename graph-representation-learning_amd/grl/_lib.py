@@ -125,6 +125,7 @@ SIGNATURES = {
     "grl_split_plan_build": (_c_i32, [_c_vp, _c_i64, _c_i32, _P(GrlSplitPlan), _c_vp, _c_size, _c_vp]),
     "grl_synth_count": (_c_i32, [_P(GrlSynthSpec), _c_vp, _c_vp]),
     "grl_synth_workspace_size": (_c_size, [_P(GrlSynthSpec), _c_i64]),
+    "grl_synth_degrees": (_c_i32, [_P(GrlSynthSpec), _c_vp, _c_vp]),
     "grl_synth_build": (_c_i32, [_P(GrlSynthSpec), _c_i64, _c_vp, _c_vp, _c_vp, _c_vp, _c_size, _c_vp]),
 }
 

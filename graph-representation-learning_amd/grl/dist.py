@@ -141,6 +141,21 @@ def halo_exchange_into(X_loc: torch.Tensor, X_ext: torch.Tensor, send_buf: torch
     dist.all_to_all_single(X_ext[plan.n_loc:], send_buf, plan.recv_counts, plan.send_counts, group=group)
 
 
+def edge_balanced_bounds(deg: torch.Tensor, world: int) -> List[int]:
+    """Node-range boundaries [b_0=0, ..., b_P=N] such that rank r's range
+    holds ~r/P of the edges (every rank computes the same bounds from the
+    same deterministic degree histogram, no communication)."""
+    cum = torch.cumsum(deg.to(torch.int64), 0)
+    total = int(cum[-1]) if cum.numel() else 0
+    targets = torch.tensor([total * r // world for r in range(1, world)], dtype=torch.int64, device=deg.device)
+    inner = (torch.searchsorted(cum, targets, right=False) + 1).cpu().tolist()
+    n = deg.numel()
+    bounds = [0] + [min(n, max(b, 0)) for b in inner] + [n]
+    for i in range(1, len(bounds)):  # monotone
+        bounds[i] = max(bounds[i], bounds[i - 1])
+    return bounds
+
+
 class ShardedGraph:
     """This rank's node-range shard of a global typed graph, ready to aggregate."""
 
@@ -155,10 +170,18 @@ class ShardedGraph:
 
     @classmethod
     def synthetic(cls, num_nodes: int, avg_deg: float, num_types: int = 6, *, kind: str = "er", seed: int = 0,
-                  device="cuda", group=None) -> "ShardedGraph":
+                  device="cuda", group=None, balance: Optional[str] = None) -> "ShardedGraph":
+        """balance "nodes": equal node ranges (ER); "edges": ranges holding
+        ~E/P candidate edges each (power-law graphs; default for R-MAT)."""
         world, rank = _world(group), _rank(group)
-        per = -(-num_nodes // world)
-        rb, re = min(num_nodes, rank * per), min(num_nodes, (rank + 1) * per)
+        balance = balance or ("edges" if kind == "rmat" else "nodes")
+        if balance == "edges" and world > 1:
+            deg = TypedGraph.synthetic_degrees(num_nodes, avg_deg, num_types, kind=kind, seed=seed, device=device)
+            bounds = edge_balanced_bounds(deg, world)
+        else:
+            per = -(-num_nodes // world)
+            bounds = [min(num_nodes, r * per) for r in range(world + 1)]
+        rb, re = bounds[rank], bounds[rank + 1]
         g = TypedGraph.synthetic(num_nodes, avg_deg, num_types, kind=kind, seed=seed, row_range=(rb, re),
                                  device=device)
         return cls(g.rowptr, g.colidx, num_types, rb, re, group=group)

@@ -292,6 +292,27 @@ class TypedGraph:
             vals = torch.as_tensor(vals, dtype=torch.float32).to(device)
         return cls(rp, ci, num_types, vals=vals, **kw)
 
+    @staticmethod
+    def _synth_spec(num_nodes, avg_deg, num_types, kind, seed, rb, re) -> GrlSynthSpec:
+        spec = GrlSynthSpec()
+        spec.kind = {"er": 0, "rmat": 1}[kind]
+        spec.num_types = num_types
+        spec.num_nodes = num_nodes
+        spec.num_candidates = int(round(num_nodes * avg_deg))
+        spec.seed = seed
+        spec.row_begin, spec.row_end = rb, re
+        return spec
+
+    @staticmethod
+    def synthetic_degrees(num_nodes: int, avg_deg: float, num_types: int = 6, *, kind: str = "er", seed: int = 0,
+                          device="cuda") -> torch.Tensor:
+        """Candidate out-degree of every node (before dedupe), int32 on device."""
+        dev = torch.device(device)
+        spec = TypedGraph._synth_spec(num_nodes, avg_deg, num_types, kind, seed, 0, num_nodes)
+        deg = torch.zeros(num_nodes, dtype=torch.int32, device=dev)
+        call("grl_synth_degrees", ctypes.byref(spec), deg.data_ptr(), current_stream_handle(dev))
+        return deg
+
     @classmethod
     def synthetic(cls, num_nodes: int, avg_deg: float, num_types: int = 6, *, kind: str = "er", seed: int = 0,
                   row_range: Optional[Tuple[int, int]] = None, device="cuda") -> "TypedGraph":
@@ -302,13 +323,7 @@ class TypedGraph:
         global node ids."""
         dev = torch.device(device)
         rb, re = (0, num_nodes) if row_range is None else row_range
-        spec = GrlSynthSpec()
-        spec.kind = {"er": 0, "rmat": 1}[kind]
-        spec.num_types = num_types
-        spec.num_nodes = num_nodes
-        spec.num_candidates = int(round(num_nodes * avg_deg))
-        spec.seed = seed
-        spec.row_begin, spec.row_end = rb, re
+        spec = cls._synth_spec(num_nodes, avg_deg, num_types, kind, seed, rb, re)
         stream = current_stream_handle(dev)
         cnt_t = torch.zeros(1, dtype=torch.int64, device=dev)
         call("grl_synth_count", ctypes.byref(spec), cnt_t.data_ptr(), stream)

@@ -253,6 +253,10 @@ typedef struct GrlSynthSpec {
 int grl_synth_count(const GrlSynthSpec* spec, int64_t* count /* device */,
                     grl_stream_t stream);
 size_t grl_synth_workspace_size(const GrlSynthSpec* spec, int64_t count);
+/* deg[v - row_begin] += candidates with src v, for v in [row_begin, row_end)
+ * (before dedupe; deg must be zeroed by the caller).  Used to choose
+ * edge-balanced node-range shard boundaries for power-law graphs. */
+int grl_synth_degrees(const GrlSynthSpec* spec, int32_t* deg, grl_stream_t stream);
 int grl_synth_build(const GrlSynthSpec* spec, int64_t count, int32_t* rowptr,
                     int32_t* colidx, int64_t* nnz /* device */,
                     void* workspace, size_t workspace_bytes,

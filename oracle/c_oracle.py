@@ -43,7 +43,7 @@ def lib():
         L.oracle_dropedge_mask.restype = None
         L.oracle_dropedge_mask.argtypes = [ctypes.POINTER(ODrop), _u64, _i64, _vp]
         L.oracle_spmm_fwd.restype = None
-        L.oracle_spmm_fwd.argtypes = [_i64, _i32, _i32, _vp, _vp, _vp, _u64, _u64, _vp, _i64, _i32, _vp,
+        L.oracle_spmm_fwd.argtypes = [_i64, _i32, _i32, _vp, _vp, _vp, _u64, _u64, _vp, _vp, _i64, _i32, _vp,
                                       ctypes.POINTER(ODrop), _i32, _i32, _i32]
         L.oracle_spmm_bwd.restype = None
         L.oracle_spmm_bwd.argtypes = [_i64, _i64, _i32, _i32, _vp, _vp, _vp, _vp, _u64, _u64, _vp, _i32, _vp, _i64,
@@ -79,9 +79,10 @@ def dropedge_mask(d: ODrop, id_base: int, count: int) -> np.ndarray:
 
 
 def spmm_fwd(rowptr, colidx, X, num_types, has_self=True, vals=None, d: ODrop | None = None, edge_base=0,
-             self_base=None, nthreads=0, split=None):
+             self_base=None, nthreads=0, split=None, X_self=None):
     """split = (threshold, chunk_edges) reproduces the engine's chunked
-    summation order for rows heavier than threshold (GrlSplitPlan)."""
+    summation order for rows heavier than threshold (GrlSplitPlan).
+    X_self: own-feature rows of the CSR rows when they are a sub-range of X."""
     rowptr = np.ascontiguousarray(rowptr, dtype=np.int32)
     colidx = np.ascontiguousarray(colidx, dtype=np.int32)
     X = np.ascontiguousarray(X, dtype=np.float32)
@@ -92,7 +93,11 @@ def spmm_fwd(rowptr, colidx, X, num_types, has_self=True, vals=None, d: ODrop | 
     if self_base is None:
         self_base = int(rowptr[-1])
     Z = np.empty((rows, (num_types + hs) * F), dtype=np.float32)
-    lib().oracle_spmm_fwd(rows, num_types, hs, _p(rowptr), _p(colidx), _p(vals), edge_base, self_base, _p(X), F, F,
+    if X_self is not None:
+        X_self = np.ascontiguousarray(X_self, dtype=np.float32)
+        assert X_self.shape[0] >= rows and X_self.shape[1] == F
+    lib().oracle_spmm_fwd(rows, num_types, hs, _p(rowptr), _p(colidx), _p(vals), edge_base, self_base, _p(X),
+                          _p(X_self), F, F,
                           _p(Z), ctypes.byref(d) if d is not None else None, nthreads,
                           *(split if split is not None else (-1, 1)))
     return Z

@@ -122,10 +122,13 @@ static void o_segment(float* acc, float* tmp, int heavy, int32_t chunk, int32_t 
   }
 }
 
+/* X: gathered rows (colidx indexes it); Xself: row n's own features
+ * (NULL = X, i.e. rows and sources share numbering). */
 void oracle_spmm_fwd(int64_t rows, int32_t S, int32_t hs, const int32_t* rowptr, const int32_t* colidx,
-                     const float* vals, uint64_t edge_base, uint64_t self_base, const float* X, int64_t ldx,
-                     int32_t F, float* Z, const ODrop* d, int32_t nthreads, int32_t split_threshold,
+                     const float* vals, uint64_t edge_base, uint64_t self_base, const float* X, const float* Xself,
+                     int64_t ldx, int32_t F, float* Z, const ODrop* d, int32_t nthreads, int32_t split_threshold,
                      int32_t split_chunk) {
+  if (!Xself) Xself = X;
   const int64_t ldz = (int64_t)(S + hs) * F;
 #ifdef _OPENMP
   if (nthreads > 0) omp_set_num_threads(nthreads);
@@ -141,7 +144,7 @@ void oracle_spmm_fwd(int64_t rows, int32_t S, int32_t hs, const int32_t* rowptr,
       if (hs) {
         float w = 1.0f;
         if (d && d->active && d->drop_self) w = o_weight(d, 1.0f, self_base + (uint64_t)n);
-        const float* xr = X + n * ldx;
+        const float* xr = Xself + n * ldx;
         for (int f = 0; f < F; ++f) zr[f] = w != 0.0f ? w * xr[f] : 0.0f;
       }
       const int heavy = split_threshold >= 0 && rowptr[(n + 1) * S] - rowptr[n * S] > split_threshold;

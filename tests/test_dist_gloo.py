@@ -96,3 +96,18 @@ def test_single_shard_plan_is_identity():
     assert plan.n_halo == 0 and torch.equal(plan.colidx_local, torch.from_numpy(colidx))
     X = torch.randn(50, 4)
     assert torch.equal(halo_exchange(X, plan), X)
+
+
+def test_edge_balanced_bounds():
+    from grl.dist import edge_balanced_bounds
+
+    src, _, _ = ohash.synth_edges(1, 6, 1 << 12, (1 << 12) * 20, 9)
+    deg = torch.from_numpy(np.bincount(src, minlength=1 << 12).astype(np.int32))
+    for world in (2, 4, 8):
+        b = edge_balanced_bounds(deg, world)
+        assert b[0] == 0 and b[-1] == deg.numel() and b == sorted(b)
+        loads = [int(deg[b[i]:b[i + 1]].sum()) for i in range(world)]
+        # every shard within one max-degree row of the ideal E/P
+        assert max(loads) - min(loads) <= 2 * int(deg.max()) + 1, loads
+    b = edge_balanced_bounds(torch.zeros(5, dtype=torch.int32), 3)  # degenerate: no edges at all
+    assert b[0] == 0 and b[-1] == 5 and b == sorted(b) and len(b) == 4

@@ -257,3 +257,10 @@ def test_split_plan_matches_definition():
     np.testing.assert_array_equal(sp["tensors"]["chunk_begin"].cpu().numpy()[:len(begins)], begins)
     np.testing.assert_array_equal(sp["tensors"]["chunk_end"].cpu().numpy()[:len(ends)], ends)
     np.testing.assert_array_equal(sp["tensors"]["heavy_cptr"].cpu().numpy()[:len(cptr)], cptr)
+
+
+@pytest.mark.parametrize("kind,N", [(0, 3000), (1, 1 << 12)])
+def test_synth_degrees_match_oracle(kind, N):
+    deg = TypedGraph.synthetic_degrees(N, 11.0, 6, kind=["er", "rmat"][kind], seed=5, device=DEV).cpu().numpy()
+    src, _, _ = ohash.synth_edges(kind, 6, N, int(round(N * 11.0)), 5)
+    np.testing.assert_array_equal(deg, np.bincount(src, minlength=N))
