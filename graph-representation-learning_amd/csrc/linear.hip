@@ -1,15 +1,22 @@
-// fp32 post-aggregation linear on the gfx950 matrix cores.
+// fp32 GEMMs of the GraphConv linear on the gfx950 matrix cores.
 //
-// Replaces  V_out = torch.matmul(new_V, self.h_weights) + self.bias
-// (gnn/models/networks/robust_gcn.py:50) and optionally the F.relu applied
-// to the layer output (gnn/models/networks/drop_robust_gcn.py:76,80,85).
+// Forward:  V_out = new_V @ h_weights + bias   (gnn/models/networks/robust_gcn.py:50)
+//           [+ F.relu]                          (drop_robust_gcn.py:76,80,85)
+// Backward (autograd MmBackward0 of robust_gcn.py:50, ReLU mask fused):
+//           dZ = (g * [out > 0]) @ h_weights^T
+//           dW = new_V^T @ (g * [out > 0]),  db = sum_rows(g * [out > 0])
 //
-// v_mfma_f32_32x32x2_f32: exact f32 products (one rounding per fmaf), the
-// only MFMA use in the engine.  Block tile 128 x 128, K staged 32 deep
-// through LDS; 4 waves, each owning a 64 x 64 sub-tile (2 x 2 MFMA tiles,
-// 64 accumulator registers).  Inside a K-step of 8 the two half-waves take
-// k = 4h + s (s = 0..3) so every operand fragment is one ds_read_b128; the
-// sum over k is the same set of products in a different order.
+// One templated kernel, v_mfma_f32_32x32x2_f32 (exact f32 products, one
+// rounding per fmaf): block tile 128 x 128, K staged 32 deep through LDS in
+// the operand's natural global layout (every global load and LDS store is a
+// float4; no transposing stores).  An operand whose K index is contiguous is
+// read as one ds_read_b128 fragment per k-step of 8 (the two half-waves take
+// k = 4h + s); one whose M/N index is contiguous as four ds_read_b32 (lanes on
+// consecutive addresses, conflict-free).  The next K tile is loaded into
+// registers while the current one is multiplied.  4 waves, each a 64 x 64
+// sub-tile = 2 x 2 MFMA tiles = 64 accumulator registers.  Long reductions
+// (dW sums over all N nodes) split K over blockIdx.z into fp32 slabs that a
+// second pass adds in split order: deterministic, no atomics.
 #include "grl_internal.h"
 
 namespace grl {
@@ -17,24 +24,135 @@ namespace {
 
 using f32x16 = __attribute__((ext_vector_type(16))) float;
 
-constexpr int BM = 128, BN = 128, BK = 32;
-constexpr int LDA = BK + 4;  // 144 B row stride: conflict-free ds_read_b128
-constexpr int LDB = BK + 4;
+constexpr int BM = 128, BN = 128;
 
-template <bool ALIGNED>
-__global__ __launch_bounds__(256) void linear_kernel(const float* __restrict__ Z, int64_t ldz,
-                                                     const float* __restrict__ W, const float* __restrict__ bias,
-                                                     float* __restrict__ out, int64_t M, int K, int C, int relu) {
-  __shared__ __attribute__((aligned(16))) float As[BM * LDA];
-  __shared__ __attribute__((aligned(16))) float Bs[BN * LDB];  // transposed: Bs[n][k]
+enum Epilogue { EPI_STORE = 0, EPI_BIAS = 1, EPI_SLAB = 2 };
+
+struct GemmArgs {
+  const float* A;
+  int64_t lda;
+  const float* Amask;  // optional: A element multiplied by [Amask > 0] (same indexing as A)
+  const float* B;
+  int64_t ldb;
+  const float* Bmask;  // optional, same indexing as B
+  float* C;
+  int64_t ldc;
+  const float* bias;
+  int64_t M, N, K;
+  int64_t k_per_split;
+  int relu;
+};
+
+__device__ __forceinline__ float4 masked(float4 v, float4 mk) {
+  v.x = mk.x > 0.f ? v.x : 0.f;
+  v.y = mk.y > 0.f ? v.y : 0.f;
+  v.z = mk.z > 0.f ? v.z : 0.f;
+  v.w = mk.w > 0.f ? v.w : 0.f;
+  return v;
+}
+
+// One operand tile (ROWS x BK) staged as 1024*BK/32 float4 slots, SLOTS per
+// thread.  KC: image [row][k] (k contiguous, stride LDK); RC: image [k][row]
+// (row contiguous, stride LDR).  Global addresses are per-thread pointers
+// advanced by one K tile per step; interior tiles load with no per-element
+// branches (clamped + selected loads only on edge tiles).
+template <bool KC, bool ALIGNED, bool MASK, int BK>
+struct Operand {
+  static constexpr int LDK = BK + 4;
+  static constexpr int LDR = BM + 4;
+  static constexpr int SLOTS = BK / 8;  // (128 * BK / 4) / 256
+  const float* base;
+  const float* mask;
+  int64_t ld, rows_total, row0;
+  int64_t kstep;  // element stride per unit of k
+  float4 reg[SLOTS];
+
+  __device__ __forceinline__ void slot(int idx, int64_t& row, int& kin) const {
+    if (KC) {
+      row = row0 + idx / (BK / 4);
+      kin = (idx % (BK / 4)) * 4;
+    } else {
+      row = row0 + (idx % 32) * 4;
+      kin = idx / 32;
+    }
+  }
+  __device__ __forceinline__ int lds_off(int idx) const {
+    return KC ? (idx / (BK / 4)) * LDK + (idx % (BK / 4)) * 4 : (idx / 32) * LDR + (idx % 32) * 4;
+  }
+  __device__ __forceinline__ void fetch(int tid, int64_t k0, int64_t kend, bool interior) {
+#pragma unroll
+    for (int it = 0; it < SLOTS; ++it) {
+      int64_t row;
+      int kin;
+      slot(tid + it * 256, row, kin);
+      const int64_t k = k0 + kin;
+      if (interior) {
+        const int64_t off = KC ? row * ld + k : k * ld + row;
+        float4 v = *reinterpret_cast<const float4*>(base + off);
+        if (MASK) v = masked(v, *reinterpret_cast<const float4*>(mask + off));
+        reg[it] = v;
+      } else {
+        float t[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int64_t r = KC ? row : row + e;
+          const int64_t kk = KC ? k + e : k;
+          const bool ok = r < rows_total && kk < kend;
+          const int64_t off = ok ? (KC ? r * ld + kk : kk * ld + r) : 0;
+          float x = base[off];
+          if (MASK) x = mask[off] > 0.f ? x : 0.f;
+          t[e] = ok ? x : 0.f;
+        }
+        reg[it] = make_float4(t[0], t[1], t[2], t[3]);
+      }
+    }
+  }
+  __device__ __forceinline__ void stash(float* lds, int tid) const {
+#pragma unroll
+    for (int it = 0; it < SLOTS; ++it) *reinterpret_cast<float4*>(&lds[lds_off(tid + it * 256)]) = reg[it];
+  }
+  // fragment of row `row` (0..127 within the tile) for k = kk + 4h + s, s = 0..3
+  __device__ __forceinline__ static float4 frag(const float* lds, int row, int kk, int h) {
+    if (KC) return *reinterpret_cast<const float4*>(&lds[row * LDK + kk + 4 * h]);
+    const float* c = &lds[(kk + 4 * h) * LDR + row];
+    return make_float4(c[0], c[LDR], c[2 * LDR], c[3 * LDR]);
+  }
+  static constexpr int lds_floats() { return KC ? BM * LDK : BK * LDR; }
+};
+
+// A(m, k): A_KC ? A[m*lda + k] : A[k*lda + m]
+// B(k, n): B_KC ? B[n*ldb + k] : B[k*ldb + n]
+template <bool A_KC, bool B_KC, int EPI, bool ALIGNED, bool MASK_A, bool MASK_B, int BK>
+__global__ __launch_bounds__(256) void gemm_kernel(GemmArgs p) {
+  using OA = Operand<A_KC, ALIGNED, MASK_A, BK>;
+  using OB = Operand<B_KC, ALIGNED, MASK_B, BK>;
+  __shared__ __attribute__((aligned(16))) float smem[OA::lds_floats() + OB::lds_floats()];
+  float* As = smem;
+  float* Bs = smem + OA::lds_floats();
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int64_t m0 = (int64_t)blockIdx.x * BM;
-  const int n0 = blockIdx.y * BN;
   const int l32 = lane & 31, h = lane >> 5;
+  const int64_t m0 = (int64_t)blockIdx.x * BM;
+  const int64_t n0 = (int64_t)blockIdx.y * BN;
+  const int64_t kbeg = (int64_t)blockIdx.z * p.k_per_split;
+  const int64_t kend = min(p.K, kbeg + p.k_per_split);
+
+  OA oa;
+  oa.base = p.A;
+  oa.mask = p.Amask;
+  oa.ld = p.lda;
+  oa.rows_total = p.M;
+  oa.row0 = m0;
+  OB ob;
+  ob.base = p.B;
+  ob.mask = p.Bmask;
+  ob.ld = p.ldb;
+  ob.rows_total = p.N;
+  ob.row0 = n0;
+  const bool rows_in = ALIGNED && (m0 + BM <= p.M) && (n0 + BN <= p.N);
 
   f32x16 acc[2][2];
 #pragma unroll
@@ -44,63 +162,28 @@ __global__ __launch_bounds__(256) void linear_kernel(const float* __restrict__ Z
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
 
-  for (int k0 = 0; k0 < K; k0 += BK) {
-    // ---- stage A tile: BM x BK (rows of Z) --------------------------------
-#pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      const int idx = tid + it * 256;  // 1024 float4 slots
-      const int r = idx >> 3, c4 = (idx & 7) * 4;
-      const int64_t gm = m0 + r;
-      const int gk = k0 + c4;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (gm < M) {
-        const float* p = Z + gm * ldz + gk;
-        if (ALIGNED) {
-          if (gk < K) v = *reinterpret_cast<const float4*>(p);
-        } else {
-          if (gk + 0 < K) v.x = p[0];
-          if (gk + 1 < K) v.y = p[1];
-          if (gk + 2 < K) v.z = p[2];
-          if (gk + 3 < K) v.w = p[3];
-        }
-      }
-      *reinterpret_cast<float4*>(&As[r * LDA + c4]) = v;
-    }
-    // ---- stage B tile: BK x BN of W, stored transposed ---------------------
-#pragma unroll
-    for (int it = 0; it < 4; ++it) {
-      const int idx = tid + it * 256;
-      const int kr = idx >> 5, c4 = (idx & 31) * 4;
-      const int gk = k0 + kr;
-      const int gn = n0 + c4;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (gk < K) {
-        const float* p = W + (int64_t)gk * C + gn;
-        if (ALIGNED) {
-          if (gn < C) v = *reinterpret_cast<const float4*>(p);
-        } else {
-          if (gn + 0 < C) v.x = p[0];
-          if (gn + 1 < C) v.y = p[1];
-          if (gn + 2 < C) v.z = p[2];
-          if (gn + 3 < C) v.w = p[3];
-        }
-      }
-      Bs[(c4 + 0) * LDB + kr] = v.x;
-      Bs[(c4 + 1) * LDB + kr] = v.y;
-      Bs[(c4 + 2) * LDB + kr] = v.z;
-      Bs[(c4 + 3) * LDB + kr] = v.w;
-    }
+  if (kbeg < kend) {
+    const bool in0 = rows_in && kbeg + BK <= kend;
+    oa.fetch(tid, kbeg, kend, in0);
+    ob.fetch(tid, kbeg, kend, in0);
+  }
+  for (int64_t k0 = kbeg; k0 < kend; k0 += BK) {
+    oa.stash(As, tid);
+    ob.stash(Bs, tid);
     __syncthreads();
-
+    const int64_t kn = k0 + BK;
+    if (kn < kend) {  // next tile in flight during the MFMAs
+      const bool in = rows_in && kn + BK <= kend;
+      oa.fetch(tid, kn, kend, in);
+      ob.fetch(tid, kn, kend, in);
+    }
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 8) {
       float4 a[2], b[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
-        a[i] = *reinterpret_cast<const float4*>(&As[(wm * 64 + i * 32 + l32) * LDA + kk + 4 * h]);
+      for (int i = 0; i < 2; ++i) a[i] = OA::frag(As, wm * 64 + i * 32 + l32, kk, h);
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
-        b[j] = *reinterpret_cast<const float4*>(&Bs[(wn * 64 + j * 32 + l32) * LDB + kk + 4 * h]);
+      for (int j = 0; j < 2; ++j) b[j] = OB::frag(Bs, wn * 64 + j * 32 + l32, kk, h);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -114,25 +197,85 @@ __global__ __launch_bounds__(256) void linear_kernel(const float* __restrict__ Z
     __syncthreads();
   }
 
-  // ---- epilogue: bias (+ReLU), C/D map col = lane&31, row = (r&3)+8(r>>2)+4h
+  // ---- epilogue: C/D map col = lane&31, row = (r&3) + 8(r>>2) + 4h --------
+  float* Cz = p.C + (EPI == EPI_SLAB ? (int64_t)blockIdx.z * p.M * p.ldc : 0);
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
-    const int gn = n0 + wn * 64 + j * 32 + l32;
-    if (gn >= C) continue;
-    const float bv = bias ? bias[gn] : 0.0f;
+    const int64_t gn = n0 + wn * 64 + j * 32 + l32;
+    if (gn >= p.N) continue;
+    const float bv = (EPI == EPI_BIAS && p.bias) ? p.bias[gn] : 0.0f;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int64_t gm = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (gm < M) {
+        if (gm < p.M) {
           float v = acc[i][j][r] + bv;
-          if (relu) v = v > 0.0f ? v : 0.0f;
-          out[gm * C + gn] = v;
+          if (EPI == EPI_BIAS && p.relu) v = v > 0.0f ? v : 0.0f;
+          Cz[gm * p.ldc + gn] = v;
         }
       }
     }
   }
+}
+
+// out[i] = sum_{z < splits} slab[z][i]  (split order: deterministic)
+__global__ void slab_reduce_kernel(const float* __restrict__ slab, int64_t n, int splits, float* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.0f;
+    for (int z = 0; z < splits; ++z) s += slab[(int64_t)z * n + i];
+    out[i] = s;
+  }
+}
+
+// partial[z][c] = sum over rows [z*rows_per, ...) of g[r][c] * [mask[r][c] > 0]
+__global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __restrict__ g, const float* __restrict__ mask,
+                                                              int64_t M, int64_t C, int64_t rows_per,
+                                                              float* __restrict__ partial) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t z = blockIdx.y;
+  if (c >= C) return;
+  const int64_t r0 = z * rows_per, r1 = min(M, r0 + rows_per);
+  float s = 0.0f;
+  for (int64_t r = r0; r < r1; ++r) {
+    const float x = g[r * C + c];
+    s += (!mask || mask[r * C + c] > 0.0f) ? x : 0.0f;
+  }
+  partial[z * C + c] = s;
+}
+
+bool al16(const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; }
+
+#ifndef GRL_GEMM_BK
+#define GRL_GEMM_BK 32
+#endif
+constexpr int GEMM_BK = GRL_GEMM_BK;
+
+template <bool A_KC, bool B_KC, int EPI>
+int launch_gemm(const GemmArgs& a, int splits, bool aligned, hipStream_t st) {
+  if (a.M == 0 || a.N == 0) return GRL_OK;
+  GRL_CHECK_ARG(ceil_div(a.M, BM) < 2147483647LL && ceil_div(a.N, BN) < 65536 && splits < 65536,
+                "gemm: grid too large");
+  const dim3 grid((unsigned)ceil_div(a.M, BM), (unsigned)ceil_div(a.N, BN), (unsigned)splits);
+  const bool ma = a.Amask != nullptr, mb = a.Bmask != nullptr;
+#define GRL_GEMM(AL, MA, MB) \
+  hipLaunchKernelGGL((gemm_kernel<A_KC, B_KC, EPI, AL, MA, MB, GEMM_BK>), grid, dim3(256), 0, st, a)
+  if (aligned) {
+    if (ma) GRL_GEMM(true, true, false); else if (mb) GRL_GEMM(true, false, true); else GRL_GEMM(true, false, false);
+  } else {
+    if (ma) GRL_GEMM(false, true, false); else if (mb) GRL_GEMM(false, false, true); else GRL_GEMM(false, false, false);
+  }
+#undef GRL_GEMM
+  GRL_LAUNCH_CHECK();
+  return GRL_OK;
+}
+
+int pick_splits(int64_t M, int64_t N, int64_t K) {
+  const int64_t tiles = ceil_div(M, BM) * ceil_div(N, BN);
+  const int64_t want = (int64_t)device_cu_count() * 4;  // ~4 blocks per CU
+  int64_t s = std::max<int64_t>(1, want / std::max<int64_t>(tiles, 1));
+  s = std::min<int64_t>(s, ceil_div(K, 4 * GEMM_BK));  // each split keeps >= 4 K tiles
+  return (int)std::max<int64_t>(1, std::min<int64_t>(s, 256));
 }
 
 }  // namespace
@@ -146,16 +289,94 @@ extern "C" int grl_linear_fwd(const float* Z, int64_t ldz, const float* W, const
   GRL_CHECK_ARG(ldz >= K, "grl_linear_fwd: ldz (%lld) < K (%d)", (long long)ldz, K);
   if (M == 0 || C == 0) return GRL_OK;
   GRL_CHECK_ARG(Z && W && out, "grl_linear_fwd: NULL pointer");
-  GRL_CHECK_ARG(ceil_div(M, BM) < 2147483647LL && ceil_div(C, BN) < 65536, "grl_linear_fwd: grid too large");
-  const bool aligned = (reinterpret_cast<uintptr_t>(Z) % 16 == 0) && (reinterpret_cast<uintptr_t>(W) % 16 == 0) &&
-                       (ldz % 4 == 0) && (K % 4 == 0) && (C % 4 == 0);
-  const dim3 grid((unsigned)ceil_div(M, BM), (unsigned)ceil_div(C, BN));
-  if (aligned)
-    hipLaunchKernelGGL(linear_kernel<true>, grid, dim3(256), 0, as_stream(stream), Z, ldz, W, bias, out, M, K, C,
-                       relu);
-  else
-    hipLaunchKernelGGL(linear_kernel<false>, grid, dim3(256), 0, as_stream(stream), Z, ldz, W, bias, out, M, K, C,
-                       relu);
-  GRL_LAUNCH_CHECK();
+  GemmArgs a{};
+  a.A = Z;
+  a.lda = ldz;
+  a.B = W;
+  a.ldb = C;
+  a.C = out;
+  a.ldc = C;
+  a.bias = bias;
+  a.M = M;
+  a.N = C;
+  a.K = K;
+  a.k_per_split = std::max<int64_t>(K, 1);
+  a.relu = relu;
+  const bool aligned = al16(Z) && al16(W) && ldz % 4 == 0 && C % 4 == 0 && K % 4 == 0;
+  return launch_gemm<true, false, EPI_BIAS>(a, 1, aligned, as_stream(stream));
+}
+
+extern "C" int grl_linear_bwd_data(const float* g, const float* relu_out, const float* W, float* dZ, int64_t lddz,
+                                   int64_t M, int32_t K, int32_t C, grl_stream_t stream) {
+  GRL_CHECK_ARG(M >= 0 && K >= 0 && C >= 0 && lddz >= K, "grl_linear_bwd_data: bad sizes");
+  if (M == 0 || K == 0) return GRL_OK;
+  GRL_CHECK_ARG(g && W && dZ, "grl_linear_bwd_data: NULL pointer");
+  GemmArgs a{};
+  a.A = g;  // (M x C), k index = c contiguous
+  a.lda = C;
+  a.Amask = relu_out;
+  a.B = W;  // B(k=c, n=kk) = W[kk][c]: K-contiguous rows of W
+  a.ldb = C;
+  a.C = dZ;
+  a.ldc = lddz;
+  a.M = M;
+  a.N = K;
+  a.K = C;
+  a.k_per_split = std::max<int64_t>(C, 1);
+  const bool aligned = al16(g) && al16(W) && (!relu_out || al16(relu_out)) && C % 4 == 0;
+  return launch_gemm<true, true, EPI_STORE>(a, 1, aligned, as_stream(stream));
+}
+
+extern "C" size_t grl_linear_bwd_weight_workspace_size(int64_t M, int32_t K, int32_t C) {
+  const int s = pick_splits(K, C, M);
+  const int zs = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(M, 4096), 1024));
+  return (size_t)s * (size_t)K * (size_t)C * 4 + (size_t)zs * (size_t)C * 4 + 512;
+}
+
+extern "C" int grl_linear_bwd_weight(const float* Z, int64_t ldz, const float* g, const float* relu_out, float* dW,
+                                     float* db, int64_t M, int32_t K, int32_t C, void* workspace,
+                                     size_t workspace_bytes, grl_stream_t stream) {
+  GRL_CHECK_ARG(M >= 0 && K >= 0 && C >= 0 && ldz >= K, "grl_linear_bwd_weight: bad sizes");
+  if (K == 0 || C == 0) return GRL_OK;
+  GRL_CHECK_ARG(Z && g && dW, "grl_linear_bwd_weight: NULL pointer");
+  const size_t need = grl_linear_bwd_weight_workspace_size(M, K, C);
+  if (!workspace || workspace_bytes < need)
+    GRL_FAIL(GRL_E_WORKSPACE, "grl_linear_bwd_weight: workspace %zu < %zu", workspace_bytes, need);
+  hipStream_t st = as_stream(stream);
+  const int splits = pick_splits(K, C, M);
+  float* slab = static_cast<float*>(workspace);
+  GemmArgs a{};
+  a.A = Z;  // A(m=kk, k=row) = Z[row][kk]: rows of Z are M-contiguous for fixed k
+  a.lda = ldz;
+  a.B = g;  // B(k=row, n=c) = g[row][c]
+  a.ldb = C;
+  a.Bmask = relu_out;
+  a.C = splits > 1 ? slab : dW;
+  a.ldc = C;
+  a.M = K;
+  a.N = C;
+  a.K = M;
+  a.k_per_split = ceil_div(ceil_div(M, splits), GEMM_BK) * GEMM_BK;
+  const bool aligned = al16(Z) && al16(g) && (!relu_out || al16(relu_out)) && ldz % 4 == 0 && C % 4 == 0 && K % 4 == 0;
+  int rc = splits > 1 ? launch_gemm<false, false, EPI_SLAB>(a, splits, aligned, st)
+                      : launch_gemm<false, false, EPI_STORE>(a, 1, aligned, st);
+  if (rc) return rc;
+  if (splits > 1) {
+    const int64_t n = (int64_t)K * C;
+    hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(n, 256), 65536)), dim3(256), 0,
+                       st, slab, n, splits, dW);
+    GRL_LAUNCH_CHECK();
+  }
+  if (db) {
+    const int zs = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(M, 4096), 1024));
+    float* part = slab + (size_t)splits * K * C;
+    const int64_t rows_per = ceil_div(std::max<int64_t>(M, 1), zs);
+    hipLaunchKernelGGL(colsum_partial_kernel, dim3((unsigned)ceil_div(C, 256), (unsigned)zs), dim3(256), 0, st, g,
+                       relu_out, M, C, rows_per, part);
+    GRL_LAUNCH_CHECK();
+    hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)ceil_div(C, 256)), dim3(256), 0, st, part, (int64_t)C, zs,
+                       db);
+    GRL_LAUNCH_CHECK();
+  }
   return GRL_OK;
 }

@@ -86,7 +86,33 @@ def linear_fwd(Z2: torch.Tensor, W: torch.Tensor, b, relu: bool) -> torch.Tensor
     return out
 
 
+def linear_bwd_data(g: torch.Tensor, relu_out, W: torch.Tensor) -> torch.Tensor:
+    M, C = g.shape
+    K = W.shape[0]
+    dZ = torch.empty(M, K, dtype=torch.float32, device=g.device)
+    call("grl_linear_bwd_data", g.data_ptr(), relu_out.data_ptr() if relu_out is not None else None, W.data_ptr(),
+         dZ.data_ptr(), K, M, K, C, current_stream_handle(g.device))
+    return dZ
+
+
+def linear_bwd_weight(Z2: torch.Tensor, g: torch.Tensor, relu_out, want_db: bool):
+    M, K = Z2.shape
+    C = g.shape[1]
+    dW = torch.empty(K, C, dtype=torch.float32, device=g.device)
+    db = torch.empty(C, dtype=torch.float32, device=g.device) if want_db else None
+    ws_bytes = _lib.lib().grl_linear_bwd_weight_workspace_size(M, K, C)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=g.device)
+    call("grl_linear_bwd_weight", Z2.data_ptr(), Z2.stride(0), g.data_ptr(),
+         relu_out.data_ptr() if relu_out is not None else None, dW.data_ptr(),
+         db.data_ptr() if db is not None else None, M, K, C, ws.data_ptr(), ws_bytes,
+         current_stream_handle(g.device))
+    return dW, db
+
+
 class _GraphLinear(torch.autograd.Function):
+    """out = Z W + b [ReLU]; backward on the same MFMA GEMM kernel with the
+    ReLU mask fused into the operand loads (no g*mask temporary)."""
+
     @staticmethod
     def forward(ctx, Z: torch.Tensor, W: torch.Tensor, b, relu: bool):
         Z2 = _rows_view(Z)
@@ -100,16 +126,15 @@ class _GraphLinear(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g: torch.Tensor):
         Z2, W, out = ctx.saved_tensors
-        g = g.contiguous()
-        if ctx.relu:
-            g = g * (out > 0).to(g.dtype)
+        g = g.contiguous().float()
+        mask = out if ctx.relu else None
         dZ = dW = db = None
         if ctx.needs_input_grad[0]:
-            dZ = g @ W.t()
-        if ctx.needs_input_grad[1]:
-            dW = Z2.t() @ g
-        if ctx.has_b and ctx.needs_input_grad[2]:
-            db = g.sum(0)
+            dZ = linear_bwd_data(g, mask, W)
+        if ctx.needs_input_grad[1] or (ctx.has_b and ctx.needs_input_grad[2]):
+            dW, db = linear_bwd_weight(Z2, g, mask, ctx.has_b and ctx.needs_input_grad[2])
+            if not ctx.needs_input_grad[1]:
+                dW = None
         return dZ, dW, db, None
 
 

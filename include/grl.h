@@ -182,6 +182,23 @@ int grl_linear_fwd(const float* Z, int64_t ldz, const float* W,
                    const float* bias, float* out, int64_t M, int32_t K,
                    int32_t C, int32_t relu, grl_stream_t stream);
 
+/* Backward of grl_linear_fwd (autograd MmBackward0 of robust_gcn.py:50, with
+ * the ReLU of drop_robust_gcn.py:76 folded in when relu_out != NULL):
+ *   dZ = (g * [relu_out > 0]) W^T           grl_linear_bwd_data,  dZ [M, K] (ld lddz)
+ *   dW = Z^T (g * [relu_out > 0])           grl_linear_bwd_weight, dW [K, C]
+ *   db = sum over rows of (g * [relu_out > 0])                     db [C] (or NULL)
+ * g, relu_out: [M, C] contiguous (relu_out = the forward's ReLU output).
+ * dW's reduction over M is split over workgroups into fp32 slabs (workspace)
+ * added in split order: deterministic, no atomics.                          */
+int grl_linear_bwd_data(const float* g, const float* relu_out, const float* W,
+                        float* dZ, int64_t lddz, int64_t M, int32_t K, int32_t C,
+                        grl_stream_t stream);
+size_t grl_linear_bwd_weight_workspace_size(int64_t M, int32_t K, int32_t C);
+int grl_linear_bwd_weight(const float* Z, int64_t ldz, const float* g,
+                          const float* relu_out, float* dW, float* db, int64_t M,
+                          int32_t K, int32_t C, void* workspace,
+                          size_t workspace_bytes, grl_stream_t stream);
+
 /* ---------------------------------------------------------------------- */
 /* Graph formats                                                           */
 /* ---------------------------------------------------------------------- */

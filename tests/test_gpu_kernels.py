@@ -264,3 +264,37 @@ def test_synth_degrees_match_oracle(kind, N):
     deg = TypedGraph.synthetic_degrees(N, 11.0, 6, kind=["er", "rmat"][kind], seed=5, device=DEV).cpu().numpy()
     src, _, _ = ohash.synth_edges(kind, 6, N, int(round(N * 11.0)), 5)
     np.testing.assert_array_equal(deg, np.bincount(src, minlength=N))
+
+
+@pytest.mark.parametrize("M,K,C", [(1, 8, 4), (74, 1792, 256), (3000, 3584, 256), (129, 10, 5), (517, 36, 200),
+                                   (70000, 1792, 128)])
+@pytest.mark.parametrize("relu", [False, True])
+def test_linear_backward_matches_fp64(M, K, C, relu):
+    from grl.ops import linear_bwd_data, linear_bwd_weight
+
+    rng = np.random.default_rng(M + K + C)
+    Z = rng.standard_normal((M, K)).astype(np.float32)
+    W = (rng.standard_normal((K, C)) / np.sqrt(K)).astype(np.float32)
+    g = rng.standard_normal((M, C)).astype(np.float32)
+    out = rng.standard_normal((M, C)).astype(np.float32) if relu else None
+    gm = g.astype(np.float64) * ((out > 0) if relu else 1.0)
+    dZ = linear_bwd_data(to_dev(g), to_dev(out) if relu else None, to_dev(W)).cpu().numpy()
+    ref = gm @ W.T.astype(np.float64)
+    scale = np.abs(gm) @ np.abs(W.T).astype(np.float64) + 1.0
+    assert np.all(np.abs(dZ - ref) <= 1e-5 * scale)
+    dW, db = linear_bwd_weight(to_dev(Z), to_dev(g), to_dev(out) if relu else None, True)
+    refW = Z.T.astype(np.float64) @ gm
+    scaleW = np.abs(Z.T).astype(np.float64) @ np.abs(gm) + 1.0
+    assert np.all(np.abs(dW.cpu().numpy() - refW) <= 1e-5 * scaleW)
+    np.testing.assert_allclose(db.cpu().numpy(), gm.sum(0), rtol=1e-5, atol=1e-4 * np.sqrt(M))
+
+
+def test_linear_backward_deterministic():
+    from grl.ops import linear_bwd_weight
+
+    rng = np.random.default_rng(0)
+    Z = to_dev(rng.standard_normal((50000, 1792)).astype(np.float32))
+    g = to_dev(rng.standard_normal((50000, 256)).astype(np.float32))
+    a = linear_bwd_weight(Z, g, g, True)
+    b = linear_bwd_weight(Z, g, g, True)
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1])
