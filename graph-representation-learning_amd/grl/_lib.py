@@ -105,6 +105,17 @@ class GrlSynthSpec(ctypes.Structure):
     ]
 
 
+class GrlLayoutItem(ctypes.Structure):
+    _fields_ = [
+        ("x1", ctypes.c_double),
+        ("y1", ctypes.c_double),
+        ("x2", ctypes.c_double),
+        ("y2", ctypes.c_double),
+        ("kind", _c_i32),
+        ("has_text", _c_i32),
+    ]
+
+
 _P = ctypes.POINTER
 # name -> (restype, argtypes); mirrors include/grl.h one for one.
 SIGNATURES = {
@@ -127,6 +138,9 @@ SIGNATURES = {
     "grl_split_plan_workspace_size": (_c_size, [_c_i64]),
     "grl_split_plan_count": (_c_i32, [_c_vp, _c_i64, _c_i32, _c_i32, _c_i32, _c_vp, _c_vp, _c_size, _c_vp]),
     "grl_split_plan_build": (_c_i32, [_c_vp, _c_i64, _c_i32, _P(GrlSplitPlan), _c_vp, _c_size, _c_vp]),
+    "grl_layout_graph_size": (_c_i32, [_c_vp, _c_i32, _c_vp]),
+    "grl_layout_graph_dense": (_c_i32, [_c_vp, _c_i32, _c_i32, _c_i32, _c_vp]),
+    "grl_layout_graph_edges": (_c_i32, [_c_vp, _c_i32, _c_i32, _c_vp, _c_i64, _c_vp]),
     "grl_synth_count": (_c_i32, [_P(GrlSynthSpec), _c_vp, _c_vp]),
     "grl_synth_workspace_size": (_c_size, [_P(GrlSynthSpec), _c_i64]),
     "grl_synth_degrees": (_c_i32, [_P(GrlSynthSpec), _c_vp, _c_vp]),

@@ -248,6 +248,35 @@ int grl_csr_to_csc(const GrlTypedCsr* g, int64_t num_cols, int32_t* colptr,
                    void* workspace, size_t workspace_bytes,
                    grl_stream_t stream);
 
+/* Heuristic spatial graph of one document (host-only, no device work).
+ * Replaces Graph(...) and Graph._get_adj_matrix
+ * (gnn/data_generator/data_process/utils/graph_utils.py:425-834) as called by
+ * HeuristicGraphBuilder.process (heuristic_graph_builder.py:56-83).
+ * Items are the sample's text lines in label-index order with their axis-
+ * aligned boxes (min/max of the polygon); kind 0 = text line, 1 = "cell",
+ * 2 = "table" (dropped, as in the reference).  Edge types are
+ * lr, rl, tb, bt, child, parent (graph_utils.py:434).
+ *   grl_layout_graph_size  -> *out_n = min(#items, #graph nodes), the side of
+ *                             the adjacency the reference keeps
+ *   grl_layout_graph_dense -> (out_n, 6, out_n) adjacency as IEEE fp16 bits
+ *                             (the reference's float16 array); edge_type
+ *                             0 = normal_binary, 1 = fc_similarity, 2 = fc_binary
+ *   grl_layout_graph_edges -> the normal_binary edges as sorted unique
+ *                             (src, type, dst) int32 triples: typed CSR input
+ *                             without the dense O(N^2) matrix.  *count is the
+ *                             number of edges; nothing is written if it
+ *                             exceeds `capacity` (call again with room).   */
+typedef struct GrlLayoutItem {
+  double x1, y1, x2, y2; /* box: min/max of the polygon's x and y            */
+  int32_t kind;          /* 0 text line, 1 cell, 2 table                      */
+  int32_t has_text;      /* str(text) != ""                                  */
+} GrlLayoutItem;
+int grl_layout_graph_size(const GrlLayoutItem* items, int32_t n, int32_t* out_n);
+int grl_layout_graph_dense(const GrlLayoutItem* items, int32_t n, int32_t edge_type,
+                           int32_t out_n, uint16_t* adj_half);
+int grl_layout_graph_edges(const GrlLayoutItem* items, int32_t n, int32_t out_n,
+                           int32_t* edges, int64_t capacity, int64_t* count);
+
 /* Synthetic graphs for the benchmark configs.
  * Candidate edge k in [0, num_candidates) is (src, type, dst) drawn from a
  * counter-based hash of (seed, k): Erdos-Renyi (kind 0: src, dst uniform in

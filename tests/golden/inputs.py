@@ -56,3 +56,47 @@ GRAPHCONV_CASES = {
     "mid": (13, 2, 128, 6, 512, 256, False, 3.0),
 }
 DROPEDGE = {"p": 0.3, "seed": 20240601, "call": 5}
+
+
+def synthetic_document(seed: int, n: int, cells: int = 0, tables: int = 0, float_coords: bool = False,
+                       empty_text: float = 0.0):
+    """A seeded OCR-like page: text lines in loose rows/columns with jitter,
+    occasional overlaps, optional empty texts, "cell" and "table" items.
+    Returns a list of region dicts in the reference's cassia layout
+    ({"location": 4 points, "text", "label"})."""
+    r = rng(seed)
+    regions = []
+    y = 10.0
+    while len(regions) < n:
+        x = float(r.integers(0, 60))
+        h = float(r.integers(12, 40))
+        for _ in range(int(r.integers(1, 6))):
+            if len(regions) >= n:
+                break
+            w = float(r.integers(15, 300))
+            jy = float(r.integers(-6, 7))
+            x1, y1 = x, y + jy
+            x2, y2 = x1 + w, y1 + h + float(r.integers(-3, 4))
+            if float_coords:
+                x1, y1, x2, y2 = (v + float(r.random()) for v in (x1, y1, x2, y2))
+            else:
+                x1, y1, x2, y2 = (float(int(v)) for v in (x1, y1, x2, y2))
+            text = "" if r.random() < empty_text else "t%d" % len(regions)
+            regions.append({"location": [[x1, y1], [x2, y1], [x2, y2], [x1, y2]], "text": text, "label": "other"})
+            x = x2 + float(r.integers(-20, 80))  # may overlap the previous box
+        y += h + float(r.integers(-8, 30))
+    kinds = ["cell"] * cells + ["table"] * tables
+    for i, kind in zip(r.choice(n, size=len(kinds), replace=False), kinds):
+        regions[int(i)]["label"] = kind
+    return regions
+
+
+LAYOUT_CASES = {
+    # name: (seed, n, cells, tables, float_coords, empty_text)
+    "plain30": (41, 30, 0, 0, False, 0.0),
+    "plain120": (42, 120, 0, 0, False, 0.0),
+    "float80": (43, 80, 0, 0, True, 0.1),
+    "cells60": (44, 60, 18, 0, False, 0.0),
+    "tables40": (45, 40, 6, 3, False, 0.05),
+    "tiny2": (46, 2, 0, 0, False, 0.0),
+}

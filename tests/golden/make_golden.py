@@ -208,10 +208,46 @@ def make_model_fixtures(GraphCNNDropEdge, HeuristicGraphBuilder, TextlineEncodin
     print(f"model_small_train: loss {loss.item():.6f}")
 
 
+def make_layout_fixtures(HeuristicGraphBuilder, TextlineEncoding):
+    """Reference HeuristicGraphBuilder (graph_utils.py Graph) adjacency for
+    seeded synthetic pages and for assets/samples/debug.json, all three
+    edge types; plus TextlineEncoding features of the same pages."""
+    with open(os.path.join(REF, "assets/samples/debug.json"), encoding="utf-8-sig") as f:
+        debug = json.load(f)
+    with open(os.path.join(REF, "assets/meta_data/master_charset.json"), encoding="utf-8-sig") as f:
+        charset = json.load(f)["charset"]
+    char_to_id = {c: i for i, c in enumerate(charset)}
+    pages = {"debug": [dict(r, label=r.get("label", "other")) for r in debug]}
+    for name, (seed, n, cells, tables, fc, empty) in gi.LAYOUT_CASES.items():
+        pages[name] = gi.synthetic_document(seed, n, cells, tables, fc, empty)
+    out = {}
+    for name, regions in pages.items():
+        label = {}
+        for i, reg in enumerate(regions):
+            label[i] = {"polygon": reg["location"], "text": reg["text"], "label": reg["label"]}
+        for et in ("normal_binary", "fc_similarity", "fc_binary"):
+            if et != "normal_binary" and name not in ("plain30", "cells60", "tiny2", "tables40"):
+                continue
+            sample = HeuristicGraphBuilder(num_edges=6, edge_type=et)({"label": dict(label)})
+            adj = sample["adjacency_matrix"]
+            out[f"{name}::{et}"] = adj.view(np.uint16) if et == "fc_similarity" else (adj != 0)
+        if name in ("debug", "float80", "plain30"):
+            enc = TextlineEncoding(is_normalized_text=True)({"label": dict(label), "char_to_id": char_to_id})
+            V = enc["textline_encoding"]
+            r_, c_ = np.nonzero(V[:, :-4])
+            out[f"{name}::bow_rows"] = r_.astype(np.int32)
+            out[f"{name}::bow_cols"] = c_.astype(np.int32)
+            out[f"{name}::spatial"] = V[:, -4:]
+        out[f"{name}::regions"] = np.array(json.dumps(regions, ensure_ascii=False))
+    np.savez_compressed(os.path.join(HERE, "layout_graphs.npz"), **out)
+    print("layout_graphs:", {k: v.shape for k, v in out.items() if k.endswith("normal_binary")})
+
+
 def main():
     GraphConv, GraphCNNDropEdge, HGB, TLE = _import_reference()
     make_graphconv_fixtures(GraphConv)
     make_model_fixtures(GraphCNNDropEdge, HGB, TLE)
+    make_layout_fixtures(HGB, TLE)
 
 
 if __name__ == "__main__":
