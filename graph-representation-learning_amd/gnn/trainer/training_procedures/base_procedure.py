@@ -1,0 +1,97 @@
+"""Shared training setup (the reference's trainer BaseProcedure,
+gnn/trainer/training_procedures/base_procedure.py:14-197): output dir,
+device choice from num_gpus, checkpoint restore (strict=False), and the
+criterion / optimizer / LR schedule resolved by name from config."""
+from __future__ import annotations
+
+import logging
+import os
+from typing import Any, Dict, List, Tuple
+
+import torch
+import torch.nn as nn
+
+from gnn.trainer import losses, lr_schedulers, optimizers
+from gnn.utils.checkpoint_handler import CheckpointHandler
+
+
+class NullWriter:
+    """Stands in for tensorboardX.SummaryWriter (logging is out of scope)."""
+
+    def add_scalar(self, *args, **kwargs):
+        pass
+
+    def add_histogram(self, *args, **kwargs):
+        pass
+
+    def close(self):
+        pass
+
+
+class BaseProcedure:
+    def __init__(self, model: nn.Module, config: Dict[str, Any], ems_exp: Any = None, **kwargs):
+        self.logger = logging.getLogger(type(self).__module__)
+        self.config = config
+        self.ems_exp = ems_exp
+        self.model_dir = self._make_output_dir()
+        self.checkpointer = CheckpointHandler()
+        self.device, self.device_ids = self._prepare_device(config.get("num_gpus", 1))
+        self.model = self._load_prev_checkpoint(model).to(self.device)
+        self.criterion = self._init_criterion()
+        self.optimizer = self._init_optimizer()
+        self.lr_scheduler = self._init_lr_scheduler()
+        self.tb_writer = NullWriter()
+
+    @classmethod
+    def _from_config(cls, model: nn.Module, config: Dict[str, Any], ems_exp: Any = None, **kwargs) -> "BaseProcedure":
+        return cls(model, config, ems_exp, **kwargs)
+
+    def _prepare_device(self, n_gpu_use: int) -> Tuple[torch.device, List[int]]:
+        n_gpu = torch.cuda.device_count()
+        if n_gpu_use > 0 and n_gpu == 0:
+            self.logger.warning("There's no GPU available on this machine; the MI355X engine will refuse CPU tensors.")
+            n_gpu_use = 0
+        n_gpu_use = min(n_gpu_use, n_gpu)
+        return torch.device("cuda:0" if n_gpu_use > 0 else "cpu"), list(range(n_gpu_use))
+
+    @staticmethod
+    def _resolve(module, section: Dict[str, Any], what: str):
+        if not section or not section.get("type"):
+            return None
+        cls = getattr(module, section["type"], None)
+        if cls is None:
+            raise ValueError(f"Cannot find {what} {section['type']}")
+        return cls._from_config(section.get("args") or {})
+
+    def _init_criterion(self):
+        return self._resolve(losses, self.config.get("loss"), "loss")
+
+    def _init_lr_scheduler(self):
+        return self._resolve(lr_schedulers, self.config.get("lr_scheduler"), "lr_scheduler")
+
+    def _init_optimizer(self):
+        opt = self._resolve(optimizers, self.config.get("optimizer"), "optimizer")
+        return opt.get_optimizer(self.model.parameters()) if opt is not None else None
+
+    def _make_output_dir(self) -> str:
+        out = os.path.join(self.config.output_dir, self.config.get("model_dir_name", "models"))
+        os.makedirs(out, exist_ok=True)
+        return out
+
+    def _load_prev_checkpoint(self, model: nn.Module) -> nn.Module:
+        path = self.config.get("checkpoint_path")
+        if path:
+            ckpt = self.checkpointer.restore_checkpoint(path)
+            if ckpt.get("state_dict") and ckpt.get("config"):
+                model.load_state_dict(ckpt["state_dict"], strict=False)
+                self.logger.info("Loading pretrained model success!")
+        return model
+
+    def _update_learning_rate(self, epoch: int, step: int) -> float:
+        lr = self.lr_scheduler._step_lr(epoch, step)
+        for group in self.optimizer.param_groups:
+            group["lr"] = lr
+        return lr
+
+    def __call__(self):
+        raise NotImplementedError

@@ -1,0 +1,153 @@
+"""Key-value node classification training loop (the reference's KVProcedure,
+gnn/trainer/training_procedures/kv_procedure.py:19-377).
+
+Per batch: V, A to the device, model.forward([V, A]) (the GraphCNNDropEdge
+hot path on libgrl), CE loss, backward, clip_grad_norm_, optimizer step;
+macro P/R/F1 over non-padding, non-"other" nodes; validation each epoch;
+checkpoint on best validation loss.  Additive: a batch produced by
+TypedEdgePadding carries "typed_edges" instead of a dense adjacency and is
+turned into a TypedGraph directly (O(E) host->device instead of O(N^2)).
+"""
+from __future__ import annotations
+
+import math
+from collections import defaultdict
+from typing import Any, Dict, List, Tuple
+
+import numpy as np
+import torch
+import torch.nn as nn
+
+from gnn.data_generator.base_dataloader import BaseDataLoader
+from gnn.trainer.training_procedures.base_procedure import BaseProcedure
+from gnn.utils.config import to_plain
+from gnn.utils.metric_tracker import Dictlist
+from grl import TypedGraph
+from grl.layout import edges_to_typed_csr
+
+
+def batch_graph(batch: Dict[str, Any], device: torch.device, num_types: int = 6):
+    """The batch's adjacency for model.forward: dense (B, N, L, N) float, or
+    a block-diagonal TypedGraph built from "typed_edges"."""
+    if "typed_edges" in batch:
+        B, N = (int(x) for x in batch["graph_shape"])
+        rowptr, colidx = edges_to_typed_csr(np.asarray(batch["typed_edges"]), B * N, num_types)
+        return TypedGraph.from_csr_host(rowptr, colidx, num_types, device, num_cols=B * N, batch_shape=(B, N))
+    return batch["adjacency_matrix"].float().to(device)
+
+
+class KVProcedure(BaseProcedure):
+    def __init__(self, model: nn.Module, config: Dict[str, Any], ems_exp: Any = None, **kwargs):
+        super().__init__(model, config, ems_exp, **kwargs)
+        self.global_step = 0
+        self.activator = torch.nn.Softmax(dim=2)
+        self.train_loader, self.val_loader, self.class_names = self._init_dataloaders()
+
+    def _init_dataloaders(self):
+        loader = BaseDataLoader(self.config)
+        dcfg = self.config.data_config
+        train_ds = loader._load_dataset(dcfg.dataset.type, dcfg.training, data_type="training")
+        val_ds = loader._load_dataset(dcfg.dataset.type, dcfg.validation, data_type="validation")
+        names = ["other"] + ["_".join(v) for _, v in sorted(train_ds.id_to_class.items())]
+        return (loader._get_dataloader(train_ds, train_ds.data_config),
+                loader._get_dataloader(val_ds, val_ds.data_config), tuple(names))
+
+    def _get_metric_scores(self, preds: torch.Tensor, gts: torch.Tensor,
+                           item_name: str = "item") -> Tuple[Dict[str, Any], Dict[str, Any]]:
+        from sklearn.metrics import classification_report
+
+        y_pred = preds.reshape(-1).cpu().numpy()
+        y_true = gts.reshape(-1).cpu().numpy()
+        args = self.config.data_config.dataset.get("args") or {}
+        ignore = [args.get("node_label_padding_value", -100), args.get("other_class_index")]
+        keep = np.isin(y_true, [v for v in ignore if v is not None], invert=True)
+        pred_names = [self.class_names[i] for i in y_pred[keep].tolist()]
+        true_names = [self.class_names[i] for i in y_true[keep].tolist()]
+        try:
+            scores = classification_report(true_names, pred_names, output_dict=True, zero_division=0)["macro avg"]
+        except Exception:
+            scores = {"precision": 0.0, "recall": 0.0, "f1-score": 0.0, "support": 0.0}
+        return ({f"{item_name}_{k}": v for k, v in scores.items()}, {"pred": pred_names, "lbl": true_names})
+
+    def _step_process(self, batch: Dict[str, Any], **kwargs):
+        V = batch["textline_encoding"].float().to(self.device)
+        A = batch_graph(batch, self.device)
+        targets = batch["node_label"].to(self.device)
+        logits = self.model.forward([V, A])
+        loss = self.criterion(logits, targets)
+        predicts = self.activator(logits).argmax(dim=-1)
+        scores, items = self._get_metric_scores(predicts, targets, item_name="Node classification")
+        scores["loss"] = loss.item()
+        return loss, scores, items
+
+    def _run_train_step(self, batch: Dict[str, Any], **kwargs):
+        self.model.train()
+        self.optimizer.zero_grad()
+        with torch.set_grad_enabled(True):
+            loss, scores, items = self._step_process(batch, **kwargs)
+            loss.backward()
+            nn.utils.clip_grad_norm_(self.model.parameters(), self.config.max_grad_norm)
+            self.optimizer.step()
+        return scores, items
+
+    def _run_val_step(self, batch: Dict[str, Any], **kwargs):
+        self.model.eval()
+        with torch.set_grad_enabled(False):
+            _, scores, items = self._step_process(batch, **kwargs)
+        return scores, items
+
+    def cosine_schedule_lambda(self, step: int, epoch: int, total_steps: int, base_value: float, max_value: float,
+                               warmup_steps: int = 0) -> float:
+        """Linear warm-up then cosine annealing (kv_procedure.py:264-292); the
+        value is stored on model.lambda_value each step like the reference."""
+        step = max(0, min(step, total_steps))
+        warmup_steps = min(warmup_steps, total_steps)
+        if step < warmup_steps:
+            return base_value + (max_value - base_value) * (step / warmup_steps)
+        progress = float(step - warmup_steps) / float(max(1, total_steps - warmup_steps))
+        return base_value + 0.5 * (max_value - base_value) * (1 + math.cos(math.pi * progress))
+
+    def _optimize_per_epoch(self, epoch: int) -> Dict[str, Any]:
+        from sklearn.metrics import classification_report
+
+        train = Dictlist()
+        for batch in self.train_loader:
+            scores, _ = self._run_train_step(batch)
+            train._update(scores)
+            self.tb_writer.add_scalar("Train_step_loss", scores["loss"], self.global_step)
+            self.model.zero_grad()
+            self.global_step += 1
+            n = len(self.train_loader)
+            self.model.lambda_value = self.cosine_schedule_lambda(self.global_step, epoch, self.config.num_epochs * n,
+                                                                  base_value=1e-4, max_value=1.0, warmup_steps=5 * n)
+        self.logger.info(f"Training epoch: {epoch} step: {self.global_step} metrics: {train._result() if train else {}}")
+        val = Dictlist()
+        items: Dict[str, List[str]] = defaultdict(list)
+        for batch in self.val_loader:
+            scores, vitems = self._run_val_step(batch)
+            val._update(scores)
+            for k, v in vitems.items():
+                items[k].extend(v)
+        val_metrics = val._result() if val else {"loss": float("inf")}
+        report = classification_report(items["lbl"], items["pred"], output_dict=True, zero_division=0) \
+            if items["lbl"] else {"macro avg": {"precision": 0.0, "recall": 0.0, "f1-score": 0.0, "support": 0}}
+        macro = dict(report["macro avg"])
+        macro["loss"] = val_metrics["loss"]
+        self.logger.info(f"Validation metrics: {val_metrics}")
+        return macro
+
+    def __call__(self) -> float:
+        best = float("inf")
+        self.model.zero_grad()
+        metrics: Dict[str, Any] = {"f1-score": 0.0}
+        for epoch in range(self.config.num_epochs):
+            metrics = self._optimize_per_epoch(epoch)
+            if self.lr_scheduler is not None:
+                self._update_learning_rate(epoch, self.global_step)
+            if metrics["loss"] < best:
+                best = metrics["loss"]
+                self.checkpointer.save_checkpoint(
+                    {"epoch": epoch, "config": to_plain(self.config), "meta_data": to_plain(metrics),
+                     "state_dict": self.model.state_dict()}, self.model_dir)
+        self.tb_writer.close()
+        return metrics["f1-score"]

@@ -243,8 +243,25 @@ def make_layout_fixtures(HeuristicGraphBuilder, TextlineEncoding):
     print("layout_graphs:", {k: v.shape for k, v in out.items() if k.endswith("normal_binary")})
 
 
+NORMALIZE_CASES = [
+    "ABC def", "１２３４５６７８９０", "It's; a_test", "tab\there\nnew\rline", "dash—en–minus−hyphen‐",
+    "ideo\u3000space\u00a0nbsp\u2028ls", "dots。．・‥…", "「括弧」（全角）［角］【隅】《二重》", "«guillemets» ‹single›",
+    "“quotes” ‘single’ „low“", "半角ｶﾀｶﾅ and ﾊﾝｶｸ", "Ⅻ ① ㈱ ㎏ ﬁ", "MiXeD 12:30 p.m. ¥1,000-", "",
+]
+
+
+def make_text_fixtures():
+    from gnn.data_generator.data_process.utils.normalize_text import normalize_text
+
+    out = [normalize_text(t) for t in NORMALIZE_CASES]
+    with open(os.path.join(HERE, "normalize_text.json"), "w", encoding="utf-8") as f:
+        json.dump({"inputs": NORMALIZE_CASES, "outputs": out}, f, ensure_ascii=False, indent=1)
+    print("normalize_text:", len(out), "cases")
+
+
 def main():
     GraphConv, GraphCNNDropEdge, HGB, TLE = _import_reference()
+    make_text_fixtures()
     make_graphconv_fixtures(GraphConv)
     make_model_fixtures(GraphCNNDropEdge, HGB, TLE)
     make_layout_fixtures(HGB, TLE)

@@ -1,0 +1,83 @@
+"""GPU: the reference's public API end to end on the engine --
+GNNLearningWarper(model, config).train() / .predict() (gnn/cl_warper.py)."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from gnn.cl_warper import GNNLearningWarper
+from gnn.models import GraphCNNDropEdge
+from test_data_pipeline import ASSETS, make_config
+
+pytestmark = pytest.mark.gpu
+
+
+def test_train_two_epochs_and_checkpoint(tmp_path):
+    cfg = make_config(str(tmp_path), epochs=2)
+    torch.manual_seed(0)
+    model = GraphCNNDropEdge(4369, 15, 6, net_size=64)
+    warper = GNNLearningWarper(model, config=cfg)
+    f1 = warper.train()
+    assert isinstance(f1, float) and 0.0 <= f1 <= 1.0
+    # the warper moves output_dir to <output_dir>/<experiment_name> (cl_warper.py:43, 81-86)
+    assert warper.config.output_dir == os.path.join(cfg.output_dir, cfg.experiment_name)
+    ckpt_path = os.path.join(warper.config.output_dir, "models", "model_latest.pt")
+    ckpt = torch.load(ckpt_path, weights_only=True)  # plain-dict config: safe loader works
+    assert set(ckpt) == {"epoch", "config", "meta_data", "state_dict"}
+    assert set(ckpt["state_dict"]) == set(model.state_dict())
+    assert warper.trainer.global_step == 2 * 3  # 5 docs, batch 2, drop_last False
+    assert hasattr(warper.trainer.model, "lambda_value")
+
+
+def test_edge_batches_equal_dense_batches(tmp_path):
+    """HeuristicGraphBuilder(emit="edges") + TypedEdgePadding gives the same
+    training step as the reference's dense adjacency + NumpyPadding."""
+    losses, grads = {}, {}
+    for emit in ("dense", "edges"):
+        cfg = make_config(str(tmp_path / emit), emit=emit, epochs=1)
+        torch.manual_seed(0)
+        model = GraphCNNDropEdge(4369, 15, 6, net_size=32)
+        warper = GNNLearningWarper(model, config=cfg)
+        proc = warper.trainer
+        batch = next(iter(proc.train_loader))
+        torch.manual_seed(7)
+        scores, _ = proc._run_train_step(batch)
+        losses[emit] = scores["loss"]
+        grads[emit] = model.gcn1.h_weights.detach().clone()
+    assert losses["dense"] == losses["edges"]
+    assert torch.equal(grads["dense"], grads["edges"])
+
+
+def test_predict_matches_reference_logits(golden, tmp_path):
+    """predict() on debug.json (cassia format) with the config-1 model under
+    torch.manual_seed(0): per-box class and confidence from the reference's
+    logits (model_debug.npz) through softmax."""
+    g = golden("model_debug.npz")
+    classes = os.path.join(str(tmp_path), "classes26.json")
+    with open(classes, "w") as f:
+        json.dump({"classes": [f"c{i}" for i in range(26)]}, f)  # 26 x {key,value} + other = 53 outputs
+    cfg = make_config(str(tmp_path), is_train=False)
+    cfg.inference_settings.datasets.args.class_path = classes
+    torch.manual_seed(0)
+    model = GraphCNNDropEdge(4369, 53, 6, 256)
+    warper = GNNLearningWarper(model, config=cfg)
+    with open(os.path.join(ASSETS, "debug.json"), encoding="utf-8-sig") as f:
+        doc = json.load(f)
+    out = warper.predict([doc])
+    assert len(out) == 1 and len(out[0]) == 74
+    logits = g["logits"].astype(np.float64)
+    p = np.exp(logits - logits.max(-1, keepdims=True))
+    p /= p.sum(-1, keepdims=True)
+    conf = np.array([b["confidence"] for b in out[0]])
+    np.testing.assert_allclose(conf, p.max(-1), rtol=0, atol=1e-4)
+    cls = p.argmax(-1)
+    id_to_class = dict(warper.inferencer.id_to_class)
+    for box, k in zip(out[0], cls):
+        if abs(np.sort(p[list(out[0]).index(box)])[-1] - np.sort(p[list(out[0]).index(box)])[-2]) > 1e-4:
+            assert (box["formal_key"], box["key_type"]) == tuple(id_to_class[int(k)])
+    # a single document (not wrapped in a list) is accepted like the reference's
+    # handle_single_input when given as a JSON path
+    one = warper.predict(os.path.join(ASSETS, "debug.json"))
+    assert len(one) == 74
