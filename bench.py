@@ -48,6 +48,12 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 disables)")
     ap.add_argument("--extras", action="store_true",
                     help="also time fused-DropEdge fwd, backward, MFMA linear and a full layer (not the headline)")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="process-group backend for N>1 (nccl = RCCL; gloo only to smoke-test the N>1 path "
+                         "with several ranks on one GPU)")
+    ap.add_argument("--halo", choices=["auto", "sparse", "dense"], default="auto",
+                    help="halo exchange layout for N>1 (grl/dist.py): sparse all-to-all-v of the referenced rows, "
+                         "dense all-gather of every shard; auto picks dense when >=75%% of remote rows are referenced")
     ap.add_argument("--only", choices=["fwd", "bwd", "linear", "layer"], default=None,
                     help="profiling aid: run just that kernel K times (no JSON line)")
     return ap.parse_args()
@@ -64,10 +70,16 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    ndev = torch.cuda.device_count()
+    if args.dist_backend == "nccl" and world > 1 and local_rank >= ndev:
+        raise SystemExit(f"rank {rank}: LOCAL_RANK {local_rank} but only {ndev} GPU(s) visible")
+    dev = torch.device("cuda", local_rank % ndev)
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.dist_backend)
 
     from grl import DropEdge
     from grl.dist import ShardedGraph, halo_exchange_into
@@ -80,7 +92,7 @@ def main():
         N = 1 << (N - 1).bit_length()
         n_loc = N // world
     t0 = time.time()
-    sg = ShardedGraph.synthetic(N, args.avg_deg, L, kind=args.graph, seed=0, device=dev)
+    sg = ShardedGraph.synthetic(N, args.avg_deg, L, kind=args.graph, seed=0, device=dev, halo=args.halo)
     graph, plan = sg.graph, sg.plan
     n_loc = plan.n_loc
     E_loc, E_tot = graph.nnz, plan.num_edges_total
@@ -88,6 +100,7 @@ def main():
     gen.manual_seed(1 + rank)
     # [own rows | halo rows]: own rows are written once, halo rows by the exchange
     X_full = torch.empty(plan.n_loc + plan.n_halo, F, device=dev)
+    X_full[n_loc:plan.stride].zero_()  # dense plans: shard padding rows (never read by the kernel)
     X_loc = X_full[:n_loc]
     X_loc.copy_(torch.randn(n_loc, F, generator=gen, device=dev, dtype=torch.float32))
     send_buf = torch.empty(plan.send_index.numel(), F, device=dev)
@@ -112,11 +125,13 @@ def main():
         gather()
         spmm()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    ev_h = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     for i in range(args.steps):
+        ev_h[i].record(stream)
         gather()
         ev[i][0].record(stream)
         spmm()
@@ -127,10 +142,12 @@ def main():
     wall = time.perf_counter() - t_start
     per_step = [a.elapsed_time(b) for a, b in ev]
     kern_ms = float(np.mean(per_step))
+    halo_ms = float(np.mean([h.elapsed_time(a) for h, (a, _) in zip(ev_h, ev)]))
     if world > 1:
-        tt = torch.tensor([wall, kern_ms], dtype=torch.float64, device=dev)
+        tt = torch.tensor([wall, kern_ms, halo_ms], dtype=torch.float64,
+                          device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        wall, kern_ms = float(tt[0]), float(tt[1])
+        wall, kern_ms, halo_ms = float(tt[0]), float(tt[1]), float(tt[2])
     ms_step = wall / args.steps * 1e3
     value = E_tot / (wall / args.steps)
 
@@ -149,7 +166,10 @@ def main():
                    "nodes_total": N, "edges_total": E_tot, "nodes_per_gpu": n_loc, "avg_deg": args.avg_deg,
                    "num_types": L, "d": F, "dropedge_p": args.p, "graph": args.graph,
                    "parallelism": "single GPU" if world == 1 else
-                   f"node-range shards x{world}, RCCL all-to-all-v halo ({plan.n_halo} halo rows on rank {rank})"},
+                   f"node-range shards x{world}, "
+                   + ("RCCL" if args.dist_backend == "nccl" else f"{args.dist_backend} (host-staged)") + " "
+                   + ("all-gather (dense halo)" if plan.mode == "dense" else "all-to-all-v (sparse halo)")
+                   + f", rank {rank} references {plan.referenced_halo_rows} of {N - n_loc} remote rows"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "spmm_kernel<4,1,8,false,false> (grl_typed_spmm_fwd)",
@@ -157,6 +177,11 @@ def main():
                      "algorithmic_bytes_per_launch": bytes_launch},
         "build_s": build_s,
     }
+    if world > 1:
+        rows_in = (world - 1) * plan.stride if plan.mode == "dense" else sum(plan.recv_counts)
+        out["halo"] = {"mode": plan.mode, "ms_max_over_ranks": halo_ms, "rows_received_rank0": rows_in,
+                       "GB_received_rank0": rows_in * F * 4 / 1e9,
+                       "GBps_rank0": rows_in * F * 4 / 1e9 / (halo_ms * 1e-3) if halo_ms > 0 else None}
     if args.graph == "rmat":
         out["config"]["split"] = graph.split_stats()
         out["config"]["max_row_edges"] = int((graph.rowptr[L::L] - graph.rowptr[:-1:L]).max())

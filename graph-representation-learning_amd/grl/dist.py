@@ -13,6 +13,21 @@ The plan is static per graph and built once (two small all-to-alls of ids).
 Edge ids stay global (edge_id_base = nnz of lower ranks, self ids
 E_total + global node), so fused DropEdge masks are identical to the
 single-GPU run and the forward is bitwise identical to it.
+
+Two exchange layouts, chosen collectively per graph (HaloPlan.mode):
+  "sparse"  X_ext = [own rows | needed remote rows in owner order]; the owner
+            packs the rows each peer asked for and one all-to-all-v moves
+            them.  Right when a shard references a small part of the rest.
+  "dense"   X_ext = [own rows padded to `stride` | every rank's rows, rank q
+            at stride*(1+q)], filled by one all_gather (no packing, no
+            id lists).  Right when nearly every remote row is referenced --
+            Erdos-Renyi graphs at avg_deg 32 need ~98% of each peer's rows,
+            where packing would cost two extra HBM passes over the halo for
+            nothing.  "auto" picks dense when the referenced remote rows are
+            >= DENSE_HALO_FRACTION of all remote rows (summed over ranks).
+Both layouts give the same Z bitwise (the kernel reads the same values in the
+same edge order) and the same dX values (peer-order sums; a peer's rows that
+no edge referenced contribute +0.0).
 """
 from __future__ import annotations
 
@@ -34,33 +49,80 @@ def _rank(group) -> int:
     return dist.get_rank(group) if dist.is_available() and dist.is_initialized() else 0
 
 
+def _host_staged(group) -> bool:
+    """gloo moves device tensors only through host copies (used to smoke-test
+    the N>1 path with several ranks on one GPU; production uses RCCL)."""
+    return dist.get_backend(group) == "gloo"
+
+
+def all_to_all_v(out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits, group=None) -> None:
+    if _host_staged(group) and (out.is_cuda or inp.is_cuda):
+        o = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits, group=group)
+        out.copy_(o)
+    else:
+        dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
+
+
+def all_gather_into(out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
+    """out = concat over ranks of inp (equal sizes)."""
+    if _host_staged(group) and (out.is_cuda or inp.is_cuda):
+        parts = all_gather_list(inp, group)
+        out.copy_(torch.cat(parts, 0))
+    else:
+        dist.all_gather_into_tensor(out, inp, group=group)
+
+
+def all_gather_list(t: torch.Tensor, group=None) -> List[torch.Tensor]:
+    src = t.cpu() if _host_staged(group) else t
+    outs = [torch.empty_like(src) for _ in range(_world(group))]
+    dist.all_gather(outs, src, group=group)
+    return outs
+
+
+DENSE_HALO_FRACTION = 0.75
+
+
 @dataclass
 class HaloPlan:
     row_begin: int
     row_end: int
     n_loc: int
-    n_halo: int
+    n_halo: int                  # rows of X_ext after the own rows (dense: padding + all gathered rows)
     bounds: List[int]            # row ranges of all ranks: [b_0, b_1, ..., b_P]
-    send_index: torch.Tensor     # int64 local rows, concatenated per destination peer
-    send_counts: List[int]       # rows I send to each peer
-    recv_counts: List[int]       # halo rows I receive from each peer (owner order)
-    halo_ids: torch.Tensor       # int64 global ids of my halo rows, ascending
-    colidx_local: torch.Tensor   # int32: own -> id - row_begin, remote -> n_loc + halo slot
+    send_index: torch.Tensor     # sparse: int64 local rows, concatenated per destination peer
+    send_counts: List[int]       # sparse: rows I send to each peer
+    recv_counts: List[int]       # sparse: halo rows I receive from each peer (owner order)
+    halo_ids: torch.Tensor       # int64 global ids of the remote rows my edges reference, ascending
+    colidx_local: torch.Tensor   # int32 column into X_ext (own -> id - row_begin)
     edge_id_base: int
     num_edges_total: int
+    mode: str = "sparse"         # "sparse" | "dense" (module docstring)
+    stride: int = 0              # dense: max shard rows; rank q's rows sit at X_ext[stride*(1+q):]
+
+    @property
+    def rank(self) -> int:
+        return next(i for i in range(len(self.bounds) - 1)
+                    if self.bounds[i] == self.row_begin and self.bounds[i + 1] == self.row_end)
+
+    @property
+    def referenced_halo_rows(self) -> int:
+        return int(self.halo_ids.numel())
 
 
-def build_halo_plan(colidx: torch.Tensor, row_begin: int, row_end: int, group=None) -> HaloPlan:
-    """Collective: every rank of `group` calls it with its own shard."""
+def build_halo_plan(colidx: torch.Tensor, row_begin: int, row_end: int, group=None,
+                    mode: str = "auto") -> HaloPlan:
+    """Collective: every rank of `group` calls it with its own shard (and the
+    same `mode`)."""
+    if mode not in ("auto", "sparse", "dense"):
+        raise ValueError(f"halo mode must be auto|sparse|dense, got {mode!r}")
     dev = colidx.device
     world, rank = _world(group), _rank(group)
     n_loc = row_end - row_begin
     c = colidx.long()
     if world > 1:
         rr = torch.tensor([row_begin, row_end, colidx.numel()], dtype=torch.int64, device=dev)
-        allr = [torch.empty_like(rr) for _ in range(world)]
-        dist.all_gather(allr, rr, group=group)
-        allr = torch.stack(allr).cpu()
+        allr = torch.stack([x.cpu() for x in all_gather_list(rr, group)])
         begins, ends, nnzs = allr[:, 0].tolist(), allr[:, 1].tolist(), allr[:, 2].tolist()
         if begins != sorted(begins) or any(ends[i] != begins[i + 1] for i in range(world - 1)):
             raise ValueError(f"node ranges must be contiguous in rank order: {list(zip(begins, ends))}")
@@ -70,18 +132,35 @@ def build_halo_plan(colidx: torch.Tensor, row_begin: int, row_end: int, group=No
     else:
         bounds = [row_begin, row_end]
         edge_id_base, num_edges_total = 0, colidx.numel()
+    if world > 1 and c.numel() and (int(c.min()) < bounds[0] or int(c.max()) >= bounds[-1]):
+        raise ValueError(f"column ids outside the global node range [{bounds[0]}, {bounds[-1]})")
     own = (c >= row_begin) & (c < row_end)
     halo_ids = torch.unique(c[~own])  # sorted ascending => grouped by owner
+    if world > 1 and mode == "auto":
+        referenced = sum(int(x) for x in all_gather_list(
+            torch.tensor([halo_ids.numel()], dtype=torch.int64, device=dev), group))
+        remote = (world - 1) * (bounds[-1] - bounds[0])
+        mode = "dense" if remote and referenced >= DENSE_HALO_FRACTION * remote else "sparse"
+    if world > 1 and mode == "dense":
+        stride = max(bounds[i + 1] - bounds[i] for i in range(world))
+        ends_t = torch.tensor(bounds[1:], dtype=torch.int64, device=dev)
+        begins_t = torch.tensor(bounds[:-1], dtype=torch.int64, device=dev)
+        owner = torch.searchsorted(ends_t, c, right=True)
+        slot = stride * (1 + owner) + (c - begins_t[owner.clamp(max=world - 1)])
+        colidx_local = torch.where(own, c - row_begin, slot).to(torch.int32)
+        empty = torch.zeros(0, dtype=torch.int64, device=dev)
+        return HaloPlan(row_begin, row_end, n_loc, stride * (world + 1) - n_loc, bounds, empty, [0] * world,
+                        [0] * world, halo_ids, colidx_local, edge_id_base, num_edges_total, "dense", stride)
     if world > 1:
         ends_t = torch.tensor(bounds[1:], dtype=torch.int64, device=dev)
         owner = torch.searchsorted(ends_t, halo_ids, right=True)
         need = torch.bincount(owner, minlength=world).to(torch.int64)
         asked_counts = torch.empty_like(need)
-        dist.all_to_all_single(asked_counts, need, group=group)
+        all_to_all_v(asked_counts, need, None, None, group)
         recv_counts = need.cpu().tolist()
         send_counts = asked_counts.cpu().tolist()
         asked = torch.empty(sum(send_counts), dtype=torch.int64, device=dev)
-        dist.all_to_all_single(asked, halo_ids.contiguous(), send_counts, recv_counts, group=group)
+        all_to_all_v(asked, halo_ids.contiguous(), send_counts, recv_counts, group)
         send_index = asked - row_begin
         if send_index.numel() and (int(send_index.min()) < 0 or int(send_index.max()) >= n_loc):
             raise RuntimeError("halo plan: a peer asked for rows this rank does not own")
@@ -93,7 +172,7 @@ def build_halo_plan(colidx: torch.Tensor, row_begin: int, row_end: int, group=No
     slot = n_loc + torch.searchsorted(halo_ids, c)
     colidx_local = torch.where(own, c - row_begin, slot).to(torch.int32)
     return HaloPlan(row_begin, row_end, n_loc, int(halo_ids.numel()), bounds, send_index, send_counts, recv_counts,
-                    halo_ids, colidx_local, edge_id_base, num_edges_total)
+                    halo_ids, colidx_local, edge_id_base, num_edges_total, "sparse", n_loc)
 
 
 class _HaloExchange(torch.autograd.Function):
@@ -102,9 +181,12 @@ class _HaloExchange(torch.autograd.Function):
         F = X_loc.shape[1]
         X_ext = X_loc.new_empty(plan.n_loc + plan.n_halo, F)
         X_ext[: plan.n_loc].copy_(X_loc)
-        if _world(group) > 1:
+        if plan.mode == "dense":
+            X_ext[plan.n_loc: plan.stride].zero_()
+            all_gather_into(X_ext[plan.stride:], X_ext[: plan.stride], group)
+        elif _world(group) > 1:
             send = X_loc.index_select(0, plan.send_index)
-            dist.all_to_all_single(X_ext[plan.n_loc:], send, plan.recv_counts, plan.send_counts, group=group)
+            all_to_all_v(X_ext[plan.n_loc:], send, plan.recv_counts, plan.send_counts, group)
         ctx.plan, ctx.group = plan, group
         return X_ext
 
@@ -113,9 +195,17 @@ class _HaloExchange(torch.autograd.Function):
         plan, group = ctx.plan, ctx.group
         dX_ext = dX_ext.contiguous()
         dX_loc = dX_ext[: plan.n_loc].clone()
-        if _world(group) > 1:
+        if plan.mode == "dense":
+            world, st = len(plan.bounds) - 1, plan.stride
+            back = dX_ext.new_empty(world * st, dX_ext.shape[1])
+            all_to_all_v(back, dX_ext[st:], [st] * world, [st] * world, group)
+            me = plan.rank
+            for q in range(world):  # peer order, like the sparse path
+                if q != me:
+                    dX_loc += back[q * st: q * st + plan.n_loc]
+        elif _world(group) > 1:
             back = dX_ext.new_empty(sum(plan.send_counts), dX_ext.shape[1])
-            dist.all_to_all_single(back, dX_ext[plan.n_loc:], plan.send_counts, plan.recv_counts, group=group)
+            all_to_all_v(back, dX_ext[plan.n_loc:], plan.send_counts, plan.recv_counts, group)
             off = 0
             for cnt in plan.send_counts:  # peer order; indices unique within a peer -> deterministic
                 if cnt:
@@ -134,11 +224,16 @@ def halo_exchange(X_loc: torch.Tensor, plan: HaloPlan, group=None) -> torch.Tens
 def halo_exchange_into(X_loc: torch.Tensor, X_ext: torch.Tensor, send_buf: torch.Tensor, plan: HaloPlan,
                        group=None) -> None:
     """No-autograd, no-allocation form for inference / benchmarking:
-    X_ext[:n_loc] must already alias or hold X_loc; fills X_ext[n_loc:]."""
+    X_ext[:n_loc] must already alias or hold X_loc; fills X_ext[n_loc:]
+    (dense plans: the pad rows X_ext[n_loc:stride] travel as they are and are
+    never read by the kernel; send_buf is unused and may be empty)."""
     if _world(group) == 1:
         return
+    if plan.mode == "dense":
+        all_gather_into(X_ext[plan.stride:], X_ext[: plan.stride], group)
+        return
     torch.index_select(X_loc, 0, plan.send_index, out=send_buf)
-    dist.all_to_all_single(X_ext[plan.n_loc:], send_buf, plan.recv_counts, plan.send_counts, group=group)
+    all_to_all_v(X_ext[plan.n_loc:], send_buf, plan.recv_counts, plan.send_counts, group)
 
 
 def edge_balanced_bounds(deg: torch.Tensor, world: int) -> List[int]:
@@ -160,9 +255,9 @@ class ShardedGraph:
     """This rank's node-range shard of a global typed graph, ready to aggregate."""
 
     def __init__(self, rowptr: torch.Tensor, colidx_global: torch.Tensor, num_types: int, row_begin: int,
-                 row_end: int, *, vals: Optional[torch.Tensor] = None, group=None):
+                 row_end: int, *, vals: Optional[torch.Tensor] = None, group=None, halo: str = "auto"):
         self.group = group
-        self.plan = build_halo_plan(colidx_global, row_begin, row_end, group)
+        self.plan = build_halo_plan(colidx_global, row_begin, row_end, group, mode=halo)
         p = self.plan
         self.graph = TypedGraph(rowptr, p.colidx_local, num_types, vals=vals, has_self=True,
                                 num_cols=p.n_loc + p.n_halo, edge_id_base=p.edge_id_base,
@@ -170,7 +265,7 @@ class ShardedGraph:
 
     @classmethod
     def synthetic(cls, num_nodes: int, avg_deg: float, num_types: int = 6, *, kind: str = "er", seed: int = 0,
-                  device="cuda", group=None, balance: Optional[str] = None) -> "ShardedGraph":
+                  device="cuda", group=None, balance: Optional[str] = None, halo: str = "auto") -> "ShardedGraph":
         """balance "nodes": equal node ranges (ER); "edges": ranges holding
         ~E/P candidate edges each (power-law graphs; default for R-MAT)."""
         world, rank = _world(group), _rank(group)
@@ -184,7 +279,7 @@ class ShardedGraph:
         rb, re = bounds[rank], bounds[rank + 1]
         g = TypedGraph.synthetic(num_nodes, avg_deg, num_types, kind=kind, seed=seed, row_range=(rb, re),
                                  device=device)
-        return cls(g.rowptr, g.colidx, num_types, rb, re, group=group)
+        return cls(g.rowptr, g.colidx, num_types, rb, re, group=group, halo=halo)
 
     @property
     def halo_rows(self) -> int:

@@ -58,7 +58,7 @@ def _reference():
     return rowptr, colidx, X, dZ, Z, dX
 
 
-def _worker(rank, world, port, bounds):
+def _worker(rank, world, port, bounds, mode):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -67,13 +67,18 @@ def _worker(rank, world, port, bounds):
         rb, re = bounds[rank], bounds[rank + 1]
         lr = rowptr[rb * L:re * L + 1] - rowptr[rb * L]
         lc = colidx[rowptr[rb * L]:rowptr[re * L]]
-        plan = build_halo_plan(torch.from_numpy(lc.copy()), rb, re)
+        plan = build_halo_plan(torch.from_numpy(lc.copy()), rb, re, mode=mode)
+        # referenced/remote rows: 99% ([0,120,240]), 93% ([0,50,170,240]), 50% (empty shard) -> auto at 75%
+        assert plan.mode == (mode if mode != "auto" else ("sparse" if bounds[1] == 0 else "dense"))
         assert plan.edge_id_base == int(rowptr[rb * L]) and plan.num_edges_total == colidx.size
         # every halo id is remote and referenced; slots are in owner order
         assert not ((plan.halo_ids >= rb) & (plan.halo_ids < re)).any()
         X_loc = torch.from_numpy(X[rb:re].copy()).requires_grad_(True)
         X_ext = halo_exchange(X_loc, plan)
-        np.testing.assert_array_equal(X_ext[plan.n_loc:].detach().numpy(), X[plan.halo_ids.numpy()])
+        # every column resolves to the right global feature row, whatever the layout
+        np.testing.assert_array_equal(X_ext[plan.colidx_local.long()].detach().numpy(), X[lc])
+        if plan.mode == "sparse":
+            np.testing.assert_array_equal(X_ext[plan.n_loc:].detach().numpy(), X[plan.halo_ids.numpy()])
         d = c_oracle.drop(*DROP, True)
         Z = _OracleAggregate.apply(X_ext, lr, plan.colidx_local.numpy(), plan.n_loc + plan.n_halo, plan.n_loc,
                                    plan.edge_id_base, plan.num_edges_total + rb, d)
@@ -84,10 +89,11 @@ def _worker(rank, world, port, bounds):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("mode", ["auto", "sparse", "dense"])
 @pytest.mark.parametrize("bounds", [[0, 120, 240], [0, 50, 170, 240], [0, 0, 100, 240]])
-def test_sharded_equals_single_process(bounds):
+def test_sharded_equals_single_process(bounds, mode):
     world = len(bounds) - 1
-    mp.spawn(_worker, args=(world, _free_port(), bounds), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, _free_port(), bounds, mode), nprocs=world, join=True)
 
 
 def test_single_shard_plan_is_identity():

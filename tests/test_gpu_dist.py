@@ -27,3 +27,65 @@ def test_world1_shard_equals_plain_graph():
     halo_exchange_into(X.detach(), X.detach(), torch.empty(0, 64, device=DEV), sg.plan)
     spmm_forward(X.detach(), sg.graph.with_dropedge(de), out=out)
     assert torch.equal(out, Z2)
+
+
+def _free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _shard_worker(rank, world, port, mode, kind):
+    """One rank of a 2-rank gloo world on the box's single GPU: the sharded
+    HIP path (halo plan, exchange, typed SpMM fwd+bwd) against the plain
+    one-GPU graph, which each rank also builds."""
+    import os
+
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        N, deg, L, F = 1 << 14, 24.0, 6, 64
+        sg = ShardedGraph.synthetic(N, deg, L, kind=kind, seed=4, device=DEV, halo=mode)
+        assert sg.plan.mode == mode
+        g = TypedGraph.synthetic(N, deg, L, kind=kind, seed=4, device=DEV)
+        rb, re = sg.plan.row_begin, sg.plan.row_end
+        X = torch.randn(N, F, generator=torch.Generator().manual_seed(11)).to(DEV)
+        dZ = torch.randn(N, (L + 1) * F, generator=torch.Generator().manual_seed(12)).to(DEV)
+        de = DropEdge(0.25, 5, 3)
+        Xg = X.clone().requires_grad_(True)
+        Zg = typed_aggregate(Xg, g.with_dropedge(de))
+        Zg.backward(dZ)
+        X_loc = X[rb:re].clone().requires_grad_(True)
+        Z = sg.aggregate(X_loc, de)
+        assert torch.equal(Z, Zg[rb:re])  # bitwise: same values, same edge order
+        Z.backward(dZ[rb:re])
+        # dX: partials from the two ranks add in peer order rather than CSC order; R-MAT hub
+        # columns sum thousands of terms, so use the north-star fp32 tolerance (1e-4)
+        torch.testing.assert_close(X_loc.grad, Xg.grad[rb:re], rtol=1e-5, atol=1e-4)
+        # the no-allocation bench form gives the same Z
+        p = sg.plan
+        X_ext = torch.zeros(p.n_loc + p.n_halo, F, device=DEV)
+        X_ext[: p.n_loc] = X[rb:re]
+        send = torch.empty(p.send_index.numel(), F, device=DEV)
+        halo_exchange_into(X_ext[: p.n_loc], X_ext, send, p)
+        out = torch.empty_like(Z)
+        spmm_forward(X_ext, sg.graph.with_dropedge(de), out=out)
+        assert torch.equal(out, Zg[rb:re].detach())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode,kind", [("sparse", "er"), ("dense", "er"), ("sparse", "rmat"), ("dense", "rmat")])
+def test_two_ranks_on_one_gpu_match_single_gpu(mode, kind):
+    """The N>1 path on real kernels (gloo moves the halo through host memory
+    here; the bench and product use RCCL)."""
+    import torch.multiprocessing as mp
+
+    mp.spawn(_shard_worker, args=(2, _free_port(), mode, kind), nprocs=2, join=True)
