@@ -54,8 +54,9 @@ def parse():
     ap.add_argument("--halo", choices=["auto", "sparse", "dense"], default="auto",
                     help="halo exchange layout for N>1 (grl/dist.py): sparse all-to-all-v of the referenced rows, "
                          "dense all-gather of every shard; auto picks dense when >=75%% of remote rows are referenced")
-    ap.add_argument("--only", choices=["fwd", "bwd", "linear", "layer"], default=None,
-                    help="profiling aid: run just that kernel K times (no JSON line)")
+    ap.add_argument("--only", choices=["fwd", "bwd", "linear", "layer", "c1"], default=None,
+                    help="profiling aid: run just that kernel K times (no JSON line); c1: print the C1 "
+                         "(debug.json model) timings alone")
     return ap.parse_args()
 
 
@@ -80,6 +81,10 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(args.dist_backend)
+
+    if args.only == "c1":
+        print(json.dumps({"c1_debug_json": c1_extras(dev, max(3, args.steps))}), flush=True)
+        return
 
     from grl import DropEdge
     from grl.dist import ShardedGraph, halo_exchange_into
@@ -189,6 +194,8 @@ def main():
         out["cpu_baseline"], out["parity"] = cpu_baseline(args, g_step, X_loc, Z, L, F)
     if args.extras:
         out["extras"] = extras(args, graph, X_full, gather, L, F, dev, E_loc, n_loc)
+        if rank == 0:
+            out["extras"]["c1_debug_json"] = c1_extras(dev)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -312,6 +319,79 @@ def extras(args, graph, X_full, gather, L, F, dev, E_loc, n_loc):
 
     res["graphconv_layer_fwd_bwd_p0.3"] = {"ms": _time(layer, max(2, iters // 2))}
     del Z, dZ, Zd
+    return res
+
+
+def c1_extras(dev, iters=20):
+    """GraphCNNDropEdge(4369, 53, 6, 256) on the
+    real debug.json page (N=74, 216 typed edges) built by the drop-in data
+    pipeline; eval latency (B=1) three ways, one Adam train step (B=4), and
+    the oracle's float64 numpy model (oracle/dense_ref.py) timed on the host
+    as the CPU baseline, with a logits parity check."""
+    from gnn.data_generator.data_process import HeuristicGraphBuilder, TextlineEncoding
+    from gnn.models import GraphCNNDropEdge
+    from oracle import dense_ref
+
+    assets = os.path.join(HERE, "tests", "golden", "assets")
+    with open(os.path.join(assets, "master_charset.json"), encoding="utf-8-sig") as f:
+        char_to_id = {c: i for i, c in enumerate(json.load(f)["charset"])}
+    with open(os.path.join(assets, "debug.json"), encoding="utf-8-sig") as f:
+        regions = json.load(f)
+    s = {"label": {i: dict(r, polygon=r["location"]) for i, r in enumerate(regions)}, "char_to_id": char_to_id}
+    s = HeuristicGraphBuilder(6, "normal_binary")(TextlineEncoding(True)(s))
+    V = torch.from_numpy(s["textline_encoding"])[None].to(dev)
+    A = torch.from_numpy(s["adjacency_matrix"].astype(np.float32))[None].to(dev)  # collate layout (B,N,L,N)
+    torch.manual_seed(0)
+    model = GraphCNNDropEdge(4369, 53, 6, 256).to(dev).eval()
+    res = {"nodes": int(V.shape[1]), "typed_edges": int((A != 0).sum())}
+    with torch.no_grad():
+        res["eval_ms_dense_A_in"] = _time(lambda: model([V, A]), iters)
+        graph = model.to_graph(A)
+        res["eval_ms_graph_prebuilt"] = _time(lambda: model([V, graph]), iters)
+        logits = model([V, graph]).double().cpu().numpy()
+        try:  # launch-bound at N=74: replay the whole forward as one HIP graph
+            side = torch.cuda.Stream(dev)
+            side.wait_stream(torch.cuda.current_stream(dev))
+            with torch.cuda.stream(side):
+                for _ in range(3):
+                    model([V, graph])
+            torch.cuda.current_stream(dev).wait_stream(side)
+            hg = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(hg):
+                out_static = model([V, graph])
+            hg.replay()
+            torch.cuda.synchronize()
+            res["eval_ms_hip_graph"] = _time(hg.replay, iters)
+            res["hip_graph_matches_eager"] = bool(torch.equal(out_static, model([V, graph])))
+        except Exception as err:  # report, never fall back silently
+            res["eval_ms_hip_graph"] = None
+            res["hip_graph_error"] = repr(err)[:200]
+    # CPU baseline (before the train steps below change the weights): the oracle's float64 restatement of the same forward
+    P = {k: v.detach().double().cpu().numpy() for k, v in model.state_dict().items()}
+    Vh, Ah = V.cpu().numpy(), A.cpu().numpy()
+    ref = dense_ref.graph_cnn_dropedge_forward(P, Vh, Ah)
+    t0, n = time.perf_counter(), 0
+    while time.perf_counter() - t0 < 2.0 or n < 3:
+        dense_ref.graph_cnn_dropedge_forward(P, Vh, Ah)
+        n += 1
+    res["cpu_eval_ms"] = (time.perf_counter() - t0) / n * 1e3
+    # train step, B=4 (the reference's training batch), Adam as BuitlinOptimizer builds it
+    model.train()
+    V4, A4 = V.expand(4, -1, -1).contiguous(), A.expand(4, -1, -1, -1).contiguous()
+    y4 = torch.randint(0, 53, (4, V.shape[1]), generator=torch.Generator().manual_seed(5)).to(dev)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    lossf = torch.nn.CrossEntropyLoss()
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        loss = lossf(model.forward([V4, A4]).reshape(-1, 53), y4.reshape(-1))
+        loss.backward()
+        opt.step()
+
+    res["train_step_ms_B4"] = _time(step, iters)
+    res["cpu_kind"] = "port: oracle/dense_ref.py float64 numpy dense model (A_pre materialised like the reference)"
+    res["logits_max_abs_diff_vs_oracle"] = float(np.abs(logits - ref).max())
+    res["tolerance"] = 1e-4
     return res
 
 

@@ -79,6 +79,28 @@ struct Operand {
   __device__ __forceinline__ int lds_off(int idx) const {
     return KC ? (idx / (BK / 4)) * LDK + (idx % (BK / 4)) * 4 : (idx / 32) * LDR + (idx % 32) * 4;
   }
+  __device__ __forceinline__ float4 load4(int64_t off) const {
+    float4 v = *reinterpret_cast<const float4*>(base + off);
+    if (MASK) v = masked(v, *reinterpret_cast<const float4*>(mask + off));
+    return v;
+  }
+  __device__ __forceinline__ float4 load_scalar(int64_t row, int64_t k, int64_t kend) const {
+    float t[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int64_t r = KC ? row : row + e;
+      const int64_t kk = KC ? k + e : k;
+      const bool ok = r < rows_total && kk < kend;
+      const int64_t off = ok ? (KC ? r * ld + kk : kk * ld + r) : 0;
+      float x = base[off];
+      if (MASK) x = mask[off] > 0.f ? x : 0.f;
+      t[e] = ok ? x : 0.f;
+    }
+    return make_float4(t[0], t[1], t[2], t[3]);
+  }
+  // interior: the whole tile is in range (no checks).  Edge tiles decide per
+  // float4 slot: all four elements valid -> one vector load; none -> zeros
+  // without a load; a ragged M/N or K tail -> per-element loads.
   __device__ __forceinline__ void fetch(int tid, int64_t k0, int64_t kend, bool interior) {
 #pragma unroll
     for (int it = 0; it < SLOTS; ++it) {
@@ -87,23 +109,18 @@ struct Operand {
       slot(tid + it * 256, row, kin);
       const int64_t k = k0 + kin;
       if (interior) {
-        const int64_t off = KC ? row * ld + k : k * ld + row;
-        float4 v = *reinterpret_cast<const float4*>(base + off);
-        if (MASK) v = masked(v, *reinterpret_cast<const float4*>(mask + off));
-        reg[it] = v;
+        reg[it] = load4(KC ? row * ld + k : k * ld + row);
+      } else if (ALIGNED) {
+        const bool none = row >= rows_total || k >= kend;
+        const bool full = KC ? (row < rows_total && k + 3 < kend) : (k < kend && row + 3 < rows_total);
+        if (full)
+          reg[it] = load4(KC ? row * ld + k : k * ld + row);
+        else if (none)
+          reg[it] = make_float4(0.f, 0.f, 0.f, 0.f);
+        else
+          reg[it] = load_scalar(row, k, kend);
       } else {
-        float t[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int64_t r = KC ? row : row + e;
-          const int64_t kk = KC ? k + e : k;
-          const bool ok = r < rows_total && kk < kend;
-          const int64_t off = ok ? (KC ? r * ld + kk : kk * ld + r) : 0;
-          float x = base[off];
-          if (MASK) x = mask[off] > 0.f ? x : 0.f;
-          t[e] = ok ? x : 0.f;
-        }
-        reg[it] = make_float4(t[0], t[1], t[2], t[3]);
+        reg[it] = load_scalar(row, k, kend);
       }
     }
   }
@@ -228,7 +245,24 @@ __global__ void slab_reduce_kernel(const float* __restrict__ slab, int64_t n, in
   }
 }
 
-// partial[z][c] = sum over rows [z*rows_per, ...) of g[r][c] * [mask[r][c] > 0]
+// Split-K epilogue of the forward / data-gradient GEMMs:
+// out[m*ldo + n] = epi(sum_{z < splits} slab[z][m][n] (+ bias[n])), split order.
+__global__ void slab_reduce_epi_kernel(const float* __restrict__ slab, int64_t M, int64_t N, int splits,
+                                       float* __restrict__ out, int64_t ldo, const float* __restrict__ bias,
+                                       int relu) {
+  const int64_t n_all = M * N;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_all; i += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.0f;
+    for (int z = 0; z < splits; ++z) s += slab[(int64_t)z * n_all + i];
+    const int64_t m = i / N, n = i - m * N;
+    if (bias) s += bias[n];
+    if (relu) s = s > 0.0f ? s : 0.0f;
+    out[m * ldo + n] = s;
+  }
+}
+
+// partial[z][c] = sum over rows [z*rows_per, ...) of g[r][c] * [mask[r][c] > 0],
+// added in row order; loads are issued 8 rows ahead of the adds (latency).
 __global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __restrict__ g, const float* __restrict__ mask,
                                                               int64_t M, int64_t C, int64_t rows_per,
                                                               float* __restrict__ partial) {
@@ -237,7 +271,18 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __rest
   if (c >= C) return;
   const int64_t r0 = z * rows_per, r1 = min(M, r0 + rows_per);
   float s = 0.0f;
-  for (int64_t r = r0; r < r1; ++r) {
+  int64_t r = r0;
+  for (; r + 8 <= r1; r += 8) {
+    float x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      x[u] = g[(r + u) * C + c];
+      if (mask) x[u] = mask[(r + u) * C + c] > 0.0f ? x[u] : 0.0f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += x[u];
+  }
+  for (; r < r1; ++r) {
     const float x = g[r * C + c];
     s += (!mask || mask[r * C + c] > 0.0f) ? x : 0.0f;
   }
@@ -278,13 +323,70 @@ int pick_splits(int64_t M, int64_t N, int64_t K) {
   return (int)std::max<int64_t>(1, std::min<int64_t>(s, 256));
 }
 
+// Split-K for an output-stationary GEMM (forward, data gradient) whose tiles
+// alone cannot fill the chip -- small graphs (a 74-node page is one 128-row
+// tile): a lone workgroup walking all of K is bound by load latency, not by
+// the matrix cores.  Large M (>= one tile per CU) never splits.
+int pick_splits_small(int64_t M, int64_t N, int64_t K) {
+  const int64_t tiles = ceil_div(M, BM) * ceil_div(N, BN);
+  const int64_t cus = device_cu_count();
+  if (tiles >= cus) return 1;
+  int64_t s = (2 * cus) / std::max<int64_t>(tiles, 1);
+  s = std::min<int64_t>(s, ceil_div(K, GEMM_BK));  // >= one K tile per split
+  return (int)std::max<int64_t>(1, std::min<int64_t>(s, 64));
+}
+
+// row blocks of the db column sum: ~512 rows each (>= 1 block, <= 1024)
+int colsum_splits(int64_t M) { return (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(M, 512), 1024)); }
+
+size_t small_ws_bytes(int64_t M, int64_t N, int64_t K) {
+  const int s = pick_splits_small(M, N, K);
+  return s > 1 ? (size_t)s * (size_t)M * (size_t)N * 4 + 256 : 0;
+}
+
+// Output-stationary GEMM with optional split-K through `ws` (slab layout
+// [split][M][N], then one ordered reduce applying bias / ReLU).
+template <bool A_KC, bool B_KC>
+int run_output_gemm(GemmArgs a, bool aligned, const char* who, void* ws, size_t ws_bytes, hipStream_t st) {
+  const int splits = pick_splits_small(a.M, a.N, a.K);
+  if (splits == 1) {
+    a.k_per_split = std::max<int64_t>(a.K, 1);
+    return a.bias || a.relu ? launch_gemm<A_KC, B_KC, EPI_BIAS>(a, 1, aligned, st)
+                            : launch_gemm<A_KC, B_KC, EPI_STORE>(a, 1, aligned, st);
+  }
+  const size_t need = small_ws_bytes(a.M, a.N, a.K);
+  if (!ws || ws_bytes < need) GRL_FAIL(GRL_E_WORKSPACE, "%s: workspace %zu < %zu", who, ws_bytes, need);
+  float* out = a.C;
+  const int64_t ldo = a.ldc;
+  const float* bias = a.bias;
+  const int relu = a.relu;
+  a.C = static_cast<float*>(ws);
+  a.ldc = a.N;
+  a.bias = nullptr;
+  a.relu = 0;
+  a.k_per_split = ceil_div(ceil_div(a.K, splits), GEMM_BK) * GEMM_BK;
+  const int used = (int)ceil_div(a.K, a.k_per_split);  // trailing splits may be empty
+  int rc = launch_gemm<A_KC, B_KC, EPI_SLAB>(a, used, aligned, st);
+  if (rc) return rc;
+  const int64_t n = a.M * a.N;
+  hipLaunchKernelGGL(slab_reduce_epi_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(n, 256), 4096)), dim3(256), 0,
+                     st, a.C, a.M, a.N, used, out, ldo, bias, relu);
+  GRL_LAUNCH_CHECK();
+  return GRL_OK;
+}
+
 }  // namespace
 }  // namespace grl
 
 using namespace grl;
 
+extern "C" size_t grl_linear_fwd_workspace_size(int64_t M, int32_t K, int32_t C) {
+  return M > 0 && K > 0 && C > 0 ? small_ws_bytes(M, C, K) : 0;
+}
+
 extern "C" int grl_linear_fwd(const float* Z, int64_t ldz, const float* W, const float* bias, float* out, int64_t M,
-                              int32_t K, int32_t C, int32_t relu, grl_stream_t stream) {
+                              int32_t K, int32_t C, int32_t relu, void* workspace, size_t workspace_bytes,
+                              grl_stream_t stream) {
   GRL_CHECK_ARG(M >= 0 && K >= 0 && C >= 0, "grl_linear_fwd: negative size");
   GRL_CHECK_ARG(ldz >= K, "grl_linear_fwd: ldz (%lld) < K (%d)", (long long)ldz, K);
   if (M == 0 || C == 0) return GRL_OK;
@@ -300,14 +402,18 @@ extern "C" int grl_linear_fwd(const float* Z, int64_t ldz, const float* W, const
   a.M = M;
   a.N = C;
   a.K = K;
-  a.k_per_split = std::max<int64_t>(K, 1);
   a.relu = relu;
   const bool aligned = al16(Z) && al16(W) && ldz % 4 == 0 && C % 4 == 0 && K % 4 == 0;
-  return launch_gemm<true, false, EPI_BIAS>(a, 1, aligned, as_stream(stream));
+  return run_output_gemm<true, false>(a, aligned, "grl_linear_fwd", workspace, workspace_bytes, as_stream(stream));
+}
+
+extern "C" size_t grl_linear_bwd_data_workspace_size(int64_t M, int32_t K, int32_t C) {
+  return M > 0 && K > 0 && C > 0 ? small_ws_bytes(M, K, C) : 0;
 }
 
 extern "C" int grl_linear_bwd_data(const float* g, const float* relu_out, const float* W, float* dZ, int64_t lddz,
-                                   int64_t M, int32_t K, int32_t C, grl_stream_t stream) {
+                                   int64_t M, int32_t K, int32_t C, void* workspace, size_t workspace_bytes,
+                                   grl_stream_t stream) {
   GRL_CHECK_ARG(M >= 0 && K >= 0 && C >= 0 && lddz >= K, "grl_linear_bwd_data: bad sizes");
   if (M == 0 || K == 0) return GRL_OK;
   GRL_CHECK_ARG(g && W && dZ, "grl_linear_bwd_data: NULL pointer");
@@ -322,14 +428,14 @@ extern "C" int grl_linear_bwd_data(const float* g, const float* relu_out, const 
   a.M = M;
   a.N = K;
   a.K = C;
-  a.k_per_split = std::max<int64_t>(C, 1);
   const bool aligned = al16(g) && al16(W) && (!relu_out || al16(relu_out)) && C % 4 == 0;
-  return launch_gemm<true, true, EPI_STORE>(a, 1, aligned, as_stream(stream));
+  return run_output_gemm<true, true>(a, aligned, "grl_linear_bwd_data", workspace, workspace_bytes,
+                                     as_stream(stream));
 }
 
 extern "C" size_t grl_linear_bwd_weight_workspace_size(int64_t M, int32_t K, int32_t C) {
   const int s = pick_splits(K, C, M);
-  const int zs = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(M, 4096), 1024));
+  const int zs = colsum_splits(M);
   return (size_t)s * (size_t)K * (size_t)C * 4 + (size_t)zs * (size_t)C * 4 + 512;
 }
 
@@ -368,7 +474,7 @@ extern "C" int grl_linear_bwd_weight(const float* Z, int64_t ldz, const float* g
     GRL_LAUNCH_CHECK();
   }
   if (db) {
-    const int zs = (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(M, 4096), 1024));
+    const int zs = colsum_splits(M);
     float* part = slab + (size_t)splits * K * C;
     const int64_t rows_per = ceil_div(std::max<int64_t>(M, 1), zs);
     hipLaunchKernelGGL(colsum_partial_kernel, dim3((unsigned)ceil_div(C, 256), (unsigned)zs), dim3(256), 0, st, g,

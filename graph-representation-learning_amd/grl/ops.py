@@ -81,8 +81,11 @@ def linear_fwd(Z2: torch.Tensor, W: torch.Tensor, b, relu: bool) -> torch.Tensor
     M, K = Z2.shape
     C = W.shape[1]
     out = torch.empty(M, C, dtype=torch.float32, device=Z2.device)
+    ws_bytes = _lib.lib().grl_linear_fwd_workspace_size(M, K, C)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=Z2.device) if ws_bytes else None
     call("grl_linear_fwd", Z2.data_ptr(), Z2.stride(0), W.data_ptr(), b.data_ptr() if b is not None else None,
-         out.data_ptr(), M, K, C, int(relu), current_stream_handle(Z2.device))
+         out.data_ptr(), M, K, C, int(relu), ws.data_ptr() if ws is not None else None, ws_bytes,
+         current_stream_handle(Z2.device))
     return out
 
 
@@ -90,8 +93,11 @@ def linear_bwd_data(g: torch.Tensor, relu_out, W: torch.Tensor) -> torch.Tensor:
     M, C = g.shape
     K = W.shape[0]
     dZ = torch.empty(M, K, dtype=torch.float32, device=g.device)
+    ws_bytes = _lib.lib().grl_linear_bwd_data_workspace_size(M, K, C)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=g.device) if ws_bytes else None
     call("grl_linear_bwd_data", g.data_ptr(), relu_out.data_ptr() if relu_out is not None else None, W.data_ptr(),
-         dZ.data_ptr(), K, M, K, C, current_stream_handle(g.device))
+         dZ.data_ptr(), K, M, K, C, ws.data_ptr() if ws is not None else None, ws_bytes,
+         current_stream_handle(g.device))
     return dZ
 
 

@@ -177,10 +177,17 @@ int grl_typed_spmm_bwd(const GrlTypedCsc* g, const float* dZ, int32_t F,
  * Replaces torch.matmul(new_V, self.h_weights) + self.bias
  * (robust_gcn.py:50) and, with relu = 1, the F.relu around the layer
  * (drop_robust_gcn.py:76).  Z [M, K] row-major (ldz), W [K, C] row-major,
- * bias [C] or NULL, out [M, C] contiguous.                                */
+ * bias [C] or NULL, out [M, C] contiguous.
+ * When the output tiles cannot fill the chip (small graphs: a 74-node page
+ * is one 128-row tile) K is split over workgroups into fp32 slabs in
+ * `workspace`, added in split order (deterministic) with bias/ReLU applied
+ * once; grl_linear_fwd_workspace_size() is 0 when no split is taken (the
+ * workspace may then be NULL), else the bytes the call requires.          */
+size_t grl_linear_fwd_workspace_size(int64_t M, int32_t K, int32_t C);
 int grl_linear_fwd(const float* Z, int64_t ldz, const float* W,
                    const float* bias, float* out, int64_t M, int32_t K,
-                   int32_t C, int32_t relu, grl_stream_t stream);
+                   int32_t C, int32_t relu, void* workspace,
+                   size_t workspace_bytes, grl_stream_t stream);
 
 /* Backward of grl_linear_fwd (autograd MmBackward0 of robust_gcn.py:50, with
  * the ReLU of drop_robust_gcn.py:76 folded in when relu_out != NULL):
@@ -189,9 +196,13 @@ int grl_linear_fwd(const float* Z, int64_t ldz, const float* W,
  *   db = sum over rows of (g * [relu_out > 0])                     db [C] (or NULL)
  * g, relu_out: [M, C] contiguous (relu_out = the forward's ReLU output).
  * dW's reduction over M is split over workgroups into fp32 slabs (workspace)
- * added in split order: deterministic, no atomics.                          */
+ * added in split order: deterministic, no atomics.  dZ splits its short
+ * reduction (C) the same way when M is small (workspace rule as
+ * grl_linear_fwd).                                                          */
+size_t grl_linear_bwd_data_workspace_size(int64_t M, int32_t K, int32_t C);
 int grl_linear_bwd_data(const float* g, const float* relu_out, const float* W,
                         float* dZ, int64_t lddz, int64_t M, int32_t K, int32_t C,
+                        void* workspace, size_t workspace_bytes,
                         grl_stream_t stream);
 size_t grl_linear_bwd_weight_workspace_size(int64_t M, int32_t K, int32_t C);
 int grl_linear_bwd_weight(const float* Z, int64_t ldz, const float* g,
