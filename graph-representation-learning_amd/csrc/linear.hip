@@ -79,28 +79,6 @@ struct Operand {
   __device__ __forceinline__ int lds_off(int idx) const {
     return KC ? (idx / (BK / 4)) * LDK + (idx % (BK / 4)) * 4 : (idx / 32) * LDR + (idx % 32) * 4;
   }
-  __device__ __forceinline__ float4 load4(int64_t off) const {
-    float4 v = *reinterpret_cast<const float4*>(base + off);
-    if (MASK) v = masked(v, *reinterpret_cast<const float4*>(mask + off));
-    return v;
-  }
-  __device__ __forceinline__ float4 load_scalar(int64_t row, int64_t k, int64_t kend) const {
-    float t[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int64_t r = KC ? row : row + e;
-      const int64_t kk = KC ? k + e : k;
-      const bool ok = r < rows_total && kk < kend;
-      const int64_t off = ok ? (KC ? r * ld + kk : kk * ld + r) : 0;
-      float x = base[off];
-      if (MASK) x = mask[off] > 0.f ? x : 0.f;
-      t[e] = ok ? x : 0.f;
-    }
-    return make_float4(t[0], t[1], t[2], t[3]);
-  }
-  // interior: the whole tile is in range (no checks).  Edge tiles decide per
-  // float4 slot: all four elements valid -> one vector load; none -> zeros
-  // without a load; a ragged M/N or K tail -> per-element loads.
   __device__ __forceinline__ void fetch(int tid, int64_t k0, int64_t kend, bool interior) {
 #pragma unroll
     for (int it = 0; it < SLOTS; ++it) {
@@ -109,18 +87,23 @@ struct Operand {
       slot(tid + it * 256, row, kin);
       const int64_t k = k0 + kin;
       if (interior) {
-        reg[it] = load4(KC ? row * ld + k : k * ld + row);
-      } else if (ALIGNED) {
-        const bool none = row >= rows_total || k >= kend;
-        const bool full = KC ? (row < rows_total && k + 3 < kend) : (k < kend && row + 3 < rows_total);
-        if (full)
-          reg[it] = load4(KC ? row * ld + k : k * ld + row);
-        else if (none)
-          reg[it] = make_float4(0.f, 0.f, 0.f, 0.f);
-        else
-          reg[it] = load_scalar(row, k, kend);
+        const int64_t off = KC ? row * ld + k : k * ld + row;
+        float4 v = *reinterpret_cast<const float4*>(base + off);
+        if (MASK) v = masked(v, *reinterpret_cast<const float4*>(mask + off));
+        reg[it] = v;
       } else {
-        reg[it] = load_scalar(row, k, kend);
+        float t[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int64_t r = KC ? row : row + e;
+          const int64_t kk = KC ? k + e : k;
+          const bool ok = r < rows_total && kk < kend;
+          const int64_t off = ok ? (KC ? r * ld + kk : kk * ld + r) : 0;
+          float x = base[off];
+          if (MASK) x = mask[off] > 0.f ? x : 0.f;
+          t[e] = ok ? x : 0.f;
+        }
+        reg[it] = make_float4(t[0], t[1], t[2], t[3]);
       }
     }
   }
@@ -236,13 +219,27 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs p) {
   }
 }
 
+// sum_{z < splits} slab[z*stride + i] in split order; loads are issued 8
+// slabs ahead of the adds (a chain of dependent loads is latency-bound).
+__device__ __forceinline__ float ordered_slab_sum(const float* __restrict__ slab, int64_t stride, int splits,
+                                                  int64_t i) {
+  float s = 0.0f;
+  int z = 0;
+  for (; z + 8 <= splits; z += 8) {
+    float x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) x[u] = slab[(int64_t)(z + u) * stride + i];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += x[u];
+  }
+  for (; z < splits; ++z) s += slab[(int64_t)z * stride + i];
+  return s;
+}
+
 // out[i] = sum_{z < splits} slab[z][i]  (split order: deterministic)
 __global__ void slab_reduce_kernel(const float* __restrict__ slab, int64_t n, int splits, float* __restrict__ out) {
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    float s = 0.0f;
-    for (int z = 0; z < splits; ++z) s += slab[(int64_t)z * n + i];
-    out[i] = s;
-  }
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = ordered_slab_sum(slab, n, splits, i);
 }
 
 // Split-K epilogue of the forward / data-gradient GEMMs:
@@ -252,8 +249,7 @@ __global__ void slab_reduce_epi_kernel(const float* __restrict__ slab, int64_t M
                                        int relu) {
   const int64_t n_all = M * N;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_all; i += (int64_t)gridDim.x * blockDim.x) {
-    float s = 0.0f;
-    for (int z = 0; z < splits; ++z) s += slab[(int64_t)z * n_all + i];
+    float s = ordered_slab_sum(slab, n_all, splits, i);
     const int64_t m = i / N, n = i - m * N;
     if (bias) s += bias[n];
     if (relu) s = s > 0.0f ? s : 0.0f;
@@ -336,8 +332,8 @@ int pick_splits_small(int64_t M, int64_t N, int64_t K) {
   return (int)std::max<int64_t>(1, std::min<int64_t>(s, 64));
 }
 
-// row blocks of the db column sum: ~512 rows each (>= 1 block, <= 1024)
-int colsum_splits(int64_t M) { return (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(M, 512), 1024)); }
+// row blocks of the db column sum: ~64 rows each (>= 1 block, <= 1024)
+int colsum_splits(int64_t M) { return (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(M, 64), 1024)); }
 
 size_t small_ws_bytes(int64_t M, int64_t N, int64_t K) {
   const int s = pick_splits_small(M, N, K);

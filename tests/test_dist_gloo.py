@@ -117,3 +117,27 @@ def test_edge_balanced_bounds():
         assert max(loads) - min(loads) <= 2 * int(deg.max()) + 1, loads
     b = edge_balanced_bounds(torch.zeros(5, dtype=torch.int32), 3)  # degenerate: no edges at all
     assert b[0] == 0 and b[-1] == 5 and b == sorted(b) and len(b) == 4
+
+
+def _allreduce_worker(rank, world, port):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from grl.dist import allreduce_gradients
+
+        ps = [torch.nn.Parameter(torch.zeros(s)) for s in [(7, 3), (5,), (1000,), (2, 2)]]
+        for i, p in enumerate(ps):
+            p.grad = torch.full_like(p, float(rank + 1) * (i + 1))
+        ps[3].grad = None  # parameters without a gradient are skipped
+        allreduce_gradients(ps, bucket_bytes=4 * 40)  # forces several buckets
+        tot = sum(r + 1 for r in range(world))
+        for i, p in enumerate(ps[:3]):
+            assert torch.equal(p.grad, torch.full_like(p, float(tot * (i + 1))))
+        assert ps[3].grad is None
+    finally:
+        dist.destroy_process_group()
+
+
+def test_allreduce_gradients_buckets():
+    mp.spawn(_allreduce_worker, args=(3, _free_port()), nprocs=3, join=True)

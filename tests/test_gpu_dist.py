@@ -78,6 +78,21 @@ def _shard_worker(rank, world, port, mode, kind):
         out = torch.empty_like(Z)
         spmm_forward(X_ext, sg.graph.with_dropedge(de), out=out)
         assert torch.equal(out, Zg[rb:re].detach())
+        # a whole sharded GraphConv layer: weight grads summed over ranks equal one GPU's
+        from gnn.models import GraphConv
+        from grl.dist import allreduce_gradients
+
+        torch.manual_seed(21)
+        layer = GraphConv(F, 48, L).to(DEV)
+        torch.manual_seed(21)
+        layer1 = GraphConv(F, 48, L).to(DEV)
+        R = torch.randn(N, 48, generator=torch.Generator().manual_seed(13)).to(DEV)
+        (layer1.propagate(X[None], g.with_dropedge(de), relu=True)[0] * R).sum().backward()
+        out_loc = sg.graphconv(X[rb:re], layer, de, relu=True)
+        (out_loc * R[rb:re]).sum().backward()
+        allreduce_gradients(layer.parameters())
+        torch.testing.assert_close(layer.h_weights.grad, layer1.h_weights.grad, rtol=1e-4, atol=1e-4)
+        torch.testing.assert_close(layer.bias.grad, layer1.bias.grad, rtol=1e-4, atol=1e-4)
     finally:
         dist.destroy_process_group()
 
