@@ -56,8 +56,14 @@ class GNNLearningWarper:
     @staticmethod
     def _prepare(cfg: AttrDict) -> AttrDict:
         if cfg.get("distributed"):
-            torch.cuda.set_device(cfg.local_rank)
-            torch.distributed.init_process_group(backend="nccl", init_method="env://")
+            # cl_warper.py:73-75.  local_rank maps onto the visible devices (several
+            # ranks may share one GPU in tests); the group is created unless the
+            # caller already did; `dist_backend` (additive, default "nccl" = RCCL).
+            n = torch.cuda.device_count()
+            if n:
+                torch.cuda.set_device(int(cfg.local_rank) % n)
+            if not torch.distributed.is_initialized():
+                torch.distributed.init_process_group(backend=cfg.get("dist_backend", "nccl"), init_method="env://")
         torch.backends.cudnn.benchmark = bool(cfg.get("benchmark", False))
         torch.backends.cudnn.deterministic = bool(cfg.get("deterministic", False))
         return cfg

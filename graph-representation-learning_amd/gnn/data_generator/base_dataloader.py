@@ -64,7 +64,7 @@ class BaseDataLoader:
             batch_size = data_config.get("batch_size", 1)
             sampler = None
             if distributed:
-                batch_size = batch_size // self.config.num_gpus
+                batch_size = max(1, batch_size // self.config.num_gpus)  # the reference can reach 0 here
                 sampler = DistributedSampler(dataset, num_replicas=self.config.num_gpus,
                                              rank=self.config.local_rank, shuffle=bool(data_config.get("shuffle")))
             return DataLoader(dataset, batch_size=batch_size, num_workers=data_config.get("num_workers", 0),

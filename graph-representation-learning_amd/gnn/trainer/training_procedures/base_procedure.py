@@ -1,7 +1,14 @@
 """Shared training setup (the reference's trainer BaseProcedure,
 gnn/trainer/training_procedures/base_procedure.py:14-197): output dir,
 device choice from num_gpus, checkpoint restore (strict=False), and the
-criterion / optimizer / LR schedule resolved by name from config."""
+criterion / optimizer / LR schedule resolved by name from config.
+
+Data parallel over documents (`distributed: true`, the reference's
+declared-but-broken DDP, base_procedure.py:79-93 / cl_warper.py:73-75):
+each rank trains on its DistributedSampler shard; parameters and buffers
+are broadcast from rank 0 once, and after every backward the gradients are
+averaged over the ranks with one bucketed all-reduce (RCCL), so the
+replicas stay identical.  Only rank 0 writes checkpoints."""
 from __future__ import annotations
 
 import logging
@@ -35,8 +42,15 @@ class BaseProcedure:
         self.ems_exp = ems_exp
         self.model_dir = self._make_output_dir()
         self.checkpointer = CheckpointHandler()
+        self.distributed = bool(config.get("distributed")) and torch.distributed.is_available() \
+            and torch.distributed.is_initialized()
+        self.rank = torch.distributed.get_rank() if self.distributed else 0
         self.device, self.device_ids = self._prepare_device(config.get("num_gpus", 1))
         self.model = self._load_prev_checkpoint(model).to(self.device)
+        if self.distributed:
+            from grl.dist import broadcast_module
+
+            broadcast_module(self.model, src=0)
         self.criterion = self._init_criterion()
         self.optimizer = self._init_optimizer()
         self.lr_scheduler = self._init_lr_scheduler()
@@ -52,7 +66,16 @@ class BaseProcedure:
             self.logger.warning("There's no GPU available on this machine; the MI355X engine will refuse CPU tensors.")
             n_gpu_use = 0
         n_gpu_use = min(n_gpu_use, n_gpu)
+        if self.distributed and n_gpu > 0:
+            return torch.device("cuda", torch.cuda.current_device()), [torch.cuda.current_device()]
         return torch.device("cuda:0" if n_gpu_use > 0 else "cpu"), list(range(n_gpu_use))
+
+    def _sync_gradients(self) -> None:
+        """DDP's gradient averaging, as one bucketed all-reduce per step."""
+        if self.distributed:
+            from grl.dist import allreduce_gradients
+
+            allreduce_gradients(self.model.parameters(), average=True)
 
     @staticmethod
     def _resolve(module, section: Dict[str, Any], what: str):

@@ -86,6 +86,7 @@ class KVProcedure(BaseProcedure):
         with torch.set_grad_enabled(True):
             loss, scores, items = self._step_process(batch, **kwargs)
             loss.backward()
+            self._sync_gradients()
             nn.utils.clip_grad_norm_(self.model.parameters(), self.config.max_grad_norm)
             self.optimizer.step()
         return scores, items
@@ -146,8 +147,9 @@ class KVProcedure(BaseProcedure):
                 self._update_learning_rate(epoch, self.global_step)
             if metrics["loss"] < best:
                 best = metrics["loss"]
-                self.checkpointer.save_checkpoint(
-                    {"epoch": epoch, "config": to_plain(self.config), "meta_data": to_plain(metrics),
-                     "state_dict": self.model.state_dict()}, self.model_dir)
+                if self.rank == 0:
+                    self.checkpointer.save_checkpoint(
+                        {"epoch": epoch, "config": to_plain(self.config), "meta_data": to_plain(metrics),
+                         "state_dict": self.model.state_dict()}, self.model_dir)
         self.tb_writer.close()
         return metrics["f1-score"]

@@ -236,14 +236,28 @@ def halo_exchange_into(X_loc: torch.Tensor, X_ext: torch.Tensor, send_buf: torch
     all_to_all_v(X_ext[plan.n_loc:], send_buf, plan.recv_counts, plan.send_counts, group)
 
 
-def allreduce_gradients(params, group=None, bucket_bytes: int = 64 << 20) -> None:
+def broadcast_module(module: torch.nn.Module, src: int = 0, group=None) -> None:
+    """Copy `src`'s parameters and buffers to every rank (replica start)."""
+    if _world(group) == 1:
+        return
+    for t in list(module.parameters()) + list(module.buffers()):
+        if _host_staged(group) and t.is_cuda:
+            h = t.detach().cpu()
+            dist.broadcast(h, src, group=group)
+            t.data.copy_(h)
+        else:
+            dist.broadcast(t.data, src, group=group)
+
+
+def allreduce_gradients(params, group=None, bucket_bytes: int = 64 << 20, average: bool = False) -> None:
     """Sum the .grad of `params` over the ranks of `group` in place.
 
     With node-range shards every rank's weight gradient of a GraphConv
     (dW = Z_r^T g_r, db = colsum g_r) is a partial sum over its own rows, so
     one all_reduce per step completes it (1.8 MB for gcn1 at
     d=256).  Gradients are packed into flat fp32 buckets of <= bucket_bytes
-    (one RCCL call each; all of GraphCNNDropEdge's fit one bucket)."""
+    (one RCCL call each; all of GraphCNNDropEdge's fit one bucket).
+    average=True divides by the world size (data parallelism's mean)."""
     if _world(group) == 1:
         return
     grads = [p.grad for p in params if p.grad is not None]
@@ -255,6 +269,8 @@ def allreduce_gradients(params, group=None, bucket_bytes: int = 64 << 20) -> Non
         if not bucket:
             return
         flat = torch.cat([g.reshape(-1) for g in bucket])
+        if average:
+            flat.div_(_world(group))
         if _host_staged(group) and flat.is_cuda:
             h = flat.cpu()
             dist.all_reduce(h, group=group)

@@ -135,6 +135,16 @@ def _allreduce_worker(rank, world, port):
         for i, p in enumerate(ps[:3]):
             assert torch.equal(p.grad, torch.full_like(p, float(tot * (i + 1))))
         assert ps[3].grad is None
+        q = torch.nn.Parameter(torch.zeros(3))
+        q.grad = torch.full((3,), float(rank + 1))
+        allreduce_gradients([q], average=True)
+        assert torch.allclose(q.grad, torch.full((3,), tot / world))
+        from grl.dist import broadcast_module
+
+        m = torch.nn.Linear(3, 2)
+        torch.nn.init.constant_(m.weight, float(rank))
+        broadcast_module(m, src=0)
+        assert torch.equal(m.weight, torch.zeros(2, 3))
     finally:
         dist.destroy_process_group()
 

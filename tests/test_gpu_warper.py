@@ -81,3 +81,38 @@ def test_predict_matches_reference_logits(golden, tmp_path):
     # handle_single_input when given as a JSON path
     one = warper.predict(os.path.join(ASSETS, "debug.json"))
     assert len(one) == 74
+
+
+def _dp_worker(rank, world, port, cfg):
+    """One rank of data-parallel warper training (distributed: true): two gloo
+    ranks sharing the box's GPU; replicas must end bitwise identical."""
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    cfg.distributed, cfg.num_gpus, cfg.local_rank, cfg.dist_backend = True, world, rank, "gloo"
+    torch.manual_seed(100 + rank)  # different inits: the procedure must broadcast rank 0's
+    model = GraphCNNDropEdge(4369, 15, 6, net_size=32)
+    warper = GNNLearningWarper(model, config=cfg)
+    assert dist.is_initialized() and warper.trainer.distributed
+    f1 = warper.train()
+    assert 0.0 <= f1 <= 1.0
+    assert warper.trainer.global_step == 3  # 5 docs / 2 ranks -> 3 per rank, per-rank batch 2 // 2 = 1
+    flat = torch.cat([p.detach().reshape(-1).cpu() for p in model.parameters()])
+    gathered = [torch.empty_like(flat) for _ in range(world)]
+    dist.all_gather(gathered, flat)
+    assert torch.equal(gathered[0], gathered[1])
+    dist.destroy_process_group()
+
+
+def test_data_parallel_training_keeps_replicas_identical(tmp_path):
+    import socket
+
+    import torch.multiprocessing as mp
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cfg = make_config(str(tmp_path), epochs=1)  # writes the dataset once, before the ranks start
+    mp.spawn(_dp_worker, args=(2, port, cfg), nprocs=2, join=True)
