@@ -1,0 +1,398 @@
+// NodeSelfAtten (gnn/models/networks/robust_gcn.py:78-99) as fused fp32
+// MFMA kernels, flash-style: the B x N x N score matrix never exists.
+//
+//   S = Q K^T            Q = f(V), K = g(V): [B, N, dk]   (no 1/sqrt(dk), :94)
+//   P = softmax_rows(S)                                    (:84, :94)
+//   out = gamma * (P H) + V                                (:95-96), H = h(V): [B, N, dv]
+//
+// Layout trick.  With v_mfma_f32_32x32x2_f32 the accumulator's column is the
+// lane (lane & 31) and its rows live in registers.  We compute the
+// TRANSPOSED products S^T = K Q^T and O^T = H^T P^T, so every lane owns one
+// query: the online-softmax max / sum are in-lane over 16 registers plus one
+// exchange with lane ^ 32 (the two half-waves hold the two key halves), and
+// the rescale of O^T is lane-local.  The P registers feed the second MFMA
+// directly as its B operand when the k index of step s in half h is the key
+// kappa(s, h) = (s & 3) + 8 (s >> 2) + 4 h -- exactly the key that register s
+// of that half holds.  Products are exact fp32; sums are fp32.
+//
+// Backward (deterministic, no atomics), with dO = gamma * d_out and
+// D = rowsum(dO * O_norm) precomputed on the host side:
+//   kernel A (query-stationary): recompute P, dP^T = H dO^T, dS = P (dP - D),
+//            dQ^T += K^T dS^T
+//   kernel B (key-stationary):   recompute S with keys on lanes, dP likewise,
+//            dH^T += dO^T P,  dK^T += Q^T dS
+#include "grl_internal.h"
+
+#include <math.h>
+
+namespace grl {
+namespace {
+
+using f32x16 = __attribute__((ext_vector_type(16))) float;
+
+struct AttnArgs {
+  const float* Q;      // [B, N, dk]
+  const float* K;      // [B, N, dk]
+  const float* H;      // [B, N, dv]
+  const float* V;      // [B, N, dv] residual
+  const float* gamma;  // [dv]
+  float* out;          // [B, N, dv]
+  float* onorm;        // [B, N, dv] or NULL: P H (normalised)
+  float* rmax;         // [B, N] or NULL
+  float* rsum;         // [B, N] or NULL
+  const float* dO;     // [B, N, dv]  gamma * d_out
+  const float* Drow;   // [B, N]      rowsum(dO * onorm)
+  const float* smax;   // [B, N]      saved row max
+  const float* ssum;   // [B, N]      saved row sum
+  float* dQ;           // [B, N, dk]
+  float* dK;           // [B, N, dk]
+  float* dH;           // [B, N, dv]
+  int64_t N;
+  int dk, dv;
+};
+
+__device__ __forceinline__ int kappa(int s, int h) { return (s & 3) + 8 * (s >> 2) + 4 * h; }
+
+__device__ __forceinline__ f32x16 zero16() {
+  f32x16 z;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) z[r] = 0.0f;
+  return z;
+}
+
+#define MFMA(a, b, c) __builtin_amdgcn_mfma_f32_32x32x2f32((a), (b), (c), 0, 0, 0)
+
+// Stage rows [r0, r0+32) of a [N, width] matrix into LDS tile[32][ld] with
+// zero fill beyond N and beyond `width` (up to `padw` columns).
+__device__ __forceinline__ void stage(float* tile, int ld, int padw, const float* src, int64_t r0, int64_t N,
+                                      int width, int tid) {
+  for (int i = tid; i < 32 * padw; i += 256) {
+    const int r = i / padw, c = i - r * padw;
+    const int64_t row = r0 + r;
+    tile[r * ld + c] = (row < N && c < width) ? src[row * width + c] : 0.0f;
+  }
+}
+
+template <int DKP, int NT>
+__global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
+  constexpr int KS = DKP / 2, DV = NT * 32, LDK = DKP + 4;
+  __shared__ float Ks[32 * LDK];
+  __shared__ float Hs[32 * DV];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, h = lane >> 5;
+  const int64_t N = a.N, b = blockIdx.y;
+  const float* Qb = a.Q + b * N * a.dk;
+  const float* Kb = a.K + b * N * a.dk;
+  const float* Hb = a.H + b * N * a.dv;
+  const int64_t q = (int64_t)blockIdx.x * 128 + wave * 32 + l32;
+
+  float qr[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int d = h * KS + s;
+    qr[s] = (q < N && d < a.dk) ? Qb[q * a.dk + d] : 0.0f;
+  }
+  f32x16 o[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) o[t] = zero16();
+  float m = -INFINITY, l = 0.0f;
+
+  for (int64_t k0 = 0; k0 < N; k0 += 32) {
+    stage(Ks, LDK, DKP, Kb, k0, N, a.dk, tid);
+    stage(Hs, DV, DV, Hb, k0, N, a.dv, tid);
+    __syncthreads();
+    f32x16 s = zero16();
+#pragma unroll
+    for (int st = 0; st < KS; ++st) s = MFMA(Ks[l32 * LDK + h * KS + st], qr[st], s);
+    float mx = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      if (k0 + kappa(r, h) >= N) s[r] = -INFINITY;
+      mx = fmaxf(mx, s[r]);
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    const float mn = fmaxf(m, mx);
+    const float alpha = expf(m - mn);
+    float ps = 0.0f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      s[r] = expf(s[r] - mn);
+      ps += s[r];
+    }
+    ps += __shfl_xor(ps, 32);
+    l = l * alpha + ps;
+    m = mn;
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
+#pragma unroll
+      for (int st = 0; st < 16; ++st) o[t] = MFMA(Hs[kappa(st, h) * DV + t * 32 + l32], s[st], o[t]);
+    }
+    __syncthreads();
+  }
+
+  if (q < N) {
+    const float inv = 1.0f / l;
+    const int64_t base = (b * N + q) * a.dv;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int f = t * 32 + kappa(r, h);
+        if (f < a.dv) {
+          const float on = o[t][r] * inv;
+          a.out[base + f] = a.gamma[f] * on + a.V[base + f];
+          if (a.onorm) a.onorm[base + f] = on;
+        }
+      }
+    if (h == 0 && a.rmax) {
+      a.rmax[b * N + q] = m;
+      a.rsum[b * N + q] = l;
+    }
+  }
+}
+
+// dQ: one wave per 32 queries, loop over key blocks.
+template <int DKP, int NT>
+__global__ __launch_bounds__(256) void attn_bwd_q_kernel(AttnArgs a) {
+  constexpr int KS = DKP / 2, DV = NT * 32, HV = DV / 2, LDK = DKP + 4;
+  __shared__ float Ks[32 * LDK];
+  __shared__ float Hs[32 * DV];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, h = lane >> 5;
+  const int64_t N = a.N, b = blockIdx.y;
+  const float* Kb = a.K + b * N * a.dk;
+  const float* Hb = a.H + b * N * a.dv;
+  const int64_t q = (int64_t)blockIdx.x * 128 + wave * 32 + l32;
+  const bool qv = q < N;
+
+  float qr[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int d = h * KS + s;
+    qr[s] = (qv && d < a.dk) ? a.Q[(b * N + q) * a.dk + d] : 0.0f;
+  }
+  float dor[HV];
+#pragma unroll
+  for (int s = 0; s < HV; ++s) {
+    const int f = h * HV + s;
+    dor[s] = (qv && f < a.dv) ? a.dO[(b * N + q) * a.dv + f] : 0.0f;
+  }
+  const float mq = qv ? a.smax[b * N + q] : 0.0f;
+  const float il = qv ? 1.0f / a.ssum[b * N + q] : 0.0f;
+  const float Dq = qv ? a.Drow[b * N + q] : 0.0f;
+  f32x16 dq = zero16();
+
+  for (int64_t k0 = 0; k0 < N; k0 += 32) {
+    stage(Ks, LDK, DKP, Kb, k0, N, a.dk, tid);
+    stage(Hs, DV, DV, Hb, k0, N, a.dv, tid);
+    __syncthreads();
+    f32x16 s = zero16();
+#pragma unroll
+    for (int st = 0; st < KS; ++st) s = MFMA(Ks[l32 * LDK + h * KS + st], qr[st], s);
+    f32x16 dp = zero16();
+#pragma unroll
+    for (int st = 0; st < HV; ++st) dp = MFMA(Hs[l32 * DV + h * HV + st], dor[st], dp);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float p = (k0 + kappa(r, h) < N) ? expf(s[r] - mq) * il : 0.0f;
+      s[r] = p * (dp[r] - Dq);  // dS
+    }
+#pragma unroll
+    for (int st = 0; st < 16; ++st) {
+      const float kv = l32 < DKP ? Ks[kappa(st, h) * LDK + l32] : 0.0f;
+      dq = MFMA(kv, s[st], dq);
+    }
+    __syncthreads();
+  }
+  if (qv) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int d = kappa(r, h);
+      if (d < a.dk) a.dQ[(b * N + q) * a.dk + d] = dq[r];
+    }
+  }
+}
+
+// dK, dH: one wave per 32 keys, loop over query blocks.
+template <int DKP, int NT>
+__global__ __launch_bounds__(256) void attn_bwd_kv_kernel(AttnArgs a) {
+  constexpr int KS = DKP / 2, DV = NT * 32, HV = DV / 2, LDK = DKP + 4;
+  __shared__ float Qs[32 * LDK];
+  __shared__ float Os[32 * DV];
+  __shared__ float Ms[32], Ls[32], Ds[32];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, h = lane >> 5;
+  const int64_t N = a.N, b = blockIdx.y;
+  const float* Qb = a.Q + b * N * a.dk;
+  const float* dOb = a.dO + b * N * a.dv;
+  const int64_t key = (int64_t)blockIdx.x * 128 + wave * 32 + l32;
+  const bool kv = key < N;
+
+  float kr[KS];
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const int d = h * KS + s;
+    kr[s] = (kv && d < a.dk) ? a.K[(b * N + key) * a.dk + d] : 0.0f;
+  }
+  float hr[HV];
+#pragma unroll
+  for (int s = 0; s < HV; ++s) {
+    const int f = h * HV + s;
+    hr[s] = (kv && f < a.dv) ? a.H[(b * N + key) * a.dv + f] : 0.0f;
+  }
+  f32x16 dh[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) dh[t] = zero16();
+  f32x16 dk = zero16();
+
+  for (int64_t q0 = 0; q0 < N; q0 += 32) {
+    stage(Qs, LDK, DKP, Qb, q0, N, a.dk, tid);
+    stage(Os, DV, DV, dOb, q0, N, a.dv, tid);
+    if (tid < 32) {
+      const int64_t qq = q0 + tid;
+      const bool v = qq < N;
+      Ms[tid] = v ? a.smax[b * N + qq] : 0.0f;
+      Ls[tid] = v ? 1.0f / a.ssum[b * N + qq] : 0.0f;  // 0 => P = 0 for padded queries
+      Ds[tid] = v ? a.Drow[b * N + qq] : 0.0f;
+    }
+    __syncthreads();
+    // S[query][key]: lanes = keys, registers = queries kappa(r, h)
+    f32x16 s = zero16();
+#pragma unroll
+    for (int st = 0; st < KS; ++st) s = MFMA(Qs[l32 * LDK + h * KS + st], kr[st], s);
+    f32x16 dp = zero16();
+#pragma unroll
+    for (int st = 0; st < HV; ++st) dp = MFMA(Os[l32 * DV + h * HV + st], hr[st], dp);
+    f32x16 ds;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int qi = kappa(r, h);
+      const float p = kv ? expf(s[r] - Ms[qi]) * Ls[qi] : 0.0f;
+      s[r] = p;
+      ds[r] = p * (dp[r] - Ds[qi]);
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int st = 0; st < 16; ++st) dh[t] = MFMA(Os[kappa(st, h) * DV + t * 32 + l32], s[st], dh[t]);
+#pragma unroll
+    for (int st = 0; st < 16; ++st) {
+      const float qv = l32 < DKP ? Qs[kappa(st, h) * LDK + l32] : 0.0f;
+      dk = MFMA(qv, ds[st], dk);
+    }
+    __syncthreads();
+  }
+  if (kv) {
+    const int64_t rowv = (b * N + key) * a.dv, rowk = (b * N + key) * a.dk;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int f = t * 32 + kappa(r, h);
+        if (f < a.dv) a.dH[rowv + f] = dh[t][r];
+      }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int d = kappa(r, h);
+      if (d < a.dk) a.dK[rowk + d] = dk[r];
+    }
+  }
+}
+
+#undef MFMA
+
+enum AttnPass { PASS_FWD, PASS_BWD_Q, PASS_BWD_KV };
+
+template <int DKP, int NT>
+int launch_attn(AttnPass pass, const AttnArgs& a, int64_t B, hipStream_t st) {
+  const dim3 grid((unsigned)ceil_div(a.N, 128), (unsigned)B);
+  if (pass == PASS_FWD)
+    hipLaunchKernelGGL((attn_fwd_kernel<DKP, NT>), grid, dim3(256), 0, st, a);
+  else if (pass == PASS_BWD_Q)
+    hipLaunchKernelGGL((attn_bwd_q_kernel<DKP, NT>), grid, dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL((attn_bwd_kv_kernel<DKP, NT>), grid, dim3(256), 0, st, a);
+  GRL_LAUNCH_CHECK();
+  return GRL_OK;
+}
+
+template <int DKP>
+int dispatch_nt(AttnPass pass, const AttnArgs& a, int64_t B, hipStream_t st) {
+  const int nt = (int)ceil_div(a.dv, 32);
+  if (nt <= 1) return launch_attn<DKP, 1>(pass, a, B, st);
+  if (nt <= 2) return launch_attn<DKP, 2>(pass, a, B, st);
+  if (nt <= 4) return launch_attn<DKP, 4>(pass, a, B, st);
+  return launch_attn<DKP, 8>(pass, a, B, st);
+}
+
+int dispatch(AttnPass pass, const AttnArgs& a, int64_t B, hipStream_t st) {
+  if (a.N == 0 || B == 0) return GRL_OK;
+  return a.dk <= 16 ? dispatch_nt<16>(pass, a, B, st) : dispatch_nt<32>(pass, a, B, st);
+}
+
+int check_dims(const char* who, int64_t B, int64_t N, int dk, int dv) {
+  GRL_CHECK_ARG(B >= 0 && N >= 0, "%s: negative size", who);
+  // dk = 0 is legal (input_dim < 8 gives Linear(F, 0) in the reference): all
+  // scores are 0 and the attention is uniform, which the kernels compute as is.
+  GRL_CHECK_ARG(dk >= 0 && dk <= 32, "%s: key width %d outside [0, 32] (NodeSelfAtten: input_dim // 8)", who, dk);
+  GRL_CHECK_ARG(dv >= 1 && dv <= 256, "%s: value width %d outside [1, 256]", who, dv);
+  GRL_CHECK_ARG(B * ceil_div(N, 128) < 2147483647LL && B < 65536, "%s: grid too large", who);
+  return GRL_OK;
+}
+
+}  // namespace
+}  // namespace grl
+
+using namespace grl;
+
+extern "C" int grl_node_attention_fwd(const float* Q, const float* K, const float* H, const float* V,
+                                      const float* gamma, float* out, float* o_norm, float* row_max, float* row_sum,
+                                      int64_t B, int64_t N, int32_t dk, int32_t dv, grl_stream_t stream) {
+  int rc = check_dims("grl_node_attention_fwd", B, N, dk, dv);
+  if (rc) return rc;
+  if (B == 0 || N == 0) return GRL_OK;
+  GRL_CHECK_ARG((dk == 0 || (Q && K)) && H && V && gamma && out, "grl_node_attention_fwd: NULL pointer");
+  GRL_CHECK_ARG((row_max == nullptr) == (row_sum == nullptr), "grl_node_attention_fwd: row_max/row_sum: both or none");
+  AttnArgs a{};
+  a.Q = Q;
+  a.K = K;
+  a.H = H;
+  a.V = V;
+  a.gamma = gamma;
+  a.out = out;
+  a.onorm = o_norm;
+  a.rmax = row_max;
+  a.rsum = row_sum;
+  a.N = N;
+  a.dk = dk;
+  a.dv = dv;
+  return dispatch(PASS_FWD, a, B, as_stream(stream));
+}
+
+extern "C" int grl_node_attention_bwd(const float* Q, const float* K, const float* H, const float* dO,
+                                      const float* row_max, const float* row_sum, const float* D, float* dQ,
+                                      float* dK, float* dH, int64_t B, int64_t N, int32_t dk, int32_t dv,
+                                      grl_stream_t stream) {
+  int rc = check_dims("grl_node_attention_bwd", B, N, dk, dv);
+  if (rc) return rc;
+  if (B == 0 || N == 0) return GRL_OK;
+  GRL_CHECK_ARG((dk == 0 || (Q && K && dQ && dK)) && H && dO && row_max && row_sum && D && dH,
+                "grl_node_attention_bwd: NULL pointer");
+  AttnArgs a{};
+  a.Q = Q;
+  a.K = K;
+  a.H = H;
+  a.dO = dO;
+  a.smax = row_max;
+  a.ssum = row_sum;
+  a.Drow = D;
+  a.dQ = dQ;
+  a.dK = dK;
+  a.dH = dH;
+  a.N = N;
+  a.dk = dk;
+  a.dv = dv;
+  hipStream_t st = as_stream(stream);
+  rc = dispatch(PASS_BWD_Q, a, B, st);
+  if (rc) return rc;
+  return dispatch(PASS_BWD_KV, a, B, st);
+}

@@ -18,7 +18,7 @@ import torch
 from torch import nn
 
 from grl import TypedGraph
-from grl.ops import graph_linear, typed_aggregate
+from grl.ops import graph_linear, node_self_attention, typed_aggregate
 
 
 def make_linear_relu(input_dim: int, output_dim: int) -> nn.Sequential:
@@ -88,8 +88,11 @@ class GraphConv(nn.Module):
 
 
 class NodeSelfAtten(nn.Module):
-    """Dense node self-attention (robust_gcn.py:78-99): gamma * softmax(f g^T) h + V.
-    Runs on torch/hipBLASLt; a fused kernel is the §8(f) 'next' row."""
+    """Node self-attention (robust_gcn.py:78-99): gamma * softmax(f g^T) h + V.
+    The f/g/h projections are torch Linear+ReLU (as in the reference); the
+    attention core is the fused flash-style libgrl kernel
+    (grl_node_attention_fwd/_bwd), so the N x N scores never exist and the
+    model runs at graph sizes where the reference's dense softmax cannot."""
 
     def __init__(self, input_dim: int):
         super().__init__()
@@ -102,8 +105,7 @@ class NodeSelfAtten(nn.Module):
         nn.init.normal_(self.gamma)
 
     def forward(self, V: torch.Tensor) -> torch.Tensor:
-        scores = torch.matmul(self.f(V), self.g(V).transpose(1, 2))  # B x N x N
-        return self.gamma * torch.matmul(self.softmax(scores), self.h(V)) + V
+        return node_self_attention(self.f(V), self.g(V), self.h(V), V, self.gamma)
 
     def __repr__(self) -> str:
         return f"NodeSelfAttention(input_dim={self.F})"

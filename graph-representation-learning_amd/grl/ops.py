@@ -148,3 +148,62 @@ def graph_linear(Z: torch.Tensor, W: torch.Tensor, b=None, relu: bool = False) -
     """out = Z W + b (optionally ReLU) on MFMA; Z rows x (L+1)F."""
     _require_device(Z, "aggregated features")
     return _GraphLinear.apply(Z, W, b, relu)
+
+
+# ---------------------------------------------------------------- attention
+def _attn_check(Q, K, H, V, gamma):
+    for t, what in ((Q, "queries"), (K, "keys"), (H, "values"), (V, "residual"), (gamma, "gamma")):
+        _require_device(t, what)
+        if t.dtype != torch.float32:
+            raise _lib.GrlError(f"attention {what} must be float32 (got {t.dtype})")
+    if Q.dim() != 3 or K.shape != Q.shape or H.dim() != 3 or H.shape[:2] != Q.shape[:2] or V.shape != H.shape \
+            or gamma.shape != (H.shape[2],):
+        raise _lib.GrlError(f"attention shapes: Q {tuple(Q.shape)}, K {tuple(K.shape)}, H {tuple(H.shape)}, "
+                            f"V {tuple(V.shape)}, gamma {tuple(gamma.shape)}")
+
+
+def node_attention_forward(Q, K, H, V, gamma, stats: bool = False):
+    """out = gamma * softmax(Q K^T) H + V (robust_gcn.py:90-96), fused.
+    stats=True also returns (o_norm, row_max, row_sum) for the backward."""
+    _attn_check(Q, K, H, V, gamma)
+    Q, K, H, V, gamma = (t.contiguous() for t in (Q, K, H, V, gamma))
+    B, N, dk = Q.shape
+    dv = H.shape[2]
+    out = torch.empty_like(V)
+    onorm = torch.empty_like(V) if stats else None
+    rmax = torch.empty(B, N, device=V.device) if stats else None
+    rsum = torch.empty(B, N, device=V.device) if stats else None
+    ptr = (lambda t: t.data_ptr() if t is not None else None)  # noqa: E731
+    call("grl_node_attention_fwd", Q.data_ptr(), K.data_ptr(), H.data_ptr(), V.data_ptr(), gamma.data_ptr(),
+         out.data_ptr(), ptr(onorm), ptr(rmax), ptr(rsum), B, N, dk, dv, current_stream_handle(V.device))
+    return (out, onorm, rmax, rsum) if stats else out
+
+
+class _NodeAttention(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, Q, K, H, V, gamma):
+        out, onorm, rmax, rsum = node_attention_forward(Q, K, H, V, gamma, stats=True)
+        ctx.save_for_backward(Q.contiguous(), K.contiguous(), H.contiguous(), gamma, onorm, rmax, rsum)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        Q, K, H, gamma, onorm, rmax, rsum = ctx.saved_tensors
+        dout = dout.contiguous().float()
+        B, N, dk = Q.shape
+        dv = H.shape[2]
+        dO = dout * gamma
+        D = (dO * onorm).sum(-1).contiguous()
+        dQ, dK, dH = torch.empty_like(Q), torch.empty_like(K), torch.empty_like(H)
+        call("grl_node_attention_bwd", Q.data_ptr(), K.data_ptr(), H.data_ptr(), dO.data_ptr(), rmax.data_ptr(),
+             rsum.data_ptr(), D.data_ptr(), dQ.data_ptr(), dK.data_ptr(), dH.data_ptr(), B, N, dk, dv,
+             current_stream_handle(Q.device))
+        dgamma = (dout * onorm).sum((0, 1))
+        return dQ, dK, dH, dout, dgamma
+
+
+def node_self_attention(Q: torch.Tensor, K: torch.Tensor, H: torch.Tensor, V: torch.Tensor,
+                        gamma: torch.Tensor) -> torch.Tensor:
+    """Autograd op: gamma * softmax_rows(Q K^T) H + V on the fused kernels
+    (grl_node_attention_fwd / _bwd); never materialises the N x N scores."""
+    return _NodeAttention.apply(Q, K, H, V, gamma)

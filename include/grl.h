@@ -211,6 +211,36 @@ int grl_linear_bwd_weight(const float* Z, int64_t ldz, const float* g,
                           size_t workspace_bytes, grl_stream_t stream);
 
 /* ---------------------------------------------------------------------- */
+/* Node self-attention                                                     */
+/* ---------------------------------------------------------------------- */
+/* NodeSelfAtten (robust_gcn.py:78-99) fused, flash-style (no B x N x N
+ * score matrix):  out = gamma * softmax_rows(Q K^T) H + V   per batch,
+ * Q = f(V), K = g(V) [B, N, dk], H = h(V), V [B, N, dv], gamma [dv], all
+ * contiguous fp32; no 1/sqrt(dk) scale and no mask (every node of the padded
+ * batch attends to every node, as the reference does).  dk in [0, 32]
+ * (input_dim // 8; 0 = uniform attention, Q/K may then be NULL), dv in
+ * [1, 256].  For training pass o_norm [B, N, dv]
+ * (= softmax(QK^T) H) and row_max/row_sum [B, N] (the softmax statistics);
+ * NULL otherwise.                                                           */
+int grl_node_attention_fwd(const float* Q, const float* K, const float* H,
+                           const float* V, const float* gamma, float* out,
+                           float* o_norm, float* row_max, float* row_sum,
+                           int64_t B, int64_t N, int32_t dk, int32_t dv,
+                           grl_stream_t stream);
+
+/* Backward of the attention core.  dO = gamma * d_out [B, N, dv] and
+ * D = rowsum(dO * o_norm) [B, N] come from the caller (elementwise); the
+ * kernels recompute P from row_max/row_sum and write dQ, dK [B, N, dk] and
+ * dH [B, N, dv] (fully overwritten).  Deterministic: dQ is query-stationary,
+ * dK/dH key-stationary, no atomics.  d gamma = sum(d_out * o_norm) and the
+ * residual's d_out are the caller's.                                        */
+int grl_node_attention_bwd(const float* Q, const float* K, const float* H,
+                           const float* dO, const float* row_max,
+                           const float* row_sum, const float* D, float* dQ,
+                           float* dK, float* dH, int64_t B, int64_t N,
+                           int32_t dk, int32_t dv, grl_stream_t stream);
+
+/* ---------------------------------------------------------------------- */
 /* Graph formats                                                           */
 /* ---------------------------------------------------------------------- */
 

@@ -1,0 +1,96 @@
+"""GPU: fused NodeSelfAtten (grl_node_attention_fwd/_bwd) against a float64
+torch restatement of robust_gcn.py:90-96 (out = gamma * softmax(f g^T) h + V),
+forward and every gradient, over ragged shapes, padded dims, large score
+magnitudes and N far beyond what a dense N x N softmax would allow."""
+import numpy as np
+import pytest
+import torch
+
+from grl import _lib
+from grl.ops import node_attention_forward, node_self_attention
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def _inputs(B, N, dk, dv, seed, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    Q = (torch.relu(torch.randn(B, N, dk, generator=g)) * scale).to(DEV)  # f, g are Linear+ReLU outputs
+    K = (torch.relu(torch.randn(B, N, dk, generator=g)) * scale).to(DEV)
+    H = torch.relu(torch.randn(B, N, dv, generator=g)).to(DEV)
+    V = torch.randn(B, N, dv, generator=g).to(DEV)
+    gamma = torch.randn(dv, generator=g).to(DEV)
+    return Q, K, H, V, gamma
+
+
+def _ref(Q, K, H, V, gamma):
+    s = torch.softmax(torch.matmul(Q, K.transpose(1, 2)), -1)
+    return gamma * torch.matmul(s, H) + V
+
+
+SHAPES = [(1, 74, 16, 128), (4, 74, 16, 128), (2, 33, 4, 32), (1, 1, 2, 16), (3, 130, 16, 128), (2, 300, 32, 256),
+          (2, 64, 5, 40), (1, 500, 16, 100), (2, 9, 0, 4)]  # dk = 0: net_size 8 (4 // 8), uniform attention
+
+
+@pytest.mark.parametrize("B,N,dk,dv", SHAPES)
+def test_forward_matches_fp64(B, N, dk, dv):
+    Q, K, H, V, gamma = _inputs(B, N, dk, dv, seed=N + dk)
+    out = node_attention_forward(Q, K, H, V, gamma)
+    ref = _ref(*(t.double() for t in (Q, K, H, V, gamma)))
+    torch.testing.assert_close(out.double(), ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("B,N,dk,dv", SHAPES)
+def test_backward_matches_fp64(B, N, dk, dv):
+    Q, K, H, V, gamma = _inputs(B, N, dk, dv, seed=7 * N + dv)
+    leaves = [t.clone().requires_grad_(True) for t in (Q, K, H, V, gamma)]
+    out = node_self_attention(*leaves)
+    dout = torch.randn(out.shape, generator=torch.Generator().manual_seed(3)).to(DEV)
+    out.backward(dout)
+    ref_leaves = [t.double().clone().requires_grad_(True) for t in (Q, K, H, V, gamma)]
+    _ref(*ref_leaves).backward(dout.double())
+    for name, a, r in zip("QKHVg", leaves, ref_leaves):
+        scale = (r.grad.abs().max().item() if r.grad.numel() else 0.0) + 1.0
+        torch.testing.assert_close(a.grad.double(), r.grad, rtol=1e-4, atol=2e-5 * scale, msg=f"d{name}")
+
+
+def test_large_scores_are_stable():
+    """No 1/sqrt(dk) scaling in the reference: scores of several hundred must
+    not overflow (online max subtraction)."""
+    Q, K, H, V, gamma = _inputs(2, 200, 16, 128, seed=5, scale=6.0)
+    out = node_attention_forward(Q, K, H, V, gamma)
+    assert torch.isfinite(out).all()
+    ref = _ref(*(t.double() for t in (Q, K, H, V, gamma)))
+    torch.testing.assert_close(out.double(), ref, rtol=1e-4, atol=1e-4)
+
+
+def test_large_n_rows_sampled():
+    """N = 20k (a dense softmax would need 1.6 GB of scores per batch): check
+    64 sampled query rows against fp64."""
+    B, N, dk, dv = 1, 20000, 16, 128
+    Q, K, H, V, gamma = _inputs(B, N, dk, dv, seed=11)
+    out = node_attention_forward(Q, K, H, V, gamma)
+    idx = torch.randperm(N, generator=torch.Generator().manual_seed(1))[:64].to(DEV)
+    s = torch.softmax(Q[0, idx].double() @ K[0].double().T, -1)
+    ref = gamma.double() * (s @ H[0].double()) + V[0, idx].double()
+    # fp32 sums over 20k keys: the north-star fp32 tolerance (1e-4)
+    torch.testing.assert_close(out[0, idx].double(), ref, rtol=1e-4, atol=1e-4)
+
+
+def test_deterministic():
+    Q, K, H, V, gamma = _inputs(2, 150, 16, 128, seed=2)
+    grads = []
+    for _ in range(2):
+        leaves = [t.clone().requires_grad_(True) for t in (Q, K, H, V, gamma)]
+        node_self_attention(*leaves).sum().backward()
+        grads.append([t.grad for t in leaves])
+    for a, b in zip(*grads):
+        assert torch.equal(a, b)
+
+
+def test_bad_widths_raise():
+    Q, K, H, V, gamma = _inputs(1, 8, 40, 16, seed=0)
+    with pytest.raises(_lib.GrlError, match="key width"):
+        node_attention_forward(Q, K, H, V, gamma)
+    with pytest.raises(_lib.GrlError, match="attention shapes"):
+        node_attention_forward(Q[..., :8], K[..., :8], H, V[..., :8], gamma)
