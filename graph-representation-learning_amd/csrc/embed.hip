@@ -1,0 +1,111 @@
+// emb1 = Linear(4369 -> net_size) + ReLU over bag-of-characters rows
+// (gnn/models/networks/drop_robust_gcn.py:36,64; the rows come from
+// TextlineEncoding, textline_encoding.py:23-42: character counts plus four
+// box features, ~7 nonzeros in 4369).
+//
+//   out[m, :] = relu(bias + sum_{k : V[m,k] != 0, ascending k} V[m,k] * Wt[k, :])
+//
+// A dense GEMM would spend 2*K*C flops per row on zeros; here one wave scans
+// its row 64 entries per load, ballots the nonzeros and gathers only those
+// rows of Wt (K x C, L2-resident: 4.5 MB at 4369 x 256).  V is read once,
+// coalesced; no CSR is built and nothing syncs with the host, so the model's
+// forward stays capturable in a HIP graph.  Sums are one fmaf per nonzero in
+// ascending k (deterministic).  The backward (dW = V^T (g * [out > 0]), db)
+// is grl_linear_bwd_weight on the MFMA GEMM.
+#include "grl_internal.h"
+
+namespace grl {
+namespace {
+
+constexpr int U = 4;  // nonzero rows of Wt in flight per wave
+
+template <int CPL>  // output columns per lane: C <= 64 * CPL
+__global__ __launch_bounds__(256) void bag_linear_kernel(const float* __restrict__ V, int64_t ldv, int64_t M, int K,
+                                                         const float* __restrict__ Wt, int C,
+                                                         const float* __restrict__ bias, int relu,
+                                                         float* __restrict__ out, int64_t ldo) {
+  const int lane = threadIdx.x & 63;
+  const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
+  for (int64_t m = wave; m < M; m += nwaves) {
+    float acc[CPL];
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) acc[c] = 0.0f;
+    const float* vrow = V + m * ldv;
+    for (int k0 = 0; k0 < K; k0 += 64) {
+      const float v = (k0 + lane < K) ? vrow[k0 + lane] : 0.0f;
+      uint64_t nz = __ballot(v != 0.0f);
+      while (nz) {
+        int jj[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          if (nz) {
+            jj[u] = __builtin_ctzll(nz);
+            nz &= nz - 1;
+          } else {
+            jj[u] = -1;
+          }
+        }
+        float w[U][CPL], vj[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          vj[u] = __shfl(v, jj[u] < 0 ? 0 : jj[u]);
+          const float* wrow = Wt + (int64_t)(k0 + (jj[u] < 0 ? 0 : jj[u])) * C;
+#pragma unroll
+          for (int c = 0; c < CPL; ++c) {
+            const int col = lane + 64 * c;
+            w[u][c] = (jj[u] >= 0 && col < C) ? wrow[col] : 0.0f;
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (jj[u] >= 0) {
+#pragma unroll
+            for (int c = 0; c < CPL; ++c) acc[c] = fmaf(vj[u], w[u][c], acc[c]);
+          }
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < CPL; ++c) {
+      const int col = lane + 64 * c;
+      if (col < C) {
+        float x = acc[c] + (bias ? bias[col] : 0.0f);
+        if (relu) x = x > 0.0f ? x : 0.0f;
+        out[m * ldo + col] = x;
+      }
+    }
+  }
+}
+
+template <int CPL>
+void launch_bag(const float* V, int64_t ldv, int64_t M, int K, const float* Wt, int C, const float* bias, int relu,
+                float* out, hipStream_t st) {
+  const int64_t blocks = std::min<int64_t>(ceil_div(M, 4), (int64_t)device_cu_count() * 16);
+  hipLaunchKernelGGL((bag_linear_kernel<CPL>), dim3((unsigned)std::max<int64_t>(blocks, 1)), dim3(256), 0, st, V, ldv,
+                     M, K, Wt, C, bias, relu, out, (int64_t)C);
+}
+
+}  // namespace
+}  // namespace grl
+
+using namespace grl;
+
+extern "C" int grl_bag_linear_fwd(const float* V, int64_t ldv, int64_t M, int32_t K, const float* Wt, int32_t C,
+                                  const float* bias, int32_t relu, float* out, grl_stream_t stream) {
+  GRL_CHECK_ARG(M >= 0 && K >= 0 && ldv >= K, "grl_bag_linear_fwd: bad sizes (M %lld, K %d, ldv %lld)", (long long)M,
+                K, (long long)ldv);
+  GRL_CHECK_ARG(C >= 1 && C <= 512, "grl_bag_linear_fwd: output width %d outside [1, 512]", C);
+  if (M == 0) return GRL_OK;
+  GRL_CHECK_ARG((V || K == 0) && Wt && out, "grl_bag_linear_fwd: NULL pointer");
+  hipStream_t st = as_stream(stream);
+  if (C <= 64)
+    launch_bag<1>(V, ldv, M, K, Wt, C, bias, relu, out, st);
+  else if (C <= 128)
+    launch_bag<2>(V, ldv, M, K, Wt, C, bias, relu, out, st);
+  else if (C <= 256)
+    launch_bag<4>(V, ldv, M, K, Wt, C, bias, relu, out, st);
+  else
+    launch_bag<8>(V, ldv, M, K, Wt, C, bias, relu, out, st);
+  GRL_LAUNCH_CHECK();
+  return GRL_OK;
+}

@@ -22,6 +22,7 @@ from torch.nn import functional as F
 from gnn.models.base_network import BaseNetwork
 from gnn.models.networks.robust_gcn import GraphConv, NodeSelfAtten, make_linear_relu
 from grl import DropEdge, TypedGraph
+from grl.ops import bag_linear
 
 RP_FACTOR = 10
 
@@ -80,6 +81,9 @@ class GraphCNNDropEdge(BaseNetwork):
         self.output_dim = output_dim
         self.net_size = net_size
         self.emb1 = make_linear_relu(input_dim, self.net_size)
+        # emb1's input is a bag-of-characters row (~7 nonzeros of 4369): run it
+        # as a sparse-row gather (grl_bag_linear_fwd); False = dense torch Linear
+        self.sparse_emb1 = True
         self.dropout = nn.Dropout(p=0.5)
         self.edge_dropout = EdgeDropout(p=0.3, seed=dropedge_seed)
         self.gcn1 = GraphConv(self.net_size, self.net_size, num_edges)
@@ -101,10 +105,17 @@ class GraphCNNDropEdge(BaseNetwork):
         dev = self.gcn1.h_weights.device
         return TypedGraph.from_dense(A if A.device == dev else A.to(dev), layout="bnln")
 
+    def _embed(self, V: torch.Tensor) -> torch.Tensor:
+        """emb1 (drop_robust_gcn.py:36,64): Linear + ReLU, same parameters."""
+        if self.sparse_emb1 and V.is_cuda:
+            lin = self.emb1[0]
+            return bag_linear(V.float(), lin.weight, lin.bias, relu=True)
+        return self.emb1(V)
+
     def forward(self, inputs, efficient_mode: bool = True):
         V, A = inputs
         graph = self.to_graph(A)
-        embedding = self.dropout(self.emb1(V))
+        embedding = self.dropout(self._embed(V))
         # efficient_mode=True: dropout covers the identity block of A_pre
         # (:69,:76); False: dropout hits raw A, identity added after (:72-74).
         ds = bool(efficient_mode)

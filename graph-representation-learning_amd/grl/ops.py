@@ -207,3 +207,47 @@ def node_self_attention(Q: torch.Tensor, K: torch.Tensor, H: torch.Tensor, V: to
     """Autograd op: gamma * softmax_rows(Q K^T) H + V on the fused kernels
     (grl_node_attention_fwd / _bwd); never materialises the N x N scores."""
     return _NodeAttention.apply(Q, K, H, V, gamma)
+
+
+# ------------------------------------------------------ bag-of-chars linear
+def bag_linear_forward(V2: torch.Tensor, Wt: torch.Tensor, b, relu: bool) -> torch.Tensor:
+    """relu?(V2 @ Wt + b) gathering only the nonzero rows of Wt per row of V2."""
+    M, K = V2.shape
+    C = Wt.shape[1]
+    out = torch.empty(M, C, dtype=torch.float32, device=V2.device)
+    call("grl_bag_linear_fwd", V2.data_ptr(), V2.stride(0), M, K, Wt.data_ptr(), C,
+         b.data_ptr() if b is not None else None, int(relu), out.data_ptr(), current_stream_handle(V2.device))
+    return out
+
+
+class _BagLinear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, V2, W, b, relu: bool):
+        Wt = W.t().contiguous()
+        out = bag_linear_forward(V2, Wt, b, relu)
+        ctx.relu = relu
+        ctx.has_b = b is not None
+        ctx.save_for_backward(V2, Wt, out)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        V2, Wt, out = ctx.saved_tensors
+        g = g.contiguous()
+        relu_out = out if ctx.relu else None
+        dV = linear_bwd_data(g, relu_out, Wt) if ctx.needs_input_grad[0] else None
+        dWt, db = linear_bwd_weight(V2, g, relu_out, ctx.has_b)
+        return dV, dWt.t(), db, None
+
+
+def bag_linear(V: torch.Tensor, W: torch.Tensor, b, relu: bool = False) -> torch.Tensor:
+    """nn.Linear(K, C) (+ReLU) for sparse inputs such as emb1's bag-of-chars
+    rows: V [..., K], W [C, K] (nn.Linear.weight), b [C] or None."""
+    _require_device(V, "bag-of-chars input")
+    if V.dtype != torch.float32 or W.dtype != torch.float32:
+        raise _lib.GrlError("bag_linear: float32 input and weight required")
+    lead = V.shape[:-1]
+    V2 = V.reshape(-1, V.shape[-1])
+    if V2.stride(-1) != 1:
+        V2 = V2.contiguous()
+    return _BagLinear.apply(V2, W, b, relu).view(*lead, W.shape[0])

@@ -210,6 +210,18 @@ int grl_linear_bwd_weight(const float* Z, int64_t ldz, const float* g,
                           int32_t K, int32_t C, void* workspace,
                           size_t workspace_bytes, grl_stream_t stream);
 
+/* emb1: Linear(K -> C) (+ReLU) over sparse bag-of-characters rows
+ * (drop_robust_gcn.py:36,64; rows from TextlineEncoding,
+ * textline_encoding.py:23-42):
+ *   out[m, :] = relu?(bias + sum_{k: V[m,k] != 0, ascending} V[m,k] Wt[k, :])
+ * V [M, K] row stride ldv (dense storage, mostly zeros), Wt [K, C]
+ * contiguous (= nn.Linear.weight^T), bias [C] or NULL, out [M, C].  Only the
+ * nonzeros cost gathers; C in [1, 512].  Backward: grl_linear_bwd_weight
+ * with Z = V gives dWt and db.                                             */
+int grl_bag_linear_fwd(const float* V, int64_t ldv, int64_t M, int32_t K,
+                       const float* Wt, int32_t C, const float* bias,
+                       int32_t relu, float* out, grl_stream_t stream);
+
 /* ---------------------------------------------------------------------- */
 /* Node self-attention                                                     */
 /* ---------------------------------------------------------------------- */

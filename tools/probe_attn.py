@@ -1,0 +1,36 @@
+"""Diagnostic: fused NodeSelfAtten throughput at large N (B=1, dk=16, dv=128,
+the config-1 model's attention shape) -- forward and forward+backward."""
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "graph-representation-learning_amd"))
+import torch  # noqa: E402
+
+from grl.ops import node_attention_forward, node_self_attention  # noqa: E402
+
+
+def timeit(fn, n=5):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(n):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / n
+
+
+dev = torch.device("cuda:0")
+for N in (2048, 16384, 65536, 131072):
+    dk, dv = 16, 128
+    Q, K = torch.relu(torch.randn(1, N, dk, device=dev)), torch.relu(torch.randn(1, N, dk, device=dev))
+    H, V, g = torch.relu(torch.randn(1, N, dv, device=dev)), torch.randn(1, N, dv, device=dev), torch.randn(dv, device=dev)
+    flops = 2.0 * N * N * (dk + dv)
+    ms = timeit(lambda: node_attention_forward(Q, K, H, V, g))
+    leaves = [t.clone().requires_grad_(True) for t in (Q, K, H, V, g)]
+    ms_fb = timeit(lambda: node_self_attention(*leaves).sum().backward(), 3)
+    # backward = 2 S recomputes (2*N^2*dk each) + 2 dP (2*N^2*dv each) + dQ, dK (2*N^2*dk each) + dH (2*N^2*dv)
+    bflops = 2.0 * N * N * (4 * dk + 3 * dv)
+    print(f"N={N:7d} fwd {ms:9.3f} ms {flops / ms / 1e9:7.1f} TFLOP/s | fwd+bwd {ms_fb:9.3f} ms "
+          f"{(flops + bflops) / ms_fb / 1e9:7.1f} TFLOP/s", flush=True)
