@@ -64,6 +64,29 @@ __device__ __forceinline__ void vadd(float4& a, const float4& b) {
 }
 __device__ __forceinline__ void vadd(float& a, const float& b) { a += b; }
 
+// Output stores are non-temporal: the 7 GB Z stream (C3) is written once and
+// should not evict gathered X rows from L2 / the MALL.  Measured A/B on the
+// same MI355X: C3 forward 7.46 -> 7.07 ms.  GRL_NT_STORE=0 restores plain stores.
+#ifndef GRL_NT_STORE
+#define GRL_NT_STORE 1
+#endif
+using f4v = __attribute__((ext_vector_type(4))) float;
+__device__ __forceinline__ void vstore(float* p, const float4& v) {
+#if GRL_NT_STORE
+  f4v t = {v.x, v.y, v.z, v.w};
+  __builtin_nontemporal_store(t, reinterpret_cast<f4v*>(p));
+#else
+  *reinterpret_cast<float4*>(p) = v;
+#endif
+}
+__device__ __forceinline__ void vstore(float* p, const float& v) {
+#if GRL_NT_STORE
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+
 // Device view of a split plan (all null / zero when the graph is not split).
 struct SplitDev {
   int threshold;  // INT_MAX: nothing is heavy
@@ -137,7 +160,7 @@ __global__ __launch_bounds__(256) void spmm_kernel(
             if (BWD)
               acc[k] = x;
             else
-              *reinterpret_cast<vec_t*>(orow + coff[k]) = x;
+              vstore(orow + coff[k], x);
           }
         }
       }
@@ -196,7 +219,7 @@ __global__ __launch_bounds__(256) void spmm_kernel(
               while (e >= seg_end) {  // flush finished segments (wave-uniform)
 #pragma unroll
                 for (int k = 0; k < NV; ++k) {
-                  if (cval[k]) *reinterpret_cast<vec_t*>(obase + t * F + coff[k]) = acc[k];
+                  if (cval[k]) vstore(obase + t * F + coff[k], acc[k]);
                   vzero(acc[k]);
                 }
                 ++t;
@@ -214,7 +237,7 @@ __global__ __launch_bounds__(256) void spmm_kernel(
     for (; t < nseg; ++t) {
 #pragma unroll
       for (int k = 0; k < NV; ++k) {
-        if (cval[k]) *reinterpret_cast<vec_t*>(obase + t * F + coff[k]) = acc[k];
+        if (cval[k]) vstore(obase + t * F + coff[k], acc[k]);
         vzero(acc[k]);
       }
     }
