@@ -26,6 +26,10 @@ using f32x16 = __attribute__((ext_vector_type(16))) float;
 
 constexpr int BM = 128, BN = 128;
 
+#ifndef GRL_GEMM_VEC_EPI
+#define GRL_GEMM_VEC_EPI 1
+#endif
+
 enum Epilogue { EPI_STORE = 0, EPI_BIAS = 1, EPI_SLAB = 2 };
 
 struct GemmArgs {
@@ -41,7 +45,41 @@ struct GemmArgs {
   int64_t M, N, K;
   int64_t k_per_split;
   int relu;
+  // tile grid (set by launch_gemm): mt x nt output tiles x zt K-splits,
+  // launched as one dimension; inner_n: which tile index runs fastest
+  int64_t mt, nt, zt;
+  int inner_n;
 };
+
+#ifndef GRL_GEMM_XCD
+#define GRL_GEMM_XCD 1
+#endif
+
+// XCD-aware tile order.  Workgroups are dealt to the 8 XCDs round-robin
+// (blockIdx % 8; speed only, never relied on for correctness), and each XCD
+// walks a contiguous run of the tile order u with the operand-sharing index
+// fastest, so the tiles that read the same A rows (inner_n: forward, dZ) or
+// the same B rows (dW) run together on one XCD and hit its L2 instead of
+// re-reading HBM once per tile (dZ: 14 N tiles share each 1 GB row block).
+__device__ __forceinline__ void tile_of(const GemmArgs& p, int64_t& mi, int64_t& ni, int64_t& zi) {
+  const int64_t T = p.mt * p.nt * p.zt;
+  const int64_t L = blockIdx.x;
+#if GRL_GEMM_XCD
+  const int64_t q = T / 8, r = T % 8, x = L % 8, s = L / 8;
+  const int64_t u = x * q + (x < r ? x : r) + s;
+#else
+  const int64_t u = L;
+  (void)T;
+#endif
+  if (p.inner_n) {
+    ni = u % p.nt;
+    mi = (u / p.nt) % p.mt;
+  } else {
+    mi = u % p.mt;
+    ni = (u / p.mt) % p.nt;
+  }
+  zi = u / (p.mt * p.nt);
+}
 
 __device__ __forceinline__ float4 masked(float4 v, float4 mk) {
   v.x = mk.x > 0.f ? v.x : 0.f;
@@ -127,6 +165,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs p) {
   using OA = Operand<A_KC, ALIGNED, MASK_A, BK>;
   using OB = Operand<B_KC, ALIGNED, MASK_B, BK>;
   __shared__ __attribute__((aligned(16))) float smem[OA::lds_floats() + OB::lds_floats()];
+  static_assert(OA::lds_floats() + OB::lds_floats() >= 4 * 64 * 32, "epilogue staging must fit the operand LDS");
   float* As = smem;
   float* Bs = smem + OA::lds_floats();
 
@@ -135,9 +174,11 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs p) {
   const int wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
   const int l32 = lane & 31, h = lane >> 5;
-  const int64_t m0 = (int64_t)blockIdx.x * BM;
-  const int64_t n0 = (int64_t)blockIdx.y * BN;
-  const int64_t kbeg = (int64_t)blockIdx.z * p.k_per_split;
+  int64_t mi, ni, zi;
+  tile_of(p, mi, ni, zi);
+  const int64_t m0 = mi * BM;
+  const int64_t n0 = ni * BN;
+  const int64_t kbeg = zi * p.k_per_split;
   const int64_t kend = min(p.K, kbeg + p.k_per_split);
 
   OA oa;
@@ -198,7 +239,48 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs p) {
   }
 
   // ---- epilogue: C/D map col = lane&31, row = (r&3) + 8(r>>2) + 4h --------
-  float* Cz = p.C + (EPI == EPI_SLAB ? (int64_t)blockIdx.z * p.M * p.ldc : 0);
+  float* Cz = p.C + (EPI == EPI_SLAB ? zi * p.M * p.ldc : 0);
+#if GRL_GEMM_VEC_EPI
+  // Through LDS, one 64 x 32 half of the wave's sub-tile at a time, so that
+  // every lane stores whole float4 rows (a register holds one column of four
+  // rows; scalar stores cost 4x the store instructions on a 7 GB output).
+  if ((p.ldc & 3) == 0 && (reinterpret_cast<uintptr_t>(Cz) & 15) == 0) {
+    float* stage = smem + wave * (64 * 32);  // 4 x 2048 floats <= operand buffers
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) stage[(i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * 32 + l32] = acc[i][j][r];
+      __syncthreads();
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        const int row = (lane >> 3) + 8 * it, c4 = (lane & 7) * 4;
+        const int64_t gm = m0 + wm * 64 + row;
+        const int64_t gn = n0 + wn * 64 + j * 32 + c4;
+        if (gm >= p.M || gn >= p.N) continue;
+        float4 v = *reinterpret_cast<const float4*>(&stage[row * 32 + c4]);
+        float* vp = reinterpret_cast<float*>(&v);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float x = vp[e];
+          if (EPI == EPI_BIAS) {
+            if (p.bias && gn + e < p.N) x += p.bias[gn + e];
+            if (p.relu) x = x > 0.0f ? x : 0.0f;
+          }
+          vp[e] = x;
+        }
+        if (gn + 3 < p.N) {
+          *reinterpret_cast<float4*>(&Cz[gm * p.ldc + gn]) = v;
+        } else {
+          for (int e = 0; gn + e < p.N; ++e) Cz[gm * p.ldc + gn + e] = vp[e];
+        }
+      }
+      __syncthreads();
+    }
+    return;
+  }
+#endif
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int64_t gn = n0 + wn * 64 + j * 32 + l32;
@@ -293,11 +375,16 @@ bool al16(const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; }
 constexpr int GEMM_BK = GRL_GEMM_BK;
 
 template <bool A_KC, bool B_KC, int EPI>
-int launch_gemm(const GemmArgs& a, int splits, bool aligned, hipStream_t st) {
+int launch_gemm(GemmArgs a, int splits, bool aligned, hipStream_t st) {
   if (a.M == 0 || a.N == 0) return GRL_OK;
-  GRL_CHECK_ARG(ceil_div(a.M, BM) < 2147483647LL && ceil_div(a.N, BN) < 65536 && splits < 65536,
-                "gemm: grid too large");
-  const dim3 grid((unsigned)ceil_div(a.M, BM), (unsigned)ceil_div(a.N, BN), (unsigned)splits);
+  a.mt = ceil_div(a.M, BM);
+  a.nt = ceil_div(a.N, BN);
+  a.zt = splits;
+  // the operand worth sharing is the one with more rows per tile: A (M x K
+  // rows of Z / g) for the forward and dZ, B (the K x N slab of g) for dW
+  a.inner_n = (A_KC ? 1 : 0);
+  GRL_CHECK_ARG(a.mt * a.nt * a.zt < 2147483647LL, "gemm: grid too large");
+  const dim3 grid((unsigned)(a.mt * a.nt * a.zt));
   const bool ma = a.Amask != nullptr, mb = a.Bmask != nullptr;
 #define GRL_GEMM(AL, MA, MB) \
   hipLaunchKernelGGL((gemm_kernel<A_KC, B_KC, EPI, AL, MA, MB, GEMM_BK>), grid, dim3(256), 0, st, a)
