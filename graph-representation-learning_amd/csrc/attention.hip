@@ -62,15 +62,53 @@ __device__ __forceinline__ f32x16 zero16() {
 
 #define MFMA(a, b, c) __builtin_amdgcn_mfma_f32_32x32x2f32((a), (b), (c), 0, 0, 0)
 
-// Stage rows [r0, r0+32) of a [N, width] matrix into LDS tile[32][ld] with
-// zero fill beyond N and beyond `width` (up to `padw` columns).
-__device__ __forceinline__ void stage(float* tile, int ld, int padw, const float* src, int64_t r0, int64_t N,
-                                      int width, int tid) {
-  for (int i = tid; i < 32 * padw; i += 256) {
-    const int r = i / padw, c = i - r * padw;
-    const int64_t row = r0 + r;
-    tile[r * ld + c] = (row < N && c < width) ? src[row * width + c] : 0.0f;
+// Rows [r0, r0+32) of a [N, width] matrix staged into an LDS tile[32][LD]
+// (zero fill beyond N and beyond `width`, up to the padded width W).  fetch()
+// issues every load of the tile into registers at once (float4 when the rows
+// allow it) and store() writes them to LDS after the barrier, so the next
+// block's loads are in flight while the current block is multiplied.
+template <int W, int LD>
+struct Stager {
+  static constexpr int NF4 = 32 * W / 4;
+  static constexpr int PER = (NF4 + 255) / 256;
+  float4 reg[PER];
+
+  __device__ __forceinline__ void fetch(const float* src, int64_t r0, int64_t N, int width, bool vec, int tid) {
+#pragma unroll
+    for (int it = 0; it < PER; ++it) {
+      const int idx = tid + it * 256;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (idx < NF4) {
+        const int r = idx / (W / 4), c = (idx % (W / 4)) * 4;
+        const int64_t row = r0 + r;
+        if (row < N) {
+          const float* sp = src + row * width + c;
+          if (vec && c + 3 < width) {
+            v = *reinterpret_cast<const float4*>(sp);
+          } else {
+            float* vp = reinterpret_cast<float*>(&v);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) vp[e] = (c + e < width) ? sp[e] : 0.0f;
+          }
+        }
+      }
+      reg[it] = v;
+    }
   }
+  __device__ __forceinline__ void store(float* tile, int tid) const {
+#pragma unroll
+    for (int it = 0; it < PER; ++it) {
+      const int idx = tid + it * 256;
+      if (idx < NF4) {
+        const int r = idx / (W / 4), c = (idx % (W / 4)) * 4;
+        *reinterpret_cast<float4*>(&tile[r * LD + c]) = reg[it];
+      }
+    }
+  }
+};
+
+__device__ __forceinline__ bool vec_ok(const float* p, int width) {
+  return p != nullptr && (width & 3) == 0 && (reinterpret_cast<uintptr_t>(p) & 15) == 0;
 }
 
 template <int DKP, int NT>
@@ -95,11 +133,20 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
 #pragma unroll
   for (int t = 0; t < NT; ++t) o[t] = zero16();
   float m = -INFINITY, l = 0.0f;
+  Stager<DKP, LDK> sk;
+  Stager<DV, DV> sh;
+  const bool vk = vec_ok(Kb, a.dk), vh = vec_ok(Hb, a.dv);
+  sk.fetch(Kb, 0, N, a.dk, vk, tid);
+  sh.fetch(Hb, 0, N, a.dv, vh, tid);
 
   for (int64_t k0 = 0; k0 < N; k0 += 32) {
-    stage(Ks, LDK, DKP, Kb, k0, N, a.dk, tid);
-    stage(Hs, DV, DV, Hb, k0, N, a.dv, tid);
+    sk.store(Ks, tid);
+    sh.store(Hs, tid);
     __syncthreads();
+    if (k0 + 32 < N) {
+      sk.fetch(Kb, k0 + 32, N, a.dk, vk, tid);
+      sh.fetch(Hb, k0 + 32, N, a.dv, vh, tid);
+    }
     f32x16 s = zero16();
 #pragma unroll
     for (int st = 0; st < KS; ++st) s = MFMA(Ks[l32 * LDK + h * KS + st], qr[st], s);
@@ -181,11 +228,20 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(AttnArgs a) {
   const float il = qv ? 1.0f / a.ssum[b * N + q] : 0.0f;
   const float Dq = qv ? a.Drow[b * N + q] : 0.0f;
   f32x16 dq = zero16();
+  Stager<DKP, LDK> sk;
+  Stager<DV, DV> sh;
+  const bool vk = vec_ok(Kb, a.dk), vh = vec_ok(Hb, a.dv);
+  sk.fetch(Kb, 0, N, a.dk, vk, tid);
+  sh.fetch(Hb, 0, N, a.dv, vh, tid);
 
   for (int64_t k0 = 0; k0 < N; k0 += 32) {
-    stage(Ks, LDK, DKP, Kb, k0, N, a.dk, tid);
-    stage(Hs, DV, DV, Hb, k0, N, a.dv, tid);
+    sk.store(Ks, tid);
+    sh.store(Hs, tid);
     __syncthreads();
+    if (k0 + 32 < N) {
+      sk.fetch(Kb, k0 + 32, N, a.dk, vk, tid);
+      sh.fetch(Hb, k0 + 32, N, a.dv, vh, tid);
+    }
     f32x16 s = zero16();
 #pragma unroll
     for (int st = 0; st < KS; ++st) s = MFMA(Ks[l32 * LDK + h * KS + st], qr[st], s);
@@ -244,17 +300,37 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(AttnArgs a) {
   for (int t = 0; t < NT; ++t) dh[t] = zero16();
   f32x16 dk = zero16();
 
-  for (int64_t q0 = 0; q0 < N; q0 += 32) {
-    stage(Qs, LDK, DKP, Qb, q0, N, a.dk, tid);
-    stage(Os, DV, DV, dOb, q0, N, a.dv, tid);
+  Stager<DKP, LDK> sq;
+  Stager<DV, DV> so;
+  const bool vq = vec_ok(Qb, a.dk), vo = vec_ok(dOb, a.dv);
+  float pm = 0.0f, pl = 0.0f, pd = 0.0f;  // this thread's row statistics (tid < 32)
+  auto fetch_stats = [&](int64_t q0) {
     if (tid < 32) {
       const int64_t qq = q0 + tid;
       const bool v = qq < N;
-      Ms[tid] = v ? a.smax[b * N + qq] : 0.0f;
-      Ls[tid] = v ? 1.0f / a.ssum[b * N + qq] : 0.0f;  // 0 => P = 0 for padded queries
-      Ds[tid] = v ? a.Drow[b * N + qq] : 0.0f;
+      pm = v ? a.smax[b * N + qq] : 0.0f;
+      pl = v ? 1.0f / a.ssum[b * N + qq] : 0.0f;  // 0 => P = 0 for padded queries
+      pd = v ? a.Drow[b * N + qq] : 0.0f;
+    }
+  };
+  sq.fetch(Qb, 0, N, a.dk, vq, tid);
+  so.fetch(dOb, 0, N, a.dv, vo, tid);
+  fetch_stats(0);
+
+  for (int64_t q0 = 0; q0 < N; q0 += 32) {
+    sq.store(Qs, tid);
+    so.store(Os, tid);
+    if (tid < 32) {
+      Ms[tid] = pm;
+      Ls[tid] = pl;
+      Ds[tid] = pd;
     }
     __syncthreads();
+    if (q0 + 32 < N) {
+      sq.fetch(Qb, q0 + 32, N, a.dk, vq, tid);
+      so.fetch(dOb, q0 + 32, N, a.dv, vo, tid);
+      fetch_stats(q0 + 32);
+    }
     // S[query][key]: lanes = keys, registers = queries kappa(r, h)
     f32x16 s = zero16();
 #pragma unroll

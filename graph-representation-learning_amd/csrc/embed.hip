@@ -17,7 +17,8 @@
 namespace grl {
 namespace {
 
-constexpr int U = 4;  // nonzero rows of Wt in flight per wave
+constexpr int U = 4;     // nonzero rows of Wt in flight per wave
+constexpr int SCAN = 8;  // 64-entry chunks of a V row loaded together
 
 template <int CPL>  // output columns per lane: C <= 64 * CPL
 __global__ __launch_bounds__(256) void bag_linear_kernel(const float* __restrict__ V, int64_t ldv, int64_t M, int K,
@@ -32,37 +33,47 @@ __global__ __launch_bounds__(256) void bag_linear_kernel(const float* __restrict
 #pragma unroll
     for (int c = 0; c < CPL; ++c) acc[c] = 0.0f;
     const float* vrow = V + m * ldv;
-    for (int k0 = 0; k0 < K; k0 += 64) {
-      const float v = (k0 + lane < K) ? vrow[k0 + lane] : 0.0f;
-      uint64_t nz = __ballot(v != 0.0f);
-      while (nz) {
-        int jj[U];
+    for (int kb = 0; kb < K; kb += 64 * SCAN) {
+      float vs[SCAN];  // SCAN chunks of the row in flight at once (latency)
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          if (nz) {
-            jj[u] = __builtin_ctzll(nz);
-            nz &= nz - 1;
-          } else {
-            jj[u] = -1;
+      for (int c = 0; c < SCAN; ++c) {
+        const int k = kb + 64 * c + lane;
+        vs[c] = k < K ? vrow[k] : 0.0f;
+      }
+#pragma unroll
+      for (int c = 0; c < SCAN; ++c) {
+        const int k0 = kb + 64 * c;
+        const float v = vs[c];
+        uint64_t nz = __ballot(v != 0.0f);
+        while (nz) {
+          int jj[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            if (nz) {
+              jj[u] = __builtin_ctzll(nz);
+              nz &= nz - 1;
+            } else {
+              jj[u] = -1;
+            }
           }
+          float w[U][CPL], vj[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            vj[u] = __shfl(v, jj[u] < 0 ? 0 : jj[u]);
+            const float* wrow = Wt + (int64_t)(k0 + (jj[u] < 0 ? 0 : jj[u])) * C;
+#pragma unroll
+            for (int cc = 0; cc < CPL; ++cc) {
+              const int col = lane + 64 * cc;
+              w[u][cc] = (jj[u] >= 0 && col < C) ? wrow[col] : 0.0f;
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < U; ++u)
+            if (jj[u] >= 0) {
+#pragma unroll
+              for (int cc = 0; cc < CPL; ++cc) acc[cc] = fmaf(vj[u], w[u][cc], acc[cc]);
+            }
         }
-        float w[U][CPL], vj[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          vj[u] = __shfl(v, jj[u] < 0 ? 0 : jj[u]);
-          const float* wrow = Wt + (int64_t)(k0 + (jj[u] < 0 ? 0 : jj[u])) * C;
-#pragma unroll
-          for (int c = 0; c < CPL; ++c) {
-            const int col = lane + 64 * c;
-            w[u][c] = (jj[u] >= 0 && col < C) ? wrow[col] : 0.0f;
-          }
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-          if (jj[u] >= 0) {
-#pragma unroll
-            for (int c = 0; c < CPL; ++c) acc[c] = fmaf(vj[u], w[u][c], acc[c]);
-          }
       }
     }
 #pragma unroll
