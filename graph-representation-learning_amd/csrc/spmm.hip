@@ -29,6 +29,8 @@
 
 #include "grl_internal.h"
 
+#include <cstdlib>
+
 namespace grl {
 namespace {
 
@@ -85,6 +87,18 @@ __device__ __forceinline__ void vstore(float* p, const float& v) {
 #else
   *p = v;
 #endif
+}
+
+// Persistent-grid size: 16 four-wave blocks per CU (tuned on C3).  The
+// GRL_SPMM_BLOCKS_PER_CU environment variable overrides it (tuning aid, e.g.
+// to leave room for a concurrent GEMM on another stream).
+int spmm_blocks_per_cu() {
+  static const int v = [] {
+    const char* e = getenv("GRL_SPMM_BLOCKS_PER_CU");
+    const int x = e ? atoi(e) : 0;
+    return x > 0 && x <= 64 ? x : 16;
+  }();
+  return v;
 }
 
 // Device view of a split plan (all null / zero when the graph is not split).
@@ -411,7 +425,7 @@ int launch_spmm(int64_t num_rows, int64_t self_rows, int S, int hs, const int32_
   if (rc) return rc;
   const LaunchShape sh = pick_shape(src, align_probe, lds, ldo, F);
   const int64_t items = num_rows + sp.num_chunks;
-  const int64_t cap = (int64_t)device_cu_count() * 16;  // 16 x 4-wave blocks per CU in flight
+  const int64_t cap = (int64_t)device_cu_count() * spmm_blocks_per_cu();  // 4-wave blocks per CU in flight
   const int64_t gx = std::min<int64_t>(ceil_div(items, 4), cap);
   const dim3 grid((unsigned)gx, (unsigned)ceil_div(F, sh.ycols));
   const dim3 block(256);

@@ -18,7 +18,7 @@ import torch
 from torch import nn
 
 from grl import TypedGraph
-from grl.ops import graph_linear, node_self_attention, typed_aggregate
+from grl.ops import graph_conv, node_self_attention
 
 
 def make_linear_relu(input_dim: int, output_dim: int) -> nn.Sequential:
@@ -74,8 +74,8 @@ class GraphConv(nn.Module):
     def propagate(self, V: torch.Tensor, graph: TypedGraph, relu: bool = False) -> torch.Tensor:
         """Aggregate + linear (+ fused ReLU) on a ready TypedGraph."""
         B, N = V.shape[0], V.shape[1]
-        Z = typed_aggregate(V, graph)  # (B*N, (L+1)F), the reference's new_V
-        out = graph_linear(Z, self.h_weights, self.bias, relu=relu)
+        # new_V = A_pre V (B*N, (L+1)F) then new_V h_weights + bias, one autograd node
+        out = graph_conv(V, graph, self.h_weights, self.bias, relu=relu)
         return out.view(B, N, self.C)
 
     def forward(self, V: torch.Tensor, A: AdjLike, preprocess_A: bool = True) -> torch.Tensor:

@@ -50,6 +50,17 @@ def spmm_forward(X: torch.Tensor, graph: TypedGraph, out: torch.Tensor = None) -
     return out
 
 
+def spmm_backward(dZ: torch.Tensor, graph: TypedGraph, F: int) -> torch.Tensor:
+    """dX = A_drop^T dZ (grl_typed_spmm_bwd over the cached CSC, same mask)."""
+    dZ = dZ.contiguous().float()
+    dX = torch.empty(graph.num_cols, F, dtype=torch.float32, device=dZ.device)
+    csc = graph.csc_c(F)
+    de = graph.dropedge.to_c() if graph.dropedge is not None else None
+    call("grl_typed_spmm_bwd", ctypes.byref(csc), dZ.data_ptr(), F, dX.data_ptr(), F,
+         ctypes.byref(de) if de is not None else None, current_stream_handle(dZ.device))
+    return dX
+
+
 class _TypedAggregate(torch.autograd.Function):
     @staticmethod
     def forward(ctx, X: torch.Tensor, graph: TypedGraph) -> torch.Tensor:
@@ -60,15 +71,7 @@ class _TypedAggregate(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dZ: torch.Tensor):
-        graph: TypedGraph = ctx.graph
-        dZ = dZ.contiguous().float()
-        F = ctx.xshape[-1]
-        dX = torch.empty(graph.num_cols, F, dtype=torch.float32, device=dZ.device)
-        csc = graph.csc_c(F)
-        de = graph.dropedge.to_c() if graph.dropedge is not None else None
-        call("grl_typed_spmm_bwd", ctypes.byref(csc), dZ.data_ptr(), F, dX.data_ptr(), F,
-             ctypes.byref(de) if de is not None else None, current_stream_handle(dZ.device))
-        return dX.view(ctx.xshape), None
+        return spmm_backward(dZ, ctx.graph, ctx.xshape[-1]).view(ctx.xshape), None
 
 
 def typed_aggregate(X: torch.Tensor, graph: TypedGraph) -> torch.Tensor:
@@ -142,6 +145,45 @@ class _GraphLinear(torch.autograd.Function):
             if not ctx.needs_input_grad[1]:
                 dW = None
         return dZ, dW, db, None
+
+
+class _GraphConv(torch.autograd.Function):
+    """One GraphConv layer, X -> Z = A_drop X -> out = Z W + b [ReLU]
+    (robust_gcn.py:45-51), as one autograd node: the same kernels and
+    results as typed_aggregate + graph_linear.  (Running dW on a second HIP
+    stream beside dZ / the transposed gather was measured and bought nothing:
+    39-41 ms per C3 layer either way, each kernel already fills the chip.)"""
+
+    @staticmethod
+    def forward(ctx, X: torch.Tensor, graph: TypedGraph, W: torch.Tensor, b, relu: bool):
+        Z = spmm_forward(X, graph)
+        Wc = W.contiguous()
+        out = linear_fwd(Z, Wc, b.contiguous() if b is not None else None, relu)
+        ctx.graph, ctx.relu, ctx.has_b, ctx.xshape = graph, relu, b is not None, X.shape
+        ctx.save_for_backward(Z, Wc, out if relu else None)
+        return out
+
+    @staticmethod
+    def backward(ctx, g: torch.Tensor):
+        Z, W, out = ctx.saved_tensors
+        g = g.contiguous().float()
+        mask = out if ctx.relu else None
+        want_w = ctx.needs_input_grad[2]
+        want_b = ctx.has_b and ctx.needs_input_grad[3]
+        dW = db = dX = None
+        if ctx.needs_input_grad[0]:
+            dZ = linear_bwd_data(g, mask, W)
+            dX = spmm_backward(dZ, ctx.graph, ctx.xshape[-1]).view(ctx.xshape)
+            del dZ
+        if want_w or want_b:
+            dW, db = linear_bwd_weight(Z, g, mask, want_b)
+        return dX, None, dW if want_w else None, db, None
+
+
+def graph_conv(X: torch.Tensor, graph: TypedGraph, W: torch.Tensor, b=None, relu: bool = False) -> torch.Tensor:
+    """GraphConv forward (aggregation + linear [+ReLU]) as one autograd node;
+    X: [num_cols, F] (or [B, N, F] for a batch graph)."""
+    return _GraphConv.apply(X, graph, W, b, relu)
 
 
 def graph_linear(Z: torch.Tensor, W: torch.Tensor, b=None, relu: bool = False) -> torch.Tensor:
