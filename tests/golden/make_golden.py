@@ -259,13 +259,82 @@ def make_text_fixtures():
     print("normalize_text:", len(out), "cases")
 
 
-def main():
+def make_model_variant_fixtures(GraphCNNDropEdge):
+    """model_variants.npz: the reduced model on a padded B=2 batch with a
+    float fc_similarity-style adjacency (eval, with and without attention),
+    and a train step with efficient_mode=False, whose edge dropout hits the
+    raw A (drop_robust_gcn.py:67-72, robust_gcn.py:42-43: the identity is
+    added afterwards and never dropped) with injected masks."""
+    B, N, L, Fin, C, out_dim = 2, 9, 6, 40, 32, 5
+    r = gi.rng(61)
+    A = (r.random((B, N, L, N)) < 0.25) * r.uniform(0.05, 1.0, (B, N, L, N))
+    A = A.astype(np.float16).astype(np.float32)  # the builders emit fp16 (graph_utils.py:794-806)
+    A[1, -3:] = 0.0
+    A[1, :, :, -3:] = 0.0  # three padded nodes in the second graph (NumpyPadding)
+    V = gi.features(62, B, N, Fin)
+    V[1, -3:] = 0.0
+    out = {"A": A, "V": V}
+    for tag, att in (("att", True), ("noatt", False)):
+        torch.manual_seed(5)
+        m = GraphCNNDropEdge(Fin, out_dim, L, net_size=C, use_attention=att)
+        m.eval()
+        with torch.no_grad():
+            out[f"{tag}::logits"] = m([_t(V), _t(A)]).numpy()
+        out.update({f"{tag}::init::{k}": v.detach().numpy() for k, v in m.state_dict().items()})
+
+    # efficient_mode=False, train mode, feature dropout off, masks on raw A
+    Ab = gi.random_adj_bnln(63, B, N, L, 3.0)
+    labels = gi.rng(64).integers(0, out_dim, size=(B, N))
+    de = gi.DROPEDGE
+    raw = []
+    for c in range(3):
+        mp = dense_ref.dropedge_weights_pre(Ab, de["p"], de["seed"], c, drop_self=False)  # (B,(L+1)N,N)
+        mp = mp.reshape(B, N, L + 1, N)[:, :, 1:, :]      # typed blocks, [b, n, t, m]
+        raw.append(np.ascontiguousarray(mp.transpose(0, 1, 3, 2)))  # raw A layout after permute: [b, n, m, t]
+
+    class InjectedRawEdgeDropout(torch.nn.Module):
+        def __init__(self, ms):
+            super().__init__()
+            self.ms = ms
+            self.i = 0
+
+        def forward(self, a):
+            m = self.ms[self.i]
+            self.i += 1
+            keep = _t((m != 0).astype(np.float32))
+            scale = float(m.max()) if (m != 0).any() else 1.0
+            return a.mul(keep).mul_(scale)
+
+    torch.manual_seed(6)
+    m = GraphCNNDropEdge(Fin, out_dim, L, net_size=C)
+    out.update({f"effF::init::{k}": v.detach().clone().numpy() for k, v in m.state_dict().items()})
+    m.train()
+    m.dropout.p = 0.0
+    m.edge_dropout = InjectedRawEdgeDropout(raw)
+    logits = m([_t(V), _t(Ab)], efficient_mode=False)
+    loss = torch.nn.functional.cross_entropy(logits.transpose(1, 2), torch.from_numpy(labels))
+    loss.backward()
+    out.update({"effF::A": Ab, "effF::labels": labels, "effF::logits": logits.detach().numpy(),
+                "effF::loss": np.array(loss.item())})
+    out.update({f"effF::grad::{k}": p.grad.numpy() for k, p in m.named_parameters() if p.grad is not None})
+    np.savez_compressed(os.path.join(HERE, "model_variants.npz"), **out)
+    print(f"model_variants: att {np.abs(out['att::logits']).max():.4g} noatt {np.abs(out['noatt::logits']).max():.4g}"
+          f" effF loss {loss.item():.6f}")
+
+
+def main(parts=("text", "graphconv", "model", "layout", "variants")):
     GraphConv, GraphCNNDropEdge, HGB, TLE = _import_reference()
-    make_text_fixtures()
-    make_graphconv_fixtures(GraphConv)
-    make_model_fixtures(GraphCNNDropEdge, HGB, TLE)
-    make_layout_fixtures(HGB, TLE)
+    if "text" in parts:
+        make_text_fixtures()
+    if "graphconv" in parts:
+        make_graphconv_fixtures(GraphConv)
+    if "model" in parts:
+        make_model_fixtures(GraphCNNDropEdge, HGB, TLE)
+    if "layout" in parts:
+        make_layout_fixtures(HGB, TLE)
+    if "variants" in parts:
+        make_model_variant_fixtures(GraphCNNDropEdge)
 
 
 if __name__ == "__main__":
-    main()
+    main(tuple(sys.argv[1:]) or ("text", "graphconv", "model", "layout", "variants"))

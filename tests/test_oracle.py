@@ -181,3 +181,24 @@ def test_oracle_model_matches_reference_train_masks(golden):
     mults = [dense_ref.dropedge_weights_pre(g["A"], de["p"], de["seed"], c) for c in range(3)]
     logits = dense_ref.graph_cnn_dropedge_forward(P, g["V"], g["A"], edge_mults=mults)
     _close(logits, g["logits"], 1e-5)
+
+
+@pytest.mark.parametrize("tag,att", [("att", True), ("noatt", False)])
+def test_oracle_model_variants_eval(golden, tag, att):
+    """Padded B=2 batch, float (fc_similarity-style) adjacency, with and
+    without NodeSelfAtten: numpy restatement vs the reference's logits."""
+    g = golden("model_variants.npz")
+    P = {k[len(f"{tag}::init::"):]: v.astype(np.float64) for k, v in g.items() if k.startswith(f"{tag}::init::")}
+    logits = dense_ref.graph_cnn_dropedge_forward(P, g["V"], g["A"], use_attention=att)
+    _close(logits, g[f"{tag}::logits"], 1e-5)
+
+
+def test_oracle_model_efficient_mode_false(golden):
+    """efficient_mode=False: the edge masks hit raw A and the identity is
+    never dropped (drop_self=False multipliers)."""
+    g = golden("model_variants.npz")
+    P = {k[len("effF::init::"):]: v.astype(np.float64) for k, v in g.items() if k.startswith("effF::init::")}
+    de = gi.DROPEDGE
+    mults = [dense_ref.dropedge_weights_pre(g["effF::A"], de["p"], de["seed"], c, drop_self=False) for c in range(3)]
+    logits = dense_ref.graph_cnn_dropedge_forward(P, g["V"], g["effF::A"], edge_mults=mults)
+    _close(logits, g["effF::logits"], 1e-5)
