@@ -54,7 +54,7 @@ def parse():
     ap.add_argument("--halo", choices=["auto", "sparse", "dense"], default="auto",
                     help="halo exchange layout for N>1 (grl/dist.py): sparse all-to-all-v of the referenced rows, "
                          "dense all-gather of every shard; auto picks dense when >=75%% of remote rows are referenced")
-    ap.add_argument("--only", choices=["fwd", "bwd", "linear", "layer", "c1"], default=None,
+    ap.add_argument("--only", choices=["fwd", "bwd", "linear", "layer", "c1", "model"], default=None,
                     help="profiling aid: run just that kernel K times (no JSON line); c1: print the C1 "
                          "(debug.json model) timings alone")
     return ap.parse_args()
@@ -84,6 +84,9 @@ def main():
 
     if args.only == "c1":
         print(json.dumps({"c1_debug_json": c1_extras(dev, max(3, args.steps))}), flush=True)
+        return
+    if args.only == "model":
+        print(json.dumps({"model_one_graph_100k": model_extras(dev)}), flush=True)
         return
 
     from grl import DropEdge
@@ -198,6 +201,7 @@ def main():
             del X_full, Z
             torch.cuda.empty_cache()  # C1 is a small-graph workload: time it without C3's 8 GB resident
             out["extras"]["c1_debug_json"] = c1_extras(dev)
+            out["extras"]["model_one_graph_100k"] = model_extras(dev)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -211,6 +215,8 @@ def workload_name(args, world, n_loc):
         return "C5" if (n_loc * world == 1 << 23 and args.dim == 512) else "C5-shape"
     if args.dim == 256 and args.avg_deg == 32 and n_loc == 1_000_000:
         return {1: "C3", 4: "C4"}.get(world, "C4-shape (1M nodes/GPU)")
+    if args.dim == 256 and args.avg_deg == 32 and n_loc * world == 4_000_000:
+        return "C4"
     if args.dim == 256 and args.avg_deg == 16 and n_loc * world == 100_000:
         return "C2"
     return "custom"
@@ -398,6 +404,41 @@ def c1_extras(dev, iters=20):
     res["logits_max_abs_diff_vs_oracle"] = float(np.abs(logits - ref).max())
     res["tolerance"] = 1e-4
     return res
+
+
+def model_extras(dev, N=100_000, avg_deg=16.0, iters=3):
+    """The whole GraphCNNDropEdge(4369, 53, 6, 256) on ONE synthetic graph of
+    N nodes (C2's ER graph, bag-of-characters rows ~7 nonzeros of 4369):
+    eval forward and one Adam train step (DropEdge p=0.3 x3, fused
+    attention over all N nodes).  The reference's dense path cannot run this
+    (A_pre alone would be (L+1)*N^2*4 B = 280 GB at N=100k)."""
+    from gnn.models import GraphCNNDropEdge
+    from grl import TypedGraph
+
+    g = TypedGraph.synthetic(N, avg_deg, 6, seed=0, device=dev)
+    gen = torch.Generator(device=dev).manual_seed(1)
+    V = torch.zeros(1, N, 4369, device=dev)
+    cols = torch.randint(0, 4365, (N, 7), generator=gen, device=dev)
+    V[0].scatter_(1, cols, 1.0)
+    V[0, :, -4:] = torch.rand(N, 4, generator=gen, device=dev)
+    torch.manual_seed(0)
+    model = GraphCNNDropEdge(4369, 53, 6, 256).to(dev)
+    y = torch.randint(0, 53, (1, N), generator=gen, device=dev)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+    lossf = torch.nn.CrossEntropyLoss()
+    model.eval()
+    with torch.no_grad():
+        ev = _time(lambda: model([V, g]), iters)
+
+    def step():
+        opt.zero_grad(set_to_none=True)
+        lossf(model.forward([V, g]).reshape(-1, 53), y.reshape(-1)).backward()
+        opt.step()
+
+    model.train()
+    tr = _time(step, iters)
+    return {"nodes": N, "typed_edges": g.nnz, "eval_ms": ev, "train_step_ms": tr,
+            "note": "one graph, B=1; reference dense A_pre would need 280 GB"}
 
 
 def run_only(args, graph, X_full, gather, spmm, L, F):
