@@ -99,11 +99,7 @@ class HaloPlan:
     num_edges_total: int
     mode: str = "sparse"         # "sparse" | "dense" (module docstring)
     stride: int = 0              # dense: max shard rows; rank q's rows sit at X_ext[stride*(1+q):]
-
-    @property
-    def rank(self) -> int:
-        return next(i for i in range(len(self.bounds) - 1)
-                    if self.bounds[i] == self.row_begin and self.bounds[i + 1] == self.row_end)
+    rank: int = 0                # this shard's rank in the group
 
     @property
     def referenced_halo_rows(self) -> int:
@@ -150,7 +146,7 @@ def build_halo_plan(colidx: torch.Tensor, row_begin: int, row_end: int, group=No
         colidx_local = torch.where(own, c - row_begin, slot).to(torch.int32)
         empty = torch.zeros(0, dtype=torch.int64, device=dev)
         return HaloPlan(row_begin, row_end, n_loc, stride * (world + 1) - n_loc, bounds, empty, [0] * world,
-                        [0] * world, halo_ids, colidx_local, edge_id_base, num_edges_total, "dense", stride)
+                        [0] * world, halo_ids, colidx_local, edge_id_base, num_edges_total, "dense", stride, rank)
     if world > 1:
         ends_t = torch.tensor(bounds[1:], dtype=torch.int64, device=dev)
         owner = torch.searchsorted(ends_t, halo_ids, right=True)
@@ -172,7 +168,7 @@ def build_halo_plan(colidx: torch.Tensor, row_begin: int, row_end: int, group=No
     slot = n_loc + torch.searchsorted(halo_ids, c)
     colidx_local = torch.where(own, c - row_begin, slot).to(torch.int32)
     return HaloPlan(row_begin, row_end, n_loc, int(halo_ids.numel()), bounds, send_index, send_counts, recv_counts,
-                    halo_ids, colidx_local, edge_id_base, num_edges_total, "sparse", n_loc)
+                    halo_ids, colidx_local, edge_id_base, num_edges_total, "sparse", n_loc, rank)
 
 
 class _HaloExchange(torch.autograd.Function):

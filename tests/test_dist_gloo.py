@@ -70,6 +70,7 @@ def _worker(rank, world, port, bounds, mode):
         plan = build_halo_plan(torch.from_numpy(lc.copy()), rb, re, mode=mode)
         # referenced/remote rows: 99% ([0,120,240]), 93% ([0,50,170,240]), 50% (empty shard) -> auto at 75%
         assert plan.mode == (mode if mode != "auto" else ("sparse" if bounds[1] == 0 else "dense"))
+        assert plan.rank == rank
         assert plan.edge_id_base == int(rowptr[rb * L]) and plan.num_edges_total == colidx.size
         # every halo id is remote and referenced; slots are in owner order
         assert not ((plan.halo_ids >= rb) & (plan.halo_ids < re)).any()
@@ -90,7 +91,7 @@ def _worker(rank, world, port, bounds, mode):
 
 
 @pytest.mark.parametrize("mode", ["auto", "sparse", "dense"])
-@pytest.mark.parametrize("bounds", [[0, 120, 240], [0, 50, 170, 240], [0, 0, 100, 240]])
+@pytest.mark.parametrize("bounds", [[0, 120, 240], [0, 50, 170, 240], [0, 0, 100, 240], [0, 0, 0, 240]])
 def test_sharded_equals_single_process(bounds, mode):
     world = len(bounds) - 1
     mp.spawn(_worker, args=(world, _free_port(), bounds, mode), nprocs=world, join=True)
