@@ -29,6 +29,10 @@ constexpr int BM = 128, BN = 128;
 #ifndef GRL_GEMM_VEC_EPI
 #define GRL_GEMM_VEC_EPI 1
 #endif
+#ifndef GRL_GEMM_INTERLEAVE
+#define GRL_GEMM_INTERLEAVE 1
+#endif
+
 
 enum Epilogue { EPI_STORE = 0, EPI_BIAS = 1, EPI_SLAB = 2 };
 
@@ -164,10 +168,9 @@ template <bool A_KC, bool B_KC, int EPI, bool ALIGNED, bool MASK_A, bool MASK_B,
 __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs p) {
   using OA = Operand<A_KC, ALIGNED, MASK_A, BK>;
   using OB = Operand<B_KC, ALIGNED, MASK_B, BK>;
-  __shared__ __attribute__((aligned(16))) float smem[OA::lds_floats() + OB::lds_floats()];
-  static_assert(OA::lds_floats() + OB::lds_floats() >= 4 * 64 * 32, "epilogue staging must fit the operand LDS");
-  float* As = smem;
-  float* Bs = smem + OA::lds_floats();
+  constexpr int STAGE = OA::lds_floats() + OB::lds_floats();
+  __shared__ __attribute__((aligned(16))) float smem[STAGE];
+  static_assert(STAGE >= 4 * 64 * 32, "epilogue staging must fit the operand LDS");
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -203,21 +206,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs p) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
 
-  if (kbeg < kend) {
-    const bool in0 = rows_in && kbeg + BK <= kend;
-    oa.fetch(tid, kbeg, kend, in0);
-    ob.fetch(tid, kbeg, kend, in0);
-  }
-  for (int64_t k0 = kbeg; k0 < kend; k0 += BK) {
-    oa.stash(As, tid);
-    ob.stash(Bs, tid);
-    __syncthreads();
-    const int64_t kn = k0 + BK;
-    if (kn < kend) {  // next tile in flight during the MFMAs
-      const bool in = rows_in && kn + BK <= kend;
-      oa.fetch(tid, kn, kend, in);
-      ob.fetch(tid, kn, kend, in);
-    }
+  auto mma_step = [&](const float* As, const float* Bs) {
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 8) {
       float4 a[2], b[2];
@@ -225,6 +214,20 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs p) {
       for (int i = 0; i < 2; ++i) a[i] = OA::frag(As, wm * 64 + i * 32 + l32, kk, h);
 #pragma unroll
       for (int j = 0; j < 2; ++j) b[j] = OB::frag(Bs, wn * 64 + j * 32 + l32, kk, h);
+#if GRL_GEMM_INTERLEAVE
+      // component-major: consecutive MFMAs hit the four independent
+      // accumulators, so none waits on the previous one's result (the
+      // per-accumulator k order is unchanged: results are bitwise the same)
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(reinterpret_cast<const float*>(&a[i])[c],
+                                                             reinterpret_cast<const float*>(&b[j])[c], acc[i][j],
+                                                             0, 0, 0);
+#else
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -234,7 +237,26 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs p) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].z, b[j].z, acc[i][j], 0, 0, 0);
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].w, b[j].w, acc[i][j], 0, 0, 0);
         }
+#endif
     }
+  };
+
+  if (kbeg < kend) {
+    const bool in0 = rows_in && kbeg + BK <= kend;
+    oa.fetch(tid, kbeg, kend, in0);
+    ob.fetch(tid, kbeg, kend, in0);
+  }
+  for (int64_t k0 = kbeg; k0 < kend; k0 += BK) {
+    oa.stash(smem, tid);
+    ob.stash(smem + OA::lds_floats(), tid);
+    __syncthreads();
+    const int64_t kn = k0 + BK;
+    if (kn < kend) {  // next tile in flight during the MFMAs
+      const bool in = rows_in && kn + BK <= kend;
+      oa.fetch(tid, kn, kend, in);
+      ob.fetch(tid, kn, kend, in);
+    }
+    mma_step(smem, smem + OA::lds_floats());
     __syncthreads();
   }
 
