@@ -104,3 +104,30 @@ def test_two_ranks_on_one_gpu_match_single_gpu(mode, kind):
     import torch.multiprocessing as mp
 
     mp.spawn(_shard_worker, args=(2, _free_port(), mode, kind), nprocs=2, join=True)
+
+
+def test_bench_two_ranks_contract():
+    """The driver's N>1 launch (torch.distributed.run, one rank per GPU) of
+    bench.py, rehearsed with two gloo ranks sharing the box's GPU: exactly
+    one JSON line from rank 0 with the contract's fields, weak scaling and
+    the halo report."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
+           "--dist-backend", "gloo", "--nodes-per-gpu", "20000", "--steps", "2", "--warmup", "1",
+           "--cpu-seconds", "0"]
+    r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "halo"):
+        assert k in out, k
+    assert out["n_gpus"] == 2 and out["scaling"] == "weak" and out["value"] > 0
+    assert out["config"]["nodes_total"] == 40000 and out["halo"]["mode"] in ("dense", "sparse")
