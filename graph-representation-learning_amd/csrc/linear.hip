@@ -19,6 +19,8 @@
 // second pass adds in split order: deterministic, no atomics.
 #include "grl_internal.h"
 
+#include <cstdlib>
+
 namespace grl {
 namespace {
 
@@ -389,6 +391,135 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __rest
   partial[z * C + c] = s;
 }
 
+// ---------------------------------------------------------------------------
+// Large-tile path for the big GraphConv shapes (M or K in the millions):
+// 256 x 256 block tile, 8 waves (2 along M x 4 along N, each 128 x 64 =
+// 4 x 2 MFMA 32x32 tiles, 128 accumulator registers), K staged 32 deep
+// through two LDS stages filled by global_load_lds_dwordx4 (LDS-DMA: no VGPR
+// staging, no ds_write pass, the address math is per stage not per k-step).
+// One block per CU (128 KB LDS); tile t+1 lands while tile t is multiplied;
+// one barrier per K tile (its vmcnt(0) retires the DMA, its s_barrier orders
+// the reads -- MI355X_MICROARCH / cdna_hip_programming "glds" rules).
+// Preconditions (launcher): 16-B aligned operands and leading dimensions,
+// K % 32 == 0, M, N >= 4, no operand masks.
+constexpr int LB_M = 256, LB_N = 256, LB_K = 32, LB_STAGE = LB_M * LB_K;  // floats per operand stage
+
+template <bool KC>
+struct BigOperand {
+  const float* base;
+  int64_t ld, rows_total, row0;
+  // 32 DMA instructions per operand stage, 4 per wave, 1 KB each.
+  //  KC: row r = 32 floats = 8 chunks of 16 B; logical chunk c of row r sits
+  //      at chunk c ^ (r & 7) (swizzled through the SOURCE address: the DMA
+  //      destination is lane-linear) so 32 rows read at one k hit 8 banks.
+  //  RC: one k row = 256 floats = exactly one instruction, linear.
+  __device__ __forceinline__ void issue(float* lds, int wave, int lane, int64_t k0) const {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int inst = wave * 4 + q;
+      const float* src;
+      if (KC) {
+        const int r = inst * 8 + (lane >> 3);
+        const int c = (lane & 7) ^ (r & 7);
+        int64_t row = row0 + r;
+        row = row < rows_total ? row : rows_total - 1;  // tail rows: any valid row, never stored
+        src = base + row * ld + k0 + c * 4;
+      } else {
+        int64_t col = row0 + lane * 4;
+        col = col + 3 < rows_total ? col : rows_total - 4;
+        src = base + (k0 + inst) * ld + col;
+      }
+      __builtin_amdgcn_global_load_lds(src, reinterpret_cast<__attribute__((address_space(3))) void*>(
+                                                reinterpret_cast<uintptr_t>(lds + inst * 256)),
+                                       16, 0, 0);
+    }
+  }
+  // k = kk + 4h + s (s = 0..3) of local row `row`, as in Operand::frag
+  __device__ __forceinline__ static float4 frag(const float* lds, int row, int kk, int h) {
+    if (KC) {
+      const int c = (kk >> 2) + h;
+      return *reinterpret_cast<const float4*>(&lds[row * LB_K + ((c ^ (row & 7)) << 2)]);
+    }
+    const float* q = &lds[(kk + 4 * h) * LB_N + row];
+    return make_float4(q[0], q[LB_N], q[2 * LB_N], q[3 * LB_N]);
+  }
+};
+
+template <bool A_KC, bool B_KC, int EPI>
+__global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs p) {
+  __shared__ __attribute__((aligned(16))) float smem[4 * LB_STAGE];  // 2 stages x (A, B): 128 KB
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int l32 = lane & 31, h = lane >> 5;
+  int64_t mi, ni, zi;
+  tile_of(p, mi, ni, zi);
+  const int64_t m0 = mi * LB_M, n0 = ni * LB_N;
+  const int64_t kbeg = zi * p.k_per_split;
+  const int64_t kend = min(p.K, kbeg + p.k_per_split);
+  const int64_t nk = kend > kbeg ? (kend - kbeg) / LB_K : 0;
+  const BigOperand<A_KC> oa{p.A, p.lda, p.M, m0};
+  const BigOperand<B_KC> ob{p.B, p.ldb, p.N, n0};
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+
+  if (nk > 0) {
+    oa.issue(smem, wave, lane, kbeg);
+    ob.issue(smem + LB_STAGE, wave, lane, kbeg);
+  }
+  __syncthreads();
+  for (int64_t t = 0; t < nk; ++t) {
+    const float* cur = smem + (t & 1) * 2 * LB_STAGE;
+    if (t + 1 < nk) {
+      float* nx = smem + ((t + 1) & 1) * 2 * LB_STAGE;
+      oa.issue(nx, wave, lane, kbeg + (t + 1) * LB_K);
+      ob.issue(nx + LB_STAGE, wave, lane, kbeg + (t + 1) * LB_K);
+    }
+#pragma unroll
+    for (int kk = 0; kk < LB_K; kk += 8) {
+      float4 a[4], b[2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[i] = BigOperand<A_KC>::frag(cur, wm * 128 + i * 32 + l32, kk, h);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b[j] = BigOperand<B_KC>::frag(cur + LB_STAGE, wn * 64 + j * 32 + l32, kk, h);
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(reinterpret_cast<const float*>(&a[i])[c],
+                                                             reinterpret_cast<const float*>(&b[j])[c], acc[i][j],
+                                                             0, 0, 0);
+    }
+    __syncthreads();  // vmcnt(0): tile t+1 landed; barrier: every wave is done reading tile t
+  }
+
+  float* Cz = p.C + (EPI == EPI_SLAB ? zi * p.M * p.ldc : 0);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int64_t gn = n0 + wn * 64 + j * 32 + l32;
+    if (gn >= p.N) continue;
+    const float bv = (EPI == EPI_BIAS && p.bias) ? p.bias[gn] : 0.0f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t gm = m0 + wm * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (gm < p.M) {
+          float v = acc[i][j][r] + bv;
+          if (EPI == EPI_BIAS && p.relu) v = v > 0.0f ? v : 0.0f;
+          Cz[gm * p.ldc + gn] = v;
+        }
+      }
+  }
+}
+
 bool al16(const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; }
 
 #ifndef GRL_GEMM_BK
@@ -449,10 +580,46 @@ size_t small_ws_bytes(int64_t M, int64_t N, int64_t K) {
   return s > 1 ? (size_t)s * (size_t)M * (size_t)N * 4 + 256 : 0;
 }
 
+// Large-tile path selection.  GRL_GEMM_BIG=0 disables it (A/B aid).
+bool big_enabled() {
+  static const bool v = [] {
+    const char* e = getenv("GRL_GEMM_BIG");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
+bool big_ok(const GemmArgs& a, bool aligned) {
+  return big_enabled() && aligned && !a.Amask && !a.Bmask && a.K % LB_K == 0 && a.M >= 4 && a.N >= 4 &&
+         2.0 * (double)a.M * (double)a.N * (double)a.K >= 1.6e10;
+}
+
+template <bool A_KC, bool B_KC, int EPI>
+int launch_gemm256(GemmArgs a, int splits, hipStream_t st) {
+  a.mt = ceil_div(a.M, LB_M);
+  a.nt = ceil_div(a.N, LB_N);
+  a.zt = splits;
+  a.inner_n = A_KC ? 1 : 0;
+  GRL_CHECK_ARG(a.mt * a.nt * a.zt < 2147483647LL, "gemm: grid too large");
+  hipLaunchKernelGGL((gemm256_kernel<A_KC, B_KC, EPI>), dim3((unsigned)(a.mt * a.nt * a.zt)), dim3(512), 0, st, a);
+  GRL_LAUNCH_CHECK();
+  return GRL_OK;
+}
+
 // Output-stationary GEMM with optional split-K through `ws` (slab layout
 // [split][M][N], then one ordered reduce applying bias / ReLU).
 template <bool A_KC, bool B_KC>
 int run_output_gemm(GemmArgs a, bool aligned, const char* who, void* ws, size_t ws_bytes, hipStream_t st) {
+  // The large tile pays for dZ = g W^T (both operands K-contiguous, short K:
+  // 7.98 -> 7.57 ms at C3); for the forward it ties the 128^2 kernel and for
+  // dW (both M/N-contiguous) it lost (7.8 -> 10.7 ms), so those keep it off.
+  if constexpr (A_KC && B_KC) {
+    if (big_ok(a, aligned)) {
+      a.k_per_split = std::max<int64_t>(a.K, 1);
+      return a.bias || a.relu ? launch_gemm256<A_KC, B_KC, EPI_BIAS>(a, 1, st)
+                              : launch_gemm256<A_KC, B_KC, EPI_STORE>(a, 1, st);
+    }
+  }
   const int splits = pick_splits_small(a.M, a.N, a.K);
   if (splits == 1) {
     a.k_per_split = std::max<int64_t>(a.K, 1);
@@ -554,7 +721,6 @@ extern "C" int grl_linear_bwd_weight(const float* Z, int64_t ldz, const float* g
   if (!workspace || workspace_bytes < need)
     GRL_FAIL(GRL_E_WORKSPACE, "grl_linear_bwd_weight: workspace %zu < %zu", workspace_bytes, need);
   hipStream_t st = as_stream(stream);
-  const int splits = pick_splits(K, C, M);
   float* slab = static_cast<float*>(workspace);
   GemmArgs a{};
   a.A = Z;  // A(m=kk, k=row) = Z[row][kk]: rows of Z are M-contiguous for fixed k
@@ -562,25 +728,27 @@ extern "C" int grl_linear_bwd_weight(const float* Z, int64_t ldz, const float* g
   a.B = g;  // B(k=row, n=c) = g[row][c]
   a.ldb = C;
   a.Bmask = relu_out;
-  a.C = splits > 1 ? slab : dW;
   a.ldc = C;
   a.M = K;
   a.N = C;
   a.K = M;
-  a.k_per_split = ceil_div(ceil_div(M, splits), GEMM_BK) * GEMM_BK;
   const bool aligned = al16(Z) && al16(g) && (!relu_out || al16(relu_out)) && ldz % 4 == 0 && C % 4 == 0 && K % 4 == 0;
-  int rc = splits > 1 ? launch_gemm<false, false, EPI_SLAB>(a, splits, aligned, st)
-                      : launch_gemm<false, false, EPI_STORE>(a, 1, aligned, st);
+  const int splits = pick_splits(K, C, M);
+  a.C = splits > 1 ? slab : dW;
+  a.k_per_split = ceil_div(ceil_div(M, splits), GEMM_BK) * GEMM_BK;
+  const int used = (int)ceil_div(M, a.k_per_split);
+  const int rc = used > 1 ? launch_gemm<false, false, EPI_SLAB>(a, used, aligned, st)
+                          : launch_gemm<false, false, EPI_STORE>(a, 1, aligned, st);
   if (rc) return rc;
-  if (splits > 1) {
+  if (used > 1) {
     const int64_t n = (int64_t)K * C;
     hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(n, 256), 65536)), dim3(256), 0,
-                       st, slab, n, splits, dW);
+                       st, slab, n, used, dW);
     GRL_LAUNCH_CHECK();
   }
   if (db) {
     const int zs = colsum_splits(M);
-    float* part = slab + (size_t)splits * K * C;
+    float* part = slab + (size_t)pick_splits(K, C, M) * K * C;
     const int64_t rows_per = ceil_div(std::max<int64_t>(M, 1), zs);
     hipLaunchKernelGGL(colsum_partial_kernel, dim3((unsigned)ceil_div(C, 256), (unsigned)zs), dim3(256), 0, st, g,
                        relu_out, M, C, rows_per, part);

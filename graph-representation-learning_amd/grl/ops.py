@@ -80,6 +80,22 @@ def typed_aggregate(X: torch.Tensor, graph: TypedGraph) -> torch.Tensor:
     return _TypedAggregate.apply(X, graph)
 
 
+# Row count from which the backward applies the ReLU mask to g once
+# (torch.where, one elementwise pass) instead of inside the GEMM loads, so the
+# two backward GEMMs qualify for libgrl's large-tile LDS-DMA path (which
+# streams operands straight into LDS and cannot mask on the way).
+PREMASK_ROWS = 65536
+
+
+def relu_grad(g: torch.Tensor, out):
+    """(g_eff, mask_for_the_gemm): g through ReLU's derivative [out > 0]."""
+    if out is None:
+        return g, None
+    if g.shape[0] >= PREMASK_ROWS:
+        return torch.where(out > 0, g, torch.zeros((), dtype=g.dtype, device=g.device)), None
+    return g, out
+
+
 def linear_fwd(Z2: torch.Tensor, W: torch.Tensor, b, relu: bool) -> torch.Tensor:
     M, K = Z2.shape
     C = W.shape[1]
@@ -135,8 +151,7 @@ class _GraphLinear(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g: torch.Tensor):
         Z2, W, out = ctx.saved_tensors
-        g = g.contiguous().float()
-        mask = out if ctx.relu else None
+        g, mask = relu_grad(g.contiguous().float(), out if ctx.relu else None)
         dZ = dW = db = None
         if ctx.needs_input_grad[0]:
             dZ = linear_bwd_data(g, mask, W)
@@ -166,8 +181,7 @@ class _GraphConv(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g: torch.Tensor):
         Z, W, out = ctx.saved_tensors
-        g = g.contiguous().float()
-        mask = out if ctx.relu else None
+        g, mask = relu_grad(g.contiguous().float(), out if ctx.relu else None)
         want_w = ctx.needs_input_grad[2]
         want_b = ctx.has_b and ctx.needs_input_grad[3]
         dW = db = dX = None
@@ -275,8 +289,7 @@ class _BagLinear(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         V2, Wt, out = ctx.saved_tensors
-        g = g.contiguous()
-        relu_out = out if ctx.relu else None
+        g, relu_out = relu_grad(g.contiguous().float(), out if ctx.relu else None)
         dV = linear_bwd_data(g, relu_out, Wt) if ctx.needs_input_grad[0] else None
         dWt, db = linear_bwd_weight(V2, g, relu_out, ctx.has_b)
         return dV, dWt.t(), db, None

@@ -323,3 +323,33 @@ def test_small_m_split_k_deterministic(M, K, C):
     d1 = linear_bwd_data(g, a1, W)
     d2 = linear_bwd_data(g, a1, W)
     assert torch.equal(d1, d2)
+
+
+@pytest.mark.parametrize("M,K,C", [(300_000, 1792, 256), (70_003, 3584, 256), (131_072, 512, 128), (65_600, 256, 1792)])
+def test_large_tile_gemms_match_fp64(M, K, C):
+    """Shapes that take the 256x256 LDS-DMA path (big_ok: aligned, K % 32 == 0,
+    >= 16 GFLOP): forward with bias+ReLU, dZ and dW/db (pre-masked g) against
+    float64 on sampled rows / the full dW; ragged M tails included."""
+    from grl.ops import linear_bwd_data, linear_bwd_weight
+
+    gen = torch.Generator(device=DEV).manual_seed(M % 1000)
+    Z = torch.randn(M, K, device=DEV, generator=gen)
+    W = torch.randn(K, C, device=DEV, generator=gen) / np.sqrt(K)
+    b = torch.randn(C, device=DEV, generator=gen)
+    out = linear_fwd(Z, W, b, True)
+    rows = torch.randint(0, M, (512,), device=DEV, generator=gen)
+    rows[0], rows[1] = 0, M - 1
+    ref = torch.relu(Z[rows].double() @ W.double() + b.double())
+    scale = Z[rows].double().abs() @ W.double().abs() + 1.0
+    assert ((out[rows].double() - ref).abs() <= 1e-5 * scale).all()
+    g = torch.randn(M, C, device=DEV, generator=gen) * (out > 0)
+    dZ = linear_bwd_data(g, None, W)
+    refz = g[rows].double() @ W.double().T
+    scz = g[rows].double().abs() @ W.double().abs().T + 1.0
+    assert ((dZ[rows].double() - refz).abs() <= 1e-5 * scz).all()
+    dW, db = linear_bwd_weight(Z, g, None, True)
+    refw = Z.double().T @ g.double()
+    scw = Z.double().abs().T @ g.double().abs() + 1.0
+    assert ((dW.double() - refw).abs() <= 1e-5 * scw).all()
+    torch.testing.assert_close(db.double(), g.double().sum(0), rtol=1e-5, atol=1e-3)
+    assert torch.equal(linear_fwd(Z, W, b, True), out)  # deterministic

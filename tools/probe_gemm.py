@@ -31,8 +31,12 @@ g = torch.randn(M, C, device=dev)
 out = torch.randn(M, C, device=dev)
 fl = 2.0 * M * K * C / 1e12
 tag = os.path.basename(os.environ.get("GRL_LIB_PATH", "libgrl.so"))
+gm = torch.where(out > 0, g, 0.0)
 for name, fn in [("fwd", lambda: linear_fwd(Z, W, b, True)), ("bwd_data", lambda: linear_bwd_data(g, out, W)),
                  ("bwd_weight", lambda: linear_bwd_weight(Z, g, out, True)),
+                 ("bwd_data_pm", lambda: linear_bwd_data(gm, None, W)),
+                 ("bwd_wgt_pm", lambda: linear_bwd_weight(Z, gm, None, True)),
+                 ("premask", lambda: torch.where(out > 0, g, 0.0)),
                  ("torch_fwd", lambda: torch.addmm(b, Z, W)), ("torch_dZ", lambda: g @ W.t()),
                  ("torch_dW", lambda: Z.t() @ g)]:
     ms = t(fn)
