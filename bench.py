@@ -316,6 +316,17 @@ def extras(args, graph, X_full, gather, L, F, dev, E_loc, n_loc):
     flops = 2.0 * Zd.shape[0] * Zd.shape[1] * F
     res["linear_mfma_fwd"] = {"ms": ms, "TFLOPs": flops / (ms * 1e-3) / 1e12,
                               "frac_of_f32_mfma_peak": flops / (ms * 1e-3) / 1e12 / F32_MFMA_PEAK_TFS}
+    from grl.ops import linear_bwd_data, linear_bwd_weight, relu_grad
+
+    out_l = linear_fwd(Zd, W, b, True)
+    g_l = torch.randn_like(out_l)
+    gm, mask = relu_grad(g_l, out_l)  # the layer backward's ReLU handling
+    for name, fn in (("linear_mfma_bwd_data", lambda: linear_bwd_data(gm, mask, W)),
+                     ("linear_mfma_bwd_weight", lambda: linear_bwd_weight(Zd, gm, mask, True))):
+        ms = _time(fn, iters)
+        res[name] = {"ms": ms, "TFLOPs": flops / (ms * 1e-3) / 1e12,
+                     "frac_of_f32_mfma_peak": flops / (ms * 1e-3) / 1e12 / F32_MFMA_PEAK_TFS}
+    del out_l, g_l, gm
     Wp = W.clone().requires_grad_(True)
     bp = b.clone().requires_grad_(True)
     Xl = X_full.detach()[: graph.num_cols].clone().requires_grad_(True)
