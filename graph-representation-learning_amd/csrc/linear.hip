@@ -392,62 +392,80 @@ __global__ __launch_bounds__(256) void colsum_partial_kernel(const float* __rest
 }
 
 // ---------------------------------------------------------------------------
-// Large-tile path for the big GraphConv shapes (M or K in the millions):
-// 256 x 256 block tile, 8 waves (2 along M x 4 along N, each 128 x 64 =
-// 4 x 2 MFMA 32x32 tiles, 128 accumulator registers), K staged 32 deep
-// through two LDS stages filled by global_load_lds_dwordx4 (LDS-DMA: no VGPR
-// staging, no ds_write pass, the address math is per stage not per k-step).
-// One block per CU (128 KB LDS); tile t+1 lands while tile t is multiplied;
-// one barrier per K tile (its vmcnt(0) retires the DMA, its s_barrier orders
-// the reads -- MI355X_MICROARCH / cdna_hip_programming "glds" rules).
-// Preconditions (launcher): 16-B aligned operands and leading dimensions,
-// K % 32 == 0, M, N >= 4, no operand masks.
-constexpr int LB_M = 256, LB_N = 256, LB_K = 32, LB_STAGE = LB_M * LB_K;  // floats per operand stage
+// Large-tile path for the big GraphConv shapes (M in the millions): 256 x 256
+// block tile, 8 waves (2 along M x 4 along N, each 128 x 64 = 4 x 2 MFMA
+// 32x32 tiles, 128 accumulator registers), one block per CU.  K is staged 16
+// deep through THREE LDS stages (96 KB) filled by global_load_lds_dwordx4
+// (LDS-DMA: no VGPR staging, no ds_write pass); tile t+1's DMA stays in
+// flight across the barrier (counted `s_waitcnt vmcnt(4)`, raw s_barrier --
+// cdna_hip_programming.md "Pipelining across barriers").  Measured at C3:
+// forward 7.97 -> 7.56 ms, dZ 8.0 -> 7.55 ms; dW (both operands M/N
+// contiguous) stays on the 128^2 kernel (7.8 ms vs 10.6 here).
+// Preconditions (big_ok): 16-B aligned operands and leading dimensions,
+// K % 16 == 0, M, N >= 4, no operand masks.
+constexpr int LB_M = 256, LB_N = 256;
+constexpr int LP_K = 16, LP_STAGE = LB_M * LP_K;  // floats per operand stage
 
 template <bool KC>
-struct BigOperand {
+struct PipeOperand {
   const float* base;
   int64_t ld, rows_total, row0;
-  // 32 DMA instructions per operand stage, 4 per wave, 1 KB each.
-  //  KC: row r = 32 floats = 8 chunks of 16 B; logical chunk c of row r sits
-  //      at chunk c ^ (r & 7) (swizzled through the SOURCE address: the DMA
-  //      destination is lane-linear) so 32 rows read at one k hit 8 banks.
-  //  RC: one k row = 256 floats = exactly one instruction, linear.
+  //  KC: row = 16 floats = 4 chunks; 16 rows per 1 KB instruction; chunk c of
+  //      row r at c ^ (r & 3).   RC: one k row (256 floats) per instruction.
   __device__ __forceinline__ void issue(float* lds, int wave, int lane, int64_t k0) const {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int inst = wave * 4 + q;
+    for (int q = 0; q < 2; ++q) {
+      const int inst = wave * 2 + q;  // 16 per operand stage
       const float* src;
       if (KC) {
-        const int r = inst * 8 + (lane >> 3);
-        const int c = (lane & 7) ^ (r & 7);
+        const int r = inst * 16 + (lane >> 2);
+        const int c = (lane & 3) ^ (r & 3);
         int64_t row = row0 + r;
-        row = row < rows_total ? row : rows_total - 1;  // tail rows: any valid row, never stored
+        row = row < rows_total ? row : rows_total - 1;
         src = base + row * ld + k0 + c * 4;
       } else {
         int64_t col = row0 + lane * 4;
         col = col + 3 < rows_total ? col : rows_total - 4;
         src = base + (k0 + inst) * ld + col;
       }
-      __builtin_amdgcn_global_load_lds(src, reinterpret_cast<__attribute__((address_space(3))) void*>(
-                                                reinterpret_cast<uintptr_t>(lds + inst * 256)),
-                                       16, 0, 0);
+      // Issued from asm so that the compiler's waitcnt pass does not see an
+      // LDS write in flight and wait vmcnt(0) before every ds_read (which
+      // would serialize the pipeline); ordering is the counted vmcnt +
+      // s_barrier in the kernel.  M0 = the wave-uniform LDS byte address.
+      const uint32_t dst = __builtin_amdgcn_readfirstlane(
+          (uint32_t)reinterpret_cast<uintptr_t>(lds + inst * 256));
+      uint32_t keep;
+      asm volatile(
+          "s_mov_b32 %0, m0\n\t"
+          "s_mov_b32 m0, %2\n\t"
+          "s_nop 0\n\t"
+          "global_load_lds_dwordx4 %1, off\n\t"
+          "s_mov_b32 m0, %0"
+          : "=&s"(keep)
+          : "v"(src), "s"(dst)
+          : "memory");
     }
   }
-  // k = kk + 4h + s (s = 0..3) of local row `row`, as in Operand::frag
   __device__ __forceinline__ static float4 frag(const float* lds, int row, int kk, int h) {
     if (KC) {
       const int c = (kk >> 2) + h;
-      return *reinterpret_cast<const float4*>(&lds[row * LB_K + ((c ^ (row & 7)) << 2)]);
+      return *reinterpret_cast<const float4*>(&lds[row * LP_K + ((c ^ (row & 3)) << 2)]);
     }
     const float* q = &lds[(kk + 4 * h) * LB_N + row];
     return make_float4(q[0], q[LB_N], q[2 * LB_N], q[3 * LB_N]);
   }
 };
 
-template <bool A_KC, bool B_KC, int EPI>
-__global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs p) {
-  __shared__ __attribute__((aligned(16))) float smem[4 * LB_STAGE];  // 2 stages x (A, B): 128 KB
+template <int N>
+__device__ __forceinline__ void wait_vm_lgkm0() {
+  if constexpr (N == 0) asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  else if constexpr (N == 4) asm volatile("s_waitcnt vmcnt(4) lgkmcnt(0)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+}
+
+template <bool A_KC, bool B_KC, int EPI, int S>
+__global__ __launch_bounds__(512) void gemm256p_kernel(GemmArgs p) {
+  __shared__ __attribute__((aligned(16))) float smem[S * 2 * LP_STAGE];  // S stages x (A, B), 32 KB each
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
   const int l32 = lane & 31, h = lane >> 5;
@@ -456,9 +474,9 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs p) {
   const int64_t m0 = mi * LB_M, n0 = ni * LB_N;
   const int64_t kbeg = zi * p.k_per_split;
   const int64_t kend = min(p.K, kbeg + p.k_per_split);
-  const int64_t nk = kend > kbeg ? (kend - kbeg) / LB_K : 0;
-  const BigOperand<A_KC> oa{p.A, p.lda, p.M, m0};
-  const BigOperand<B_KC> ob{p.B, p.ldb, p.N, n0};
+  const int64_t nk = kend > kbeg ? (kend - kbeg) / LP_K : 0;
+  const PipeOperand<A_KC> oa{p.A, p.lda, p.M, m0};
+  const PipeOperand<B_KC> ob{p.B, p.ldb, p.N, n0};
 
   f32x16 acc[4][2];
 #pragma unroll
@@ -468,25 +486,36 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs p) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
 
-  if (nk > 0) {
-    oa.issue(smem, wave, lane, kbeg);
-    ob.issue(smem + LB_STAGE, wave, lane, kbeg);
+  auto stage_ptr = [&](int64_t t) { return smem + (int)(t % S) * 2 * LP_STAGE; };
+  for (int64_t t = 0; t < S - 1 && t < nk; ++t) {
+    oa.issue(stage_ptr(t), wave, lane, kbeg + t * LP_K);
+    ob.issue(stage_ptr(t) + LP_STAGE, wave, lane, kbeg + t * LP_K);
   }
-  __syncthreads();
   for (int64_t t = 0; t < nk; ++t) {
-    const float* cur = smem + (t & 1) * 2 * LB_STAGE;
-    if (t + 1 < nk) {
-      float* nx = smem + ((t + 1) & 1) * 2 * LB_STAGE;
-      oa.issue(nx, wave, lane, kbeg + (t + 1) * LB_K);
-      ob.issue(nx + LB_STAGE, wave, lane, kbeg + (t + 1) * LB_K);
+    // tile t landed (the next min(S-2, nk-1-t) tiles' DMA, 4 instructions
+    // per wave each, may stay in flight); every wave's reads of the stage
+    // about to be refilled (tile t-1) are retired
+    const int64_t ahead = nk - 1 - t;
+    if (S >= 4 && ahead >= 2)
+      wait_vm_lgkm0<8>();
+    else if (ahead >= 1)
+      wait_vm_lgkm0<4>();
+    else
+      wait_vm_lgkm0<0>();
+    __builtin_amdgcn_s_barrier();
+    if (t + S - 1 < nk) {
+      float* nx = stage_ptr(t + S - 1);
+      oa.issue(nx, wave, lane, kbeg + (t + S - 1) * LP_K);
+      ob.issue(nx + LP_STAGE, wave, lane, kbeg + (t + S - 1) * LP_K);
     }
+    const float* cur = stage_ptr(t);
 #pragma unroll
-    for (int kk = 0; kk < LB_K; kk += 8) {
+    for (int kk = 0; kk < LP_K; kk += 8) {
       float4 a[4], b[2];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) a[i] = BigOperand<A_KC>::frag(cur, wm * 128 + i * 32 + l32, kk, h);
+      for (int i = 0; i < 4; ++i) a[i] = PipeOperand<A_KC>::frag(cur, wm * 128 + i * 32 + l32, kk, h);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) b[j] = BigOperand<B_KC>::frag(cur + LB_STAGE, wn * 64 + j * 32 + l32, kk, h);
+      for (int j = 0; j < 2; ++j) b[j] = PipeOperand<B_KC>::frag(cur + LP_STAGE, wn * 64 + j * 32 + l32, kk, h);
 #pragma unroll
       for (int c = 0; c < 4; ++c)
 #pragma unroll
@@ -497,7 +526,6 @@ __global__ __launch_bounds__(512) void gemm256_kernel(GemmArgs p) {
                                                              reinterpret_cast<const float*>(&b[j])[c], acc[i][j],
                                                              0, 0, 0);
     }
-    __syncthreads();  // vmcnt(0): tile t+1 landed; barrier: every wave is done reading tile t
   }
 
   float* Cz = p.C + (EPI == EPI_SLAB ? zi * p.M * p.ldc : 0);
@@ -590,18 +618,19 @@ bool big_enabled() {
 }
 
 bool big_ok(const GemmArgs& a, bool aligned) {
-  return big_enabled() && aligned && !a.Amask && !a.Bmask && a.K % LB_K == 0 && a.M >= 4 && a.N >= 4 &&
+  return big_enabled() && aligned && !a.Amask && !a.Bmask && a.K % LP_K == 0 && a.M >= 4 && a.N >= 4 &&
          2.0 * (double)a.M * (double)a.N * (double)a.K >= 1.6e10;
 }
 
 template <bool A_KC, bool B_KC, int EPI>
-int launch_gemm256(GemmArgs a, int splits, hipStream_t st) {
+int launch_gemm256p(GemmArgs a, int splits, hipStream_t st) {
   a.mt = ceil_div(a.M, LB_M);
   a.nt = ceil_div(a.N, LB_N);
   a.zt = splits;
   a.inner_n = A_KC ? 1 : 0;
   GRL_CHECK_ARG(a.mt * a.nt * a.zt < 2147483647LL, "gemm: grid too large");
-  hipLaunchKernelGGL((gemm256_kernel<A_KC, B_KC, EPI>), dim3((unsigned)(a.mt * a.nt * a.zt)), dim3(512), 0, st, a);
+  hipLaunchKernelGGL((gemm256p_kernel<A_KC, B_KC, EPI, 3>), dim3((unsigned)(a.mt * a.nt * a.zt)), dim3(512), 0, st,
+                     a);
   GRL_LAUNCH_CHECK();
   return GRL_OK;
 }
@@ -610,15 +639,10 @@ int launch_gemm256(GemmArgs a, int splits, hipStream_t st) {
 // [split][M][N], then one ordered reduce applying bias / ReLU).
 template <bool A_KC, bool B_KC>
 int run_output_gemm(GemmArgs a, bool aligned, const char* who, void* ws, size_t ws_bytes, hipStream_t st) {
-  // The large tile pays for dZ = g W^T (both operands K-contiguous, short K:
-  // 7.98 -> 7.57 ms at C3); for the forward it ties the 128^2 kernel and for
-  // dW (both M/N-contiguous) it lost (7.8 -> 10.7 ms), so those keep it off.
-  if constexpr (A_KC && B_KC) {
-    if (big_ok(a, aligned)) {
-      a.k_per_split = std::max<int64_t>(a.K, 1);
-      return a.bias || a.relu ? launch_gemm256<A_KC, B_KC, EPI_BIAS>(a, 1, st)
-                              : launch_gemm256<A_KC, B_KC, EPI_STORE>(a, 1, st);
-    }
+  if (big_ok(a, aligned)) {  // forward and dZ at large M: the pipelined 256^2 LDS-DMA tile
+    a.k_per_split = std::max<int64_t>(a.K, 1);
+    return a.bias || a.relu ? launch_gemm256p<A_KC, B_KC, EPI_BIAS>(a, 1, st)
+                            : launch_gemm256p<A_KC, B_KC, EPI_STORE>(a, 1, st);
   }
   const int splits = pick_splits_small(a.M, a.N, a.K);
   if (splits == 1) {
