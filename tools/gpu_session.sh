@@ -4,7 +4,7 @@
 # out (exit 124/134/137/139 or a signal).  Ordinary test failures (pytest
 # rc 1) do not stop later steps.  Usage: tools/gpu_session.sh STEP...
 #   steps: tests smoke bench bench_extras bench_drop bench_c5 bench_c5s prof_bench prof_fwd prof_bwd
-#          prof_linear prof_attn prof_c1 pmc_fwd_fetch pmc_fwd_write
+#          prof_linear prof_layer prof_attn prof_c1 pmc_fwd_fetch pmc_fwd_write
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
 OUT=gpurun_out
@@ -42,6 +42,8 @@ for step in "$@"; do
                   -- python bench.py --only bwd --steps 10 --warmup 2 ;;
     prof_linear) run prof_linear 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_linear" -o run --output-format csv \
                   -- python bench.py --only linear --steps 10 --warmup 2 ;;
+    prof_layer) run prof_layer 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_layer" -o run --output-format csv \
+                  -- python bench.py --only layer --steps 5 --warmup 2 ;;
     prof_attn) run prof_attn 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_attn" -o run --output-format csv \
                   -- python tools/probe_attn.py ;;
     prof_c1) run prof_c1 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c1" -o run --output-format csv \
