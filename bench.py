@@ -233,7 +233,7 @@ def load_traffic(args, n_loc, world):
         d = json.load(open(path))
         key = f"{args.graph}_n{n_loc}_deg{args.avg_deg:g}_L{args.types}_d{args.dim}_p{args.p:g}"
         return d.get(key, {}).get("hbm_bytes_per_launch")
-    except Exception:
+    except (OSError, ValueError):  # unreadable summary: report traffic as unmeasured
         return None
 
 
