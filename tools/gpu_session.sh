@@ -4,7 +4,8 @@
 # out (exit 124/134/137/139 or a signal).  Ordinary test failures (pytest
 # rc 1) do not stop later steps.  Usage: tools/gpu_session.sh STEP...
 #   steps: tests smoke bench bench_extras bench_drop bench_c5 bench_c5s prof_bench prof_fwd prof_bwd
-#          prof_linear prof_layer prof_attn prof_c1 pmc_fwd_fetch pmc_fwd_write
+#          prof_linear prof_layer prof_attn prof_c1 pmc_fwd_fetch pmc_fwd_write pmc_list pmc_linear_mfma
+#          pmc_fwd_tlb pmc_c4_tlb
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
 OUT=gpurun_out
@@ -52,6 +53,16 @@ for step in "$@"; do
                   --output-format csv -- python bench.py --only fwd --steps 5 --warmup 1 ;;
     pmc_fwd_write) run pmc_fwd_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_fwd_write" -o run \
                   --output-format csv -- python bench.py --only fwd --steps 5 --warmup 1 ;;
+    pmc_list) run pmc_list 120 rocprofv3 -L ;;
+    pmc_linear_mfma) run pmc_linear_mfma 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CU_CYCLES \
+                  --kernel-trace -d "$OUT/pmc_linear_mfma" -o run --output-format csv \
+                  -- python bench.py --only linear --steps 5 --warmup 1 ;;
+    pmc_fwd_tlb) run pmc_fwd_tlb 300 rocprofv3 --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum \
+                  --kernel-trace -d "$OUT/pmc_fwd_tlb" -o run --output-format csv \
+                  -- python bench.py --only fwd --steps 5 --warmup 1 ;;
+    pmc_c4_tlb) run pmc_c4_tlb 400 rocprofv3 --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum \
+                  --kernel-trace -d "$OUT/pmc_c4_tlb" -o run --output-format csv \
+                  -- python bench.py --only fwd --nodes-per-gpu 4000000 --steps 5 --warmup 1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
