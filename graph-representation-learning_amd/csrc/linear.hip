@@ -548,6 +548,195 @@ __global__ __launch_bounds__(512) void gemm256p_kernel(GemmArgs p) {
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// fp32 GEMM on the bf16 matrix cores by exact three-way splitting ("x6").
+// Every fp32 operand value v is written as v = v0 + v1 + v2 with
+// v0 = bf16(v), v1 = bf16(v - v0), v2 = bf16(v - v0 - v1) (round to nearest
+// even; the differences are exact by Sterbenz, and 3 x 8 significant bits
+// hold all 24 of an fp32, so the split is exact for finite |v| < 3.39e38).
+// Products of two bf16 are exact in fp32; of the nine a_i b_j the six with
+// i + j <= 2 are accumulated (v_mfma_f32_32x32x16_bf16, fp32 accumulators);
+// the three dropped terms are <= ~2^-24 |a b| each -- the size of one fp32
+// rounding.  One 32x32x16 bf16 MFMA costs 32 SIMD cycles against 8 x 64 for
+// the same K on v_mfma_f32_32x32x2_f32, so six of them take 0.375x the
+// matrix-core time of the fp32 instruction (MI355X_MICROARCH.md: f32 MFMA =
+// 1/16 of bf16).
+//
+// A (M x K, K contiguous: Z for the forward, g for dZ) is split inside the
+// kernel while it is staged into LDS; B arrives pre-split (split_planes_kernel,
+// once per call: W is 1.8 MB) as three bf16 planes [3][Np][K] with K
+// contiguous.  256 x 256 block tile, 8 waves of 128 x 64 (4 x 2 MFMA tiles,
+// 128 accumulators), K staged 16 deep through two LDS stages (48 KB each:
+// 3 planes x (A, B) x 256 rows x 32 B), one barrier per stage; the next
+// stage's global loads are in registers during the MFMAs.
+// Preconditions (x6_ok): K % 16 == 0, 16-B aligned A and lda % 4 == 0.
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+
+constexpr int X6_K = 16;
+constexpr int X6_PLANE = 256 * X6_K;  // bf16 elements per plane per operand stage
+constexpr int X6_STAGE = 6 * X6_PLANE;  // A planes then B planes
+
+__device__ __forceinline__ uint32_t pack_bf16(float a, float b) {
+  f32x2_t p = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(p, bf16x2_t));
+}
+__device__ __forceinline__ float lo_f(uint32_t u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float hi_f(uint32_t u) { return __uint_as_float(u & 0xFFFF0000u); }
+
+// v -> three planes of 4 bf16 (v == p0 + p1 + p2 exactly)
+__device__ __forceinline__ void split3(float4 v, uint2& p0, uint2& p1, uint2& p2) {
+  p0.x = pack_bf16(v.x, v.y);
+  p0.y = pack_bf16(v.z, v.w);
+  float4 r = make_float4(v.x - lo_f(p0.x), v.y - hi_f(p0.x), v.z - lo_f(p0.y), v.w - hi_f(p0.y));
+  p1.x = pack_bf16(r.x, r.y);
+  p1.y = pack_bf16(r.z, r.w);
+  r = make_float4(r.x - lo_f(p1.x), r.y - hi_f(p1.x), r.z - lo_f(p1.y), r.w - hi_f(p1.y));
+  p2.x = pack_bf16(r.x, r.y);
+  p2.y = pack_bf16(r.z, r.w);
+}
+
+// planes[p][n][k] (n < Np, k < K; zero for n >= N) of B(k, n) = B_KC ? B[n*ldb + k] : B[k*ldb + n]
+__global__ void split_planes_kernel(const float* __restrict__ B, int64_t ldb, int b_kc, int64_t N, int64_t K,
+                                    int64_t Np, uint16_t* __restrict__ planes) {
+  const int64_t total = Np * K;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t n = i / K, k = i - n * K;
+    const float v = n < N ? (b_kc ? B[n * ldb + k] : B[k * ldb + n]) : 0.0f;
+    const uint32_t h0 = pack_bf16(v, 0.0f) & 0xFFFFu;
+    const float r1 = v - lo_f(h0);
+    const uint32_t h1 = pack_bf16(r1, 0.0f) & 0xFFFFu;
+    const float r2 = r1 - lo_f(h1);
+    const uint32_t h2 = pack_bf16(r2, 0.0f) & 0xFFFFu;
+    planes[i] = (uint16_t)h0;
+    planes[total + i] = (uint16_t)h1;
+    planes[2 * total + i] = (uint16_t)h2;
+  }
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512) void gemm_x6_kernel(GemmArgs p, const uint16_t* __restrict__ Bp, int64_t Np) {
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * X6_STAGE];  // 2 stages x 48 KB
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int l32 = lane & 31, h = lane >> 5;
+  int64_t mi, ni, zi;
+  tile_of(p, mi, ni, zi);
+  const int64_t m0 = mi * LB_M, n0 = ni * LB_N;
+  const int64_t K = p.K;
+  const int64_t nk = K / X6_K;
+
+  // staging: A = 2 float4 per thread (row = idx >> 2, 4 k at (idx & 3) * 4);
+  //          B = 3 x 16 B of bf16 per thread (plane = it, n = tid >> 1, 8 k at (tid & 1) * 8)
+  // (plain scalars, no arrays or capturing lambdas: hipcc would otherwise
+  // promote the staging registers to LDS)
+  const int64_t r0 = min<int64_t>(m0 + (tid >> 2), p.M - 1);
+  const int64_t r1 = min<int64_t>(m0 + ((tid + 512) >> 2), p.M - 1);
+  const float* __restrict__ a_src0 = p.A + r0 * p.lda + (tid & 3) * 4;
+  const float* __restrict__ a_src1 = p.A + r1 * p.lda + (tid & 3) * 4;
+  const int64_t plane_stride = Np * K;
+  const uint16_t* __restrict__ b_src = Bp + (n0 + (tid >> 1)) * K + (tid & 1) * 8;
+  const int a_off0 = (tid >> 2) * X6_K + (tid & 3) * 4;
+  const int a_off1 = ((tid + 512) >> 2) * X6_K + (tid & 3) * 4;
+  const int b_off = 3 * X6_PLANE + (tid >> 1) * X6_K + (tid & 1) * 8;
+  float4 ra0, ra1;
+  uint4 rb0, rb1, rb2;
+#define X6_LOAD(t)                                                                   \
+  do {                                                                               \
+    const int64_t k0_ = (t) * X6_K;                                                  \
+    ra0 = *reinterpret_cast<const float4*>(a_src0 + k0_);                            \
+    ra1 = *reinterpret_cast<const float4*>(a_src1 + k0_);                            \
+    rb0 = *reinterpret_cast<const uint4*>(b_src + k0_);                              \
+    rb1 = *reinterpret_cast<const uint4*>(b_src + plane_stride + k0_);               \
+    rb2 = *reinterpret_cast<const uint4*>(b_src + 2 * plane_stride + k0_);           \
+  } while (0)
+#define X6_STASH(st)                                                                 \
+  do {                                                                               \
+    uint2 q0_, q1_, q2_;                                                             \
+    split3(ra0, q0_, q1_, q2_);                                                      \
+    *reinterpret_cast<uint2*>((st) + a_off0) = q0_;                                  \
+    *reinterpret_cast<uint2*>((st) + X6_PLANE + a_off0) = q1_;                       \
+    *reinterpret_cast<uint2*>((st) + 2 * X6_PLANE + a_off0) = q2_;                   \
+    split3(ra1, q0_, q1_, q2_);                                                      \
+    *reinterpret_cast<uint2*>((st) + a_off1) = q0_;                                  \
+    *reinterpret_cast<uint2*>((st) + X6_PLANE + a_off1) = q1_;                       \
+    *reinterpret_cast<uint2*>((st) + 2 * X6_PLANE + a_off1) = q2_;                   \
+    *reinterpret_cast<uint4*>((st) + b_off) = rb0;                                   \
+    *reinterpret_cast<uint4*>((st) + b_off + X6_PLANE) = rb1;                        \
+    *reinterpret_cast<uint4*>((st) + b_off + 2 * X6_PLANE) = rb2;                    \
+  } while (0)
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+
+  if (nk > 0) {
+    X6_LOAD(0);
+    X6_STASH(smem);
+    if (nk > 1) X6_LOAD(1);
+  }
+  __syncthreads();
+  for (int64_t t = 0; t < nk; ++t) {
+    const uint16_t* cur = smem + (t & 1) * X6_STAGE;
+    bf16x8_t a[4][3], b[2][3];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        a[i][q] = *reinterpret_cast<const bf16x8_t*>(cur + q * X6_PLANE + (wm * 128 + i * 32 + l32) * X6_K + h * 8);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        b[j][q] = *reinterpret_cast<const bf16x8_t*>(cur + (3 + q) * X6_PLANE + (wn * 64 + j * 32 + l32) * X6_K +
+                                                     h * 8);
+    // small terms first (i + j = 2, then 1, then the leading product)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][2], b[j][0], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[j][1], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][2], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[j][0], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][1], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][0], acc[i][j], 0, 0, 0);
+      }
+    if (t + 1 < nk) {
+      X6_STASH(smem + ((t + 1) & 1) * X6_STAGE);  // the other stage: last read in step t-1
+      if (t + 2 < nk) X6_LOAD(t + 2);
+    }
+    __syncthreads();
+  }
+
+#undef X6_LOAD
+#undef X6_STASH
+  float* Cz = p.C;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int64_t gn = n0 + wn * 64 + j * 32 + l32;
+    if (gn >= p.N) continue;
+    const float bv = (EPI == EPI_BIAS && p.bias) ? p.bias[gn] : 0.0f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t gm = m0 + wm * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (gm < p.M) {
+          float v = acc[i][j][r] + bv;
+          if (EPI == EPI_BIAS && p.relu) v = v > 0.0f ? v : 0.0f;
+          Cz[gm * p.ldc + gn] = v;
+        }
+      }
+  }
+}
+
 bool al16(const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; }
 
 #ifndef GRL_GEMM_BK
@@ -635,10 +824,56 @@ int launch_gemm256p(GemmArgs a, int splits, hipStream_t st) {
   return GRL_OK;
 }
 
+// Split-bf16 ("x6") path selection.  GRL_GEMM_X6=0 keeps the fp32-MFMA
+// kernels (A/B aid and tests; read on every call, so a workspace query and
+// the call it sizes must see the same setting).
+bool x6_enabled() {
+  const char* e = getenv("GRL_GEMM_X6");
+  return !(e && e[0] == '0');
+}
+
+bool x6_shape_ok(int64_t M, int64_t N, int64_t K) {
+  return x6_enabled() && K % X6_K == 0 && K > 0 && M >= 4 && N >= 4 &&
+         2.0 * (double)M * (double)N * (double)K >= 1.6e10;
+}
+
+int64_t x6_np(int64_t N) { return ceil_div(N, LB_N) * LB_N; }
+
+// workspace of the x6 path: B's three bf16 planes
+size_t x6_ws_bytes(int64_t M, int64_t N, int64_t K) {
+  return x6_shape_ok(M, N, K) ? (size_t)3 * (size_t)x6_np(N) * (size_t)K * 2 + 256 : 0;
+}
+
+template <bool B_KC>
+int launch_x6(GemmArgs a, void* ws, hipStream_t st) {
+  const int64_t Np = x6_np(a.N);
+  uint16_t* planes = static_cast<uint16_t*>(ws);
+  const int64_t n_el = Np * a.K;
+  hipLaunchKernelGGL(split_planes_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(n_el, 256), 4096)), dim3(256), 0,
+                     st, a.B, a.ldb, B_KC ? 1 : 0, a.N, a.K, Np, planes);
+  GRL_LAUNCH_CHECK();
+  a.mt = ceil_div(a.M, LB_M);
+  a.nt = Np / LB_N;
+  a.zt = 1;
+  a.inner_n = 1;
+  a.k_per_split = a.K;
+  GRL_CHECK_ARG(a.mt * a.nt < 2147483647LL, "gemm: grid too large");
+  const dim3 grid((unsigned)(a.mt * a.nt));
+  if (a.bias || a.relu)
+    hipLaunchKernelGGL(gemm_x6_kernel<EPI_BIAS>, grid, dim3(512), 0, st, a, planes, Np);
+  else
+    hipLaunchKernelGGL(gemm_x6_kernel<EPI_STORE>, grid, dim3(512), 0, st, a, planes, Np);
+  GRL_LAUNCH_CHECK();
+  return GRL_OK;
+}
+
 // Output-stationary GEMM with optional split-K through `ws` (slab layout
 // [split][M][N], then one ordered reduce applying bias / ReLU).
 template <bool A_KC, bool B_KC>
 int run_output_gemm(GemmArgs a, bool aligned, const char* who, void* ws, size_t ws_bytes, hipStream_t st) {
+  if (A_KC && aligned && !a.Amask && !a.Bmask && x6_shape_ok(a.M, a.N, a.K) && ws && al16(ws) &&
+      ws_bytes >= x6_ws_bytes(a.M, a.N, a.K))  // large M: fp32 on the bf16 matrix cores
+    return launch_x6<B_KC>(a, ws, st);
   if (big_ok(a, aligned)) {  // forward and dZ at large M: the pipelined 256^2 LDS-DMA tile
     a.k_per_split = std::max<int64_t>(a.K, 1);
     return a.bias || a.relu ? launch_gemm256p<A_KC, B_KC, EPI_BIAS>(a, 1, st)
@@ -677,7 +912,7 @@ int run_output_gemm(GemmArgs a, bool aligned, const char* who, void* ws, size_t 
 using namespace grl;
 
 extern "C" size_t grl_linear_fwd_workspace_size(int64_t M, int32_t K, int32_t C) {
-  return M > 0 && K > 0 && C > 0 ? small_ws_bytes(M, C, K) : 0;
+  return M > 0 && K > 0 && C > 0 ? std::max(small_ws_bytes(M, C, K), x6_ws_bytes(M, C, K)) : 0;
 }
 
 extern "C" int grl_linear_fwd(const float* Z, int64_t ldz, const float* W, const float* bias, float* out, int64_t M,
@@ -704,7 +939,7 @@ extern "C" int grl_linear_fwd(const float* Z, int64_t ldz, const float* W, const
 }
 
 extern "C" size_t grl_linear_bwd_data_workspace_size(int64_t M, int32_t K, int32_t C) {
-  return M > 0 && K > 0 && C > 0 ? small_ws_bytes(M, K, C) : 0;
+  return M > 0 && K > 0 && C > 0 ? std::max(small_ws_bytes(M, K, C), x6_ws_bytes(M, K, C)) : 0;
 }
 
 extern "C" int grl_linear_bwd_data(const float* g, const float* relu_out, const float* W, float* dZ, int64_t lddz,

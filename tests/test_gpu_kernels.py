@@ -309,7 +309,9 @@ def test_small_m_split_k_deterministic(M, K, C):
     from grl.ops import linear_bwd_data
 
     assert _lib.lib().grl_linear_fwd_workspace_size(M, K, C) > 0  # the split path is what runs
-    assert _lib.lib().grl_linear_fwd_workspace_size(1_000_000, K, C) == 0
+    # large M never splits K; it needs only the x6 path's bf16 planes of W (3 x 256-padded C x K)
+    big = _lib.lib().grl_linear_fwd_workspace_size(1_000_000, K, C)
+    assert big == (3 * (-(-C // 256) * 256) * K * 2 + 256 if K % 16 == 0 else 0)
     rng = np.random.default_rng(M)
     Zw = to_dev(rng.standard_normal((M, K + 8)).astype(np.float32))
     Z = Zw[:, :K]
@@ -325,12 +327,18 @@ def test_small_m_split_k_deterministic(M, K, C):
     assert torch.equal(d1, d2)
 
 
-@pytest.mark.parametrize("M,K,C", [(300_000, 1792, 256), (70_003, 3584, 256), (131_072, 512, 128), (65_600, 256, 1792)])
-def test_large_tile_gemms_match_fp64(M, K, C):
-    """Shapes that take the 256x256 LDS-DMA path (big_ok: aligned, K % 32 == 0,
-    >= 16 GFLOP): forward with bias+ReLU, dZ and dW/db (pre-masked g) against
-    float64 on sampled rows / the full dW; ragged M tails included."""
+@pytest.mark.parametrize("x6", ["1", "0"])
+@pytest.mark.parametrize("M,K,C", [(300_000, 1792, 256), (70_003, 3584, 256), (131_072, 512, 128), (65_600, 256, 1792),
+                                   (45_001, 1792, 200)])
+def test_large_tile_gemms_match_fp64(M, K, C, x6, monkeypatch):
+    """Shapes that take the large-M paths (>= 16 GFLOP, aligned, K % 16 == 0):
+    x6 = "1" the split-bf16 kernel (gemm_x6_kernel), "0" the fp32 256x256
+    LDS-DMA tile (gemm256p_kernel).  Forward with bias+ReLU, dZ and dW/db
+    (pre-masked g) against float64 on sampled rows / the full dW; ragged M
+    tails and a C that is not a multiple of the 256-column tile included."""
     from grl.ops import linear_bwd_data, linear_bwd_weight
+
+    monkeypatch.setenv("GRL_GEMM_X6", x6)
 
     gen = torch.Generator(device=DEV).manual_seed(M % 1000)
     Z = torch.randn(M, K, device=DEV, generator=gen)
@@ -353,3 +361,29 @@ def test_large_tile_gemms_match_fp64(M, K, C):
     assert ((dW.double() - refw).abs() <= 1e-5 * scw).all()
     torch.testing.assert_close(db.double(), g.double().sum(0), rtol=1e-5, atol=1e-3)
     assert torch.equal(linear_fwd(Z, W, b, True), out)  # deterministic
+
+
+def test_x6_split_is_exact_on_wide_dynamic_range(monkeypatch):
+    """The x6 GEMM splits every fp32 value into three bf16 parts exactly: rows
+    of Z scaled over 2^-60 .. 2^60 and W columns over 2^-30 .. 2^30 keep the
+    per-element error at the fp32 level (<= 1e-6 of sum |terms|), the same
+    bound the fp32-MFMA kernel meets; integer data is exact."""
+    from grl.ops import linear_bwd_data
+
+    monkeypatch.setenv("GRL_GEMM_X6", "1")
+    M, K, C = 40_000, 1792, 256
+    gen = torch.Generator(device=DEV).manual_seed(7)
+    rs = torch.pow(2.0, torch.randint(-60, 61, (M, 1), device=DEV, generator=gen).float())
+    cs = torch.pow(2.0, torch.randint(-30, 31, (1, C), device=DEV, generator=gen).float())
+    Z = torch.randn(M, K, device=DEV, generator=gen) * rs
+    W = torch.randn(K, C, device=DEV, generator=gen) * cs
+    out = linear_fwd(Z, W, None, False)
+    rows = torch.randint(0, M, (1024,), device=DEV, generator=gen)
+    ref = Z[rows].double() @ W.double()
+    scale = Z[rows].double().abs() @ W.double().abs()
+    assert ((out[rows].double() - ref).abs() <= 1e-6 * scale).all()
+    Zi = torch.randint(-64, 65, (M, K), device=DEV, generator=gen).float()
+    Wi = torch.randint(-64, 65, (K, C), device=DEV, generator=gen).float()
+    assert torch.equal(linear_fwd(Zi, Wi, None, False), (Zi.double() @ Wi.double()).float())
+    gi = torch.randint(-64, 65, (M, C), device=DEV, generator=gen).float()
+    assert torch.equal(linear_bwd_data(gi, None, Wi), (gi.double() @ Wi.double().T).float())

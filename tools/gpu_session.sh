@@ -47,6 +47,7 @@ for step in "$@"; do
                   -- python bench.py --only layer --steps 5 --warmup 2 ;;
     prof_attn) run prof_attn 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_attn" -o run --output-format csv \
                   -- python tools/probe_attn.py ;;
+    probe_x6) run probe_x6 300 python tools/probe_x6.py ;;
     prof_c1) run prof_c1 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c1" -o run --output-format csv \
                   -- python bench.py --only c1 --steps 20 ;;
     pmc_fwd_fetch) run pmc_fwd_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fwd_fetch" -o run \
