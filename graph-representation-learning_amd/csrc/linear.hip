@@ -616,9 +616,36 @@ __global__ void split_planes_kernel(const float* __restrict__ B, int64_t ldb, in
   }
 }
 
+// global -> LDS DMA of one 16 B chunk per lane (lane l lands at lds_base + 16 l).
+// Issued from asm so that hipcc's waitcnt pass neither sees nor waits on it;
+// completion is ordered by the kernel's counted `s_waitcnt vmcnt`.
+__device__ __forceinline__ void dma16(const void* src, const void* lds_base) {
+  const uint32_t dst = __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>(lds_base));
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(dst)
+      : "memory");
+}
+
+// LDS: two plane stages (48 KB each: A planes 0-2, B planes 3-5, 256 rows x
+// 16 k bf16) + three A landing slots (16 KB each: [wave][2 instr][lane] x 16 B
+// of fp32, each lane reading back only what it fetched itself).
+// Step t:  barrier | DMA B(t+1) -> stage (t+1)&1, DMA A(t+2) -> slot (t+2)%3 |
+//          MFMAs on stage t&1 | vmcnt(2): own A(t+1), B(t+1) landed |
+//          split own A(t+1) from its slot into stage (t+1)&1.
+// A's loads get two compute phases to land, B's (L2-resident planes) one.
+constexpr int X6_SLOT = 512 * 8;  // floats per landing slot (16 KB)
+
 template <int EPI>
 __global__ __launch_bounds__(512) void gemm_x6_kernel(GemmArgs p, const uint16_t* __restrict__ Bp, int64_t Np) {
-  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * X6_STAGE];  // 2 stages x 48 KB
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * X6_STAGE];  // 2 plane stages x 48 KB
+  __shared__ __attribute__((aligned(16))) float land[3 * X6_SLOT];      // 3 landing slots x 16 KB
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 2, wn = wave & 3;
   const int l32 = lane & 31, h = lane >> 5;
@@ -628,45 +655,48 @@ __global__ __launch_bounds__(512) void gemm_x6_kernel(GemmArgs p, const uint16_t
   const int64_t K = p.K;
   const int64_t nk = K / X6_K;
 
-  // staging: A = 2 float4 per thread (row = idx >> 2, 4 k at (idx & 3) * 4);
-  //          B = 3 x 16 B of bf16 per thread (plane = it, n = tid >> 1, 8 k at (tid & 1) * 8)
-  // (plain scalars, no arrays or capturing lambdas: hipcc would otherwise
-  // promote the staging registers to LDS)
+  // A: this lane's two float4 (idx = tid + 512 i: row idx >> 2, 4 k at (idx & 3) * 4)
   const int64_t r0 = min<int64_t>(m0 + (tid >> 2), p.M - 1);
   const int64_t r1 = min<int64_t>(m0 + ((tid + 512) >> 2), p.M - 1);
-  const float* __restrict__ a_src0 = p.A + r0 * p.lda + (tid & 3) * 4;
-  const float* __restrict__ a_src1 = p.A + r1 * p.lda + (tid & 3) * 4;
-  const int64_t plane_stride = Np * K;
-  const uint16_t* __restrict__ b_src = Bp + (n0 + (tid >> 1)) * K + (tid & 1) * 8;
+  const float* a_src0 = p.A + r0 * p.lda + (tid & 3) * 4;
+  const float* a_src1 = p.A + r1 * p.lda + (tid & 3) * 4;
   const int a_off0 = (tid >> 2) * X6_K + (tid & 3) * 4;
   const int a_off1 = ((tid + 512) >> 2) * X6_K + (tid & 3) * 4;
-  const int b_off = 3 * X6_PLANE + (tid >> 1) * X6_K + (tid & 1) * 8;
-  float4 ra0, ra1;
-  uint4 rb0, rb1, rb2;
-#define X6_LOAD(t)                                                                   \
-  do {                                                                               \
-    const int64_t k0_ = (t) * X6_K;                                                  \
-    ra0 = *reinterpret_cast<const float4*>(a_src0 + k0_);                            \
-    ra1 = *reinterpret_cast<const float4*>(a_src1 + k0_);                            \
-    rb0 = *reinterpret_cast<const uint4*>(b_src + k0_);                              \
-    rb1 = *reinterpret_cast<const uint4*>(b_src + plane_stride + k0_);               \
-    rb2 = *reinterpret_cast<const uint4*>(b_src + 2 * plane_stride + k0_);           \
-  } while (0)
-#define X6_STASH(st)                                                                 \
-  do {                                                                               \
-    uint2 q0_, q1_, q2_;                                                             \
-    split3(ra0, q0_, q1_, q2_);                                                      \
-    *reinterpret_cast<uint2*>((st) + a_off0) = q0_;                                  \
-    *reinterpret_cast<uint2*>((st) + X6_PLANE + a_off0) = q1_;                       \
-    *reinterpret_cast<uint2*>((st) + 2 * X6_PLANE + a_off0) = q2_;                   \
-    split3(ra1, q0_, q1_, q2_);                                                      \
-    *reinterpret_cast<uint2*>((st) + a_off1) = q0_;                                  \
-    *reinterpret_cast<uint2*>((st) + X6_PLANE + a_off1) = q1_;                       \
-    *reinterpret_cast<uint2*>((st) + 2 * X6_PLANE + a_off1) = q2_;                   \
-    *reinterpret_cast<uint4*>((st) + b_off) = rb0;                                   \
-    *reinterpret_cast<uint4*>((st) + b_off + X6_PLANE) = rb1;                        \
-    *reinterpret_cast<uint4*>((st) + b_off + 2 * X6_PLANE) = rb2;                    \
-  } while (0)
+  // B: chunk c = (3 wave + j) * 64 + lane of 1536 per stage: plane c / 512,
+  // n = (c % 512) / 2, 8 k at (c & 1) * 8; lands at B region + 8 c
+  const int64_t plane_stride = Np * K;
+  const uint16_t* b_src[3];
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const int c = (wave * 3 + j) * 64 + lane;
+    b_src[j] = Bp + (c >> 9) * plane_stride + (n0 + ((c & 511) >> 1)) * K + (c & 1) * 8;
+  }
+  float* const my_land = land + wave * 512;  // 2 x 1 KB per wave; + slot * X6_SLOT, + 256 per instr, + 4 lane
+
+  auto issue_a = [&](int64_t t) {
+    float* sl = my_land + (int)(t % 3) * X6_SLOT;
+    dma16(a_src0 + t * X6_K, sl);
+    dma16(a_src1 + t * X6_K, sl + 256);
+  };
+  auto issue_b = [&](int64_t t, uint16_t* st) {
+    uint16_t* bb = st + 3 * X6_PLANE + wave * 3 * 512;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) dma16(b_src[j] + t * X6_K, bb + j * 512);
+  };
+  auto stash_a = [&](int64_t t, uint16_t* st) {
+    const float* sl = my_land + (int)(t % 3) * X6_SLOT + lane * 4;
+    const float4 v0 = *reinterpret_cast<const float4*>(sl);
+    const float4 v1 = *reinterpret_cast<const float4*>(sl + 256);
+    uint2 q0, q1, q2;
+    split3(v0, q0, q1, q2);
+    *reinterpret_cast<uint2*>(st + a_off0) = q0;
+    *reinterpret_cast<uint2*>(st + X6_PLANE + a_off0) = q1;
+    *reinterpret_cast<uint2*>(st + 2 * X6_PLANE + a_off0) = q2;
+    split3(v1, q0, q1, q2);
+    *reinterpret_cast<uint2*>(st + a_off1) = q0;
+    *reinterpret_cast<uint2*>(st + X6_PLANE + a_off1) = q1;
+    *reinterpret_cast<uint2*>(st + 2 * X6_PLANE + a_off1) = q2;
+  };
 
   f32x16 acc[4][2];
 #pragma unroll
@@ -677,46 +707,57 @@ __global__ __launch_bounds__(512) void gemm_x6_kernel(GemmArgs p, const uint16_t
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
 
   if (nk > 0) {
-    X6_LOAD(0);
-    X6_STASH(smem);
-    if (nk > 1) X6_LOAD(1);
-  }
-  __syncthreads();
-  for (int64_t t = 0; t < nk; ++t) {
-    const uint16_t* cur = smem + (t & 1) * X6_STAGE;
-    bf16x8_t a[4][3], b[2][3];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int q = 0; q < 3; ++q)
-        a[i][q] = *reinterpret_cast<const bf16x8_t*>(cur + q * X6_PLANE + (wm * 128 + i * 32 + l32) * X6_K + h * 8);
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int q = 0; q < 3; ++q)
-        b[j][q] = *reinterpret_cast<const bf16x8_t*>(cur + (3 + q) * X6_PLANE + (wn * 64 + j * 32 + l32) * X6_K +
-                                                     h * 8);
-    // small terms first (i + j = 2, then 1, then the leading product)
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][2], b[j][0], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[j][1], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][2], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][1], b[j][0], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][1], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i][0], b[j][0], acc[i][j], 0, 0, 0);
-      }
-    if (t + 1 < nk) {
-      X6_STASH(smem + ((t + 1) & 1) * X6_STAGE);  // the other stage: last read in step t-1
-      if (t + 2 < nk) X6_LOAD(t + 2);
+    issue_a(0);
+    issue_b(0, smem);
+    if (nk > 1) {
+      issue_a(1);
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    __syncthreads();
+    stash_a(0, smem);
   }
-
-#undef X6_LOAD
-#undef X6_STASH
+  for (int64_t t = 0; t < nk; ++t) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    uint16_t* cur = smem + (int)(t & 1) * X6_STAGE;
+    uint16_t* nxt = smem + (int)((t + 1) & 1) * X6_STAGE;
+    if (t + 1 < nk) issue_b(t + 1, nxt);
+    if (t + 2 < nk) issue_a(t + 2);
+    {
+      bf16x8_t a_[4][3], b_[2][3];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+          a_[i][q] = *reinterpret_cast<const bf16x8_t*>(cur + q * X6_PLANE + (wm * 128 + i * 32 + l32) * X6_K + h * 8);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int q = 0; q < 3; ++q)
+          b_[j][q] = *reinterpret_cast<const bf16x8_t*>(cur + (3 + q) * X6_PLANE + (wn * 64 + j * 32 + l32) * X6_K +
+                                                        h * 8);
+      // small terms first (i + j = 2, then 1, then the leading product)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_[i][2], b_[j][0], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_[i][1], b_[j][1], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_[i][0], b_[j][2], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_[i][1], b_[j][0], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_[i][0], b_[j][1], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_[i][0], b_[j][0], acc[i][j], 0, 0, 0);
+        }
+    }
+    if (t + 1 < nk) {
+      if (t + 2 < nk)
+        asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // A(t+2) may stay in flight
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      stash_a(t + 1, nxt);
+    }
+  }
   float* Cz = p.C;
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
