@@ -660,8 +660,12 @@ __global__ __launch_bounds__(512) void gemm_x6_kernel(GemmArgs p, const uint16_t
   const int64_t r1 = min<int64_t>(m0 + ((tid + 512) >> 2), p.M - 1);
   const float* a_src0 = p.A + r0 * p.lda + (tid & 3) * 4;
   const float* a_src1 = p.A + r1 * p.lda + (tid & 3) * 4;
-  const int a_off0 = (tid >> 2) * X6_K + (tid & 3) * 4;
-  const int a_off1 = ((tid + 512) >> 2) * X6_K + (tid & 3) * 4;
+  // 16-B half h of a 32-B plane row r sits at position h ^ ((r >> 3) & 1): the
+  // ds_read_b128 lane groups {0-3,12-15,20-27}, ... then hit 16 distinct
+  // slots (2-way bank conflicts without it; MI355X_MICROARCH.md §LDS)
+  auto sw = [](int r, int k) { return r * X6_K + ((((k >> 3) ^ (r >> 3)) & 1) << 3) + (k & 7); };
+  const int a_off0 = sw(tid >> 2, (tid & 3) * 4);
+  const int a_off1 = sw((tid + 512) >> 2, (tid & 3) * 4);
   // B: chunk c = (3 wave + j) * 64 + lane of 1536 per stage: plane c / 512,
   // n = (c % 512) / 2, 8 k at (c & 1) * 8; lands at B region + 8 c
   const int64_t plane_stride = Np * K;
@@ -669,7 +673,8 @@ __global__ __launch_bounds__(512) void gemm_x6_kernel(GemmArgs p, const uint16_t
 #pragma unroll
   for (int j = 0; j < 3; ++j) {
     const int c = (wave * 3 + j) * 64 + lane;
-    b_src[j] = Bp + (c >> 9) * plane_stride + (n0 + ((c & 511) >> 1)) * K + (c & 1) * 8;
+    const int n = (c & 511) >> 1;
+    b_src[j] = Bp + (c >> 9) * plane_stride + (n0 + n) * K + (((c & 1) ^ (n >> 3)) & 1) * 8;
   }
   float* const my_land = land + wave * 512;  // 2 x 1 KB per wave; + slot * X6_SLOT, + 256 per instr, + 4 lane
 
@@ -730,13 +735,12 @@ __global__ __launch_bounds__(512) void gemm_x6_kernel(GemmArgs p, const uint16_t
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int q = 0; q < 3; ++q)
-          a_[i][q] = *reinterpret_cast<const bf16x8_t*>(cur + q * X6_PLANE + (wm * 128 + i * 32 + l32) * X6_K + h * 8);
+          a_[i][q] = *reinterpret_cast<const bf16x8_t*>(cur + q * X6_PLANE + sw(wm * 128 + i * 32 + l32, h * 8));
 #pragma unroll
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int q = 0; q < 3; ++q)
-          b_[j][q] = *reinterpret_cast<const bf16x8_t*>(cur + (3 + q) * X6_PLANE + (wn * 64 + j * 32 + l32) * X6_K +
-                                                        h * 8);
+          b_[j][q] = *reinterpret_cast<const bf16x8_t*>(cur + (3 + q) * X6_PLANE + sw(wn * 64 + j * 32 + l32, h * 8));
       // small terms first (i + j = 2, then 1, then the leading product)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -774,6 +778,150 @@ __global__ __launch_bounds__(512) void gemm_x6_kernel(GemmArgs p, const uint16_t
           if (EPI == EPI_BIAS && p.relu) v = v > 0.0f ? v : 0.0f;
           Cz[gm * p.ldc + gn] = v;
         }
+      }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// x6 for the weight gradient dW = Z^T g (grl_linear_bwd_weight at large M):
+// both operands are M/N-contiguous (A(m, k) = Z[k][m], B(k, n) = g[k][n], k =
+// node).  Each K16 step's rows are split into bf16 planes stored as they lie,
+// [16 k][256 m] (512 B per k row; the 8-B group at column m of row k sits at
+// m ^ ((k & 3) << 5), so stores and reads are bank-conflict free), and the
+// MFMA fragments (8 consecutive k of one column) come out of
+// ds_read_b64_tr_b16, the gfx950 transposing LDS read: per 16-lane group a
+// 4 k x 16 column block, lane i receiving column i (cdna_hip_programming.md
+// T10).  K (the node count) is split over blockIdx.z into fp32 slabs added in
+// split order afterwards (deterministic).  Register-staged: the next step's
+// loads are in flight during the MFMAs.  Preconditions (x6t_ok): 16-B
+// aligned operands, lda, ldb, M, N multiples of 4.
+typedef short i16x4_t __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ bf16x8_t tr_pair(const uint16_t* plane, int k, int col) {
+  // k = 8h + qq for this lane's first block row (qq = (lane & 15) >> 2); the
+  // second read is the same block 4 k further
+  typedef __attribute__((address_space(3))) i16x4_t lds_v4;
+  const uint16_t* p0 = plane + k * 256 + (col ^ ((k & 3) << 5));
+  const uint16_t* p1 = plane + (k + 4) * 256 + (col ^ ((k & 3) << 5));
+  const i16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(uintptr_t)(uint32_t)(uintptr_t)p0);
+  const i16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(uintptr_t)(uint32_t)(uintptr_t)p1);
+  typedef short i16x8_t __attribute__((ext_vector_type(8)));
+  const i16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512) void gemm_x6t_kernel(GemmArgs p) {
+  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * X6_STAGE];  // 2 stages x (A, B) x 3 planes x 8 KB
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 2, wn = wave & 3;
+  const int l32 = lane & 31, h = lane >> 5;
+  int64_t mi, ni, zi;
+  tile_of(p, mi, ni, zi);
+  const int64_t m0 = mi * LB_M, n0 = ni * LB_N;
+  const int64_t kbeg = zi * p.k_per_split;
+  const int64_t kend = min(p.K, kbeg + p.k_per_split);
+  const int64_t nk = kend > kbeg ? (kend - kbeg + X6_K - 1) / X6_K : 0;
+
+  // staging: float4 f = tid + 512 i of each operand: k row f >> 6, 4 columns at (f & 63) * 4
+  const int kr0 = tid >> 6, kr1 = (tid + 512) >> 6;
+  const int col = (tid & 63) * 4;
+  const int64_t am = min<int64_t>(m0 + col, p.M - 4), bn = min<int64_t>(n0 + col, p.N - 4);
+  const float* __restrict__ a_base = p.A + am;
+  const float* __restrict__ b_base = p.B + bn;
+  const int st_off0 = kr0 * 256 + (col ^ ((kr0 & 3) << 5));
+  const int st_off1 = kr1 * 256 + (col ^ ((kr1 & 3) << 5));
+  float4 ra0, ra1, rb0, rb1;
+  const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
+#define X6T_LOAD(t)                                                                                       \
+  do {                                                                                                    \
+    const int64_t k_ = kbeg + (t) * X6_K;                                                                 \
+    const bool in0_ = k_ + kr0 < kend, in1_ = k_ + kr1 < kend;                                            \
+    const int64_t r0_ = in0_ ? k_ + kr0 : kbeg, r1_ = in1_ ? k_ + kr1 : kbeg;                             \
+    ra0 = *reinterpret_cast<const float4*>(a_base + r0_ * p.lda);                                         \
+    ra1 = *reinterpret_cast<const float4*>(a_base + r1_ * p.lda);                                         \
+    rb0 = *reinterpret_cast<const float4*>(b_base + r0_ * p.ldb);                                         \
+    rb1 = *reinterpret_cast<const float4*>(b_base + r1_ * p.ldb);                                         \
+    if (!in0_) ra0 = rb0 = zero4;                                                                         \
+    if (!in1_) ra1 = rb1 = zero4;                                                                         \
+  } while (0)
+#define X6T_SPLIT(v, base, off)                                                                           \
+  do {                                                                                                    \
+    uint2 q0_, q1_, q2_;                                                                                  \
+    split3(v, q0_, q1_, q2_);                                                                             \
+    *reinterpret_cast<uint2*>((base) + (off)) = q0_;                                                      \
+    *reinterpret_cast<uint2*>((base) + X6_PLANE + (off)) = q1_;                                           \
+    *reinterpret_cast<uint2*>((base) + 2 * X6_PLANE + (off)) = q2_;                                       \
+  } while (0)
+#define X6T_STASH(st)                                                                                     \
+  do {                                                                                                    \
+    X6T_SPLIT(ra0, (st), st_off0);                                                                        \
+    X6T_SPLIT(ra1, (st), st_off1);                                                                        \
+    X6T_SPLIT(rb0, (st) + 3 * X6_PLANE, st_off0);                                                         \
+    X6T_SPLIT(rb1, (st) + 3 * X6_PLANE, st_off1);                                                         \
+  } while (0)
+
+  // this lane's transposed-read coordinates: k = 8h + ((lane & 15) >> 2),
+  // column = block base + 16 ((lane >> 4) & 1) + 4 (lane & 3)
+  const int tk = 8 * h + ((lane & 15) >> 2);
+  const int tc = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+
+  f32x16 acc[4][2];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+
+  if (nk > 0) {
+    X6T_LOAD(0);
+    X6T_STASH(smem);
+    if (nk > 1) X6T_LOAD(1);
+  }
+  __syncthreads();
+  for (int64_t t = 0; t < nk; ++t) {
+    const uint16_t* cur = smem + (t & 1) * X6_STAGE;
+    bf16x8_t a_[4][3], b_[2][3];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) a_[i][q] = tr_pair(cur + q * X6_PLANE, tk, wm * 128 + i * 32 + tc);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int q = 0; q < 3; ++q) b_[j][q] = tr_pair(cur + (3 + q) * X6_PLANE, tk, wn * 64 + j * 32 + tc);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_[i][2], b_[j][0], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_[i][1], b_[j][1], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_[i][0], b_[j][2], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_[i][1], b_[j][0], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_[i][0], b_[j][1], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_[i][0], b_[j][0], acc[i][j], 0, 0, 0);
+      }
+    if (t + 1 < nk) {
+      X6T_STASH(smem + ((t + 1) & 1) * X6_STAGE);  // the other stage: last read in step t-1
+      if (t + 2 < nk) X6T_LOAD(t + 2);
+    }
+    __syncthreads();
+  }
+#undef X6T_LOAD
+#undef X6T_SPLIT
+#undef X6T_STASH
+  float* Cz = p.C + (EPI == EPI_SLAB ? zi * p.M * p.ldc : 0);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int64_t gn = n0 + wn * 64 + j * 32 + l32;
+    if (gn >= p.N) continue;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int64_t gm = m0 + wm * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        if (gm < p.M) Cz[gm * p.ldc + gn] = acc[i][j][r];
       }
   }
 }
@@ -1005,8 +1153,34 @@ extern "C" int grl_linear_bwd_data(const float* g, const float* relu_out, const 
                                      as_stream(stream));
 }
 
+namespace grl {
+namespace {
+// x6t (split-bf16 dW) selection: same switch and size floor as the forward
+bool x6t_shape_ok(int64_t M, int64_t K, int64_t C) {  // M nodes, K = rows of dW, C = its columns
+  return x6_enabled() && M >= 16 && K >= 4 && C >= 4 && K % 4 == 0 && C % 4 == 0 &&
+         2.0 * (double)M * (double)K * (double)C >= 1.6e10;
+}
+
+// K splits of the x6t dW: about two 256 x 256 workgroups per CU, >= 16 K16 steps each
+int x6t_splits(int64_t M, int64_t K, int64_t C) {
+  const int64_t tiles = ceil_div(K, LB_M) * ceil_div(C, LB_N);
+  int64_t s = ceil_div(2 * (int64_t)device_cu_count(), tiles);
+  s = std::min<int64_t>(s, ceil_div(M, 16 * X6_K));
+  return (int)std::max<int64_t>(1, std::min<int64_t>(s, 512));
+}
+
+// slabs reserved in the dW workspace: enough for whichever path runs
+int wgt_slab_splits(int64_t M, int64_t K, int64_t C) {
+  int s = pick_splits(K, C, M);
+  if (x6t_shape_ok(M, K, C)) s = std::max(s, x6t_splits(M, K, C));
+  return s;
+}
+
+}  // namespace
+}  // namespace grl
+
 extern "C" size_t grl_linear_bwd_weight_workspace_size(int64_t M, int32_t K, int32_t C) {
-  const int s = pick_splits(K, C, M);
+  const int s = wgt_slab_splits(M, K, C);
   const int zs = colsum_splits(M);
   return (size_t)s * (size_t)K * (size_t)C * 4 + (size_t)zs * (size_t)C * 4 + 512;
 }
@@ -1033,13 +1207,32 @@ extern "C" int grl_linear_bwd_weight(const float* Z, int64_t ldz, const float* g
   a.N = C;
   a.K = M;
   const bool aligned = al16(Z) && al16(g) && (!relu_out || al16(relu_out)) && ldz % 4 == 0 && C % 4 == 0 && K % 4 == 0;
-  const int splits = pick_splits(K, C, M);
-  a.C = splits > 1 ? slab : dW;
-  a.k_per_split = ceil_div(ceil_div(M, splits), GEMM_BK) * GEMM_BK;
-  const int used = (int)ceil_div(M, a.k_per_split);
-  const int rc = used > 1 ? launch_gemm<false, false, EPI_SLAB>(a, used, aligned, st)
-                          : launch_gemm<false, false, EPI_STORE>(a, 1, aligned, st);
-  if (rc) return rc;
+  int used;
+  if (aligned && !relu_out && x6t_shape_ok(M, K, C)) {  // large M: fp32 on the bf16 matrix cores
+    const int splits = x6t_splits(M, K, C);
+    a.C = splits > 1 ? slab : dW;
+    a.k_per_split = ceil_div(ceil_div(M, splits), X6_K) * X6_K;
+    used = (int)ceil_div(M, a.k_per_split);
+    a.mt = ceil_div(a.M, LB_M);
+    a.nt = ceil_div(a.N, LB_N);
+    a.zt = used;
+    a.inner_n = 0;
+    GRL_CHECK_ARG(a.mt * a.nt * a.zt < 2147483647LL, "gemm: grid too large");
+    const dim3 grid((unsigned)(a.mt * a.nt * a.zt));
+    if (used > 1)
+      hipLaunchKernelGGL(gemm_x6t_kernel<EPI_SLAB>, grid, dim3(512), 0, st, a);
+    else
+      hipLaunchKernelGGL(gemm_x6t_kernel<EPI_STORE>, grid, dim3(512), 0, st, a);
+    GRL_LAUNCH_CHECK();
+  } else {
+    const int splits = pick_splits(K, C, M);
+    a.C = splits > 1 ? slab : dW;
+    a.k_per_split = ceil_div(ceil_div(M, splits), GEMM_BK) * GEMM_BK;
+    used = (int)ceil_div(M, a.k_per_split);
+    const int rc = used > 1 ? launch_gemm<false, false, EPI_SLAB>(a, used, aligned, st)
+                            : launch_gemm<false, false, EPI_STORE>(a, 1, aligned, st);
+    if (rc) return rc;
+  }
   if (used > 1) {
     const int64_t n = (int64_t)K * C;
     hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(n, 256), 65536)), dim3(256), 0,
@@ -1048,7 +1241,7 @@ extern "C" int grl_linear_bwd_weight(const float* Z, int64_t ldz, const float* g
   }
   if (db) {
     const int zs = colsum_splits(M);
-    float* part = slab + (size_t)pick_splits(K, C, M) * K * C;
+    float* part = slab + (size_t)wgt_slab_splits(M, K, C) * K * C;
     const int64_t rows_per = ceil_div(std::max<int64_t>(M, 1), zs);
     hipLaunchKernelGGL(colsum_partial_kernel, dim3((unsigned)ceil_div(C, 256), (unsigned)zs), dim3(256), 0, st, g,
                        relu_out, M, C, rows_per, part);

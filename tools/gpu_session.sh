@@ -64,6 +64,14 @@ for step in "$@"; do
     pmc_c4_tlb) run pmc_c4_tlb 400 rocprofv3 --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum \
                   --kernel-trace -d "$OUT/pmc_c4_tlb" -o run --output-format csv \
                   -- python bench.py --only fwd --nodes-per-gpu 4000000 --steps 5 --warmup 1 ;;
+    pmc_x6_a) run pmc_x6_a 300 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS \
+                  SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_BUSY_CYCLES GRBM_GUI_ACTIVE \
+                  --kernel-trace -d "$OUT/pmc_x6_a" -o run --output-format csv \
+                  -- python bench.py --only linear --steps 5 --warmup 1 ;;
+    pmc_x6_b) run pmc_x6_b 300 rocprofv3 --pmc SQ_LDS_ADDR_CONFLICT SQ_LDS_UNALIGNED_STALL SQ_LDS_DATA_FIFO_FULL \
+                  SQ_LDS_CMD_FIFO_FULL SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY SQ_INSTS_VALU_MFMA_MOPS_BF16 \
+                  --kernel-trace -d "$OUT/pmc_x6_b" -o run --output-format csv \
+                  -- python bench.py --only linear --steps 5 --warmup 1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
