@@ -277,9 +277,10 @@ def cpu_baseline(args, graph, X, Z, L, F):
     return cpu, parity
 
 
-def _time(fn, iters):
+def _time(fn, iters, warm=1):
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    fn()
+    for _ in range(warm):
+        fn()
     torch.cuda.synchronize()
     s.record()
     for _ in range(iters):
@@ -338,8 +339,9 @@ def extras(args, graph, X_full, gather, L, F, dev, E_loc, n_loc):
     def layer_two_ops():
         graph_linear(typed_aggregate(Xl, gl), Wp, bp, relu=True).sum().backward()
 
-    res["graphconv_layer_fwd_bwd_p0.3"] = {"ms": _time(layer, max(2, iters // 2))}
-    res["graphconv_layer_fwd_bwd_p0.3_two_ops"] = {"ms": _time(layer_two_ops, max(2, iters // 2))}
+    # 3 warm calls: the first builds the CSC and grows the caching allocator's pool
+    res["graphconv_layer_fwd_bwd_p0.3"] = {"ms": _time(layer, max(3, iters // 2), warm=3)}
+    res["graphconv_layer_fwd_bwd_p0.3_two_ops"] = {"ms": _time(layer_two_ops, max(3, iters // 2), warm=2)}
     del Z, dZ, Zd
     return res
 
