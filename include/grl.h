@@ -173,16 +173,22 @@ int grl_typed_spmm_bwd(const GrlTypedCsc* g, const float* dZ, int32_t F,
                        float* dX, int64_t lddx, const GrlDropEdge* de,
                        grl_stream_t stream);
 
-/* out = Z W + bias (optionally ReLU), fp32 on MFMA (v_mfma_f32_32x32x2_f32).
+/* out = Z W + bias (optionally ReLU), fp32-accurate on the matrix cores.
  * Replaces torch.matmul(new_V, self.h_weights) + self.bias
  * (robust_gcn.py:50) and, with relu = 1, the F.relu around the layer
  * (drop_robust_gcn.py:76).  Z [M, K] row-major (ldz), W [K, C] row-major,
  * bias [C] or NULL, out [M, C] contiguous.
+ * Large M (>= 16 GFLOP, K % 16 == 0, 16-B aligned): fp32 values split
+ * exactly into three bf16 parts, six partial products on
+ * v_mfma_f32_32x32x16_bf16 (error at the fp32-rounding level, DESIGN.md
+ * §4.2); W's bf16 planes go to `workspace`.  Environment GRL_GEMM_X6=0
+ * (read per call) selects v_mfma_f32_32x32x2_f32 instead.
  * When the output tiles cannot fill the chip (small graphs: a 74-node page
  * is one 128-row tile) K is split over workgroups into fp32 slabs in
  * `workspace`, added in split order (deterministic) with bias/ReLU applied
- * once; grl_linear_fwd_workspace_size() is 0 when no split is taken (the
- * workspace may then be NULL), else the bytes the call requires.          */
+ * once.  grl_linear_fwd_workspace_size() is 0 when neither applies (the
+ * workspace may then be NULL), else the bytes the call requires; a large-M
+ * call given less falls back to the fp32-MFMA kernel.                    */
 size_t grl_linear_fwd_workspace_size(int64_t M, int32_t K, int32_t C);
 int grl_linear_fwd(const float* Z, int64_t ldz, const float* W,
                    const float* bias, float* out, int64_t M, int32_t K,
