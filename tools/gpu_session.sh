@@ -58,6 +58,9 @@ for step in "$@"; do
     pmc_linear_mfma) run pmc_linear_mfma 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CU_CYCLES \
                   --kernel-trace -d "$OUT/pmc_linear_mfma" -o run --output-format csv \
                   -- python bench.py --only linear --steps 5 --warmup 1 ;;
+    pmc_linear_mfma_f32) export GRL_GEMM_X6=0; run pmc_linear_mfma_f32 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES \
+                  GRBM_GUI_ACTIVE SQ_BUSY_CU_CYCLES --kernel-trace -d "$OUT/pmc_linear_mfma_f32" -o run \
+                  --output-format csv -- python bench.py --only linear --steps 5 --warmup 1; unset GRL_GEMM_X6 ;;
     pmc_fwd_tlb) run pmc_fwd_tlb 300 rocprofv3 --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum \
                   --kernel-trace -d "$OUT/pmc_fwd_tlb" -o run --output-format csv \
                   -- python bench.py --only fwd --steps 5 --warmup 1 ;;

@@ -36,23 +36,37 @@ def per_kernel(path, substr):
 def main():
     root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out"
     out = {}
-    c, t, n = per_kernel(os.path.join(root, "pmc_linear_mfma"), "gemm256p_kernel<true, false, 0, 3>")
-    clk = c["GRBM_GUI_ACTIVE"] / 8 / t
-    out["linear_fwd_C3"] = {
-        "kernel": "gemm256p_kernel<true,false,0,3> (grl_linear_fwd, M=1e6, K=1792, C=256)", "dispatches": n,
-        "duration_ms": t * 1e3, "counters_avg": c, "clock_GHz": clk / 1e9,
-        "mfma_busy_frac": c["SQ_VALU_MFMA_BUSY_CYCLES"] / (c["GRBM_GUI_ACTIVE"] / 8 * SIMDS),
-        "tflops": 2 * 1e6 * 1792 * 256 / t / 1e12,
-        "note": "SQ_VALU_MFMA_BUSY_CYCLES = 64 x number of 32x32x2 f32 MFMAs (224M per launch); "
-                "busy fraction is against the clock the chip held, TFLOP/s against wall time"}
+    for key, d, kern, desc, note in (
+            ("linear_fwd_C3_x6", "pmc_linear_mfma", "gemm_x6_kernel<0>",
+             "gemm_x6_kernel<STORE> (grl_linear_fwd, M=1e6, K=1792, C=256; default large-M path)",
+             "SQ_VALU_MFMA_BUSY_CYCLES = 32 x number of 32x32x16 bf16 MFMAs (6 per fp32 32x32x16 block: 168M "
+             "per launch); TFLOP/s = fp32-equivalent flops (2MKC) over wall time"),
+            ("linear_fwd_C3_f32mfma", "pmc_linear_mfma_f32", "gemm256p_kernel<true, false, 0, 3>",
+             "gemm256p_kernel<KC,RC,STORE,3> (grl_linear_fwd with GRL_GEMM_X6=0)",
+             "SQ_VALU_MFMA_BUSY_CYCLES = 64 x number of 32x32x2 f32 MFMAs (224M per launch)")):
+        if not os.path.isdir(os.path.join(root, d)):
+            continue
+        c, t, n = per_kernel(os.path.join(root, d), kern)
+        clk = c["GRBM_GUI_ACTIVE"] / 8 / t
+        out[key] = {"kernel": desc, "dispatches": n, "duration_ms": t * 1e3, "counters_avg": c,
+                    "clock_GHz": clk / 1e9,
+                    "mfma_busy_frac": c["SQ_VALU_MFMA_BUSY_CYCLES"] / (c["GRBM_GUI_ACTIVE"] / 8 * SIMDS),
+                    "tflops": 2 * 1e6 * 1792 * 256 / t / 1e12,
+                    "note": note + "; busy fraction is against the clock the chip held"}
     for key, d, desc in (("spmm_fwd_C3_tlb", "pmc_fwd_tlb", "C3: N=1M, X 1.02 GB"),
                          ("spmm_fwd_C4shape_tlb", "pmc_c4_tlb", "C4 shape on one GPU: N=4M, X 4.1 GB")):
+        if not os.path.isdir(os.path.join(root, d)):
+            continue
         c, t, n = per_kernel(os.path.join(root, d), "spmm_kernel<4, 1, 8, false, false>")
         hit, miss = c["TCP_UTCL1_TRANSLATION_HIT_sum"], c["TCP_UTCL1_TRANSLATION_MISS_sum"]
         out[key] = {"kernel": "spmm_kernel<4,1,8,false,false> (grl_typed_spmm_fwd)", "workload": desc,
                     "dispatches": n, "duration_ms": t * 1e3, "counters_avg": c,
                     "utcl1_miss_rate": miss / (hit + miss)}
     path = os.path.join(HERE, "..", "profiles", "r01_pmc_mfma_tlb.json")
+    if os.path.exists(path):  # keep entries this run did not re-measure
+        old = json.load(open(path))
+        old.update(out)
+        out = old
     json.dump(out, open(path, "w"), indent=1, sort_keys=True)
     print(json.dumps(out, indent=1, sort_keys=True))
 
