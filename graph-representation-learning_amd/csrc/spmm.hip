@@ -383,13 +383,27 @@ struct LaunchShape {
   int vec, nv, ycols;
 };
 
-LaunchShape pick_shape(const float* a, const float* b, int64_t lda, int64_t ldb, int F) {
+// Gathered tables above this size keep a whole row (up to 512 columns) in one
+// wave.  GRL_SPMM_WIDE=1/0 forces whole-row / 256-column waves (A/B aid and
+// tests; read on every launch).
+int64_t wide_table_bytes() {
+  const char* e = getenv("GRL_SPMM_WIDE");
+  if (e && e[0] == '1') return 0;
+  if (e && e[0] == '0') return INT64_MAX;
+  return (int64_t)4 << 30;
+}
+
+LaunchShape pick_shape(const float* a, const float* b, int64_t lda, int64_t ldb, int F, int64_t table_bytes) {
   const bool al = (reinterpret_cast<uintptr_t>(a) % 16 == 0) && (reinterpret_cast<uintptr_t>(b) % 16 == 0) &&
                   (lda % 4 == 0) && (ldb % 4 == 0) && (F % 4 == 0);
   if (al) {
-    // one float4 per lane, 256 columns per wave: wider rows go to more waves
-    // along grid.y (each re-reads the row's indices) instead of more registers
-    // per wave -- ER d=512: 14.7 -> 13.2 ms; R-MAT d=512 unchanged
+    // One float4 per lane, 256 columns per wave: wider rows go to more waves
+    // along grid.y (each re-reads the row's indices) instead of more
+    // registers per wave -- ER d=512 (X 2 GB): 14.7 -> 13.2 ms.  On a table
+    // far beyond the Infinity Cache each half-row visit pays its own address
+    // translation, so there a wave gathers the whole 2 KB row -- C5 (R-MAT,
+    // X 17 GB): 293 ms with half rows, 236 ms with whole rows.
+    if (F > 256 && F <= 512 && table_bytes > wide_table_bytes()) return {4, 2, 64 * 4 * 2};
     return {4, 1, 64 * 4};
   }
   const int nv = F <= 64 ? 1 : (F <= 128 ? 2 : 4);
@@ -425,7 +439,9 @@ int launch_spmm(int64_t num_rows, int64_t self_rows, int S, int hs, const int32_
   SplitDev sp;
   int rc = to_split_dev(plan, F, sp);
   if (rc) return rc;
-  const LaunchShape sh = pick_shape(src, align_probe, lds, ldo, F);
+  // gathered table: X (~num_rows rows of lds floats) forward, dZ rows (S per node) backward
+  const int64_t table_bytes = BWD ? num_rows * (int64_t)S * F * 4 : num_rows * lds * 4;
+  const LaunchShape sh = pick_shape(src, align_probe, lds, ldo, F, table_bytes);
   const int64_t items = num_rows + sp.num_chunks;
   const int64_t cap = (int64_t)device_cu_count() * spmm_blocks_per_cu();  // 4-wave blocks per CU in flight
   const int64_t gx = std::min<int64_t>(ceil_div(items, 4), cap);

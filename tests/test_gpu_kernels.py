@@ -387,3 +387,15 @@ def test_x6_split_is_exact_on_wide_dynamic_range(monkeypatch):
     assert torch.equal(linear_fwd(Zi, Wi, None, False), (Zi.double() @ Wi.double()).float())
     gi = torch.randint(-64, 65, (M, C), device=DEV, generator=gen).float()
     assert torch.equal(linear_bwd_data(gi, None, Wi), (gi.double() @ Wi.double().T).float())
+
+
+@pytest.mark.parametrize("wide", ["1", "0"])
+def test_spmm_wide_rows_bitwise(wide, monkeypatch):
+    """F in (256, 512]: one wave per whole row (GRL_SPMM_WIDE=1, the choice for
+    gathered tables above 4 GB) or 256-column waves along grid.y ("0"); both
+    bitwise equal to the oracle, forward and backward, with DropEdge, float
+    edge values and split heavy rows."""
+    monkeypatch.setenv("GRL_SPMM_WIDE", wide)
+    test_spmm_fwd_bwd_bitwise((300, 6, 16.0, 512, 0, True, True), 1)
+    test_spmm_fwd_bwd_bitwise((200, 6, 8.0, 384, 0, False, True), 2)
+    test_split_rows_bitwise_rmat((300, 128), 1, 512, True)
