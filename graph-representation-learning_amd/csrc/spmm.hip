@@ -383,14 +383,14 @@ struct LaunchShape {
   int vec, nv, ycols;
 };
 
-// Gathered tables above this size keep a whole row (up to 512 columns) in one
+// Gathered tables above 12 GB keep a whole row (up to 512 columns) in one
 // wave.  GRL_SPMM_WIDE=1/0 forces whole-row / 256-column waves (A/B aid and
 // tests; read on every launch).
 int64_t wide_table_bytes() {
   const char* e = getenv("GRL_SPMM_WIDE");
   if (e && e[0] == '1') return 0;
   if (e && e[0] == '0') return INT64_MAX;
-  return (int64_t)4 << 30;
+  return (int64_t)12 << 30;
 }
 
 LaunchShape pick_shape(const float* a, const float* b, int64_t lda, int64_t ldb, int F, int64_t table_bytes) {
@@ -399,10 +399,11 @@ LaunchShape pick_shape(const float* a, const float* b, int64_t lda, int64_t ldb,
   if (al) {
     // One float4 per lane, 256 columns per wave: wider rows go to more waves
     // along grid.y (each re-reads the row's indices) instead of more
-    // registers per wave -- ER d=512 (X 2 GB): 14.7 -> 13.2 ms.  On a table
-    // far beyond the Infinity Cache each half-row visit pays its own address
-    // translation, so there a wave gathers the whole 2 KB row -- C5 (R-MAT,
-    // X 17 GB): 293 ms with half rows, 236 ms with whole rows.
+    // registers per wave.  Half / whole rows (tools/ab_spmm_wide.sh): ER
+    // d=512 X 2 GB 12.6 / 13.7 ms, X 8 GB 57.6 / 61.2; R-MAT d=512 X 2 GB
+    // 25.6 / 28.3.  Far beyond that each half-row visit pays its own address
+    // translation and a wave gathers the whole 2 KB row: C5 (R-MAT, X 17 GB)
+    // 293 / 233 ms.  Threshold between the measured 8 and 17 GB.
     if (F > 256 && F <= 512 && table_bytes > wide_table_bytes()) return {4, 2, 64 * 4 * 2};
     return {4, 1, 64 * 4};
   }

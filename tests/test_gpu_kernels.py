@@ -392,7 +392,7 @@ def test_x6_split_is_exact_on_wide_dynamic_range(monkeypatch):
 @pytest.mark.parametrize("wide", ["1", "0"])
 def test_spmm_wide_rows_bitwise(wide, monkeypatch):
     """F in (256, 512]: one wave per whole row (GRL_SPMM_WIDE=1, the choice for
-    gathered tables above 4 GB) or 256-column waves along grid.y ("0"); both
+    gathered tables above 12 GB) or 256-column waves along grid.y ("0"); both
     bitwise equal to the oracle, forward and backward, with DropEdge, float
     edge values and split heavy rows."""
     monkeypatch.setenv("GRL_SPMM_WIDE", wide)
