@@ -25,6 +25,8 @@
 
 #include <math.h>
 
+#include <cstdlib>
+
 namespace grl {
 namespace {
 
@@ -374,14 +376,236 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(AttnArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Forward on the bf16 matrix cores by exact three-way splitting (the "x6"
+// scheme of linear.hip): every fp32 operand value is
+// v0 + v1 + v2 in bf16 exactly, and the six products with i + j <= 2 run on
+// v_mfma_f32_32x32x16_bf16 with fp32 accumulation -- fp32-level accuracy at
+// 6 x 32 MFMA cycles per 32x32x16 block instead of 8 x 64.  Same transposed
+// products as attn_fwd_kernel (S^T = K Q^T, O^T += H^T P^T, one query per
+// lane, keys in registers).  Q is split once into registers; each 32-key block
+// of K and H is split while staged into LDS planes; P is split in registers.
+// O^T's MFMA u (u = 0, 1) takes key slot 8h + j <-> key kappa(8u + j, h) --
+// P registers 8u..8u+7 as the B operand -- and the matching H^T rows come
+// out of ds_read_b64_tr_b16, whose 16-lane groups gather 4 rows (keys) x 16
+// columns (features) from per-lane row addresses.  H plane rows keep column c
+// at c ^ ((key & 3) << 5) so the four keys of a transposed read sit in
+// different banks (DV >= 128).
+typedef __bf16 abf16x8_t __attribute__((ext_vector_type(8)));
+typedef __bf16 abf16x2_t __attribute__((ext_vector_type(2)));
+typedef float af32x2_t __attribute__((ext_vector_type(2)));
+typedef short ai16x4_t __attribute__((ext_vector_type(4)));
+typedef short ai16x8_t __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ uint32_t apack(float a, float b) {
+  af32x2_t p = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(p, abf16x2_t));
+}
+__device__ __forceinline__ float alo(uint32_t u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float ahi(uint32_t u) { return __uint_as_float(u & 0xFFFF0000u); }
+
+// v (4 floats) -> three planes of 4 bf16 with v == p0 + p1 + p2 exactly
+__device__ __forceinline__ void asplit3(float4 v, uint2& p0, uint2& p1, uint2& p2) {
+  p0.x = apack(v.x, v.y);
+  p0.y = apack(v.z, v.w);
+  float4 r = make_float4(v.x - alo(p0.x), v.y - ahi(p0.x), v.z - alo(p0.y), v.w - ahi(p0.y));
+  p1.x = apack(r.x, r.y);
+  p1.y = apack(r.z, r.w);
+  r = make_float4(r.x - alo(p1.x), r.y - ahi(p1.x), r.z - alo(p1.y), r.w - ahi(p1.y));
+  p2.x = apack(r.x, r.y);
+  p2.y = apack(r.z, r.w);
+}
+
+// 8 floats -> three bf16x8 planes
+__device__ __forceinline__ void asplit8(float4 lo, float4 hi, abf16x8_t& a0, abf16x8_t& a1, abf16x8_t& a2) {
+  uint2 l0, l1, l2, h0, h1, h2;
+  asplit3(lo, l0, l1, l2);
+  asplit3(hi, h0, h1, h2);
+  a0 = __builtin_bit_cast(abf16x8_t, make_uint4(l0.x, l0.y, h0.x, h0.y));
+  a1 = __builtin_bit_cast(abf16x8_t, make_uint4(l1.x, l1.y, h1.x, h1.y));
+  a2 = __builtin_bit_cast(abf16x8_t, make_uint4(l2.x, l2.y, h2.x, h2.y));
+}
+
+#define MFMA6(acc, a0, a1, a2, b0, b1, b2)                                  \
+  do {                                                                      \
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b0, acc, 0, 0, 0);   \
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b1, acc, 0, 0, 0);   \
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b2, acc, 0, 0, 0);   \
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, b0, acc, 0, 0, 0);   \
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc, 0, 0, 0);   \
+    acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc, 0, 0, 0);   \
+  } while (0)
+
+template <int W>
+__device__ __forceinline__ int hswz(int key, int col) {  // H plane element offset
+  return key * W + (W >= 128 ? (col ^ ((key & 3) << 5)) : col);
+}
+
+template <int DKP, int NT>
+__global__ __launch_bounds__(256) void attn_fwd_x6_kernel(AttnArgs a) {
+  constexpr int DV = NT * 32, KC = DKP / 16;
+  constexpr int KPL = 32 * DKP, HPL = 32 * DV;  // bf16 per plane
+  __shared__ __attribute__((aligned(16))) uint16_t Kp[3 * KPL];
+  __shared__ __attribute__((aligned(16))) uint16_t Hp[3 * HPL];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, h = lane >> 5;
+  const int64_t N = a.N, b = blockIdx.y;
+  const float* Qb = a.Q + b * N * a.dk;
+  const float* Kb = a.K + b * N * a.dk;
+  const float* Hb = a.H + b * N * a.dv;
+  const int64_t q = (int64_t)blockIdx.x * 128 + wave * 32 + l32;
+
+  // this lane's query, dims kc*16 + 8h + 0..7, split into three planes
+  abf16x8_t qp[KC][3];
+#pragma unroll
+  for (int kc = 0; kc < KC; ++kc) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int d = kc * 16 + 8 * h + j;
+      v[j] = (q < N && d < a.dk) ? Qb[q * a.dk + d] : 0.0f;
+    }
+    asplit8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]), qp[kc][0], qp[kc][1],
+            qp[kc][2]);
+  }
+  f32x16 o[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) o[t] = zero16();
+  float m = -INFINITY, l = 0.0f;
+  Stager<DKP, DKP> sk;
+  Stager<DV, DV> sh;
+  const bool vk = vec_ok(Kb, a.dk), vh = vec_ok(Hb, a.dv);
+  sk.fetch(Kb, 0, N, a.dk, vk, tid);
+  sh.fetch(Hb, 0, N, a.dv, vh, tid);
+  // transposed-read coordinates: group row q' = (lane & 15) >> 2, columns 16 ((lane >> 4) & 1) + 4 (lane & 3)
+  const int trq = (lane & 15) >> 2;
+  const int trc = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+
+  for (int64_t k0 = 0; k0 < N; k0 += 32) {
+    // split-store the staged K and H block
+#pragma unroll
+    for (int it = 0; it < Stager<DKP, DKP>::PER; ++it) {
+      const int idx = tid + it * 256;
+      if (idx < Stager<DKP, DKP>::NF4) {
+        const int r = idx / (DKP / 4), c = (idx % (DKP / 4)) * 4;
+        uint2 p0, p1, p2;
+        asplit3(sk.reg[it], p0, p1, p2);
+        *reinterpret_cast<uint2*>(&Kp[r * DKP + c]) = p0;
+        *reinterpret_cast<uint2*>(&Kp[KPL + r * DKP + c]) = p1;
+        *reinterpret_cast<uint2*>(&Kp[2 * KPL + r * DKP + c]) = p2;
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < Stager<DV, DV>::PER; ++it) {
+      const int idx = tid + it * 256;
+      if (idx < Stager<DV, DV>::NF4) {
+        const int r = idx / (DV / 4), c = (idx % (DV / 4)) * 4;
+        uint2 p0, p1, p2;
+        asplit3(sh.reg[it], p0, p1, p2);
+        const int off = hswz<DV>(r, c);
+        *reinterpret_cast<uint2*>(&Hp[off]) = p0;
+        *reinterpret_cast<uint2*>(&Hp[HPL + off]) = p1;
+        *reinterpret_cast<uint2*>(&Hp[2 * HPL + off]) = p2;
+      }
+    }
+    __syncthreads();
+    if (k0 + 32 < N) {
+      sk.fetch(Kb, k0 + 32, N, a.dk, vk, tid);
+      sh.fetch(Hb, k0 + 32, N, a.dv, vh, tid);
+    }
+    // S^T = K Q^T: A = K[key l32][kc*16 + 8h ..], B = Q
+    f32x16 s = zero16();
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      const int off = l32 * DKP + kc * 16 + 8 * h;
+      const abf16x8_t k0p = *reinterpret_cast<const abf16x8_t*>(&Kp[off]);
+      const abf16x8_t k1p = *reinterpret_cast<const abf16x8_t*>(&Kp[KPL + off]);
+      const abf16x8_t k2p = *reinterpret_cast<const abf16x8_t*>(&Kp[2 * KPL + off]);
+      MFMA6(s, k0p, k1p, k2p, qp[kc][0], qp[kc][1], qp[kc][2]);
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      if (k0 + kappa(r, h) >= N) s[r] = -INFINITY;
+      mx = fmaxf(mx, s[r]);
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    const float mn = fmaxf(m, mx);
+    const float alpha = expf(m - mn);
+    float ps = 0.0f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      s[r] = expf(s[r] - mn);
+      ps += s[r];
+    }
+    ps += __shfl_xor(ps, 32);
+    l = l * alpha + ps;
+    m = mn;
+    abf16x8_t pp[2][3];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      asplit8(make_float4(s[8 * u], s[8 * u + 1], s[8 * u + 2], s[8 * u + 3]),
+              make_float4(s[8 * u + 4], s[8 * u + 5], s[8 * u + 6], s[8 * u + 7]), pp[u][0], pp[u][1], pp[u][2]);
+#pragma unroll
+    for (int t = 0; t < NT; ++t) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        abf16x8_t hp[3];
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) {
+          typedef __attribute__((address_space(3))) ai16x4_t lds_v4;
+          const int key0 = kappa(8 * u + trq, h), key1 = kappa(8 * u + 4 + trq, h);
+          const uint16_t* p0 = &Hp[pl * HPL + hswz<DV>(key0, t * 32 + trc)];
+          const uint16_t* p1 = &Hp[pl * HPL + hswz<DV>(key1, t * 32 + trc)];
+          const ai16x4_t x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(uintptr_t)(uint32_t)(uintptr_t)p0);
+          const ai16x4_t x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(uintptr_t)(uint32_t)(uintptr_t)p1);
+          const ai16x8_t v = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+          hp[pl] = __builtin_bit_cast(abf16x8_t, v);
+        }
+        MFMA6(o[t], hp[0], hp[1], hp[2], pp[u][0], pp[u][1], pp[u][2]);
+      }
+    }
+    __syncthreads();
+  }
+
+  if (q < N) {
+    const float inv = 1.0f / l;
+    const int64_t base = (b * N + q) * a.dv;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int f = t * 32 + kappa(r, h);
+        if (f < a.dv) {
+          const float on = o[t][r] * inv;
+          a.out[base + f] = a.gamma[f] * on + a.V[base + f];
+          if (a.onorm) a.onorm[base + f] = on;
+        }
+      }
+    if (h == 0 && a.rmax) {
+      a.rmax[b * N + q] = m;
+      a.rsum[b * N + q] = l;
+    }
+  }
+}
+
 #undef MFMA
 
 enum AttnPass { PASS_FWD, PASS_BWD_Q, PASS_BWD_KV };
 
+// GRL_ATTN_X6=0 (read per call) keeps the fp32-MFMA kernels
+bool attn_x6_enabled() {
+  const char* e = getenv("GRL_ATTN_X6");
+  return !(e && e[0] == '0');
+}
+
 template <int DKP, int NT>
 int launch_attn(AttnPass pass, const AttnArgs& a, int64_t B, hipStream_t st) {
   const dim3 grid((unsigned)ceil_div(a.N, 128), (unsigned)B);
-  if (pass == PASS_FWD)
+  if (pass == PASS_FWD && attn_x6_enabled())
+    hipLaunchKernelGGL((attn_fwd_x6_kernel<DKP, NT>), grid, dim3(256), 0, st, a);
+  else if (pass == PASS_FWD)
     hipLaunchKernelGGL((attn_fwd_kernel<DKP, NT>), grid, dim3(256), 0, st, a);
   else if (pass == PASS_BWD_Q)
     hipLaunchKernelGGL((attn_bwd_q_kernel<DKP, NT>), grid, dim3(256), 0, st, a);
