@@ -590,6 +590,293 @@ __global__ __launch_bounds__(256) void attn_fwd_x6_kernel(AttnArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Backward on the bf16 matrix cores (x6), for dv in (96, 128] (NT = 4: the
+// model's 128-wide values).  Three kernels instead of two: the key-stationary
+// work is split into dH (needs P only) and dK (needs dP, so the lane's H row
+// in registers) so that neither holds both a 64-register dH accumulator and
+// the 96 registers of H's planes.  Each recomputes S (6 MFMAs per block).
+// The 128-column planes (H, dO) use the guide's 256-B-row image (b)
+// (cdna_hip_programming.md T10): 16-B chunk ch of row r at
+// ch ^ (((r & 3) << 2) | ((r >> 2) & 3)), conflict-free for both the
+// ds_read_b128 row reads and the ds_read_b64_tr_b16 reads of 4 consecutive
+// rows.  The 32-column planes (K, Q; dk padded with zeros) are read
+// transposed over 4 consecutive rows of 64 B: conflict-free as they lie.
+__device__ __forceinline__ int swz128(int row, int col) {
+  const int sw = ((row & 3) << 2) | ((row >> 2) & 3);
+  return row * 128 + ((((col >> 3) ^ sw)) << 3) + (col & 7);
+}
+
+__device__ __forceinline__ abf16x8_t tr8(const uint16_t* p0, const uint16_t* p1) {
+  typedef __attribute__((address_space(3))) ai16x4_t lds_v4;
+  const ai16x4_t x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(uintptr_t)(uint32_t)(uintptr_t)p0);
+  const ai16x4_t x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(uintptr_t)(uint32_t)(uintptr_t)p1);
+  const ai16x8_t v = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+  return __builtin_bit_cast(abf16x8_t, v);
+}
+
+// split-store a staged 32-row block: narrow (row width W <= 32) into
+// [3][32][32] planes, or 128 wide into swizzled [3][32][128] planes
+template <int W, bool WIDE>
+__device__ __forceinline__ void stash_planes(const Stager<W, W>& st, uint16_t* planes, int tid) {
+  constexpr int PL = WIDE ? 32 * 128 : 32 * 32;
+#pragma unroll
+  for (int it = 0; it < Stager<W, W>::PER; ++it) {
+    const int idx = tid + it * 256;
+    if (idx < Stager<W, W>::NF4) {
+      const int r = idx / (W / 4), c = (idx % (W / 4)) * 4;
+      uint2 p0, p1, p2;
+      asplit3(st.reg[it], p0, p1, p2);
+      const int off = WIDE ? swz128(r, c) : r * 32 + c;
+      *reinterpret_cast<uint2*>(&planes[off]) = p0;
+      *reinterpret_cast<uint2*>(&planes[PL + off]) = p1;
+      *reinterpret_cast<uint2*>(&planes[2 * PL + off]) = p2;
+    }
+  }
+}
+
+// lane's own 8-value slices v[c*16 + 8h + j] of a row, split into planes
+template <int NC>
+__device__ __forceinline__ void row_planes(const float* row, bool valid, int width, int h, abf16x8_t (&pl)[NC][3]) {
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int d = c * 16 + 8 * h + j;
+      v[j] = (valid && d < width) ? row[d] : 0.0f;
+    }
+    asplit8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]), pl[c][0], pl[c][1], pl[c][2]);
+  }
+}
+
+// 16 fp32 registers (keys / queries kappa(r, h)) -> the two B operands u = 0, 1
+__device__ __forceinline__ void reg_planes(const f32x16& x, abf16x8_t (&pl)[2][3]) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+    asplit8(make_float4(x[8 * u], x[8 * u + 1], x[8 * u + 2], x[8 * u + 3]),
+            make_float4(x[8 * u + 4], x[8 * u + 5], x[8 * u + 6], x[8 * u + 7]), pl[u][0], pl[u][1], pl[u][2]);
+}
+
+// query-stationary: dQ^T += K^T dS^T
+template <int DKP>
+__global__ __launch_bounds__(256, 2) void attn_bwd_q_x6_kernel(AttnArgs a) {
+  constexpr int KC = DKP / 16, FC = 8;  // 128 value columns = 8 chunks of 16
+  __shared__ __attribute__((aligned(16))) uint16_t Kp[3 * 32 * 32];
+  __shared__ __attribute__((aligned(16))) uint16_t Hp[3 * 32 * 128];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, h = lane >> 5;
+  const int64_t N = a.N, b = blockIdx.y;
+  const float* Kb = a.K + b * N * a.dk;
+  const float* Hb = a.H + b * N * a.dv;
+  const int64_t q = (int64_t)blockIdx.x * 128 + wave * 32 + l32;
+  const bool qv = q < N;
+  abf16x8_t qp[KC][3], dop[FC][3];
+  row_planes<KC>(a.Q + (b * N + q) * a.dk, qv, a.dk, h, qp);
+  row_planes<FC>(a.dO + (b * N + q) * a.dv, qv, a.dv, h, dop);
+  const float mq = qv ? a.smax[b * N + q] : 0.0f;
+  const float il = qv ? 1.0f / a.ssum[b * N + q] : 0.0f;
+  const float Dq = qv ? a.Drow[b * N + q] : 0.0f;
+  f32x16 dq = zero16();
+  if (DKP < 32)  // zero pad columns of the K planes, never written by the staging
+    for (int i = tid; i < 3 * 32 * (32 - DKP); i += 256) {
+      const int pl = i / (32 * (32 - DKP)), rc = i % (32 * (32 - DKP));
+      Kp[pl * 1024 + (rc / (32 - DKP)) * 32 + DKP + rc % (32 - DKP)] = 0;
+    }
+  Stager<DKP, DKP> sk;
+  Stager<128, 128> sh;
+  const bool vk = vec_ok(Kb, a.dk), vh = vec_ok(Hb, a.dv);
+  sk.fetch(Kb, 0, N, a.dk, vk, tid);
+  sh.fetch(Hb, 0, N, a.dv, vh, tid);
+  const int trq = (lane & 15) >> 2, trc = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+
+  for (int64_t k0 = 0; k0 < N; k0 += 32) {
+    stash_planes<DKP, false>(sk, Kp, tid);
+    stash_planes<128, true>(sh, Hp, tid);
+    __syncthreads();
+    if (k0 + 32 < N) {
+      sk.fetch(Kb, k0 + 32, N, a.dk, vk, tid);
+      sh.fetch(Hb, k0 + 32, N, a.dv, vh, tid);
+    }
+    f32x16 s = zero16();
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      const int off = l32 * 32 + kc * 16 + 8 * h;
+      const abf16x8_t k0p = *reinterpret_cast<const abf16x8_t*>(&Kp[off]);
+      const abf16x8_t k1p = *reinterpret_cast<const abf16x8_t*>(&Kp[1024 + off]);
+      const abf16x8_t k2p = *reinterpret_cast<const abf16x8_t*>(&Kp[2048 + off]);
+      MFMA6(s, k0p, k1p, k2p, qp[kc][0], qp[kc][1], qp[kc][2]);
+    }
+    f32x16 dp = zero16();  // dP^T[key][query] = sum_f H[key][f] dO[query][f]
+#pragma unroll
+    for (int fc = 0; fc < FC; ++fc) {
+      const int off = swz128(l32, fc * 16 + 8 * h);
+      const abf16x8_t h0 = *reinterpret_cast<const abf16x8_t*>(&Hp[off]);
+      const abf16x8_t h1 = *reinterpret_cast<const abf16x8_t*>(&Hp[4096 + off]);
+      const abf16x8_t h2 = *reinterpret_cast<const abf16x8_t*>(&Hp[8192 + off]);
+      MFMA6(dp, h0, h1, h2, dop[fc][0], dop[fc][1], dop[fc][2]);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float p = (k0 + kappa(r, h) < N) ? expf(s[r] - mq) * il : 0.0f;
+      s[r] = p * (dp[r] - Dq);  // dS^T
+    }
+    abf16x8_t dsp[2][3];
+    reg_planes(s, dsp);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int r0 = kappa(8 * u + trq, h), r1 = kappa(8 * u + 4 + trq, h);
+      abf16x8_t kt[3];
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) kt[pl] = tr8(&Kp[pl * 1024 + r0 * 32 + trc], &Kp[pl * 1024 + r1 * 32 + trc]);
+      MFMA6(dq, kt[0], kt[1], kt[2], dsp[u][0], dsp[u][1], dsp[u][2]);
+    }
+    __syncthreads();
+  }
+  if (qv) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int d = kappa(r, h);
+      if (d < a.dk) a.dQ[(b * N + q) * a.dk + d] = dq[r];
+    }
+  }
+}
+
+// key-stationary.  WANT_H: dH^T += dO^T P;  else dK^T += Q^T dS (needs dP)
+template <int DKP, bool WANT_H>
+__global__ __launch_bounds__(256, 2) void attn_bwd_kv_x6_kernel(AttnArgs a) {
+  constexpr int KC = DKP / 16, FC = 8;
+  __shared__ __attribute__((aligned(16))) uint16_t Qp[3 * 32 * 32];
+  __shared__ __attribute__((aligned(16))) uint16_t Op[3 * 32 * 128];
+  __shared__ float Ms[32], Ls[32], Ds[32];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, h = lane >> 5;
+  const int64_t N = a.N, b = blockIdx.y;
+  const float* Qb = a.Q + b * N * a.dk;
+  const float* dOb = a.dO + b * N * a.dv;
+  const int64_t key = (int64_t)blockIdx.x * 128 + wave * 32 + l32;
+  const bool kv = key < N;
+  abf16x8_t kp[KC][3];
+  row_planes<KC>(a.K + (b * N + key) * a.dk, kv, a.dk, h, kp);
+  abf16x8_t hp[WANT_H ? 1 : FC][3];
+  if (!WANT_H) row_planes<WANT_H ? 1 : FC>(a.H + (b * N + key) * a.dv, kv, a.dv, h, hp);
+  f32x16 acc[WANT_H ? 4 : 1];
+#pragma unroll
+  for (int t = 0; t < (WANT_H ? 4 : 1); ++t) acc[t] = zero16();
+  if (DKP < 32)
+    for (int i = tid; i < 3 * 32 * (32 - DKP); i += 256) {
+      const int pl = i / (32 * (32 - DKP)), rc = i % (32 * (32 - DKP));
+      Qp[pl * 1024 + (rc / (32 - DKP)) * 32 + DKP + rc % (32 - DKP)] = 0;
+    }
+  Stager<DKP, DKP> sq;
+  Stager<128, 128> so;
+  const bool vq = vec_ok(Qb, a.dk), vo = vec_ok(dOb, a.dv);
+  float pm = 0.0f, pl_ = 0.0f, pd = 0.0f;
+  auto fetch_stats = [&](int64_t q0) {
+    if (tid < 32) {
+      const int64_t qq = q0 + tid;
+      const bool v = qq < N;
+      pm = v ? a.smax[b * N + qq] : 0.0f;
+      pl_ = v ? 1.0f / a.ssum[b * N + qq] : 0.0f;  // 0 => P = 0 for padded queries
+      pd = v ? a.Drow[b * N + qq] : 0.0f;
+    }
+  };
+  sq.fetch(Qb, 0, N, a.dk, vq, tid);
+  so.fetch(dOb, 0, N, a.dv, vo, tid);
+  fetch_stats(0);
+  const int trq = (lane & 15) >> 2, trc = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+
+  for (int64_t q0 = 0; q0 < N; q0 += 32) {
+    stash_planes<DKP, false>(sq, Qp, tid);
+    stash_planes<128, true>(so, Op, tid);
+    if (tid < 32) {
+      Ms[tid] = pm;
+      Ls[tid] = pl_;
+      Ds[tid] = pd;
+    }
+    __syncthreads();
+    if (q0 + 32 < N) {
+      sq.fetch(Qb, q0 + 32, N, a.dk, vq, tid);
+      so.fetch(dOb, q0 + 32, N, a.dv, vo, tid);
+      fetch_stats(q0 + 32);
+    }
+    // S[query][key]: lanes = keys, registers = queries kappa(r, h)
+    f32x16 s = zero16();
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      const int off = l32 * 32 + kc * 16 + 8 * h;
+      const abf16x8_t q0p = *reinterpret_cast<const abf16x8_t*>(&Qp[off]);
+      const abf16x8_t q1p = *reinterpret_cast<const abf16x8_t*>(&Qp[1024 + off]);
+      const abf16x8_t q2p = *reinterpret_cast<const abf16x8_t*>(&Qp[2048 + off]);
+      MFMA6(s, q0p, q1p, q2p, kp[kc][0], kp[kc][1], kp[kc][2]);
+    }
+    if (WANT_H) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int qi = kappa(r, h);
+        s[r] = kv ? expf(s[r] - Ms[qi]) * Ls[qi] : 0.0f;  // P
+      }
+      abf16x8_t pp[2][3];
+      reg_planes(s, pp);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int r0 = kappa(8 * u + trq, h), r1 = kappa(8 * u + 4 + trq, h);
+          abf16x8_t ot[3];
+#pragma unroll
+          for (int pl = 0; pl < 3; ++pl)
+            ot[pl] = tr8(&Op[pl * 4096 + swz128(r0, t * 32 + trc)], &Op[pl * 4096 + swz128(r1, t * 32 + trc)]);
+          MFMA6(acc[t], ot[0], ot[1], ot[2], pp[u][0], pp[u][1], pp[u][2]);
+        }
+    } else {
+      f32x16 dp = zero16();  // dP[query][key] = sum_f dO[query][f] H[key][f]
+#pragma unroll
+      for (int fc = 0; fc < FC; ++fc) {
+        const int off = swz128(l32, fc * 16 + 8 * h);
+        const abf16x8_t o0 = *reinterpret_cast<const abf16x8_t*>(&Op[off]);
+        const abf16x8_t o1 = *reinterpret_cast<const abf16x8_t*>(&Op[4096 + off]);
+        const abf16x8_t o2 = *reinterpret_cast<const abf16x8_t*>(&Op[8192 + off]);
+        MFMA6(dp, o0, o1, o2, hp[fc][0], hp[fc][1], hp[fc][2]);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int qi = kappa(r, h);
+        const float p = kv ? expf(s[r] - Ms[qi]) * Ls[qi] : 0.0f;
+        s[r] = p * (dp[r] - Ds[qi]);  // dS
+      }
+      abf16x8_t dsp[2][3];
+      reg_planes(s, dsp);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int r0 = kappa(8 * u + trq, h), r1 = kappa(8 * u + 4 + trq, h);
+        abf16x8_t qt[3];
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) qt[pl] = tr8(&Qp[pl * 1024 + r0 * 32 + trc], &Qp[pl * 1024 + r1 * 32 + trc]);
+        MFMA6(acc[0], qt[0], qt[1], qt[2], dsp[u][0], dsp[u][1], dsp[u][2]);
+      }
+    }
+    __syncthreads();
+  }
+  if (kv) {
+    if (WANT_H) {
+      const int64_t rowv = (b * N + key) * a.dv;
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int f = t * 32 + kappa(r, h);
+          if (f < a.dv) a.dH[rowv + f] = acc[t][r];
+        }
+    } else {
+      const int64_t rowk = (b * N + key) * a.dk;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int d = kappa(r, h);
+        if (d < a.dk) a.dK[rowk + d] = acc[0][r];
+      }
+    }
+  }
+}
+
 #undef MFMA
 
 enum AttnPass { PASS_FWD, PASS_BWD_Q, PASS_BWD_KV };
@@ -607,7 +894,15 @@ int launch_attn(AttnPass pass, const AttnArgs& a, int64_t B, hipStream_t st) {
     hipLaunchKernelGGL((attn_fwd_x6_kernel<DKP, NT>), grid, dim3(256), 0, st, a);
   else if (pass == PASS_FWD)
     hipLaunchKernelGGL((attn_fwd_kernel<DKP, NT>), grid, dim3(256), 0, st, a);
-  else if (pass == PASS_BWD_Q)
+  else if (NT == 4 && attn_x6_enabled()) {  // backward x6: dv in (96, 128]
+    if (pass == PASS_BWD_Q) {
+      hipLaunchKernelGGL((attn_bwd_q_x6_kernel<DKP>), grid, dim3(256), 0, st, a);
+    } else {
+      hipLaunchKernelGGL((attn_bwd_kv_x6_kernel<DKP, true>), grid, dim3(256), 0, st, a);
+      GRL_LAUNCH_CHECK();
+      hipLaunchKernelGGL((attn_bwd_kv_x6_kernel<DKP, false>), grid, dim3(256), 0, st, a);
+    }
+  } else if (pass == PASS_BWD_Q)
     hipLaunchKernelGGL((attn_bwd_q_kernel<DKP, NT>), grid, dim3(256), 0, st, a);
   else
     hipLaunchKernelGGL((attn_bwd_kv_kernel<DKP, NT>), grid, dim3(256), 0, st, a);

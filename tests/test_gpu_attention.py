@@ -32,16 +32,20 @@ SHAPES = [(1, 74, 16, 128), (4, 74, 16, 128), (2, 33, 4, 32), (1, 1, 2, 16), (3,
           (2, 64, 5, 40), (1, 500, 16, 100), (2, 9, 0, 4)]  # dk = 0: net_size 8 (4 // 8), uniform attention
 
 
+@pytest.mark.parametrize("x6", ["1", "0"])  # split-bf16 kernels (default) / fp32-MFMA kernels
 @pytest.mark.parametrize("B,N,dk,dv", SHAPES)
-def test_forward_matches_fp64(B, N, dk, dv):
+def test_forward_matches_fp64(B, N, dk, dv, x6, monkeypatch):
+    monkeypatch.setenv("GRL_ATTN_X6", x6)
     Q, K, H, V, gamma = _inputs(B, N, dk, dv, seed=N + dk)
     out = node_attention_forward(Q, K, H, V, gamma)
     ref = _ref(*(t.double() for t in (Q, K, H, V, gamma)))
     torch.testing.assert_close(out.double(), ref, rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("x6", ["1", "0"])
 @pytest.mark.parametrize("B,N,dk,dv", SHAPES)
-def test_backward_matches_fp64(B, N, dk, dv):
+def test_backward_matches_fp64(B, N, dk, dv, x6, monkeypatch):
+    monkeypatch.setenv("GRL_ATTN_X6", x6)
     Q, K, H, V, gamma = _inputs(B, N, dk, dv, seed=7 * N + dv)
     leaves = [t.clone().requires_grad_(True) for t in (Q, K, H, V, gamma)]
     out = node_self_attention(*leaves)
