@@ -315,8 +315,10 @@ def extras(args, graph, X_full, gather, L, F, dev, E_loc, n_loc):
     Zd = Z.detach()
     ms = _time(lambda: linear_fwd(Zd, W, b, True), iters)
     flops = 2.0 * Zd.shape[0] * Zd.shape[1] * F
-    res["linear_mfma_fwd"] = {"ms": ms, "TFLOPs": flops / (ms * 1e-3) / 1e12,
-                              "frac_of_f32_mfma_peak": flops / (ms * 1e-3) / 1e12 / F32_MFMA_PEAK_TFS}
+    path = ("x6: fp32 split into 3 bf16 parts, 6 products on v_mfma_f32_32x32x16_bf16 (DESIGN 4.2)"
+            if os.environ.get("GRL_GEMM_X6", "1") != "0" else "fp32 MFMA v_mfma_f32_32x32x2_f32")
+    res["linear_mfma_fwd"] = {"ms": ms, "TFLOPs_fp32_equivalent": flops / (ms * 1e-3) / 1e12,
+                              "vs_f32_mfma_peak": flops / (ms * 1e-3) / 1e12 / F32_MFMA_PEAK_TFS, "path": path}
     from grl.ops import linear_bwd_data, linear_bwd_weight, relu_grad
 
     out_l = linear_fwd(Zd, W, b, True)
@@ -325,8 +327,8 @@ def extras(args, graph, X_full, gather, L, F, dev, E_loc, n_loc):
     for name, fn in (("linear_mfma_bwd_data", lambda: linear_bwd_data(gm, mask, W)),
                      ("linear_mfma_bwd_weight", lambda: linear_bwd_weight(Zd, gm, mask, True))):
         ms = _time(fn, iters)
-        res[name] = {"ms": ms, "TFLOPs": flops / (ms * 1e-3) / 1e12,
-                     "frac_of_f32_mfma_peak": flops / (ms * 1e-3) / 1e12 / F32_MFMA_PEAK_TFS}
+        res[name] = {"ms": ms, "TFLOPs_fp32_equivalent": flops / (ms * 1e-3) / 1e12,
+                     "vs_f32_mfma_peak": flops / (ms * 1e-3) / 1e12 / F32_MFMA_PEAK_TFS, "path": path}
     del out_l, g_l, gm
     Wp = W.clone().requires_grad_(True)
     bp = b.clone().requires_grad_(True)
