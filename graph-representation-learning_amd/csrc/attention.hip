@@ -25,6 +25,7 @@
 
 #include <math.h>
 
+#include <algorithm>
 #include <cstdlib>
 
 namespace grl {
@@ -49,6 +50,11 @@ struct AttnArgs {
   float* dQ;           // [B, N, dk]
   float* dK;           // [B, N, dk]
   float* dH;           // [B, N, dv]
+  // x6 PRE staging: bf16 planes [3][B*N][W] split once per call (or NULL)
+  const uint16_t* Kpl;  // W = DKP
+  const uint16_t* Hpl;  // W = DV
+  const uint16_t* Qpl;  // W = DKP
+  const uint16_t* Opl;  // W = DV (dO)
   int64_t N;
   int dk, dv;
 };
@@ -441,12 +447,149 @@ __device__ __forceinline__ int hswz(int key, int col) {  // H plane element offs
   return key * W + (W >= 128 ? (col ^ ((key & 3) << 5)) : col);
 }
 
-template <int DKP, int NT>
+__device__ __forceinline__ int swz128(int row, int col) {
+  const int sw = ((row & 3) << 2) | ((row >> 2) & 3);
+  return row * 128 + ((((col >> 3) ^ sw)) << 3) + (col & 7);
+}
+
+// LDS plane layouts of a 32-row block: PLAIN [32][LW], HSWZ (forward H:
+// column c of row r at c ^ ((r & 3) << 5) when W >= 128), SWZ128 (backward
+// 128-wide planes, image (b) of cdna_hip_programming.md T10)
+enum PlaneLayout { PL_PLAIN = 0, PL_HSWZ = 1, PL_SWZ128 = 2 };
+
+template <int W, int LW, int LAYOUT>
+__device__ __forceinline__ int plane_off(int r, int c) {
+  if (LAYOUT == PL_SWZ128) return swz128(r, c);
+  if (LAYOUT == PL_HSWZ) return hswz<W>(r, c);
+  return r * LW + c;
+}
+
+// One operand's 32-row blocks -> three bf16 LDS planes of LW-element rows.
+// PRE = false: fp32 rows are fetched (float4, zero fill) and split at store;
+// PRE = true: the rows were split once per call into global bf16 planes
+// [3][rows][W] (attn_split_rows_kernel) and are copied 16 B at a time.
+// fetch() is issued for the next block before the current one's MFMAs.
+template <int W, int LW, int LAYOUT, bool PRE>
+struct XStage {
+  static constexpr int PL = 32 * LW;       // LDS elements per plane
+  static constexpr int NU = 3 * 32 * W / 8;  // PRE: uint4 per block
+  static constexpr int PER = PRE ? (NU + 255) / 256 : 1;
+  Stager<W, W> f32;
+  uint4 reg[PER];
+
+  __device__ __forceinline__ void fetch(const float* src, const uint16_t* planes, int64_t ps, int64_t r0, int64_t N,
+                                        int width, bool vec, int tid) {
+    if (!PRE) {
+      f32.fetch(src, r0, N, width, vec, tid);
+      return;
+    }
+#pragma unroll
+    for (int it = 0; it < PER; ++it) {
+      const int idx = tid + it * 256;
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if (idx < NU) {
+        const int pl = idx / (32 * W / 8), rem = idx % (32 * W / 8);
+        const int64_t row = r0 + rem / (W / 8);
+        if (row < N) v = *reinterpret_cast<const uint4*>(planes + pl * ps + row * W + (rem % (W / 8)) * 8);
+      }
+      reg[it] = v;
+    }
+  }
+  __device__ __forceinline__ void store(uint16_t* lds, int tid) const {
+    if (!PRE) {
+#pragma unroll
+      for (int it = 0; it < Stager<W, W>::PER; ++it) {
+        const int idx = tid + it * 256;
+        if (idx < Stager<W, W>::NF4) {
+          const int r = idx / (W / 4), c = (idx % (W / 4)) * 4;
+          uint2 p0, p1, p2;
+          asplit3(f32.reg[it], p0, p1, p2);
+          const int off = plane_off<W, LW, LAYOUT>(r, c);
+          *reinterpret_cast<uint2*>(&lds[off]) = p0;
+          *reinterpret_cast<uint2*>(&lds[PL + off]) = p1;
+          *reinterpret_cast<uint2*>(&lds[2 * PL + off]) = p2;
+        }
+      }
+      return;
+    }
+#pragma unroll
+    for (int it = 0; it < PER; ++it) {
+      const int idx = tid + it * 256;
+      if (idx < NU) {
+        const int pl = idx / (32 * W / 8), rem = idx % (32 * W / 8);
+        const int r = rem / (W / 8), c = (rem % (W / 8)) * 8;
+        *reinterpret_cast<uint4*>(&lds[pl * PL + plane_off<W, LW, LAYOUT>(r, c)]) = reg[it];
+      }
+    }
+  }
+};
+
+// planes[p][r][0..W) = bf16 part p of src[r][0..width) (zero beyond width):
+// the once-per-call split of an attention operand for the PRE staging path
+__global__ void attn_split_rows_kernel(const float* __restrict__ src, int64_t rows, int width, int W,
+                                       uint16_t* __restrict__ planes) {
+  const int64_t n4 = rows * (W / 4), ps = rows * W;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t r = i / (W / 4);
+    const int c = (int)(i % (W / 4)) * 4;
+    float v[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = c + e < width ? src[r * width + c + e] : 0.0f;
+    uint2 p0, p1, p2;
+    asplit3(make_float4(v[0], v[1], v[2], v[3]), p0, p1, p2);
+    *reinterpret_cast<uint2*>(planes + r * W + c) = p0;
+    *reinterpret_cast<uint2*>(planes + ps + r * W + c) = p1;
+    *reinterpret_cast<uint2*>(planes + 2 * ps + r * W + c) = p2;
+  }
+}
+
+// global -> LDS DMA of one 16 B chunk per lane (lane l lands at lds_base + 16 l),
+// issued from asm so that hipcc's waitcnt pass neither sees nor waits on it
+__device__ __forceinline__ void adma16(const void* src, const void* lds_base) {
+  const uint32_t dst = __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>(lds_base));
+  uint32_t keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(src), "s"(dst)
+      : "memory");
+}
+
+// PRE staging: one 32-row block of pre-split planes [3][rows][W] -> LDS
+// [3][32][W] in LAYOUT by LDS-DMA (no VGPRs, no VALU).  The DMA lands
+// lane-linear, so each lane fetches the source chunk whose swizzled position
+// is its destination.  Rows past N re-read row N-1 (finite values whose
+// scores / probabilities the kernels mask to zero).  Completion: the
+// caller's vmcnt(0) + barrier at the top of the block that reads it.
+template <int W, int LAYOUT>
+__device__ __forceinline__ void dma_block(const uint16_t* planes, int64_t ps, int64_t r0, int64_t N, uint16_t* lds,
+                                          int wave, int lane) {
+  constexpr int PL = 32 * W, NI = 3 * PL / 512;
+#pragma unroll
+  for (int j = 0; j < (NI + 3) / 4; ++j) {
+    const int i = wave + 4 * j;
+    if (i < NI) {
+      const int e = i * 512 + lane * 8;
+      const int pl = e / PL, rem = e % PL, r = rem / W, pos = rem % W;
+      int c = pos;
+      if (LAYOUT == PL_HSWZ && W >= 128) c = pos ^ ((r & 3) << 5);
+      if (LAYOUT == PL_SWZ128) c = ((pos >> 3) ^ (((r & 3) << 2) | ((r >> 2) & 3))) << 3;
+      const int64_t row = min<int64_t>(r0 + r, N - 1);
+      adma16(planes + pl * ps + row * W + c, lds + i * 512);
+    }
+  }
+}
+
+template <int DKP, int NT, bool PRE>
 __global__ __launch_bounds__(256) void attn_fwd_x6_kernel(AttnArgs a) {
   constexpr int DV = NT * 32, KC = DKP / 16;
   constexpr int KPL = 32 * DKP, HPL = 32 * DV;  // bf16 per plane
-  __shared__ __attribute__((aligned(16))) uint16_t Kp[3 * KPL];
-  __shared__ __attribute__((aligned(16))) uint16_t Hp[3 * HPL];
+  __shared__ __attribute__((aligned(16))) uint16_t Kp_s[(PRE ? 2 : 1) * 3 * KPL];  // PRE: 2 stages
+  __shared__ __attribute__((aligned(16))) uint16_t Hp_s[(PRE ? 2 : 1) * 3 * HPL];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, h = lane >> 5;
   const int64_t N = a.N, b = blockIdx.y;
   const float* Qb = a.Q + b * N * a.dk;
@@ -471,46 +614,44 @@ __global__ __launch_bounds__(256) void attn_fwd_x6_kernel(AttnArgs a) {
 #pragma unroll
   for (int t = 0; t < NT; ++t) o[t] = zero16();
   float m = -INFINITY, l = 0.0f;
-  Stager<DKP, DKP> sk;
-  Stager<DV, DV> sh;
+  XStage<DKP, DKP, PL_PLAIN, false> sk;
+  XStage<DV, DV, PL_HSWZ, false> sh;
+  const int64_t kps = (int64_t)gridDim.y * N * DKP, hps = (int64_t)gridDim.y * N * DV;
+  const uint16_t* Kpb = a.Kpl + b * N * DKP;
+  const uint16_t* Hpb = a.Hpl + b * N * DV;
   const bool vk = vec_ok(Kb, a.dk), vh = vec_ok(Hb, a.dv);
-  sk.fetch(Kb, 0, N, a.dk, vk, tid);
-  sh.fetch(Hb, 0, N, a.dv, vh, tid);
+  if constexpr (PRE) {
+    dma_block<DKP, PL_PLAIN>(Kpb, kps, 0, N, Kp_s, wave, lane);
+    dma_block<DV, PL_HSWZ>(Hpb, hps, 0, N, Hp_s, wave, lane);
+  } else {
+    sk.fetch(Kb, nullptr, 0, 0, N, a.dk, vk, tid);
+    sh.fetch(Hb, nullptr, 0, 0, N, a.dv, vh, tid);
+  }
   // transposed-read coordinates: group row q' = (lane & 15) >> 2, columns 16 ((lane >> 4) & 1) + 4 (lane & 3)
   const int trq = (lane & 15) >> 2;
   const int trc = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
 
   for (int64_t k0 = 0; k0 < N; k0 += 32) {
-    // split-store the staged K and H block
-#pragma unroll
-    for (int it = 0; it < Stager<DKP, DKP>::PER; ++it) {
-      const int idx = tid + it * 256;
-      if (idx < Stager<DKP, DKP>::NF4) {
-        const int r = idx / (DKP / 4), c = (idx % (DKP / 4)) * 4;
-        uint2 p0, p1, p2;
-        asplit3(sk.reg[it], p0, p1, p2);
-        *reinterpret_cast<uint2*>(&Kp[r * DKP + c]) = p0;
-        *reinterpret_cast<uint2*>(&Kp[KPL + r * DKP + c]) = p1;
-        *reinterpret_cast<uint2*>(&Kp[2 * KPL + r * DKP + c]) = p2;
+    const int stg = PRE ? (int)((k0 >> 5) & 1) : 0;
+    uint16_t* Kp = Kp_s + stg * 3 * KPL;
+    uint16_t* Hp = Hp_s + stg * 3 * HPL;
+    if constexpr (PRE) {
+      // this block's DMA landed (every wave's), and every wave is done with
+      // the other stage (block k0 - 32): refill it with the next block
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (k0 + 32 < N) {
+        dma_block<DKP, PL_PLAIN>(Kpb, kps, k0 + 32, N, Kp_s + (stg ^ 1) * 3 * KPL, wave, lane);
+        dma_block<DV, PL_HSWZ>(Hpb, hps, k0 + 32, N, Hp_s + (stg ^ 1) * 3 * HPL, wave, lane);
       }
-    }
-#pragma unroll
-    for (int it = 0; it < Stager<DV, DV>::PER; ++it) {
-      const int idx = tid + it * 256;
-      if (idx < Stager<DV, DV>::NF4) {
-        const int r = idx / (DV / 4), c = (idx % (DV / 4)) * 4;
-        uint2 p0, p1, p2;
-        asplit3(sh.reg[it], p0, p1, p2);
-        const int off = hswz<DV>(r, c);
-        *reinterpret_cast<uint2*>(&Hp[off]) = p0;
-        *reinterpret_cast<uint2*>(&Hp[HPL + off]) = p1;
-        *reinterpret_cast<uint2*>(&Hp[2 * HPL + off]) = p2;
+    } else {
+      sk.store(Kp, tid);  // the staged K and H block -> bf16 planes
+      sh.store(Hp, tid);
+      __syncthreads();
+      if (k0 + 32 < N) {
+        sk.fetch(Kb, nullptr, 0, k0 + 32, N, a.dk, vk, tid);
+        sh.fetch(Hb, nullptr, 0, k0 + 32, N, a.dv, vh, tid);
       }
-    }
-    __syncthreads();
-    if (k0 + 32 < N) {
-      sk.fetch(Kb, k0 + 32, N, a.dk, vk, tid);
-      sh.fetch(Hb, k0 + 32, N, a.dv, vh, tid);
     }
     // S^T = K Q^T: A = K[key l32][kc*16 + 8h ..], B = Q
     f32x16 s = zero16();
@@ -566,7 +707,7 @@ __global__ __launch_bounds__(256) void attn_fwd_x6_kernel(AttnArgs a) {
         MFMA6(o[t], hp[0], hp[1], hp[2], pp[u][0], pp[u][1], pp[u][2]);
       }
     }
-    __syncthreads();
+    if constexpr (!PRE) __syncthreads();
   }
 
   if (q < N) {
@@ -602,37 +743,12 @@ __global__ __launch_bounds__(256) void attn_fwd_x6_kernel(AttnArgs a) {
 // ds_read_b128 row reads and the ds_read_b64_tr_b16 reads of 4 consecutive
 // rows.  The 32-column planes (K, Q; dk padded with zeros) are read
 // transposed over 4 consecutive rows of 64 B: conflict-free as they lie.
-__device__ __forceinline__ int swz128(int row, int col) {
-  const int sw = ((row & 3) << 2) | ((row >> 2) & 3);
-  return row * 128 + ((((col >> 3) ^ sw)) << 3) + (col & 7);
-}
-
 __device__ __forceinline__ abf16x8_t tr8(const uint16_t* p0, const uint16_t* p1) {
   typedef __attribute__((address_space(3))) ai16x4_t lds_v4;
   const ai16x4_t x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(uintptr_t)(uint32_t)(uintptr_t)p0);
   const ai16x4_t x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(uintptr_t)(uint32_t)(uintptr_t)p1);
   const ai16x8_t v = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
   return __builtin_bit_cast(abf16x8_t, v);
-}
-
-// split-store a staged 32-row block: narrow (row width W <= 32) into
-// [3][32][32] planes, or 128 wide into swizzled [3][32][128] planes
-template <int W, bool WIDE>
-__device__ __forceinline__ void stash_planes(const Stager<W, W>& st, uint16_t* planes, int tid) {
-  constexpr int PL = WIDE ? 32 * 128 : 32 * 32;
-#pragma unroll
-  for (int it = 0; it < Stager<W, W>::PER; ++it) {
-    const int idx = tid + it * 256;
-    if (idx < Stager<W, W>::NF4) {
-      const int r = idx / (W / 4), c = (idx % (W / 4)) * 4;
-      uint2 p0, p1, p2;
-      asplit3(st.reg[it], p0, p1, p2);
-      const int off = WIDE ? swz128(r, c) : r * 32 + c;
-      *reinterpret_cast<uint2*>(&planes[off]) = p0;
-      *reinterpret_cast<uint2*>(&planes[PL + off]) = p1;
-      *reinterpret_cast<uint2*>(&planes[2 * PL + off]) = p2;
-    }
-  }
 }
 
 // lane's own 8-value slices v[c*16 + 8h + j] of a row, split into planes
@@ -659,11 +775,11 @@ __device__ __forceinline__ void reg_planes(const f32x16& x, abf16x8_t (&pl)[2][3
 }
 
 // query-stationary: dQ^T += K^T dS^T
-template <int DKP>
+template <int DKP, bool PRE>
 __global__ __launch_bounds__(256, 2) void attn_bwd_q_x6_kernel(AttnArgs a) {
   constexpr int KC = DKP / 16, FC = 8;  // 128 value columns = 8 chunks of 16
-  __shared__ __attribute__((aligned(16))) uint16_t Kp[3 * 32 * 32];
-  __shared__ __attribute__((aligned(16))) uint16_t Hp[3 * 32 * 128];
+  __shared__ __attribute__((aligned(16))) uint16_t Kp_s[(PRE ? 2 : 1) * 3 * 32 * 32];  // PRE: 2 stages
+  __shared__ __attribute__((aligned(16))) uint16_t Hp_s[(PRE ? 2 : 1) * 3 * 32 * 128];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, h = lane >> 5;
   const int64_t N = a.N, b = blockIdx.y;
   const float* Kb = a.K + b * N * a.dk;
@@ -677,25 +793,46 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_x6_kernel(AttnArgs a) {
   const float il = qv ? 1.0f / a.ssum[b * N + q] : 0.0f;
   const float Dq = qv ? a.Drow[b * N + q] : 0.0f;
   f32x16 dq = zero16();
-  if (DKP < 32)  // zero pad columns of the K planes, never written by the staging
+  if (!PRE && DKP < 32)  // zero pad columns of the K planes, never written by the staging
     for (int i = tid; i < 3 * 32 * (32 - DKP); i += 256) {
       const int pl = i / (32 * (32 - DKP)), rc = i % (32 * (32 - DKP));
-      Kp[pl * 1024 + (rc / (32 - DKP)) * 32 + DKP + rc % (32 - DKP)] = 0;
+      Kp_s[pl * 1024 + (rc / (32 - DKP)) * 32 + DKP + rc % (32 - DKP)] = 0;
     }
-  Stager<DKP, DKP> sk;
-  Stager<128, 128> sh;
+  XStage<DKP, 32, PL_PLAIN, false> sk;
+  XStage<128, 128, PL_SWZ128, false> sh;
+  // PRE planes: K split 32 wide (zero columns >= dk), H 128 wide
+  const int64_t kps = (int64_t)gridDim.y * N * 32, hps = (int64_t)gridDim.y * N * 128;
+  const uint16_t* Kpb = a.Kpl + b * N * 32;
+  const uint16_t* Hpb = a.Hpl + b * N * 128;
   const bool vk = vec_ok(Kb, a.dk), vh = vec_ok(Hb, a.dv);
-  sk.fetch(Kb, 0, N, a.dk, vk, tid);
-  sh.fetch(Hb, 0, N, a.dv, vh, tid);
+  if constexpr (PRE) {
+    dma_block<32, PL_PLAIN>(Kpb, kps, 0, N, Kp_s, wave, lane);
+    dma_block<128, PL_SWZ128>(Hpb, hps, 0, N, Hp_s, wave, lane);
+  } else {
+    sk.fetch(Kb, nullptr, 0, 0, N, a.dk, vk, tid);
+    sh.fetch(Hb, nullptr, 0, 0, N, a.dv, vh, tid);
+  }
   const int trq = (lane & 15) >> 2, trc = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
 
   for (int64_t k0 = 0; k0 < N; k0 += 32) {
-    stash_planes<DKP, false>(sk, Kp, tid);
-    stash_planes<128, true>(sh, Hp, tid);
-    __syncthreads();
-    if (k0 + 32 < N) {
-      sk.fetch(Kb, k0 + 32, N, a.dk, vk, tid);
-      sh.fetch(Hb, k0 + 32, N, a.dv, vh, tid);
+    const int stg = PRE ? (int)((k0 >> 5) & 1) : 0;
+    uint16_t* Kp = Kp_s + stg * 3 * 1024;
+    uint16_t* Hp = Hp_s + stg * 3 * 4096;
+    if constexpr (PRE) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (k0 + 32 < N) {
+        dma_block<32, PL_PLAIN>(Kpb, kps, k0 + 32, N, Kp_s + (stg ^ 1) * 3 * 1024, wave, lane);
+        dma_block<128, PL_SWZ128>(Hpb, hps, k0 + 32, N, Hp_s + (stg ^ 1) * 3 * 4096, wave, lane);
+      }
+    } else {
+      sk.store(Kp, tid);
+      sh.store(Hp, tid);
+      __syncthreads();
+      if (k0 + 32 < N) {
+        sk.fetch(Kb, nullptr, 0, k0 + 32, N, a.dk, vk, tid);
+        sh.fetch(Hb, nullptr, 0, k0 + 32, N, a.dv, vh, tid);
+      }
     }
     f32x16 s = zero16();
 #pragma unroll
@@ -730,7 +867,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_x6_kernel(AttnArgs a) {
       for (int pl = 0; pl < 3; ++pl) kt[pl] = tr8(&Kp[pl * 1024 + r0 * 32 + trc], &Kp[pl * 1024 + r1 * 32 + trc]);
       MFMA6(dq, kt[0], kt[1], kt[2], dsp[u][0], dsp[u][1], dsp[u][2]);
     }
-    __syncthreads();
+    if constexpr (!PRE) __syncthreads();
   }
   if (qv) {
 #pragma unroll
@@ -742,12 +879,12 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_x6_kernel(AttnArgs a) {
 }
 
 // key-stationary.  WANT_H: dH^T += dO^T P;  else dK^T += Q^T dS (needs dP)
-template <int DKP, bool WANT_H>
+template <int DKP, bool WANT_H, bool PRE>
 __global__ __launch_bounds__(256, 2) void attn_bwd_kv_x6_kernel(AttnArgs a) {
   constexpr int KC = DKP / 16, FC = 8;
-  __shared__ __attribute__((aligned(16))) uint16_t Qp[3 * 32 * 32];
-  __shared__ __attribute__((aligned(16))) uint16_t Op[3 * 32 * 128];
-  __shared__ float Ms[32], Ls[32], Ds[32];
+  __shared__ __attribute__((aligned(16))) uint16_t Qp_s[(PRE ? 2 : 1) * 3 * 32 * 32];  // PRE: 2 stages
+  __shared__ __attribute__((aligned(16))) uint16_t Op_s[(PRE ? 2 : 1) * 3 * 32 * 128];
+  __shared__ float Ms_s[(PRE ? 2 : 1) * 32], Ls_s[(PRE ? 2 : 1) * 32], Ds_s[(PRE ? 2 : 1) * 32];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, h = lane >> 5;
   const int64_t N = a.N, b = blockIdx.y;
   const float* Qb = a.Q + b * N * a.dk;
@@ -761,13 +898,16 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_x6_kernel(AttnArgs a) {
   f32x16 acc[WANT_H ? 4 : 1];
 #pragma unroll
   for (int t = 0; t < (WANT_H ? 4 : 1); ++t) acc[t] = zero16();
-  if (DKP < 32)
+  if (!PRE && DKP < 32)
     for (int i = tid; i < 3 * 32 * (32 - DKP); i += 256) {
       const int pl = i / (32 * (32 - DKP)), rc = i % (32 * (32 - DKP));
-      Qp[pl * 1024 + (rc / (32 - DKP)) * 32 + DKP + rc % (32 - DKP)] = 0;
+      Qp_s[pl * 1024 + (rc / (32 - DKP)) * 32 + DKP + rc % (32 - DKP)] = 0;
     }
-  Stager<DKP, DKP> sq;
-  Stager<128, 128> so;
+  XStage<DKP, 32, PL_PLAIN, false> sq;
+  XStage<128, 128, PL_SWZ128, false> so;
+  const int64_t qps = (int64_t)gridDim.y * N * 32, ops = (int64_t)gridDim.y * N * 128;
+  const uint16_t* Qpb = a.Qpl + b * N * 32;
+  const uint16_t* Opb = a.Opl + b * N * 128;
   const bool vq = vec_ok(Qb, a.dk), vo = vec_ok(dOb, a.dv);
   float pm = 0.0f, pl_ = 0.0f, pd = 0.0f;
   auto fetch_stats = [&](int64_t q0) {
@@ -779,23 +919,42 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_x6_kernel(AttnArgs a) {
       pd = v ? a.Drow[b * N + qq] : 0.0f;
     }
   };
-  sq.fetch(Qb, 0, N, a.dk, vq, tid);
-  so.fetch(dOb, 0, N, a.dv, vo, tid);
+  if constexpr (PRE) {
+    dma_block<32, PL_PLAIN>(Qpb, qps, 0, N, Qp_s, wave, lane);
+    dma_block<128, PL_SWZ128>(Opb, ops, 0, N, Op_s, wave, lane);
+  } else {
+    sq.fetch(Qb, nullptr, 0, 0, N, a.dk, vq, tid);
+    so.fetch(dOb, nullptr, 0, 0, N, a.dv, vo, tid);
+  }
   fetch_stats(0);
   const int trq = (lane & 15) >> 2, trc = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
 
   for (int64_t q0 = 0; q0 < N; q0 += 32) {
-    stash_planes<DKP, false>(sq, Qp, tid);
-    stash_planes<128, true>(so, Op, tid);
+    const int stg = PRE ? (int)((q0 >> 5) & 1) : 0;
+    uint16_t* Qp = Qp_s + stg * 3 * 1024;
+    uint16_t* Op = Op_s + stg * 3 * 4096;
+    float* Ms = Ms_s + stg * 32;
+    float* Ls = Ls_s + stg * 32;
+    float* Ds = Ds_s + stg * 32;
+    if (!PRE) {
+      sq.store(Qp, tid);
+      so.store(Op, tid);
+    }
     if (tid < 32) {
       Ms[tid] = pm;
       Ls[tid] = pl_;
       Ds[tid] = pd;
     }
+    if constexpr (PRE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (q0 + 32 < N) {
-      sq.fetch(Qb, q0 + 32, N, a.dk, vq, tid);
-      so.fetch(dOb, q0 + 32, N, a.dv, vo, tid);
+      if constexpr (PRE) {
+        dma_block<32, PL_PLAIN>(Qpb, qps, q0 + 32, N, Qp_s + (stg ^ 1) * 3 * 1024, wave, lane);
+        dma_block<128, PL_SWZ128>(Opb, ops, q0 + 32, N, Op_s + (stg ^ 1) * 3 * 4096, wave, lane);
+      } else {
+        sq.fetch(Qb, nullptr, 0, q0 + 32, N, a.dk, vq, tid);
+        so.fetch(dOb, nullptr, 0, q0 + 32, N, a.dv, vo, tid);
+      }
       fetch_stats(q0 + 32);
     }
     // S[query][key]: lanes = keys, registers = queries kappa(r, h)
@@ -854,7 +1013,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_x6_kernel(AttnArgs a) {
         MFMA6(acc[0], qt[0], qt[1], qt[2], dsp[u][0], dsp[u][1], dsp[u][2]);
       }
     }
-    __syncthreads();
+    if constexpr (!PRE) __syncthreads();
   }
   if (kv) {
     if (WANT_H) {
@@ -890,38 +1049,75 @@ bool attn_x6_enabled() {
 template <int DKP, int NT>
 int launch_attn(AttnPass pass, const AttnArgs& a, int64_t B, hipStream_t st) {
   const dim3 grid((unsigned)ceil_div(a.N, 128), (unsigned)B);
-  if (pass == PASS_FWD && attn_x6_enabled())
-    hipLaunchKernelGGL((attn_fwd_x6_kernel<DKP, NT>), grid, dim3(256), 0, st, a);
-  else if (pass == PASS_FWD)
+  const bool pre = pass == PASS_BWD_KV ? (a.Qpl && a.Opl) : (a.Kpl && a.Hpl);
+  if (pass == PASS_FWD && attn_x6_enabled()) {
+    if (pre)
+      hipLaunchKernelGGL((attn_fwd_x6_kernel<DKP, NT, true>), grid, dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL((attn_fwd_x6_kernel<DKP, NT, false>), grid, dim3(256), 0, st, a);
+  } else if (pass == PASS_FWD) {
     hipLaunchKernelGGL((attn_fwd_kernel<DKP, NT>), grid, dim3(256), 0, st, a);
-  else if (NT == 4 && attn_x6_enabled()) {  // backward x6: dv in (96, 128]
+  } else if (NT == 4 && attn_x6_enabled()) {  // backward x6: dv in (96, 128]
     if (pass == PASS_BWD_Q) {
-      hipLaunchKernelGGL((attn_bwd_q_x6_kernel<DKP>), grid, dim3(256), 0, st, a);
-    } else {
-      hipLaunchKernelGGL((attn_bwd_kv_x6_kernel<DKP, true>), grid, dim3(256), 0, st, a);
+      if (pre)
+        hipLaunchKernelGGL((attn_bwd_q_x6_kernel<DKP, true>), grid, dim3(256), 0, st, a);
+      else
+        hipLaunchKernelGGL((attn_bwd_q_x6_kernel<DKP, false>), grid, dim3(256), 0, st, a);
+    } else if (pre) {
+      hipLaunchKernelGGL((attn_bwd_kv_x6_kernel<DKP, true, true>), grid, dim3(256), 0, st, a);
       GRL_LAUNCH_CHECK();
-      hipLaunchKernelGGL((attn_bwd_kv_x6_kernel<DKP, false>), grid, dim3(256), 0, st, a);
+      hipLaunchKernelGGL((attn_bwd_kv_x6_kernel<DKP, false, true>), grid, dim3(256), 0, st, a);
+    } else {
+      hipLaunchKernelGGL((attn_bwd_kv_x6_kernel<DKP, true, false>), grid, dim3(256), 0, st, a);
+      GRL_LAUNCH_CHECK();
+      hipLaunchKernelGGL((attn_bwd_kv_x6_kernel<DKP, false, false>), grid, dim3(256), 0, st, a);
     }
-  } else if (pass == PASS_BWD_Q)
+  } else if (pass == PASS_BWD_Q) {
     hipLaunchKernelGGL((attn_bwd_q_kernel<DKP, NT>), grid, dim3(256), 0, st, a);
-  else
+  } else {
     hipLaunchKernelGGL((attn_bwd_kv_kernel<DKP, NT>), grid, dim3(256), 0, st, a);
+  }
   GRL_LAUNCH_CHECK();
   return GRL_OK;
 }
 
+int attn_dkp(int dk) { return dk <= 16 ? 16 : 32; }
+int attn_dvp(int dv) {
+  const int nt = (int)ceil_div(dv, 32);
+  return 32 * (nt <= 1 ? 1 : nt <= 2 ? 2 : nt <= 4 ? 4 : 8);
+}
+
 template <int DKP>
 int dispatch_nt(AttnPass pass, const AttnArgs& a, int64_t B, hipStream_t st) {
-  const int nt = (int)ceil_div(a.dv, 32);
-  if (nt <= 1) return launch_attn<DKP, 1>(pass, a, B, st);
-  if (nt <= 2) return launch_attn<DKP, 2>(pass, a, B, st);
-  if (nt <= 4) return launch_attn<DKP, 4>(pass, a, B, st);
+  const int nt = attn_dvp(a.dv) / 32;
+  if (nt == 1) return launch_attn<DKP, 1>(pass, a, B, st);
+  if (nt == 2) return launch_attn<DKP, 2>(pass, a, B, st);
+  if (nt == 4) return launch_attn<DKP, 4>(pass, a, B, st);
   return launch_attn<DKP, 8>(pass, a, B, st);
 }
 
 int dispatch(AttnPass pass, const AttnArgs& a, int64_t B, hipStream_t st) {
   if (a.N == 0 || B == 0) return GRL_OK;
   return a.dk <= 16 ? dispatch_nt<16>(pass, a, B, st) : dispatch_nt<32>(pass, a, B, st);
+}
+
+// Workspace of the PRE staging: bf16 planes [3][B*N][W] of K, H (forward and
+// backward) and Q, dO (backward), each section 256-B aligned
+size_t attn_plane_bytes(int64_t rows, int W) { return ((size_t)3 * rows * W * 2 + 255) / 256 * 256; }
+
+// Split `src` [rows][width] into planes at *cursor (advanced); false when
+// the workspace is too small (the caller then runs the in-kernel split)
+bool attn_split(const float* src, int64_t rows, int width, int W, unsigned char*& cursor, const unsigned char* end,
+                const uint16_t** out, hipStream_t st) {
+  const size_t need = attn_plane_bytes(rows, W);
+  if (!src || cursor + need > end) return false;
+  uint16_t* planes = reinterpret_cast<uint16_t*>(cursor);
+  const int64_t n4 = rows * (W / 4);
+  hipLaunchKernelGGL(attn_split_rows_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(n4, 256), 8192)), dim3(256),
+                     0, st, src, rows, width, W, planes);
+  cursor += need;
+  *out = planes;
+  return true;
 }
 
 int check_dims(const char* who, int64_t B, int64_t N, int dk, int dv) {
@@ -939,9 +1135,16 @@ int check_dims(const char* who, int64_t B, int64_t N, int dk, int dv) {
 
 using namespace grl;
 
+extern "C" size_t grl_node_attention_workspace_size(int64_t B, int64_t N, int32_t dk, int32_t dv) {
+  if (B <= 0 || N <= 0 || dk < 0 || dk > 32 || dv < 1 || dv > 256) return 0;
+  const int64_t rows = B * N;
+  return 2 * attn_plane_bytes(rows, 32) + 2 * attn_plane_bytes(rows, attn_dvp(dv)) + 256;
+}
+
 extern "C" int grl_node_attention_fwd(const float* Q, const float* K, const float* H, const float* V,
                                       const float* gamma, float* out, float* o_norm, float* row_max, float* row_sum,
-                                      int64_t B, int64_t N, int32_t dk, int32_t dv, grl_stream_t stream) {
+                                      int64_t B, int64_t N, int32_t dk, int32_t dv, void* workspace,
+                                      size_t workspace_bytes, grl_stream_t stream) {
   int rc = check_dims("grl_node_attention_fwd", B, N, dk, dv);
   if (rc) return rc;
   if (B == 0 || N == 0) return GRL_OK;
@@ -960,13 +1163,25 @@ extern "C" int grl_node_attention_fwd(const float* Q, const float* K, const floa
   a.N = N;
   a.dk = dk;
   a.dv = dv;
-  return dispatch(PASS_FWD, a, B, as_stream(stream));
+  hipStream_t st = as_stream(stream);
+  if (workspace && attn_x6_enabled()) {  // split K and H once for every query block
+    unsigned char* cur = reinterpret_cast<unsigned char*>((reinterpret_cast<uintptr_t>(workspace) + 255) & ~(uintptr_t)255);
+    const unsigned char* end = static_cast<unsigned char*>(workspace) + workspace_bytes;
+    const uint16_t *kp = nullptr, *hp = nullptr;
+    if (attn_split(K, B * N, dk, attn_dkp(dk), cur, end, &kp, st) &&
+        attn_split(H, B * N, dv, attn_dvp(dv), cur, end, &hp, st)) {
+      a.Kpl = kp;
+      a.Hpl = hp;
+    }
+    GRL_LAUNCH_CHECK();
+  }
+  return dispatch(PASS_FWD, a, B, st);
 }
 
 extern "C" int grl_node_attention_bwd(const float* Q, const float* K, const float* H, const float* dO,
                                       const float* row_max, const float* row_sum, const float* D, float* dQ,
                                       float* dK, float* dH, int64_t B, int64_t N, int32_t dk, int32_t dv,
-                                      grl_stream_t stream) {
+                                      void* workspace, size_t workspace_bytes, grl_stream_t stream) {
   int rc = check_dims("grl_node_attention_bwd", B, N, dk, dv);
   if (rc) return rc;
   if (B == 0 || N == 0) return GRL_OK;
@@ -987,6 +1202,19 @@ extern "C" int grl_node_attention_bwd(const float* Q, const float* K, const floa
   a.dk = dk;
   a.dv = dv;
   hipStream_t st = as_stream(stream);
+  if (workspace && attn_x6_enabled() && attn_dvp(dv) == 128) {  // the x6 backward's operands, split once
+    unsigned char* cur = reinterpret_cast<unsigned char*>((reinterpret_cast<uintptr_t>(workspace) + 255) & ~(uintptr_t)255);
+    const unsigned char* end = static_cast<unsigned char*>(workspace) + workspace_bytes;
+    const uint16_t *kp = nullptr, *hp = nullptr, *qp = nullptr, *op = nullptr;
+    if (attn_split(K, B * N, dk, 32, cur, end, &kp, st) && attn_split(H, B * N, dv, 128, cur, end, &hp, st) &&
+        attn_split(Q, B * N, dk, 32, cur, end, &qp, st) && attn_split(dO, B * N, dv, 128, cur, end, &op, st)) {
+      a.Kpl = kp;
+      a.Hpl = hp;
+      a.Qpl = qp;
+      a.Opl = op;
+    }
+    GRL_LAUNCH_CHECK();
+  }
   rc = dispatch(PASS_BWD_Q, a, B, st);
   if (rc) return rc;
   return dispatch(PASS_BWD_KV, a, B, st);

@@ -143,10 +143,11 @@ SIGNATURES = {
     "grl_split_plan_count": (_c_i32, [_c_vp, _c_i64, _c_i32, _c_i32, _c_i32, _c_vp, _c_vp, _c_size, _c_vp]),
     "grl_split_plan_build": (_c_i32, [_c_vp, _c_i64, _c_i32, _P(GrlSplitPlan), _c_vp, _c_size, _c_vp]),
     "grl_bag_linear_fwd": (_c_i32, [_c_vp, _c_i64, _c_i64, _c_i32, _c_vp, _c_i32, _c_vp, _c_i32, _c_vp, _c_vp]),
+    "grl_node_attention_workspace_size": (_c_size, [_c_i64, _c_i64, _c_i32, _c_i32]),
     "grl_node_attention_fwd": (_c_i32, [_c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_i64,
-                                        _c_i32, _c_i32, _c_vp]),
+                                        _c_i32, _c_i32, _c_vp, _c_size, _c_vp]),
     "grl_node_attention_bwd": (_c_i32, [_c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_i64,
-                                        _c_i64, _c_i32, _c_i32, _c_vp]),
+                                        _c_i64, _c_i32, _c_i32, _c_vp, _c_size, _c_vp]),
     "grl_layout_graph_size": (_c_i32, [_c_vp, _c_i32, _c_vp]),
     "grl_layout_graph_dense": (_c_i32, [_c_vp, _c_i32, _c_i32, _c_i32, _c_vp]),
     "grl_layout_graph_edges": (_c_i32, [_c_vp, _c_i32, _c_i32, _c_vp, _c_i64, _c_vp]),

@@ -218,6 +218,12 @@ def _attn_check(Q, K, H, V, gamma):
                             f"V {tuple(V.shape)}, gamma {tuple(gamma.shape)}")
 
 
+def _attn_workspace(B, N, dk, dv, device):
+    """bf16 planes of the attention operands, split once per call (grl.h)."""
+    n = _lib.lib().grl_node_attention_workspace_size(B, N, dk, dv)
+    return (torch.empty(n, dtype=torch.uint8, device=device), n) if n else (None, 0)
+
+
 def node_attention_forward(Q, K, H, V, gamma, stats: bool = False):
     """out = gamma * softmax(Q K^T) H + V (robust_gcn.py:90-96), fused.
     stats=True also returns (o_norm, row_max, row_sum) for the backward."""
@@ -230,8 +236,10 @@ def node_attention_forward(Q, K, H, V, gamma, stats: bool = False):
     rmax = torch.empty(B, N, device=V.device) if stats else None
     rsum = torch.empty(B, N, device=V.device) if stats else None
     ptr = (lambda t: t.data_ptr() if t is not None else None)  # noqa: E731
+    ws, ws_bytes = _attn_workspace(B, N, dk, dv, V.device)
     call("grl_node_attention_fwd", Q.data_ptr(), K.data_ptr(), H.data_ptr(), V.data_ptr(), gamma.data_ptr(),
-         out.data_ptr(), ptr(onorm), ptr(rmax), ptr(rsum), B, N, dk, dv, current_stream_handle(V.device))
+         out.data_ptr(), ptr(onorm), ptr(rmax), ptr(rsum), B, N, dk, dv, ptr(ws), ws_bytes,
+         current_stream_handle(V.device))
     return (out, onorm, rmax, rsum) if stats else out
 
 
@@ -251,9 +259,10 @@ class _NodeAttention(torch.autograd.Function):
         dO = dout * gamma
         D = (dO * onorm).sum(-1).contiguous()
         dQ, dK, dH = torch.empty_like(Q), torch.empty_like(K), torch.empty_like(H)
+        ws, ws_bytes = _attn_workspace(B, N, dk, dv, Q.device)
         call("grl_node_attention_bwd", Q.data_ptr(), K.data_ptr(), H.data_ptr(), dO.data_ptr(), rmax.data_ptr(),
              rsum.data_ptr(), D.data_ptr(), dQ.data_ptr(), dK.data_ptr(), dH.data_ptr(), B, N, dk, dv,
-             current_stream_handle(Q.device))
+             ws.data_ptr() if ws is not None else None, ws_bytes, current_stream_handle(Q.device))
         dgamma = (dout * onorm).sum((0, 1))
         return dQ, dK, dH, dout, dgamma
 

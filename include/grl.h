@@ -239,11 +239,19 @@ int grl_bag_linear_fwd(const float* V, int64_t ldv, int64_t M, int32_t K,
  * (input_dim // 8; 0 = uniform attention, Q/K may then be NULL), dv in
  * [1, 256].  For training pass o_norm [B, N, dv]
  * (= softmax(QK^T) H) and row_max/row_sum [B, N] (the softmax statistics);
- * NULL otherwise.                                                           */
+ * NULL otherwise.
+ * fp32-accurate on the bf16 matrix cores (each fp32 value split exactly into
+ * three bf16 parts, six partial products; GRL_ATTN_X6=0 selects the
+ * fp32-MFMA kernels).  `workspace` (grl_node_attention_workspace_size bytes,
+ * or NULL) holds the once-per-call bf16 splits of K and H (backward: also Q
+ * and dO); NULL or too small makes every workgroup split its own blocks.   */
+size_t grl_node_attention_workspace_size(int64_t B, int64_t N, int32_t dk,
+                                         int32_t dv);
 int grl_node_attention_fwd(const float* Q, const float* K, const float* H,
                            const float* V, const float* gamma, float* out,
                            float* o_norm, float* row_max, float* row_sum,
                            int64_t B, int64_t N, int32_t dk, int32_t dv,
+                           void* workspace, size_t workspace_bytes,
                            grl_stream_t stream);
 
 /* Backward of the attention core.  dO = gamma * d_out [B, N, dv] and
@@ -256,7 +264,8 @@ int grl_node_attention_bwd(const float* Q, const float* K, const float* H,
                            const float* dO, const float* row_max,
                            const float* row_sum, const float* D, float* dQ,
                            float* dK, float* dH, int64_t B, int64_t N,
-                           int32_t dk, int32_t dv, grl_stream_t stream);
+                           int32_t dk, int32_t dv, void* workspace,
+                           size_t workspace_bytes, grl_stream_t stream);
 
 /* ---------------------------------------------------------------------- */
 /* Graph formats                                                           */

@@ -32,20 +32,34 @@ SHAPES = [(1, 74, 16, 128), (4, 74, 16, 128), (2, 33, 4, 32), (1, 1, 2, 16), (3,
           (2, 64, 5, 40), (1, 500, 16, 100), (2, 9, 0, 4)]  # dk = 0: net_size 8 (4 // 8), uniform attention
 
 
-@pytest.mark.parametrize("x6", ["1", "0"])  # split-bf16 kernels (default) / fp32-MFMA kernels
+MODES = ["x6", "x6-no-workspace", "f32"]
+
+
+def _set_mode(mode, monkeypatch):
+    """x6: split-bf16 kernels with the once-per-call operand planes (default);
+    x6-no-workspace: the same kernels splitting every block themselves;
+    f32: the fp32-MFMA kernels (GRL_ATTN_X6=0)."""
+    import grl.ops
+
+    monkeypatch.setenv("GRL_ATTN_X6", "0" if mode == "f32" else "1")
+    if mode == "x6-no-workspace":
+        monkeypatch.setattr(grl.ops, "_attn_workspace", lambda *a: (None, 0))
+
+
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("B,N,dk,dv", SHAPES)
-def test_forward_matches_fp64(B, N, dk, dv, x6, monkeypatch):
-    monkeypatch.setenv("GRL_ATTN_X6", x6)
+def test_forward_matches_fp64(B, N, dk, dv, mode, monkeypatch):
+    _set_mode(mode, monkeypatch)
     Q, K, H, V, gamma = _inputs(B, N, dk, dv, seed=N + dk)
     out = node_attention_forward(Q, K, H, V, gamma)
     ref = _ref(*(t.double() for t in (Q, K, H, V, gamma)))
     torch.testing.assert_close(out.double(), ref, rtol=1e-5, atol=1e-5)
 
 
-@pytest.mark.parametrize("x6", ["1", "0"])
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("B,N,dk,dv", SHAPES)
-def test_backward_matches_fp64(B, N, dk, dv, x6, monkeypatch):
-    monkeypatch.setenv("GRL_ATTN_X6", x6)
+def test_backward_matches_fp64(B, N, dk, dv, mode, monkeypatch):
+    _set_mode(mode, monkeypatch)
     Q, K, H, V, gamma = _inputs(B, N, dk, dv, seed=7 * N + dv)
     leaves = [t.clone().requires_grad_(True) for t in (Q, K, H, V, gamma)]
     out = node_self_attention(*leaves)
