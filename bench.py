@@ -86,7 +86,8 @@ def main():
         print(json.dumps({"c1_debug_json": c1_extras(dev, max(3, args.steps))}), flush=True)
         return
     if args.only == "model":
-        print(json.dumps({"model_one_graph_100k": model_extras(dev)}), flush=True)
+        print(json.dumps({"model_one_graph_100k": model_extras(dev),
+                          "model_dense_A_mid_n": model_mid_extras(dev)}), flush=True)
         return
 
     from grl import DropEdge
@@ -202,6 +203,7 @@ def main():
             torch.cuda.empty_cache()  # C1 is a small-graph workload: time it without C3's 8 GB resident
             out["extras"]["c1_debug_json"] = c1_extras(dev)
             out["extras"]["model_one_graph_100k"] = model_extras(dev)
+            out["extras"]["model_dense_A_mid_n"] = model_mid_extras(dev)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -454,6 +456,37 @@ def model_extras(dev, N=100_000, avg_deg=16.0, iters=3):
     tr = _time(step, iters)
     return {"nodes": N, "typed_edges": g.nnz, "eval_ms": ev, "train_step_ms": tr,
             "note": "one graph, B=1; reference dense A_pre would need 280 GB"}
+
+
+def model_mid_extras(dev, sizes=(512, 2048, 4096), iters=5):
+    """BASELINE.md §2's orientation row "train fwd+bwd, B=1, random A (~3
+    edges/node), N = 512 / 2048 / 4096" -- 0.16 s / 1.7-3.0 s / 9.2 s for the
+    reference on an 8-core CPU -- through the drop-in: the same dense
+    (B, N, 6, N) A the collate produces, GraphCNNDropEdge(4369, 53, 6, 256) in
+    train mode (DropEdge and dropout active), cross-entropy, backward."""
+    from gnn.models import GraphCNNDropEdge
+
+    out = {}
+    torch.manual_seed(0)
+    model = GraphCNNDropEdge(4369, 53, 6, 256).to(dev)
+    model.train()
+    lossf = torch.nn.CrossEntropyLoss()
+    ref = {512: "0.16 s", 2048: "1.7-3.0 s", 4096: "9.2 s"}
+    for N in sizes:
+        gen = torch.Generator(device=dev).manual_seed(N)
+        A = (torch.rand(1, N, 6, N, generator=gen, device=dev) < 3.0 / (6 * N)).float()
+        V = torch.zeros(1, N, 4369, device=dev)
+        V[0].scatter_(1, torch.randint(0, 4365, (N, 7), generator=gen, device=dev), 1.0)
+        y = torch.randint(0, 53, (1, N), generator=gen, device=dev)
+
+        def step():
+            model.zero_grad(set_to_none=True)
+            lossf(model.forward([V, A]).reshape(-1, 53), y.reshape(-1)).backward()
+
+        out[f"N{N}"] = {"train_fwd_bwd_ms": _time(step, iters, warm=2), "typed_edges": int(A.sum()),
+                        "reference_cpu_orientation": ref.get(N)}
+        del A, V
+    return out
 
 
 def run_only(args, graph, X_full, gather, spmm, L, F):

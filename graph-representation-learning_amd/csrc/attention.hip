@@ -55,6 +55,10 @@ struct AttnArgs {
   const uint16_t* Hpl;  // W = DV
   const uint16_t* Qpl;  // W = DKP
   const uint16_t* Opl;  // W = DV (dO)
+  // key / query split (small N): keys per split, and partial slabs (or NULL)
+  int64_t kr;
+  float* part;   // fwd: o [S][B*N][dv] + m, l [S][B*N]; bwd_q: dQ [S][B*N][dk]; bwd_kv: dH [S][B*N][dv]
+  float* part2;  // bwd_kv: dK [S][B*N][dk]
   int64_t N;
   int dk, dv;
 };
@@ -569,11 +573,12 @@ template <int W, int LAYOUT>
 __device__ __forceinline__ void dma_block(const uint16_t* planes, int64_t ps, int64_t r0, int64_t N, uint16_t* lds,
                                           int wave, int lane) {
   constexpr int PL = 32 * W, NI = 3 * PL / 512;
+  const int ln = lane;
 #pragma unroll
   for (int j = 0; j < (NI + 3) / 4; ++j) {
     const int i = wave + 4 * j;
     if (i < NI) {
-      const int e = i * 512 + lane * 8;
+      const int e = i * 512 + ln * 8;
       const int pl = e / PL, rem = e % PL, r = rem / W, pos = rem % W;
       int c = pos;
       if (LAYOUT == PL_HSWZ && W >= 128) c = pos ^ ((r & 3) << 5);
@@ -584,7 +589,7 @@ __device__ __forceinline__ void dma_block(const uint16_t* planes, int64_t ps, in
   }
 }
 
-template <int DKP, int NT, bool PRE>
+template <int DKP, int NT, bool PRE, bool SPLIT>
 __global__ __launch_bounds__(256) void attn_fwd_x6_kernel(AttnArgs a) {
   constexpr int DV = NT * 32, KC = DKP / 16;
   constexpr int KPL = 32 * DKP, HPL = 32 * DV;  // bf16 per plane
@@ -596,6 +601,8 @@ __global__ __launch_bounds__(256) void attn_fwd_x6_kernel(AttnArgs a) {
   const float* Kb = a.K + b * N * a.dk;
   const float* Hb = a.H + b * N * a.dv;
   const int64_t q = (int64_t)blockIdx.x * 128 + wave * 32 + l32;
+  // key split blockIdx.z covers keys [k_lo, k_hi) (the whole range when unsplit)
+  const int64_t k_lo = SPLIT ? (int64_t)blockIdx.z * a.kr : 0, k_hi = SPLIT ? min<int64_t>(N, k_lo + a.kr) : N;
 
   // this lane's query, dims kc*16 + 8h + 0..7, split into three planes
   abf16x8_t qp[KC][3];
@@ -621,18 +628,18 @@ __global__ __launch_bounds__(256) void attn_fwd_x6_kernel(AttnArgs a) {
   const uint16_t* Hpb = a.Hpl + b * N * DV;
   const bool vk = vec_ok(Kb, a.dk), vh = vec_ok(Hb, a.dv);
   if constexpr (PRE) {
-    dma_block<DKP, PL_PLAIN>(Kpb, kps, 0, N, Kp_s, wave, lane);
-    dma_block<DV, PL_HSWZ>(Hpb, hps, 0, N, Hp_s, wave, lane);
+    dma_block<DKP, PL_PLAIN>(Kpb, kps, k_lo, N, Kp_s, wave, lane);
+    dma_block<DV, PL_HSWZ>(Hpb, hps, k_lo, N, Hp_s, wave, lane);
   } else {
-    sk.fetch(Kb, nullptr, 0, 0, N, a.dk, vk, tid);
-    sh.fetch(Hb, nullptr, 0, 0, N, a.dv, vh, tid);
+    sk.fetch(Kb, nullptr, 0, k_lo, N, a.dk, vk, tid);
+    sh.fetch(Hb, nullptr, 0, k_lo, N, a.dv, vh, tid);
   }
   // transposed-read coordinates: group row q' = (lane & 15) >> 2, columns 16 ((lane >> 4) & 1) + 4 (lane & 3)
   const int trq = (lane & 15) >> 2;
   const int trc = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
 
-  for (int64_t k0 = 0; k0 < N; k0 += 32) {
-    const int stg = PRE ? (int)((k0 >> 5) & 1) : 0;
+  for (int64_t k0 = k_lo; k0 < k_hi; k0 += 32) {
+    const int stg = PRE ? (int)(((k0 - k_lo) >> 5) & 1) : 0;
     uint16_t* Kp = Kp_s + stg * 3 * KPL;
     uint16_t* Hp = Hp_s + stg * 3 * HPL;
     if constexpr (PRE) {
@@ -640,7 +647,7 @@ __global__ __launch_bounds__(256) void attn_fwd_x6_kernel(AttnArgs a) {
       // the other stage (block k0 - 32): refill it with the next block
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (k0 + 32 < N) {
+      if (k0 + 32 < k_hi) {
         dma_block<DKP, PL_PLAIN>(Kpb, kps, k0 + 32, N, Kp_s + (stg ^ 1) * 3 * KPL, wave, lane);
         dma_block<DV, PL_HSWZ>(Hpb, hps, k0 + 32, N, Hp_s + (stg ^ 1) * 3 * HPL, wave, lane);
       }
@@ -648,7 +655,7 @@ __global__ __launch_bounds__(256) void attn_fwd_x6_kernel(AttnArgs a) {
       sk.store(Kp, tid);  // the staged K and H block -> bf16 planes
       sh.store(Hp, tid);
       __syncthreads();
-      if (k0 + 32 < N) {
+      if (k0 + 32 < k_hi) {
         sk.fetch(Kb, nullptr, 0, k0 + 32, N, a.dk, vk, tid);
         sh.fetch(Hb, nullptr, 0, k0 + 32, N, a.dv, vh, tid);
       }
@@ -666,7 +673,7 @@ __global__ __launch_bounds__(256) void attn_fwd_x6_kernel(AttnArgs a) {
     float mx = -INFINITY;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      if (k0 + kappa(r, h) >= N) s[r] = -INFINITY;
+      if (k0 + kappa(r, h) >= k_hi) s[r] = -INFINITY;
       mx = fmaxf(mx, s[r]);
     }
     mx = fmaxf(mx, __shfl_xor(mx, 32));
@@ -710,7 +717,22 @@ __global__ __launch_bounds__(256) void attn_fwd_x6_kernel(AttnArgs a) {
     if constexpr (!PRE) __syncthreads();
   }
 
-  if (q < N) {
+  if (SPLIT && q < N) {  // key split: unnormalised partials, combined by attn_fwd_combine_kernel
+    const int64_t rows = (int64_t)gridDim.y * N, row = b * N + q, zs = blockIdx.z;
+    float* po = a.part + zs * rows * a.dv + row * a.dv;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int f = t * 32 + kappa(r, h);
+        if (f < a.dv) po[f] = o[t][r];
+      }
+    if (h == 0) {
+      float* pm = a.part + (int64_t)gridDim.z * rows * a.dv;
+      pm[zs * rows + row] = m;
+      pm[((int64_t)gridDim.z + zs) * rows + row] = l;
+    }
+  } else if (q < N) {
     const float inv = 1.0f / l;
     const int64_t base = (b * N + q) * a.dv;
 #pragma unroll
@@ -775,7 +797,7 @@ __device__ __forceinline__ void reg_planes(const f32x16& x, abf16x8_t (&pl)[2][3
 }
 
 // query-stationary: dQ^T += K^T dS^T
-template <int DKP, bool PRE>
+template <int DKP, bool PRE, bool SPLIT>
 __global__ __launch_bounds__(256, 2) void attn_bwd_q_x6_kernel(AttnArgs a) {
   constexpr int KC = DKP / 16, FC = 8;  // 128 value columns = 8 chunks of 16
   __shared__ __attribute__((aligned(16))) uint16_t Kp_s[(PRE ? 2 : 1) * 3 * 32 * 32];  // PRE: 2 stages
@@ -786,6 +808,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_x6_kernel(AttnArgs a) {
   const float* Hb = a.H + b * N * a.dv;
   const int64_t q = (int64_t)blockIdx.x * 128 + wave * 32 + l32;
   const bool qv = q < N;
+  const int64_t k_lo = SPLIT ? (int64_t)blockIdx.z * a.kr : 0, k_hi = SPLIT ? min<int64_t>(N, k_lo + a.kr) : N;
   abf16x8_t qp[KC][3], dop[FC][3];
   row_planes<KC>(a.Q + (b * N + q) * a.dk, qv, a.dk, h, qp);
   row_planes<FC>(a.dO + (b * N + q) * a.dv, qv, a.dv, h, dop);
@@ -806,22 +829,22 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_x6_kernel(AttnArgs a) {
   const uint16_t* Hpb = a.Hpl + b * N * 128;
   const bool vk = vec_ok(Kb, a.dk), vh = vec_ok(Hb, a.dv);
   if constexpr (PRE) {
-    dma_block<32, PL_PLAIN>(Kpb, kps, 0, N, Kp_s, wave, lane);
-    dma_block<128, PL_SWZ128>(Hpb, hps, 0, N, Hp_s, wave, lane);
+    dma_block<32, PL_PLAIN>(Kpb, kps, k_lo, N, Kp_s, wave, lane);
+    dma_block<128, PL_SWZ128>(Hpb, hps, k_lo, N, Hp_s, wave, lane);
   } else {
-    sk.fetch(Kb, nullptr, 0, 0, N, a.dk, vk, tid);
-    sh.fetch(Hb, nullptr, 0, 0, N, a.dv, vh, tid);
+    sk.fetch(Kb, nullptr, 0, k_lo, N, a.dk, vk, tid);
+    sh.fetch(Hb, nullptr, 0, k_lo, N, a.dv, vh, tid);
   }
   const int trq = (lane & 15) >> 2, trc = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
 
-  for (int64_t k0 = 0; k0 < N; k0 += 32) {
-    const int stg = PRE ? (int)((k0 >> 5) & 1) : 0;
+  for (int64_t k0 = k_lo; k0 < k_hi; k0 += 32) {
+    const int stg = PRE ? (int)(((k0 - k_lo) >> 5) & 1) : 0;
     uint16_t* Kp = Kp_s + stg * 3 * 1024;
     uint16_t* Hp = Hp_s + stg * 3 * 4096;
     if constexpr (PRE) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (k0 + 32 < N) {
+      if (k0 + 32 < k_hi) {
         dma_block<32, PL_PLAIN>(Kpb, kps, k0 + 32, N, Kp_s + (stg ^ 1) * 3 * 1024, wave, lane);
         dma_block<128, PL_SWZ128>(Hpb, hps, k0 + 32, N, Hp_s + (stg ^ 1) * 3 * 4096, wave, lane);
       }
@@ -829,15 +852,16 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_x6_kernel(AttnArgs a) {
       sk.store(Kp, tid);
       sh.store(Hp, tid);
       __syncthreads();
-      if (k0 + 32 < N) {
+      if (k0 + 32 < k_hi) {
         sk.fetch(Kb, nullptr, 0, k0 + 32, N, a.dk, vk, tid);
         sh.fetch(Hb, nullptr, 0, k0 + 32, N, a.dv, vh, tid);
       }
     }
+    const int l32o = l32, trqo = trq, trco = trc;
     f32x16 s = zero16();
 #pragma unroll
     for (int kc = 0; kc < KC; ++kc) {
-      const int off = l32 * 32 + kc * 16 + 8 * h;
+      const int off = l32o * 32 + kc * 16 + 8 * h;
       const abf16x8_t k0p = *reinterpret_cast<const abf16x8_t*>(&Kp[off]);
       const abf16x8_t k1p = *reinterpret_cast<const abf16x8_t*>(&Kp[1024 + off]);
       const abf16x8_t k2p = *reinterpret_cast<const abf16x8_t*>(&Kp[2048 + off]);
@@ -846,7 +870,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_x6_kernel(AttnArgs a) {
     f32x16 dp = zero16();  // dP^T[key][query] = sum_f H[key][f] dO[query][f]
 #pragma unroll
     for (int fc = 0; fc < FC; ++fc) {
-      const int off = swz128(l32, fc * 16 + 8 * h);
+      const int off = swz128(l32o, fc * 16 + 8 * h);
       const abf16x8_t h0 = *reinterpret_cast<const abf16x8_t*>(&Hp[off]);
       const abf16x8_t h1 = *reinterpret_cast<const abf16x8_t*>(&Hp[4096 + off]);
       const abf16x8_t h2 = *reinterpret_cast<const abf16x8_t*>(&Hp[8192 + off]);
@@ -854,32 +878,33 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_x6_kernel(AttnArgs a) {
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const float p = (k0 + kappa(r, h) < N) ? expf(s[r] - mq) * il : 0.0f;
+      const float p = (k0 + kappa(r, h) < k_hi) ? expf(s[r] - mq) * il : 0.0f;
       s[r] = p * (dp[r] - Dq);  // dS^T
     }
     abf16x8_t dsp[2][3];
     reg_planes(s, dsp);
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const int r0 = kappa(8 * u + trq, h), r1 = kappa(8 * u + 4 + trq, h);
+      const int r0 = kappa(8 * u + trqo, h), r1 = kappa(8 * u + 4 + trqo, h);
       abf16x8_t kt[3];
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl) kt[pl] = tr8(&Kp[pl * 1024 + r0 * 32 + trc], &Kp[pl * 1024 + r1 * 32 + trc]);
+      for (int pl = 0; pl < 3; ++pl) kt[pl] = tr8(&Kp[pl * 1024 + r0 * 32 + trco], &Kp[pl * 1024 + r1 * 32 + trco]);
       MFMA6(dq, kt[0], kt[1], kt[2], dsp[u][0], dsp[u][1], dsp[u][2]);
     }
     if constexpr (!PRE) __syncthreads();
   }
-  if (qv) {
+  if (qv) {  // key split: partial dQ into slab blockIdx.z (summed in split order afterwards)
+    float* dst = SPLIT ? a.part + (int64_t)blockIdx.z * gridDim.y * N * a.dk : a.dQ;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int d = kappa(r, h);
-      if (d < a.dk) a.dQ[(b * N + q) * a.dk + d] = dq[r];
+      if (d < a.dk) dst[(b * N + q) * a.dk + d] = dq[r];
     }
   }
 }
 
 // key-stationary.  WANT_H: dH^T += dO^T P;  else dK^T += Q^T dS (needs dP)
-template <int DKP, bool WANT_H, bool PRE>
+template <int DKP, bool WANT_H, bool PRE, bool SPLIT>
 __global__ __launch_bounds__(256, 2) void attn_bwd_kv_x6_kernel(AttnArgs a) {
   constexpr int KC = DKP / 16, FC = 8;
   __shared__ __attribute__((aligned(16))) uint16_t Qp_s[(PRE ? 2 : 1) * 3 * 32 * 32];  // PRE: 2 stages
@@ -891,6 +916,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_x6_kernel(AttnArgs a) {
   const float* dOb = a.dO + b * N * a.dv;
   const int64_t key = (int64_t)blockIdx.x * 128 + wave * 32 + l32;
   const bool kv = key < N;
+  const int64_t q_lo = SPLIT ? (int64_t)blockIdx.z * a.kr : 0, q_hi = SPLIT ? min<int64_t>(N, q_lo + a.kr) : N;
   abf16x8_t kp[KC][3];
   row_planes<KC>(a.K + (b * N + key) * a.dk, kv, a.dk, h, kp);
   abf16x8_t hp[WANT_H ? 1 : FC][3];
@@ -913,24 +939,24 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_x6_kernel(AttnArgs a) {
   auto fetch_stats = [&](int64_t q0) {
     if (tid < 32) {
       const int64_t qq = q0 + tid;
-      const bool v = qq < N;
+      const bool v = qq < q_hi;
       pm = v ? a.smax[b * N + qq] : 0.0f;
       pl_ = v ? 1.0f / a.ssum[b * N + qq] : 0.0f;  // 0 => P = 0 for padded queries
       pd = v ? a.Drow[b * N + qq] : 0.0f;
     }
   };
   if constexpr (PRE) {
-    dma_block<32, PL_PLAIN>(Qpb, qps, 0, N, Qp_s, wave, lane);
-    dma_block<128, PL_SWZ128>(Opb, ops, 0, N, Op_s, wave, lane);
+    dma_block<32, PL_PLAIN>(Qpb, qps, q_lo, N, Qp_s, wave, lane);
+    dma_block<128, PL_SWZ128>(Opb, ops, q_lo, N, Op_s, wave, lane);
   } else {
-    sq.fetch(Qb, nullptr, 0, 0, N, a.dk, vq, tid);
-    so.fetch(dOb, nullptr, 0, 0, N, a.dv, vo, tid);
+    sq.fetch(Qb, nullptr, 0, q_lo, N, a.dk, vq, tid);
+    so.fetch(dOb, nullptr, 0, q_lo, N, a.dv, vo, tid);
   }
-  fetch_stats(0);
+  fetch_stats(q_lo);
   const int trq = (lane & 15) >> 2, trc = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
 
-  for (int64_t q0 = 0; q0 < N; q0 += 32) {
-    const int stg = PRE ? (int)((q0 >> 5) & 1) : 0;
+  for (int64_t q0 = q_lo; q0 < q_hi; q0 += 32) {
+    const int stg = PRE ? (int)(((q0 - q_lo) >> 5) & 1) : 0;
     uint16_t* Qp = Qp_s + stg * 3 * 1024;
     uint16_t* Op = Op_s + stg * 3 * 4096;
     float* Ms = Ms_s + stg * 32;
@@ -947,7 +973,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_x6_kernel(AttnArgs a) {
     }
     if constexpr (PRE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (q0 + 32 < N) {
+    if (q0 + 32 < q_hi) {
       if constexpr (PRE) {
         dma_block<32, PL_PLAIN>(Qpb, qps, q0 + 32, N, Qp_s + (stg ^ 1) * 3 * 1024, wave, lane);
         dma_block<128, PL_SWZ128>(Opb, ops, q0 + 32, N, Op_s + (stg ^ 1) * 3 * 4096, wave, lane);
@@ -1015,24 +1041,65 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_x6_kernel(AttnArgs a) {
     }
     if constexpr (!PRE) __syncthreads();
   }
-  if (kv) {
+  if (kv) {  // query split: partial dH / dK into slab blockIdx.z (summed in split order afterwards)
+    const int64_t rows = (int64_t)gridDim.y * N;
     if (WANT_H) {
+      float* dst = SPLIT ? a.part + (int64_t)blockIdx.z * rows * a.dv : a.dH;
       const int64_t rowv = (b * N + key) * a.dv;
 #pragma unroll
       for (int t = 0; t < 4; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int f = t * 32 + kappa(r, h);
-          if (f < a.dv) a.dH[rowv + f] = acc[t][r];
+          if (f < a.dv) dst[rowv + f] = acc[t][r];
         }
     } else {
+      float* dst = SPLIT ? a.part2 + (int64_t)blockIdx.z * rows * a.dk : a.dK;
       const int64_t rowk = (b * N + key) * a.dk;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int d = kappa(r, h);
-        if (d < a.dk) a.dK[rowk + d] = acc[0][r];
+        if (d < a.dk) dst[rowk + d] = acc[0][r];
       }
     }
+  }
+}
+
+
+// Key split of the forward: out / o_norm / row_max / row_sum from the S
+// partial (o, m, l) in split order (deterministic):
+//   M = max_s m_s,  L = sum_s l_s e^(m_s - M),  O = sum_s o_s e^(m_s - M) / L
+__global__ void attn_fwd_combine_kernel(AttnArgs a, int64_t rows, int S) {
+  const int64_t n_all = rows * a.dv;
+  const float* pm = a.part + (int64_t)S * rows * a.dv;
+  const float* pl = pm + (int64_t)S * rows;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_all; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t row = i / a.dv;
+    const int f = (int)(i - row * a.dv);
+    float M = -INFINITY;
+    for (int s = 0; s < S; ++s) M = fmaxf(M, pm[s * rows + row]);
+    float L = 0.0f, O = 0.0f;
+    for (int s = 0; s < S; ++s) {
+      const float w = expf(pm[s * rows + row] - M);
+      L += pl[s * rows + row] * w;
+      O += a.part[(int64_t)s * n_all + i] * w;
+    }
+    O /= L;
+    a.out[i] = a.gamma[f] * O + a.V[i];
+    if (a.onorm) a.onorm[i] = O;
+    if (f == 0 && a.rmax) {
+      a.rmax[row] = M;
+      a.rsum[row] = L;
+    }
+  }
+}
+
+// out[i] = sum_{s < S} slab[s][i] in split order
+__global__ void attn_slab_sum_kernel(const float* __restrict__ slab, int64_t n, int S, float* __restrict__ out) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float acc = 0.0f;
+    for (int s = 0; s < S; ++s) acc += slab[(int64_t)s * n + i];
+    out[i] = acc;
   }
 }
 
@@ -1047,31 +1114,59 @@ bool attn_x6_enabled() {
 }
 
 template <int DKP, int NT>
-int launch_attn(AttnPass pass, const AttnArgs& a, int64_t B, hipStream_t st) {
-  const dim3 grid((unsigned)ceil_div(a.N, 128), (unsigned)B);
+int launch_attn(AttnPass pass, const AttnArgs& a0, int64_t B, int S, hipStream_t st) {
+  AttnArgs a = a0;
+  const bool x6 = attn_x6_enabled() && (pass == PASS_FWD || NT == 4);
+  if (!x6 || !a.part) S = 1;
+  if (S == 1) {
+    a.part = a.part2 = nullptr;
+    a.kr = a.N;
+  }
+  const dim3 grid((unsigned)ceil_div(a.N, 128), (unsigned)B, (unsigned)S);
   const bool pre = pass == PASS_BWD_KV ? (a.Qpl && a.Opl) : (a.Kpl && a.Hpl);
-  if (pass == PASS_FWD && attn_x6_enabled()) {
-    if (pre)
-      hipLaunchKernelGGL((attn_fwd_x6_kernel<DKP, NT, true>), grid, dim3(256), 0, st, a);
-    else
-      hipLaunchKernelGGL((attn_fwd_x6_kernel<DKP, NT, false>), grid, dim3(256), 0, st, a);
+  const int64_t rows = B * a.N;
+  const unsigned red = (unsigned)std::min<int64_t>(ceil_div(rows * std::max(a.dv, 1), 256), 8192);
+#define GRL_X6L(KERNEL, ...)                                                                      \
+  do {                                                                                              \
+    if (pre && S > 1)                                                                               \
+      hipLaunchKernelGGL((KERNEL<__VA_ARGS__, true, true>), grid, dim3(256), 0, st, a);             \
+    else if (pre)                                                                                   \
+      hipLaunchKernelGGL((KERNEL<__VA_ARGS__, true, false>), grid, dim3(256), 0, st, a);            \
+    else if (S > 1)                                                                                 \
+      hipLaunchKernelGGL((KERNEL<__VA_ARGS__, false, true>), grid, dim3(256), 0, st, a);            \
+    else                                                                                            \
+      hipLaunchKernelGGL((KERNEL<__VA_ARGS__, false, false>), grid, dim3(256), 0, st, a);           \
+  } while (0)
+  if (pass == PASS_FWD && x6) {
+    GRL_X6L(attn_fwd_x6_kernel, DKP, NT);
+    if (S > 1) {
+      GRL_LAUNCH_CHECK();
+      hipLaunchKernelGGL(attn_fwd_combine_kernel, dim3(red), dim3(256), 0, st, a, rows, S);
+    }
   } else if (pass == PASS_FWD) {
     hipLaunchKernelGGL((attn_fwd_kernel<DKP, NT>), grid, dim3(256), 0, st, a);
-  } else if (NT == 4 && attn_x6_enabled()) {  // backward x6: dv in (96, 128]
+  } else if (x6) {  // backward x6: dv in (96, 128]
     if (pass == PASS_BWD_Q) {
-      if (pre)
-        hipLaunchKernelGGL((attn_bwd_q_x6_kernel<DKP, true>), grid, dim3(256), 0, st, a);
-      else
-        hipLaunchKernelGGL((attn_bwd_q_x6_kernel<DKP, false>), grid, dim3(256), 0, st, a);
-    } else if (pre) {
-      hipLaunchKernelGGL((attn_bwd_kv_x6_kernel<DKP, true, true>), grid, dim3(256), 0, st, a);
-      GRL_LAUNCH_CHECK();
-      hipLaunchKernelGGL((attn_bwd_kv_x6_kernel<DKP, false, true>), grid, dim3(256), 0, st, a);
+      GRL_X6L(attn_bwd_q_x6_kernel, DKP);
+      if (S > 1 && a.dk > 0) {
+        GRL_LAUNCH_CHECK();
+        hipLaunchKernelGGL(attn_slab_sum_kernel, dim3(red), dim3(256), 0, st, a.part, rows * a.dk, S, a.dQ);
+      }
     } else {
-      hipLaunchKernelGGL((attn_bwd_kv_x6_kernel<DKP, true, false>), grid, dim3(256), 0, st, a);
+      if (S > 1) a.part2 = a.part + (int64_t)S * rows * a.dv;
+      GRL_X6L(attn_bwd_kv_x6_kernel, DKP, true);
       GRL_LAUNCH_CHECK();
-      hipLaunchKernelGGL((attn_bwd_kv_x6_kernel<DKP, false, false>), grid, dim3(256), 0, st, a);
+      GRL_X6L(attn_bwd_kv_x6_kernel, DKP, false);
+      if (S > 1) {
+        GRL_LAUNCH_CHECK();
+        hipLaunchKernelGGL(attn_slab_sum_kernel, dim3(red), dim3(256), 0, st, a.part, rows * a.dv, S, a.dH);
+        if (a.dk > 0) {
+          GRL_LAUNCH_CHECK();
+          hipLaunchKernelGGL(attn_slab_sum_kernel, dim3(red), dim3(256), 0, st, a.part2, rows * a.dk, S, a.dK);
+        }
+      }
     }
+#undef GRL_X6L
   } else if (pass == PASS_BWD_Q) {
     hipLaunchKernelGGL((attn_bwd_q_kernel<DKP, NT>), grid, dim3(256), 0, st, a);
   } else {
@@ -1081,6 +1176,18 @@ int launch_attn(AttnPass pass, const AttnArgs& a, int64_t B, hipStream_t st) {
   return GRL_OK;
 }
 
+// Key (forward, dQ) / query (dH, dK) split for small N: one workgroup per 128
+// rows leaves the chip idle below ~2 x CUs workgroups; split the loop range
+// into S pieces of >= 256 rows (multiples of 32) whose partials are combined
+// in split order (deterministic).  Returns S, sets *kr (rows per split).
+int attn_splits(int64_t B, int64_t N, int64_t* kr) {
+  const int64_t blocks = ceil_div(N, 128) * B, want = 2 * (int64_t)device_cu_count();
+  int64_t S = blocks >= want ? 1 : std::min<int64_t>(ceil_div(want, blocks), std::max<int64_t>(1, N / 256));
+  S = std::max<int64_t>(1, std::min<int64_t>(S, 64));
+  *kr = ceil_div(ceil_div(N, S), 32) * 32;
+  return (int)ceil_div(N, *kr);
+}
+
 int attn_dkp(int dk) { return dk <= 16 ? 16 : 32; }
 int attn_dvp(int dv) {
   const int nt = (int)ceil_div(dv, 32);
@@ -1088,17 +1195,17 @@ int attn_dvp(int dv) {
 }
 
 template <int DKP>
-int dispatch_nt(AttnPass pass, const AttnArgs& a, int64_t B, hipStream_t st) {
+int dispatch_nt(AttnPass pass, const AttnArgs& a, int64_t B, int S, hipStream_t st) {
   const int nt = attn_dvp(a.dv) / 32;
-  if (nt == 1) return launch_attn<DKP, 1>(pass, a, B, st);
-  if (nt == 2) return launch_attn<DKP, 2>(pass, a, B, st);
-  if (nt == 4) return launch_attn<DKP, 4>(pass, a, B, st);
-  return launch_attn<DKP, 8>(pass, a, B, st);
+  if (nt == 1) return launch_attn<DKP, 1>(pass, a, B, S, st);
+  if (nt == 2) return launch_attn<DKP, 2>(pass, a, B, S, st);
+  if (nt == 4) return launch_attn<DKP, 4>(pass, a, B, S, st);
+  return launch_attn<DKP, 8>(pass, a, B, S, st);
 }
 
-int dispatch(AttnPass pass, const AttnArgs& a, int64_t B, hipStream_t st) {
+int dispatch(AttnPass pass, const AttnArgs& a, int64_t B, int S, hipStream_t st) {
   if (a.N == 0 || B == 0) return GRL_OK;
-  return a.dk <= 16 ? dispatch_nt<16>(pass, a, B, st) : dispatch_nt<32>(pass, a, B, st);
+  return a.dk <= 16 ? dispatch_nt<16>(pass, a, B, S, st) : dispatch_nt<32>(pass, a, B, S, st);
 }
 
 // Workspace of the PRE staging: bf16 planes [3][B*N][W] of K, H (forward and
@@ -1138,7 +1245,10 @@ using namespace grl;
 extern "C" size_t grl_node_attention_workspace_size(int64_t B, int64_t N, int32_t dk, int32_t dv) {
   if (B <= 0 || N <= 0 || dk < 0 || dk > 32 || dv < 1 || dv > 256) return 0;
   const int64_t rows = B * N;
-  return 2 * attn_plane_bytes(rows, 32) + 2 * attn_plane_bytes(rows, attn_dvp(dv)) + 256;
+  int64_t kr;
+  const int S = attn_splits(B, N, &kr);
+  const size_t part = S > 1 ? ((size_t)S * rows * (dv + std::max(dk, 2) + 2) * 4 + 255) / 256 * 256 : 0;
+  return 2 * attn_plane_bytes(rows, 32) + 2 * attn_plane_bytes(rows, attn_dvp(dv)) + part + 512;
 }
 
 extern "C" int grl_node_attention_fwd(const float* Q, const float* K, const float* H, const float* V,
@@ -1164,6 +1274,7 @@ extern "C" int grl_node_attention_fwd(const float* Q, const float* K, const floa
   a.dk = dk;
   a.dv = dv;
   hipStream_t st = as_stream(stream);
+  int S = 1;
   if (workspace && attn_x6_enabled()) {  // split K and H once for every query block
     unsigned char* cur = reinterpret_cast<unsigned char*>((reinterpret_cast<uintptr_t>(workspace) + 255) & ~(uintptr_t)255);
     const unsigned char* end = static_cast<unsigned char*>(workspace) + workspace_bytes;
@@ -1174,8 +1285,16 @@ extern "C" int grl_node_attention_fwd(const float* Q, const float* K, const floa
       a.Hpl = hp;
     }
     GRL_LAUNCH_CHECK();
+    int64_t kr;
+    S = attn_splits(B, N, &kr);  // small N: key split with (o, m, l) partials
+    if (S > 1 && cur + (size_t)S * B * N * (dv + 2) * 4 <= end) {
+      a.part = reinterpret_cast<float*>(cur);
+      a.kr = kr;
+    } else {
+      S = 1;
+    }
   }
-  return dispatch(PASS_FWD, a, B, st);
+  return dispatch(PASS_FWD, a, B, S, st);
 }
 
 extern "C" int grl_node_attention_bwd(const float* Q, const float* K, const float* H, const float* dO,
@@ -1202,6 +1321,7 @@ extern "C" int grl_node_attention_bwd(const float* Q, const float* K, const floa
   a.dk = dk;
   a.dv = dv;
   hipStream_t st = as_stream(stream);
+  int S = 1;
   if (workspace && attn_x6_enabled() && attn_dvp(dv) == 128) {  // the x6 backward's operands, split once
     unsigned char* cur = reinterpret_cast<unsigned char*>((reinterpret_cast<uintptr_t>(workspace) + 255) & ~(uintptr_t)255);
     const unsigned char* end = static_cast<unsigned char*>(workspace) + workspace_bytes;
@@ -1214,8 +1334,16 @@ extern "C" int grl_node_attention_bwd(const float* Q, const float* K, const floa
       a.Opl = op;
     }
     GRL_LAUNCH_CHECK();
+    int64_t kr;
+    S = attn_splits(B, N, &kr);  // small N: key / query split with ordered partial sums
+    if (S > 1 && cur + (size_t)S * B * N * (dv + dk) * 4 <= end) {
+      a.part = reinterpret_cast<float*>(cur);
+      a.kr = kr;
+    } else {
+      S = 1;
+    }
   }
-  rc = dispatch(PASS_BWD_Q, a, B, st);
+  rc = dispatch(PASS_BWD_Q, a, B, S, st);
   if (rc) return rc;
-  return dispatch(PASS_BWD_KV, a, B, st);
+  return dispatch(PASS_BWD_KV, a, B, S, st);
 }
