@@ -572,6 +572,12 @@ __global__ __launch_bounds__(512) void gemm256p_kernel(GemmArgs p) {
 // stage's global loads are in registers during the MFMAs.
 // Preconditions (x6_ok): K % 16 == 0, 16-B aligned A and lda % 4 == 0.
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+#ifndef GRL_X6_PRIO
+#define GRL_X6_PRIO 0
+#endif
+#ifndef GRL_X6_ORDER
+#define GRL_X6_ORDER 0
+#endif
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
 
@@ -742,6 +748,20 @@ __global__ __launch_bounds__(512) void gemm_x6_kernel(GemmArgs p, const uint16_t
         for (int q = 0; q < 3; ++q)
           b_[j][q] = *reinterpret_cast<const bf16x8_t*>(cur + (3 + q) * X6_PLANE + sw(wn * 64 + j * 32 + l32, h * 8));
       // small terms first (i + j = 2, then 1, then the leading product)
+#if GRL_X6_PRIO
+      __builtin_amdgcn_s_setprio(1);
+#endif
+#if GRL_X6_ORDER
+      // product-major: eight independent accumulators between two uses of one
+      constexpr int PA[6] = {2, 1, 0, 1, 0, 0}, PB[6] = {0, 1, 2, 0, 1, 0};
+#pragma unroll
+      for (int pr = 0; pr < 6; ++pr)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_[i][PA[pr]], b_[j][PB[pr]], acc[i][j], 0, 0, 0);
+#else
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -753,6 +773,10 @@ __global__ __launch_bounds__(512) void gemm_x6_kernel(GemmArgs p, const uint16_t
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_[i][0], b_[j][1], acc[i][j], 0, 0, 0);
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_[i][0], b_[j][0], acc[i][j], 0, 0, 0);
         }
+#endif
+#if GRL_X6_PRIO
+      __builtin_amdgcn_s_setprio(0);
+#endif
     }
     if (t + 1 < nk) {
       if (t + 2 < nk)
