@@ -693,10 +693,16 @@ __global__ __launch_bounds__(256) void attn_fwd_x6_kernel(AttnArgs a) {
     for (int u = 0; u < 2; ++u)
       asplit8(make_float4(s[8 * u], s[8 * u + 1], s[8 * u + 2], s[8 * u + 3]),
               make_float4(s[8 * u + 4], s[8 * u + 5], s[8 * u + 6], s[8 * u + 7]), pp[u][0], pp[u][1], pp[u][2]);
+    // the running max of a wave's 32 queries rarely moves after the first
+    // key blocks: alpha == 1 exactly then, and the 16 x NT rescale multiplies
+    // are skipped wave-uniformly (x * 1 == x, so results are unchanged)
+    const bool rescale = __any(alpha != 1.0f);
 #pragma unroll
     for (int t = 0; t < NT; ++t) {
+      if (rescale) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
+        for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
+      }
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         abf16x8_t hp[3];
