@@ -399,3 +399,17 @@ def test_spmm_wide_rows_bitwise(wide, monkeypatch):
     test_spmm_fwd_bwd_bitwise((300, 6, 16.0, 512, 0, True, True), 1)
     test_spmm_fwd_bwd_bitwise((200, 6, 8.0, 384, 0, False, True), 2)
     test_split_rows_bitwise_rmat((300, 128), 1, 512, True)
+
+
+def test_x6_strided_z_matches_contiguous(monkeypatch):
+    """The x6 forward reads Z through its row stride (ldz > K, as a column
+    slice of a wider buffer gives): bitwise the same as on a contiguous copy."""
+    monkeypatch.setenv("GRL_GEMM_X6", "1")
+    M, K, C = 40_000, 1792, 256
+    gen = torch.Generator(device=DEV).manual_seed(11)
+    big = torch.randn(M, K + 32, device=DEV, generator=gen)
+    Z = big[:, 16:16 + K]
+    W = torch.randn(K, C, device=DEV, generator=gen) / np.sqrt(K)
+    b = torch.randn(C, device=DEV, generator=gen)
+    assert Z.stride(0) == K + 32
+    assert torch.equal(linear_fwd(Z, W, b, True), linear_fwd(Z.contiguous(), W, b, True))
