@@ -468,61 +468,31 @@ __device__ __forceinline__ int plane_off(int r, int c) {
   return r * LW + c;
 }
 
-// One operand's 32-row blocks -> three bf16 LDS planes of LW-element rows.
-// PRE = false: fp32 rows are fetched (float4, zero fill) and split at store;
-// PRE = true: the rows were split once per call into global bf16 planes
-// [3][rows][W] (attn_split_rows_kernel) and are copied 16 B at a time.
-// fetch() is issued for the next block before the current one's MFMAs.
-template <int W, int LW, int LAYOUT, bool PRE>
+// One operand's 32-row blocks -> three bf16 LDS planes of LW-element rows,
+// for the kernels' no-workspace path: fp32 rows are fetched (float4, zero
+// fill) into registers and split at store.  fetch() is issued for the next
+// block before the current one's MFMAs.  (With a workspace the operands are
+// split once per call and staged by LDS-DMA instead: dma_block.)
+template <int W, int LW, int LAYOUT>
 struct XStage {
-  static constexpr int PL = 32 * LW;       // LDS elements per plane
-  static constexpr int NU = 3 * 32 * W / 8;  // PRE: uint4 per block
-  static constexpr int PER = PRE ? (NU + 255) / 256 : 1;
+  static constexpr int PL = 32 * LW;  // LDS elements per plane
   Stager<W, W> f32;
-  uint4 reg[PER];
 
-  __device__ __forceinline__ void fetch(const float* src, const uint16_t* planes, int64_t ps, int64_t r0, int64_t N,
-                                        int width, bool vec, int tid) {
-    if (!PRE) {
-      f32.fetch(src, r0, N, width, vec, tid);
-      return;
-    }
-#pragma unroll
-    for (int it = 0; it < PER; ++it) {
-      const int idx = tid + it * 256;
-      uint4 v = make_uint4(0u, 0u, 0u, 0u);
-      if (idx < NU) {
-        const int pl = idx / (32 * W / 8), rem = idx % (32 * W / 8);
-        const int64_t row = r0 + rem / (W / 8);
-        if (row < N) v = *reinterpret_cast<const uint4*>(planes + pl * ps + row * W + (rem % (W / 8)) * 8);
-      }
-      reg[it] = v;
-    }
+  __device__ __forceinline__ void fetch(const float* src, int64_t r0, int64_t N, int width, bool vec, int tid) {
+    f32.fetch(src, r0, N, width, vec, tid);
   }
   __device__ __forceinline__ void store(uint16_t* lds, int tid) const {
-    if (!PRE) {
 #pragma unroll
-      for (int it = 0; it < Stager<W, W>::PER; ++it) {
-        const int idx = tid + it * 256;
-        if (idx < Stager<W, W>::NF4) {
-          const int r = idx / (W / 4), c = (idx % (W / 4)) * 4;
-          uint2 p0, p1, p2;
-          asplit3(f32.reg[it], p0, p1, p2);
-          const int off = plane_off<W, LW, LAYOUT>(r, c);
-          *reinterpret_cast<uint2*>(&lds[off]) = p0;
-          *reinterpret_cast<uint2*>(&lds[PL + off]) = p1;
-          *reinterpret_cast<uint2*>(&lds[2 * PL + off]) = p2;
-        }
-      }
-      return;
-    }
-#pragma unroll
-    for (int it = 0; it < PER; ++it) {
+    for (int it = 0; it < Stager<W, W>::PER; ++it) {
       const int idx = tid + it * 256;
-      if (idx < NU) {
-        const int pl = idx / (32 * W / 8), rem = idx % (32 * W / 8);
-        const int r = rem / (W / 8), c = (rem % (W / 8)) * 8;
-        *reinterpret_cast<uint4*>(&lds[pl * PL + plane_off<W, LW, LAYOUT>(r, c)]) = reg[it];
+      if (idx < Stager<W, W>::NF4) {
+        const int r = idx / (W / 4), c = (idx % (W / 4)) * 4;
+        uint2 p0, p1, p2;
+        asplit3(f32.reg[it], p0, p1, p2);
+        const int off = plane_off<W, LW, LAYOUT>(r, c);
+        *reinterpret_cast<uint2*>(&lds[off]) = p0;
+        *reinterpret_cast<uint2*>(&lds[PL + off]) = p1;
+        *reinterpret_cast<uint2*>(&lds[2 * PL + off]) = p2;
       }
     }
   }
@@ -621,8 +591,8 @@ __global__ __launch_bounds__(256) void attn_fwd_x6_kernel(AttnArgs a) {
 #pragma unroll
   for (int t = 0; t < NT; ++t) o[t] = zero16();
   float m = -INFINITY, l = 0.0f;
-  XStage<DKP, DKP, PL_PLAIN, false> sk;
-  XStage<DV, DV, PL_HSWZ, false> sh;
+  XStage<DKP, DKP, PL_PLAIN> sk;
+  XStage<DV, DV, PL_HSWZ> sh;
   const int64_t kps = (int64_t)gridDim.y * N * DKP, hps = (int64_t)gridDim.y * N * DV;
   const uint16_t* Kpb = a.Kpl + b * N * DKP;
   const uint16_t* Hpb = a.Hpl + b * N * DV;
@@ -631,8 +601,8 @@ __global__ __launch_bounds__(256) void attn_fwd_x6_kernel(AttnArgs a) {
     dma_block<DKP, PL_PLAIN>(Kpb, kps, k_lo, N, Kp_s, wave, lane);
     dma_block<DV, PL_HSWZ>(Hpb, hps, k_lo, N, Hp_s, wave, lane);
   } else {
-    sk.fetch(Kb, nullptr, 0, k_lo, N, a.dk, vk, tid);
-    sh.fetch(Hb, nullptr, 0, k_lo, N, a.dv, vh, tid);
+    sk.fetch(Kb, k_lo, N, a.dk, vk, tid);
+    sh.fetch(Hb, k_lo, N, a.dv, vh, tid);
   }
   // transposed-read coordinates: group row q' = (lane & 15) >> 2, columns 16 ((lane >> 4) & 1) + 4 (lane & 3)
   const int trq = (lane & 15) >> 2;
@@ -656,8 +626,8 @@ __global__ __launch_bounds__(256) void attn_fwd_x6_kernel(AttnArgs a) {
       sh.store(Hp, tid);
       __syncthreads();
       if (k0 + 32 < k_hi) {
-        sk.fetch(Kb, nullptr, 0, k0 + 32, N, a.dk, vk, tid);
-        sh.fetch(Hb, nullptr, 0, k0 + 32, N, a.dv, vh, tid);
+        sk.fetch(Kb, k0 + 32, N, a.dk, vk, tid);
+        sh.fetch(Hb, k0 + 32, N, a.dv, vh, tid);
       }
     }
     // S^T = K Q^T: A = K[key l32][kc*16 + 8h ..], B = Q
@@ -827,8 +797,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_x6_kernel(AttnArgs a) {
       const int pl = i / (32 * (32 - DKP)), rc = i % (32 * (32 - DKP));
       Kp_s[pl * 1024 + (rc / (32 - DKP)) * 32 + DKP + rc % (32 - DKP)] = 0;
     }
-  XStage<DKP, 32, PL_PLAIN, false> sk;
-  XStage<128, 128, PL_SWZ128, false> sh;
+  XStage<DKP, 32, PL_PLAIN> sk;
+  XStage<128, 128, PL_SWZ128> sh;
   // PRE planes: K split 32 wide (zero columns >= dk), H 128 wide
   const int64_t kps = (int64_t)gridDim.y * N * 32, hps = (int64_t)gridDim.y * N * 128;
   const uint16_t* Kpb = a.Kpl + b * N * 32;
@@ -838,8 +808,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_x6_kernel(AttnArgs a) {
     dma_block<32, PL_PLAIN>(Kpb, kps, k_lo, N, Kp_s, wave, lane);
     dma_block<128, PL_SWZ128>(Hpb, hps, k_lo, N, Hp_s, wave, lane);
   } else {
-    sk.fetch(Kb, nullptr, 0, k_lo, N, a.dk, vk, tid);
-    sh.fetch(Hb, nullptr, 0, k_lo, N, a.dv, vh, tid);
+    sk.fetch(Kb, k_lo, N, a.dk, vk, tid);
+    sh.fetch(Hb, k_lo, N, a.dv, vh, tid);
   }
   const int trq = (lane & 15) >> 2, trc = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
 
@@ -859,8 +829,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_x6_kernel(AttnArgs a) {
       sh.store(Hp, tid);
       __syncthreads();
       if (k0 + 32 < k_hi) {
-        sk.fetch(Kb, nullptr, 0, k0 + 32, N, a.dk, vk, tid);
-        sh.fetch(Hb, nullptr, 0, k0 + 32, N, a.dv, vh, tid);
+        sk.fetch(Kb, k0 + 32, N, a.dk, vk, tid);
+        sh.fetch(Hb, k0 + 32, N, a.dv, vh, tid);
       }
     }
     const int l32o = l32, trqo = trq, trco = trc;
@@ -935,8 +905,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_x6_kernel(AttnArgs a) {
       const int pl = i / (32 * (32 - DKP)), rc = i % (32 * (32 - DKP));
       Qp_s[pl * 1024 + (rc / (32 - DKP)) * 32 + DKP + rc % (32 - DKP)] = 0;
     }
-  XStage<DKP, 32, PL_PLAIN, false> sq;
-  XStage<128, 128, PL_SWZ128, false> so;
+  XStage<DKP, 32, PL_PLAIN> sq;
+  XStage<128, 128, PL_SWZ128> so;
   const int64_t qps = (int64_t)gridDim.y * N * 32, ops = (int64_t)gridDim.y * N * 128;
   const uint16_t* Qpb = a.Qpl + b * N * 32;
   const uint16_t* Opb = a.Opl + b * N * 128;
@@ -955,8 +925,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_x6_kernel(AttnArgs a) {
     dma_block<32, PL_PLAIN>(Qpb, qps, q_lo, N, Qp_s, wave, lane);
     dma_block<128, PL_SWZ128>(Opb, ops, q_lo, N, Op_s, wave, lane);
   } else {
-    sq.fetch(Qb, nullptr, 0, q_lo, N, a.dk, vq, tid);
-    so.fetch(dOb, nullptr, 0, q_lo, N, a.dv, vo, tid);
+    sq.fetch(Qb, q_lo, N, a.dk, vq, tid);
+    so.fetch(dOb, q_lo, N, a.dv, vo, tid);
   }
   fetch_stats(q_lo);
   const int trq = (lane & 15) >> 2, trc = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
@@ -984,8 +954,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_x6_kernel(AttnArgs a) {
         dma_block<32, PL_PLAIN>(Qpb, qps, q0 + 32, N, Qp_s + (stg ^ 1) * 3 * 1024, wave, lane);
         dma_block<128, PL_SWZ128>(Opb, ops, q0 + 32, N, Op_s + (stg ^ 1) * 3 * 4096, wave, lane);
       } else {
-        sq.fetch(Qb, nullptr, 0, q0 + 32, N, a.dk, vq, tid);
-        so.fetch(dOb, nullptr, 0, q0 + 32, N, a.dv, vo, tid);
+        sq.fetch(Qb, q0 + 32, N, a.dk, vq, tid);
+        so.fetch(dOb, q0 + 32, N, a.dv, vo, tid);
       }
       fetch_stats(q0 + 32);
     }

@@ -567,10 +567,11 @@ __global__ __launch_bounds__(512) void gemm256p_kernel(GemmArgs p) {
 // kernel while it is staged into LDS; B arrives pre-split (split_planes_kernel,
 // once per call: W is 1.8 MB) as three bf16 planes [3][Np][K] with K
 // contiguous.  256 x 256 block tile, 8 waves of 128 x 64 (4 x 2 MFMA tiles,
-// 128 accumulators), K staged 16 deep through two LDS stages (48 KB each:
-// 3 planes x (A, B) x 256 rows x 32 B), one barrier per stage; the next
-// stage's global loads are in registers during the MFMAs.
-// Preconditions (x6_ok): K % 16 == 0, 16-B aligned A and lda % 4 == 0.
+// 128 accumulators), K staged 16 deep through two LDS plane stages (48 KB
+// each: 3 planes x (A, B) x 256 rows x 32 B), one barrier per stage.  A and
+// B arrive by LDS-DMA (layout and pipeline at gemm_x6_kernel below).
+// Preconditions (x6_shape_ok + aligned): K % 16 == 0, 16-B aligned A,
+// lda % 4 == 0, no operand masks.
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 #ifndef GRL_X6_PRIO
 #define GRL_X6_PRIO 0
