@@ -1184,6 +1184,8 @@ int dispatch(AttnPass pass, const AttnArgs& a, int64_t B, int S, hipStream_t st)
   return a.dk <= 16 ? dispatch_nt<16>(pass, a, B, S, st) : dispatch_nt<32>(pass, a, B, S, st);
 }
 
+constexpr int64_t kAttnPlaneMinRows = 4096;
+
 // Workspace of the PRE staging: bf16 planes [3][B*N][W] of K, H (forward and
 // backward) and Q, dO (backward), each section 256-B aligned
 size_t attn_plane_bytes(int64_t rows, int W) { return ((size_t)3 * rows * W * 2 + 255) / 256 * 256; }
@@ -1224,7 +1226,9 @@ extern "C" size_t grl_node_attention_workspace_size(int64_t B, int64_t N, int32_
   int64_t kr;
   const int S = attn_splits(B, N, &kr);
   const size_t part = S > 1 ? ((size_t)S * rows * (dv + std::max(dk, 2) + 2) * 4 + 255) / 256 * 256 : 0;
-  return 2 * attn_plane_bytes(rows, 32) + 2 * attn_plane_bytes(rows, attn_dvp(dv)) + part + 512;
+  const size_t planes =
+      rows >= kAttnPlaneMinRows ? 2 * attn_plane_bytes(rows, 32) + 2 * attn_plane_bytes(rows, attn_dvp(dv)) : 0;
+  return planes + part ? planes + part + 512 : 0;
 }
 
 extern "C" int grl_node_attention_fwd(const float* Q, const float* K, const float* H, const float* V,
@@ -1251,11 +1255,13 @@ extern "C" int grl_node_attention_fwd(const float* Q, const float* K, const floa
   a.dv = dv;
   hipStream_t st = as_stream(stream);
   int S = 1;
+  // below ~4k rows the per-call split launches cost more than the in-kernel
+  // splits they save (a 74-node page: 2 extra launches per call)
   if (workspace && attn_x6_enabled()) {  // split K and H once for every query block
     unsigned char* cur = reinterpret_cast<unsigned char*>((reinterpret_cast<uintptr_t>(workspace) + 255) & ~(uintptr_t)255);
     const unsigned char* end = static_cast<unsigned char*>(workspace) + workspace_bytes;
     const uint16_t *kp = nullptr, *hp = nullptr;
-    if (attn_split(K, B * N, dk, attn_dkp(dk), cur, end, &kp, st) &&
+    if (B * N >= kAttnPlaneMinRows && attn_split(K, B * N, dk, attn_dkp(dk), cur, end, &kp, st) &&
         attn_split(H, B * N, dv, attn_dvp(dv), cur, end, &hp, st)) {
       a.Kpl = kp;
       a.Hpl = hp;
@@ -1302,7 +1308,8 @@ extern "C" int grl_node_attention_bwd(const float* Q, const float* K, const floa
     unsigned char* cur = reinterpret_cast<unsigned char*>((reinterpret_cast<uintptr_t>(workspace) + 255) & ~(uintptr_t)255);
     const unsigned char* end = static_cast<unsigned char*>(workspace) + workspace_bytes;
     const uint16_t *kp = nullptr, *hp = nullptr, *qp = nullptr, *op = nullptr;
-    if (attn_split(K, B * N, dk, 32, cur, end, &kp, st) && attn_split(H, B * N, dv, 128, cur, end, &hp, st) &&
+    if (B * N >= kAttnPlaneMinRows && attn_split(K, B * N, dk, 32, cur, end, &kp, st) &&
+        attn_split(H, B * N, dv, 128, cur, end, &hp, st) &&
         attn_split(Q, B * N, dk, 32, cur, end, &qp, st) && attn_split(dO, B * N, dv, 128, cur, end, &op, st)) {
       a.Kpl = kp;
       a.Hpl = hp;

@@ -30,7 +30,8 @@ def _ref(Q, K, H, V, gamma):
 
 SHAPES = [(1, 74, 16, 128), (4, 74, 16, 128), (2, 33, 4, 32), (1, 1, 2, 16), (3, 130, 16, 128), (2, 300, 32, 256),
           (2, 64, 5, 40), (1, 500, 16, 100), (2, 9, 0, 4),  # dk = 0: net_size 8 (4 // 8), uniform attention
-          (1, 2048, 16, 128), (2, 1000, 5, 100), (1, 777, 32, 128)]  # small-N key / query splits (S = 8, 3, 3)
+          (1, 2048, 16, 128), (2, 1000, 5, 100), (1, 777, 32, 128),  # small-N key / query splits (S = 8, 3, 3)
+          (64, 1024, 16, 128), (4, 1100, 16, 128)]  # >= 4096 rows: LDS-DMA planes, unsplit / split (S = 4)
 
 
 MODES = ["x6", "x6-no-workspace", "f32"]
