@@ -554,7 +554,8 @@ __global__ __launch_bounds__(512) void gemm256p_kernel(GemmArgs p) {
 // Every fp32 operand value v is written as v = v0 + v1 + v2 with
 // v0 = bf16(v), v1 = bf16(v - v0), v2 = bf16(v - v0 - v1) (round to nearest
 // even; the differences are exact by Sterbenz, and 3 x 8 significant bits
-// hold all 24 of an fp32, so the split is exact for finite |v| < 3.39e38).
+// hold all 24 of an fp32, so the split is exact for 2^-100 <= |v| < 3.39e38;
+// below, the third part is a bf16 subnormal, off by <= 2^-133: tests/test_x6_split.py).
 // Products of two bf16 are exact in fp32; of the nine a_i b_j the six with
 // i + j <= 2 are accumulated (v_mfma_f32_32x32x16_bf16, fp32 accumulators);
 // the three dropped terms are <= ~2^-24 |a b| each -- the size of one fp32
