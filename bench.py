@@ -309,7 +309,8 @@ def extras(args, graph, X_full, gather, L, F, dev, E_loc, n_loc):
     dZ = torch.randn_like(Z)
     graph.csc()  # one-time CSC build (cached per graph), not part of the step
     ms = _time(lambda: torch.autograd.grad(Z, Xg, dZ, retain_graph=True), iters)
-    bwd_bytes = E_loc * F * 4 + 8 * E_loc + 4 * (graph.num_cols + 1) + graph.num_cols * F * 4 * 2
+    # no DropEdge on this graph: the CSC edge ids are not read, only the row indices (4 B/edge)
+    bwd_bytes = E_loc * F * 4 + 4 * E_loc + 4 * (graph.num_cols + 1) + graph.num_cols * F * 4 * 2
     res["spmm_bwd"] = {"ms": ms, "edges_per_s": E_loc / (ms * 1e-3), "alg_GBps": bwd_bytes / (ms * 1e-3) / 1e9}
     torch.manual_seed(3)
     W = torch.randn((L + 1) * F, F, device=dev) / np.sqrt((L + 1) * F)

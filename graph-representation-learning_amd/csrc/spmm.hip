@@ -194,9 +194,12 @@ __global__ __launch_bounds__(256) void spmm_kernel(
       if (lane < cnt) {
         sidx = idx[c0 + lane];
         const float v = VALS ? vals[c0 + lane] : 1.0f;
-        const uint64_t id = BWD ? edge_base + (uint64_t)(uint32_t)eidv[c0 + lane]
-                                : edge_base + (uint64_t)(c0 + lane);
-        w = dropedge_weight(de, v, id);
+        w = v;
+        if (de.active) {  // the CSC edge-id list is only read when DropEdge draws
+          const uint64_t id = BWD ? edge_base + (uint64_t)(uint32_t)eidv[c0 + lane]
+                                  : edge_base + (uint64_t)(c0 + lane);
+          w = dropedge_weight(de, v, id);
+        }
       }
       uint64_t kept = __ballot(w != 0.0f);
       while (kept) {
