@@ -348,6 +348,12 @@ def extras(args, graph, X_full, gather, L, F, dev, E_loc, n_loc):
     res["graphconv_layer_fwd_bwd_p0.3"] = {"ms": _time(layer, max(3, iters // 2), warm=3)}
     res["graphconv_layer_fwd_bwd_p0.3_two_ops"] = {"ms": _time(layer_two_ops, max(3, iters // 2), warm=2)}
     del Z, dZ, Zd
+    # inference: one grl_graphconv_fwd call, Z whole (7.2 GB) or in 1 GiB row chunks
+    from grl.ops import graph_conv_infer
+    Xe = X_full.detach()[: graph.num_cols]
+    res["graphconv_infer_fwd"] = {"ms": _time(lambda: graph_conv_infer(Xe, graph, W, b, True), iters, warm=2)}
+    res["graphconv_infer_fwd_z_chunks_1GiB"] = {
+        "ms": _time(lambda: graph_conv_infer(Xe, graph, W, b, True, max_workspace_bytes=1 << 30), iters, warm=2)}
     return res
 
 

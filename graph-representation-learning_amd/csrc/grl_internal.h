@@ -63,6 +63,10 @@ __host__ __device__ __forceinline__ uint64_t synth_bits(uint64_t seed, uint64_t 
   return mix64(mix64(seed + 0x243F6A8885A308D3ull * (uint64_t)(lane + 1)) ^ (k * 0x9E3779B97F4A7C15ull));
 }
 
+// Row-range typed-SpMM forward (spmm.hip) used by grl_graphconv_fwd.
+int spmm_fwd_rows(const GrlTypedCsr* g, int64_t r0, int64_t rows, const float* X, int64_t ldx, int F, float* Z,
+                  const GrlDropEdge* de, hipStream_t st);
+
 // Plain-data copy of GrlDropEdge passed by value to kernels.
 struct DropDev {
   uint64_t key;

@@ -1060,13 +1060,18 @@ size_t x6_ws_bytes(int64_t M, int64_t N, int64_t K) {
 }
 
 template <bool B_KC>
-int launch_x6(GemmArgs a, void* ws, hipStream_t st) {
+int split_b_planes(const GemmArgs& a, uint16_t* planes, hipStream_t st) {
   const int64_t Np = x6_np(a.N);
-  uint16_t* planes = static_cast<uint16_t*>(ws);
   const int64_t n_el = Np * a.K;
   hipLaunchKernelGGL(split_planes_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(n_el, 256), 4096)), dim3(256), 0,
                      st, a.B, a.ldb, B_KC ? 1 : 0, a.N, a.K, Np, planes);
   GRL_LAUNCH_CHECK();
+  return GRL_OK;
+}
+
+// the x6 GEMM on B planes already split into `planes`
+int launch_x6_gemm(GemmArgs a, const uint16_t* planes, hipStream_t st) {
+  const int64_t Np = x6_np(a.N);
   a.mt = ceil_div(a.M, LB_M);
   a.nt = Np / LB_N;
   a.zt = 1;
@@ -1080,6 +1085,13 @@ int launch_x6(GemmArgs a, void* ws, hipStream_t st) {
     hipLaunchKernelGGL(gemm_x6_kernel<EPI_STORE>, grid, dim3(512), 0, st, a, planes, Np);
   GRL_LAUNCH_CHECK();
   return GRL_OK;
+}
+
+template <bool B_KC>
+int launch_x6(GemmArgs a, void* ws, hipStream_t st) {
+  uint16_t* planes = static_cast<uint16_t*>(ws);
+  const int rc = split_b_planes<B_KC>(a, planes, st);
+  return rc ? rc : launch_x6_gemm(a, planes, st);
 }
 
 // Output-stationary GEMM with optional split-K through `ws` (slab layout
@@ -1151,6 +1163,80 @@ extern "C" int grl_linear_fwd(const float* Z, int64_t ldz, const float* W, const
   a.relu = relu;
   const bool aligned = al16(Z) && al16(W) && ldz % 4 == 0 && C % 4 == 0 && K % 4 == 0;
   return run_output_gemm<true, false>(a, aligned, "grl_linear_fwd", workspace, workspace_bytes, as_stream(stream));
+}
+
+static size_t ws_align(size_t b) { return (b + 255) & ~(size_t)255; }
+
+extern "C" size_t grl_graphconv_fwd_workspace_size(int64_t num_rows, int32_t num_types, int32_t has_self, int32_t F,
+                                                   int32_t C) {
+  if (num_rows <= 0 || num_types < 1 || F <= 0 || C <= 0) return 0;
+  const int64_t K = (int64_t)(num_types + (has_self ? 1 : 0)) * F;
+  if (K > 2147483647LL) return 0;
+  return ws_align((size_t)num_rows * (size_t)K * 4) + grl_linear_fwd_workspace_size(num_rows, (int32_t)K, C);
+}
+
+extern "C" int grl_graphconv_fwd(const GrlTypedCsr* g, const float* X, int64_t ldx, int32_t F, const float* W,
+                                 const float* bias, int32_t C, int32_t relu, float* out, const GrlDropEdge* de,
+                                 void* workspace, size_t workspace_bytes, grl_stream_t stream) {
+  GRL_CHECK_ARG(g != nullptr, "grl_graphconv_fwd: graph is NULL");
+  GRL_CHECK_ARG(g->num_rows >= 0 && g->num_types >= 1 && g->num_types <= 63,
+                "grl_graphconv_fwd: num_types must be in [1, 63] (got %d)", g->num_types);
+  GRL_CHECK_ARG(F > 0 && ldx >= F && C > 0, "grl_graphconv_fwd: need F > 0, ldx >= F, C > 0");
+  const int64_t M = g->num_rows;
+  if (M == 0) return GRL_OK;
+  GRL_CHECK_ARG(X && W && out && g->rowptr && (g->nnz == 0 || g->colidx), "grl_graphconv_fwd: NULL pointer");
+  const int hs = g->has_self ? 1 : 0;
+  const int64_t K64 = (int64_t)(g->num_types + hs) * F;
+  GRL_CHECK_ARG(K64 <= 2147483647LL, "grl_graphconv_fwd: (has_self + num_types) * F exceeds int32");
+  const int32_t K = (int32_t)K64;
+  hipStream_t st = as_stream(stream);
+  char* ws = static_cast<char*>(workspace);
+  GRL_CHECK_ARG(ws == nullptr || al16(ws), "grl_graphconv_fwd: workspace must be 16-B aligned");
+  const size_t zfull = ws_align((size_t)M * (size_t)K * 4);
+  if (ws && workspace_bytes >= grl_graphconv_fwd_workspace_size(M, g->num_types, hs, F, C)) {
+    // whole graph: Z in the workspace, then the linear (its workspace behind Z)
+    float* Z = reinterpret_cast<float*>(ws);
+    int rc = grl_typed_spmm_fwd(g, X, ldx, F, Z, de, stream);
+    if (rc) return rc;
+    return grl_linear_fwd(Z, K, W, bias, out, M, K, C, relu, ws + zfull, workspace_bytes - zfull, stream);
+  }
+  // Row chunks: Z for R rows at a time (bounded memory), on the x6 GEMM only,
+  // whose per-element arithmetic does not depend on M -- so the result is
+  // bitwise that of the whole-graph call.
+  const bool x6 = x6_shape_ok(M, C, K) && al16(W) && C % 4 == 0;
+  if (!x6 || (g->split && g->split->num_heavy > 0) || !ws)
+    GRL_FAIL(GRL_E_WORKSPACE, "grl_graphconv_fwd: workspace %zu < %zu (row chunking needs the x6 GEMM shape and no "
+             "heavy-row split plan)", workspace_bytes, grl_graphconv_fwd_workspace_size(M, g->num_types, hs, F, C));
+  const size_t planes_bytes = ws_align(x6_ws_bytes(M, C, K));
+  const int64_t per_row = (int64_t)K * 4;
+  int64_t R = workspace_bytes > planes_bytes ? (int64_t)((workspace_bytes - planes_bytes) / per_row) : 0;
+  R = R / LB_M * LB_M;
+  if (R < LB_M)
+    GRL_FAIL(GRL_E_WORKSPACE, "grl_graphconv_fwd: workspace %zu holds fewer than %d rows of Z", workspace_bytes, LB_M);
+  uint16_t* planes = reinterpret_cast<uint16_t*>(ws);
+  float* Z = reinterpret_cast<float*>(ws + planes_bytes);
+  GemmArgs a{};
+  a.B = W;
+  a.ldb = C;
+  a.N = C;
+  a.K = K;
+  a.bias = bias;
+  a.relu = relu;
+  a.lda = K;
+  a.ldc = C;
+  int rc = split_b_planes<false>(a, planes, st);
+  if (rc) return rc;
+  for (int64_t r0 = 0; r0 < M; r0 += R) {
+    const int64_t rows = std::min<int64_t>(R, M - r0);
+    rc = spmm_fwd_rows(g, r0, rows, X, ldx, F, Z, de, st);
+    if (rc) return rc;
+    a.A = Z;
+    a.M = rows;
+    a.C = out + r0 * C;
+    rc = launch_x6_gemm(a, planes, st);
+    if (rc) return rc;
+  }
+  return GRL_OK;
 }
 
 extern "C" size_t grl_linear_bwd_data_workspace_size(int64_t M, int32_t K, int32_t C) {

@@ -121,6 +121,7 @@ __global__ __launch_bounds__(256) void spmm_kernel(
     const int32_t* __restrict__ idx,   // fwd: colidx; bwd: zrow
     const int32_t* __restrict__ eidv,  // bwd: eid (CSR positions); fwd: unused
     const float* __restrict__ vals, uint64_t edge_base, uint64_t self_base,
+    int64_t self_row0,  // fwd: X row of item row 0's self term (row-range launches)
     const float* __restrict__ src, int64_t lds,  // gathered matrix + row stride
     int F, float* __restrict__ out, int64_t ldo, DropDev de, SplitDev sp) {
   using vec_t = typename VecT<VEC>::type;
@@ -162,7 +163,7 @@ __global__ __launch_bounds__(256) void spmm_kernel(
       if (hs && (!BWD || (n < self_rows && !heavy))) {
         float w = 1.0f;
         if (de.active && de.drop_self) w = dropedge_weight(de, 1.0f, self_base + (uint64_t)n);
-        const float* srow = BWD ? (src + n * zstride) : (src + n * lds);
+        const float* srow = BWD ? (src + n * zstride) : (src + (n + self_row0) * lds);
 #pragma unroll
         for (int k = 0; k < NV; ++k) {
           if (cval[k]) {
@@ -438,13 +439,14 @@ template <bool BWD>
 int launch_spmm(int64_t num_rows, int64_t self_rows, int S, int hs, const int32_t* ptr, const int32_t* idx,
                 const int32_t* eid, const float* vals, uint64_t edge_base, uint64_t self_base, const float* src,
                 int64_t lds, int F, float* out, int64_t ldo, const DropDev& de, const GrlSplitPlan* plan,
-                hipStream_t stream, const float* align_probe) {
+                hipStream_t stream, const float* align_probe, int64_t self_row0 = 0, int64_t table_rows = -1) {
   if (num_rows == 0) return GRL_OK;
   SplitDev sp;
   int rc = to_split_dev(plan, F, sp);
   if (rc) return rc;
   // gathered table: X (~num_rows rows of lds floats) forward, dZ rows (S per node) backward
-  const int64_t table_bytes = BWD ? num_rows * (int64_t)S * F * 4 : num_rows * lds * 4;
+  if (table_rows < 0) table_rows = num_rows;
+  const int64_t table_bytes = BWD ? table_rows * (int64_t)S * F * 4 : table_rows * lds * 4;
   const LaunchShape sh = pick_shape(src, align_probe, lds, ldo, F, table_bytes);
   const int64_t items = num_rows + sp.num_chunks;
   const int64_t cap = (int64_t)device_cu_count() * spmm_blocks_per_cu();  // 4-wave blocks per CU in flight
@@ -454,7 +456,7 @@ int launch_spmm(int64_t num_rows, int64_t self_rows, int S, int hs, const int32_
   const bool v = vals != nullptr;
 #define GRL_SPMM_LAUNCH(VEC, NV, U, VALS)                                                                  \
   hipLaunchKernelGGL((spmm_kernel<VEC, NV, U, VALS, BWD>), grid, block, 0, stream, num_rows, self_rows, S, \
-                     hs, ptr, idx, eid, vals, edge_base, self_base, src, lds, F, out, ldo, de, sp)
+                     hs, ptr, idx, eid, vals, edge_base, self_base, self_row0, src, lds, F, out, ldo, de, sp)
   if (sh.vec == 4) {
     if (sh.nv == 1) {
       if (v) GRL_SPMM_LAUNCH(4, 1, 8, true); else GRL_SPMM_LAUNCH(4, 1, 8, false);
@@ -491,6 +493,20 @@ int launch_spmm(int64_t num_rows, int64_t self_rows, int S, int hs, const int32_
 }
 
 }  // namespace
+
+// Z rows [0, rows) = rows [r0, r0 + rows) of A_drop X (grl_graphconv_fwd's
+// row chunks): rowptr offset by r0 rows (edge positions, hence edge ids, stay
+// absolute), self term X row and self id shifted by r0.  Per row identical to
+// the whole-graph launch; no split plan (the caller checks).
+int spmm_fwd_rows(const GrlTypedCsr* g, int64_t r0, int64_t rows, const float* X, int64_t ldx, int F, float* Z,
+                  const GrlDropEdge* de, hipStream_t st) {
+  const int hs = g->has_self ? 1 : 0;
+  const int64_t ldz = (int64_t)(g->num_types + hs) * F;
+  return launch_spmm<false>(rows, rows, g->num_types, hs, g->rowptr + r0 * g->num_types, g->colidx, nullptr, g->vals,
+                            g->edge_id_base, g->self_id_base + (uint64_t)r0, X, ldx, F, Z, ldz, to_dev(de), nullptr,
+                            st, Z, r0, g->num_rows);
+}
+
 }  // namespace grl
 
 using namespace grl;

@@ -194,9 +194,44 @@ class _GraphConv(torch.autograd.Function):
         return dX, None, dW if want_w else None, db, None
 
 
+def graph_conv_infer(X: torch.Tensor, graph: TypedGraph, W: torch.Tensor, b=None, relu: bool = False,
+                     max_workspace_bytes: int = None) -> torch.Tensor:
+    """GraphConv forward for inference through one grl_graphconv_fwd call
+    (aggregation + linear [+ReLU]).  Z lives only in the call's workspace;
+    max_workspace_bytes bounds it (the call then works in row chunks, bitwise
+    equal to the whole-graph result)."""
+    _require_device(X, "node features")
+    if X.dtype != torch.float32 or W.dtype != torch.float32:
+        raise _lib.GrlError("graph_conv_infer: features and weights must be float32")
+    X2 = _rows_view(X)
+    if X2.shape[0] != graph.num_cols:
+        raise _lib.GrlError(f"features have {X2.shape[0]} rows, graph gathers from {graph.num_cols}")
+    F = X2.shape[1]
+    Wc = W.contiguous()
+    C = Wc.shape[1]
+    if Wc.shape[0] != graph.segments * F:
+        raise _lib.GrlError(f"weights have {Wc.shape[0]} rows, expected {graph.segments} x {F}")
+    bc = b.contiguous() if b is not None else None
+    out = torch.empty(graph.num_rows, C, dtype=torch.float32, device=X.device)
+    full = _lib.lib().grl_graphconv_fwd_workspace_size(graph.num_rows, graph.num_types, int(graph.has_self), F, C)
+    ws_bytes = full if max_workspace_bytes is None else min(full, int(max_workspace_bytes))
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=X.device) if ws_bytes else None
+    csr = graph.csr_c(F)
+    de = graph.dropedge.to_c() if graph.dropedge is not None else None
+    call("grl_graphconv_fwd", ctypes.byref(csr), X2.data_ptr(), X2.stride(0), F, Wc.data_ptr(),
+         bc.data_ptr() if bc is not None else None, C, int(relu), out.data_ptr(),
+         ctypes.byref(de) if de is not None else None, ws.data_ptr() if ws is not None else None, ws_bytes,
+         current_stream_handle(X.device))
+    return out
+
+
 def graph_conv(X: torch.Tensor, graph: TypedGraph, W: torch.Tensor, b=None, relu: bool = False) -> torch.Tensor:
     """GraphConv forward (aggregation + linear [+ReLU]) as one autograd node;
-    X: [num_cols, F] (or [B, N, F] for a batch graph)."""
+    X: [num_cols, F] (or [B, N, F] for a batch graph).  When no gradient is
+    wanted (eval, torch.no_grad) it is one grl_graphconv_fwd call instead:
+    the same kernels, so the same bits."""
+    if not (torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in (X, W, b))):
+        return graph_conv_infer(X, graph, W, b, relu)
     return _GraphConv.apply(X, graph, W, b, relu)
 
 

@@ -195,6 +195,26 @@ int grl_linear_fwd(const float* Z, int64_t ldz, const float* W,
                    int32_t C, int32_t relu, void* workspace,
                    size_t workspace_bytes, grl_stream_t stream);
 
+/* One GraphConv layer forward in one call (inference):
+ *   out = relu?( (A_drop X) W + bias )       robust_gcn.py:45-51 (+ the F.relu
+ * of drop_robust_gcn.py:76), i.e. grl_typed_spmm_fwd then grl_linear_fwd with
+ * Z = A_drop X held in `workspace` (W [(has_self+num_types)*F, C] row-major,
+ * bias [C] or NULL, out [num_rows, C] contiguous).  With the workspace of
+ * grl_graphconv_fwd_workspace_size() Z exists whole (7.2 GB at C3); a smaller
+ * workspace makes the call aggregate and multiply rows in chunks that fit
+ * (>= 256 rows of Z plus W's bf16 planes), bitwise equal to the whole-graph
+ * result -- allowed when the linear takes the x6 path (large graphs) and the
+ * graph has no heavy-row split plan, else GRL_E_WORKSPACE.  Replaces the
+ * GraphConv.forward pair `torch.matmul(A, V)` / `matmul(new_V, h_weights)`
+ * for eval; training keeps Z for dW (grl_linear_bwd_weight).              */
+size_t grl_graphconv_fwd_workspace_size(int64_t num_rows, int32_t num_types,
+                                        int32_t has_self, int32_t F, int32_t C);
+int grl_graphconv_fwd(const GrlTypedCsr* g, const float* X, int64_t ldx,
+                      int32_t F, const float* W, const float* bias, int32_t C,
+                      int32_t relu, float* out, const GrlDropEdge* de,
+                      void* workspace, size_t workspace_bytes,
+                      grl_stream_t stream);
+
 /* Backward of grl_linear_fwd (autograd MmBackward0 of robust_gcn.py:50, with
  * the ReLU of drop_robust_gcn.py:76 folded in when relu_out != NULL):
  *   dZ = (g * [relu_out > 0]) W^T           grl_linear_bwd_data,  dZ [M, K] (ld lddz)

@@ -1,0 +1,94 @@
+"""GPU: grl_graphconv_fwd, one GraphConv layer forward in one call
+(robust_gcn.py:45-51): bitwise equal to the two-op path (typed SpMM then the
+linear), for whole-graph and row-chunked workspaces, and within fp32
+tolerance of the oracle's aggregation times W in fp64."""
+import numpy as np
+import pytest
+import torch
+
+from grl import DropEdge, TypedGraph, _lib
+from grl.ops import graph_conv, graph_conv_infer, linear_fwd, typed_aggregate
+from oracle import c_oracle
+from oracle import hash as ohash
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda:0")
+
+
+def _two_op(X, g, W, b, relu):
+    Z = typed_aggregate(X, g)
+    return linear_fwd(Z, W, b, relu)
+
+
+def _planes_bytes(K, C):
+    return 3 * ((C + 255) // 256 * 256) * K * 2 + 256 + 256
+
+
+@pytest.mark.parametrize("N,L,deg,F,C,has_self", [(300, 6, 16.0, 256, 64, True), (129, 6, 8.0, 10, 7, True),
+                                                   (200, 3, 12.0, 100, 36, False), (74, 6, 3.0, 256, 256, True)])
+@pytest.mark.parametrize("relu,bias", [(True, True), (False, False)])
+@pytest.mark.parametrize("di", [0, 1])
+def test_graphconv_small_matches_two_ops_and_oracle(N, L, deg, F, C, has_self, relu, bias, di):
+    rowptr, colidx = ohash.synth_csr(0, L, N, int(N * deg), 11)
+    de = [None, DropEdge(0.3, 7, 1, True)][di]
+    g = TypedGraph.from_csr_host(rowptr, colidx, L, DEV, has_self=has_self).with_dropedge(de)
+    rng = np.random.default_rng(N + F)
+    X = rng.standard_normal((N, F)).astype(np.float32)
+    K = (L + (1 if has_self else 0)) * F
+    W = (rng.standard_normal((K, C)) / np.sqrt(K)).astype(np.float32)
+    b = rng.standard_normal(C).astype(np.float32) if bias else None
+    Xt, Wt = torch.from_numpy(X).to(DEV), torch.from_numpy(W).to(DEV)
+    bt = torch.from_numpy(b).to(DEV) if bias else None
+    out = graph_conv_infer(Xt, g, Wt, bt, relu)
+    ref = _two_op(Xt, g, Wt, bt, relu)
+    assert torch.equal(out, ref)
+    with torch.no_grad():  # graph_conv routes here when no gradient is wanted
+        assert torch.equal(graph_conv(Xt, g, Wt, bt, relu), out)
+    d = None if de is None else c_oracle.drop(de.p, de.seed, de.call, de.drop_self)
+    Z = c_oracle.spmm_fwd(rowptr, colidx, X, L, has_self, d=d).astype(np.float64)
+    o = Z @ W.astype(np.float64) + (b.astype(np.float64) if bias else 0.0)
+    if relu:
+        o = np.maximum(o, 0.0)
+    scale = np.abs(Z) @ np.abs(W.astype(np.float64)) + (np.abs(b.astype(np.float64)) if bias else 0.0)
+    assert np.all(np.abs(out.cpu().numpy() - o) <= 1e-5 * scale + 1e-6)
+
+
+@pytest.mark.parametrize("di", [0, 1])
+def test_graphconv_row_chunks_bitwise(di):
+    """Bounded workspace: rows in chunks (here 12 chunks, the last partial)
+    give the whole-graph bits, which are the two-op bits."""
+    N, L, F, C = 100_003, 6, 256, 256
+    de = [None, DropEdge(0.3, 2, 0, True)][di]
+    g = TypedGraph.synthetic(N, 16.0, L, seed=0, device=DEV).with_dropedge(de)
+    gen = torch.Generator(device=DEV).manual_seed(1)
+    X = torch.randn(N, F, device=DEV, generator=gen)
+    K = (L + 1) * F
+    W = torch.randn(K, C, device=DEV, generator=gen) / K ** 0.5
+    b = torch.randn(C, device=DEV, generator=gen)
+    full = graph_conv_infer(X, g, W, b, True)
+    chunked = graph_conv_infer(X, g, W, b, True, max_workspace_bytes=_planes_bytes(K, C) + 8704 * K * 4)
+    assert torch.equal(full, chunked)
+    assert torch.equal(full, _two_op(X, g, W, b, True))
+
+
+def test_graphconv_workspace_errors():
+    """Chunking needs the x6 GEMM shape and no heavy-row split plan: else a
+    too-small workspace is an error, never a silent fallback."""
+    rowptr, colidx = ohash.synth_csr(0, 6, 300, 4800, 3)
+    g = TypedGraph.from_csr_host(rowptr, colidx, 6, DEV)
+    X = torch.randn(300, 64, device=DEV)
+    W = torch.randn(7 * 64, 32, device=DEV)
+    with pytest.raises(_lib.GrlError, match="workspace"):
+        graph_conv_infer(X, g, W, None, False, max_workspace_bytes=4096)
+    # power-law graph whose heavy rows are split: whole-graph workspace only
+    N, L, F, C = 1 << 16, 6, 256, 256
+    rp, ci = ohash.synth_csr(1, L, N, N * 16, 21)
+    gr = TypedGraph.from_csr_host(rp, ci, L, DEV)
+    gr.split_threshold, gr.split_chunk = 256, 128
+    Xr = torch.randn(N, F, device=DEV)
+    Wr = torch.randn(7 * F, C, device=DEV) / (7 * F) ** 0.5
+    out = graph_conv_infer(Xr, gr, Wr, None, False)
+    assert gr.split_stats()["csr"]["heavy_segments"] > 0
+    assert torch.equal(out, _two_op(Xr, gr, Wr, None, False))
+    with pytest.raises(_lib.GrlError, match="split plan"):
+        graph_conv_infer(Xr, gr, Wr, None, False, max_workspace_bytes=_planes_bytes(7 * F, C) + 4096 * 7 * F * 4)
