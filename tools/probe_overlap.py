@@ -51,6 +51,15 @@ def both():
     torch.cuda.current_stream(dev).wait_stream(s2)
 
 
+def both_gemm_first():
+    s2.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s2):
+        gemm()
+    spmm()
+    torch.cuda.current_stream(dev).wait_stream(s2)
+
+
 a, c = timeit(spmm), timeit(gemm)
 print(f"blocks/CU={os.environ.get('GRL_SPMM_BLOCKS_PER_CU', '16')}: spmm {a:.3f} ms, gemm {c:.3f} ms, "
-      f"sum {a + c:.3f}, concurrent {timeit(both):.3f} ms", flush=True)
+      f"sum {a + c:.3f}, concurrent {timeit(both):.3f} ms, gemm launched first {timeit(both_gemm_first):.3f} ms",
+      flush=True)
