@@ -53,15 +53,17 @@ def test_graphconv_small_matches_two_ops_and_oracle(N, L, deg, F, C, has_self, r
     assert np.all(np.abs(out.cpu().numpy() - o) <= 1e-5 * scale + 1e-6)
 
 
-@pytest.mark.parametrize("di", [0, 1])
-def test_graphconv_row_chunks_bitwise(di):
+@pytest.mark.parametrize("di,strided", [(0, False), (1, False), (2, True)])
+def test_graphconv_row_chunks_bitwise(di, strided):
     """Bounded workspace: rows in chunks (here 12 chunks, the last partial)
-    give the whole-graph bits, which are the two-op bits."""
+    give the whole-graph bits, which are the two-op bits (also with X a
+    column slice of a wider matrix, and DropEdge sparing the self loops)."""
     N, L, F, C = 100_003, 6, 256, 256
-    de = [None, DropEdge(0.3, 2, 0, True)][di]
+    de = [None, DropEdge(0.3, 2, 0, True), DropEdge(0.2, 5, 3, False)][di]
     g = TypedGraph.synthetic(N, 16.0, L, seed=0, device=DEV).with_dropedge(de)
     gen = torch.Generator(device=DEV).manual_seed(1)
-    X = torch.randn(N, F, device=DEV, generator=gen)
+    X = torch.randn(N, F + 64 if strided else F, device=DEV, generator=gen)[:, :F]
+    assert X.stride(0) == (F + 64 if strided else F)
     K = (L + 1) * F
     W = torch.randn(K, C, device=DEV, generator=gen) / K ** 0.5
     b = torch.randn(C, device=DEV, generator=gen)
