@@ -6,7 +6,7 @@
 //   out[m, :] = relu(bias + sum_{k : V[m,k] != 0, ascending k} V[m,k] * Wt[k, :])
 //
 // A dense GEMM would spend 2*K*C flops per row on zeros; here one wave scans
-// its row 64 entries per load, ballots the nonzeros and gathers only those
+// its row 64 entries per lane-load, ballots the nonzeros and gathers only those
 // rows of Wt (K x C, L2-resident: 4.5 MB at 4369 x 256).  V is read once,
 // coalesced; no CSR is built and nothing syncs with the host, so the model's
 // forward stays capturable in a HIP graph.  Sums are one fmaf per nonzero in
@@ -17,24 +17,61 @@
 namespace grl {
 namespace {
 
-constexpr int U = 4;     // nonzero rows of Wt in flight per wave
-constexpr int SCAN = 8;  // 64-entry chunks of a V row loaded together
+constexpr int U = 8;      // nonzero rows of Wt in flight per wave
+constexpr int SCAN = 24;  // 64-entry chunks of a V row loaded together
+constexpr int CAP = 512;  // (k, v) list entries per wave in LDS
 
+// Two phases per row, so that the row's latency is a few load rounds rather
+// than one per nonzero-holding chunk: (1) scan the row SCAN chunks at a time,
+// appending its nonzeros (k ascending) to a per-wave LDS list; (2) walk the
+// list U entries at a time, gathering those Wt rows together.  The list is
+// flushed early when it would overflow (dense rows), which keeps the order.
 template <int CPL>  // output columns per lane: C <= 64 * CPL
 __global__ __launch_bounds__(256) void bag_linear_kernel(const float* __restrict__ V, int64_t ldv, int64_t M, int K,
                                                          const float* __restrict__ Wt, int C,
                                                          const float* __restrict__ bias, int relu,
                                                          float* __restrict__ out, int64_t ldo) {
+  __shared__ int list_k[4][CAP];
+  __shared__ float list_v[4][CAP];
   const int lane = threadIdx.x & 63;
+  int* const lk = list_k[threadIdx.x >> 6];
+  float* const lv = list_v[threadIdx.x >> 6];
+  const uint64_t below = (1ull << lane) - 1;
   const int64_t wave = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int64_t nwaves = ((int64_t)gridDim.x * blockDim.x) >> 6;
   for (int64_t m = wave; m < M; m += nwaves) {
     float acc[CPL];
 #pragma unroll
     for (int c = 0; c < CPL; ++c) acc[c] = 0.0f;
+    int cnt = 0;  // wave-uniform list length
+    auto flush = [&]() {
+      __builtin_amdgcn_wave_barrier();
+      for (int i0 = 0; i0 < cnt; i0 += U) {
+        float w[U][CPL], vj[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const bool ok = i0 + u < cnt;
+          vj[u] = ok ? lv[i0 + u] : 0.0f;
+          const float* wrow = Wt + (int64_t)(ok ? lk[i0 + u] : 0) * C;
+#pragma unroll
+          for (int cc = 0; cc < CPL; ++cc) {
+            const int col = lane + 64 * cc;
+            w[u][cc] = (ok && col < C) ? wrow[col] : 0.0f;
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (i0 + u < cnt) {
+#pragma unroll
+            for (int cc = 0; cc < CPL; ++cc) acc[cc] = fmaf(vj[u], w[u][cc], acc[cc]);
+          }
+      }
+      __builtin_amdgcn_wave_barrier();
+      cnt = 0;
+    };
     const float* vrow = V + m * ldv;
     for (int kb = 0; kb < K; kb += 64 * SCAN) {
-      float vs[SCAN];  // SCAN chunks of the row in flight at once (latency)
+      float vs[SCAN];  // SCAN chunks of the row in flight at once
 #pragma unroll
       for (int c = 0; c < SCAN; ++c) {
         const int k = kb + 64 * c + lane;
@@ -42,40 +79,20 @@ __global__ __launch_bounds__(256) void bag_linear_kernel(const float* __restrict
       }
 #pragma unroll
       for (int c = 0; c < SCAN; ++c) {
-        const int k0 = kb + 64 * c;
-        const float v = vs[c];
-        uint64_t nz = __ballot(v != 0.0f);
-        while (nz) {
-          int jj[U];
-#pragma unroll
-          for (int u = 0; u < U; ++u) {
-            if (nz) {
-              jj[u] = __builtin_ctzll(nz);
-              nz &= nz - 1;
-            } else {
-              jj[u] = -1;
-            }
+        const uint64_t nz = __ballot(vs[c] != 0.0f);
+        if (nz) {
+          const int n = __popcll(nz);
+          if (cnt + n > CAP) flush();
+          if (vs[c] != 0.0f) {
+            const int pos = cnt + __popcll(nz & below);
+            lk[pos] = kb + 64 * c + lane;
+            lv[pos] = vs[c];
           }
-          float w[U][CPL], vj[U];
-#pragma unroll
-          for (int u = 0; u < U; ++u) {
-            vj[u] = __shfl(v, jj[u] < 0 ? 0 : jj[u]);
-            const float* wrow = Wt + (int64_t)(k0 + (jj[u] < 0 ? 0 : jj[u])) * C;
-#pragma unroll
-            for (int cc = 0; cc < CPL; ++cc) {
-              const int col = lane + 64 * cc;
-              w[u][cc] = (jj[u] >= 0 && col < C) ? wrow[col] : 0.0f;
-            }
-          }
-#pragma unroll
-          for (int u = 0; u < U; ++u)
-            if (jj[u] >= 0) {
-#pragma unroll
-              for (int cc = 0; cc < CPL; ++cc) acc[cc] = fmaf(vj[u], w[u][cc], acc[cc]);
-            }
+          cnt += n;
         }
       }
     }
+    flush();
 #pragma unroll
     for (int c = 0; c < CPL; ++c) {
       const int col = lane + 64 * c;
