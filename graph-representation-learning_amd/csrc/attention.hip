@@ -65,6 +65,11 @@ struct AttnArgs {
 
 __device__ __forceinline__ int kappa(int s, int h) { return (s & 3) + 8 * (s >> 2) + 4 * h; }
 
+// e^x for x <= 0 (softmax): one v_mul + v_exp_f32 (1 ulp) instead of expf's
+// range-reduced sequence; exact at x = 0 (so alpha == 1 still detects an
+// unchanged running max) and 0 at x = -inf
+__device__ __forceinline__ float aexp(float x) { return __builtin_amdgcn_exp2f(x * 1.44269504088896341f); }
+
 __device__ __forceinline__ f32x16 zero16() {
   f32x16 z;
 #pragma unroll
@@ -170,11 +175,11 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
     }
     mx = fmaxf(mx, __shfl_xor(mx, 32));
     const float mn = fmaxf(m, mx);
-    const float alpha = expf(m - mn);
+    const float alpha = aexp(m - mn);
     float ps = 0.0f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      s[r] = expf(s[r] - mn);
+      s[r] = aexp(s[r] - mn);
       ps += s[r];
     }
     ps += __shfl_xor(ps, 32);
@@ -262,7 +267,7 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(AttnArgs a) {
     for (int st = 0; st < HV; ++st) dp = MFMA(Hs[l32 * DV + h * HV + st], dor[st], dp);
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const float p = (k0 + kappa(r, h) < N) ? expf(s[r] - mq) * il : 0.0f;
+      const float p = (k0 + kappa(r, h) < N) ? aexp(s[r] - mq) * il : 0.0f;
       s[r] = p * (dp[r] - Dq);  // dS
     }
 #pragma unroll
@@ -354,7 +359,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(AttnArgs a) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int qi = kappa(r, h);
-      const float p = kv ? expf(s[r] - Ms[qi]) * Ls[qi] : 0.0f;
+      const float p = kv ? aexp(s[r] - Ms[qi]) * Ls[qi] : 0.0f;
       s[r] = p;
       ds[r] = p * (dp[r] - Ds[qi]);
     }
@@ -640,19 +645,21 @@ __global__ __launch_bounds__(256) void attn_fwd_x6_kernel(AttnArgs a) {
       const abf16x8_t k2p = *reinterpret_cast<const abf16x8_t*>(&Kp[2 * KPL + off]);
       MFMA6(s, k0p, k1p, k2p, qp[kc][0], qp[kc][1], qp[kc][2]);
     }
+    if (k0 + 32 > k_hi) {  // the last, partial key block only (wave-uniform)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (k0 + kappa(r, h) >= k_hi) s[r] = -INFINITY;
+    }
     float mx = -INFINITY;
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      if (k0 + kappa(r, h) >= k_hi) s[r] = -INFINITY;
-      mx = fmaxf(mx, s[r]);
-    }
+    for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[r]);
     mx = fmaxf(mx, __shfl_xor(mx, 32));
     const float mn = fmaxf(m, mx);
-    const float alpha = expf(m - mn);
+    const float alpha = aexp(m - mn);
     float ps = 0.0f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      s[r] = expf(s[r] - mn);
+      s[r] = aexp(s[r] - mn);
       ps += s[r];
     }
     ps += __shfl_xor(ps, 32);
@@ -854,7 +861,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_x6_kernel(AttnArgs a) {
     }
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const float p = (k0 + kappa(r, h) < k_hi) ? expf(s[r] - mq) * il : 0.0f;
+      const float p = (k0 + kappa(r, h) < k_hi) ? aexp(s[r] - mq) * il : 0.0f;
       s[r] = p * (dp[r] - Dq);  // dS^T
     }
     abf16x8_t dsp[2][3];
@@ -973,7 +980,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_x6_kernel(AttnArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int qi = kappa(r, h);
-        s[r] = kv ? expf(s[r] - Ms[qi]) * Ls[qi] : 0.0f;  // P
+        s[r] = kv ? aexp(s[r] - Ms[qi]) * Ls[qi] : 0.0f;  // P
       }
       abf16x8_t pp[2][3];
       reg_planes(s, pp);
@@ -1001,7 +1008,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_x6_kernel(AttnArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int qi = kappa(r, h);
-        const float p = kv ? expf(s[r] - Ms[qi]) * Ls[qi] : 0.0f;
+        const float p = kv ? aexp(s[r] - Ms[qi]) * Ls[qi] : 0.0f;
         s[r] = p * (dp[r] - Ds[qi]);  // dS
       }
       abf16x8_t dsp[2][3];
@@ -1056,7 +1063,7 @@ __global__ void attn_fwd_combine_kernel(AttnArgs a, int64_t rows, int S) {
     for (int s = 0; s < S; ++s) M = fmaxf(M, pm[s * rows + row]);
     float L = 0.0f, O = 0.0f;
     for (int s = 0; s < S; ++s) {
-      const float w = expf(pm[s * rows + row] - M);
+      const float w = aexp(pm[s * rows + row] - M);
       L += pl[s * rows + row] * w;
       O += a.part[(int64_t)s * n_all + i] * w;
     }
