@@ -860,9 +860,11 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_x6_kernel(AttnArgs a) {
       MFMA6(dp, h0, h1, h2, dop[fc][0], dop[fc][1], dop[fc][2]);
     }
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float p = (k0 + kappa(r, h) < k_hi) ? aexp(s[r] - mq) * il : 0.0f;
-      s[r] = p * (dp[r] - Dq);  // dS^T
+    for (int r = 0; r < 16; ++r) s[r] = aexp(s[r] - mq) * il * (dp[r] - Dq);  // dS^T = P (dP - D)
+    if (k0 + 32 > k_hi) {  // the last, partial key block only (wave-uniform)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        if (k0 + kappa(r, h) >= k_hi) s[r] = 0.0f;
     }
     abf16x8_t dsp[2][3];
     reg_planes(s, dsp);
