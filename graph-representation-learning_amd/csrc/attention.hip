@@ -564,6 +564,42 @@ __device__ __forceinline__ void dma_block(const uint16_t* planes, int64_t ps, in
   }
 }
 
+// dma_block with this lane's chunk addresses computed once: per block only a
+// uniform row offset is added (the last, partial block takes dma_block's
+// clamped path).  Costs 2 VGPRs per chunk slot (the forward has the room).
+template <int W, int LAYOUT>
+struct DmaRows {
+  static constexpr int PL = 32 * W, NI = 3 * PL / 512, NJ = (NI + 3) / 4;
+  const uint16_t* planes;
+  const uint16_t* src[NJ];
+  int64_t ps;
+  __device__ __forceinline__ void init(const uint16_t* planes_, int64_t ps_, int wave, int lane) {
+    planes = planes_;
+    ps = ps_;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int i = wave + 4 * j;
+      const int e = (i < NI ? i : 0) * 512 + lane * 8;
+      const int pl = e / PL, rem = e % PL, r = rem / W, pos = rem % W;
+      int c = pos;
+      if (LAYOUT == PL_HSWZ && W >= 128) c = pos ^ ((r & 3) << 5);
+      if (LAYOUT == PL_SWZ128) c = ((pos >> 3) ^ (((r & 3) << 2) | ((r >> 2) & 3))) << 3;
+      src[j] = planes_ + pl * ps_ + (int64_t)r * W + c;
+    }
+  }
+  __device__ __forceinline__ void issue(int64_t r0, int64_t N, uint16_t* lds, int wave, int lane) const {
+    if (r0 + 32 <= N) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const int i = wave + 4 * j;
+        if (i < NI) adma16(src[j] + r0 * W, lds + i * 512);
+      }
+    } else {
+      dma_block<W, LAYOUT>(planes, ps, r0, N, lds, wave, lane);
+    }
+  }
+};
+
 template <int DKP, int NT, bool PRE, bool SPLIT>
 __global__ __launch_bounds__(256) void attn_fwd_x6_kernel(AttnArgs a) {
   constexpr int DV = NT * 32, KC = DKP / 16;
@@ -602,9 +638,13 @@ __global__ __launch_bounds__(256) void attn_fwd_x6_kernel(AttnArgs a) {
   const uint16_t* Kpb = a.Kpl + b * N * DKP;
   const uint16_t* Hpb = a.Hpl + b * N * DV;
   const bool vk = vec_ok(Kb, a.dk), vh = vec_ok(Hb, a.dv);
+  DmaRows<DKP, PL_PLAIN> kd;
+  DmaRows<DV, PL_HSWZ> hd;
   if constexpr (PRE) {
-    dma_block<DKP, PL_PLAIN>(Kpb, kps, k_lo, N, Kp_s, wave, lane);
-    dma_block<DV, PL_HSWZ>(Hpb, hps, k_lo, N, Hp_s, wave, lane);
+    kd.init(Kpb, kps, wave, lane);
+    hd.init(Hpb, hps, wave, lane);
+    kd.issue(k_lo, N, Kp_s, wave, lane);
+    hd.issue(k_lo, N, Hp_s, wave, lane);
   } else {
     sk.fetch(Kb, k_lo, N, a.dk, vk, tid);
     sh.fetch(Hb, k_lo, N, a.dv, vh, tid);
@@ -623,8 +663,8 @@ __global__ __launch_bounds__(256) void attn_fwd_x6_kernel(AttnArgs a) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
       if (k0 + 32 < k_hi) {
-        dma_block<DKP, PL_PLAIN>(Kpb, kps, k0 + 32, N, Kp_s + (stg ^ 1) * 3 * KPL, wave, lane);
-        dma_block<DV, PL_HSWZ>(Hpb, hps, k0 + 32, N, Hp_s + (stg ^ 1) * 3 * HPL, wave, lane);
+        kd.issue(k0 + 32, N, Kp_s + (stg ^ 1) * 3 * KPL, wave, lane);
+        hd.issue(k0 + 32, N, Hp_s + (stg ^ 1) * 3 * HPL, wave, lane);
       }
     } else {
       sk.store(Kp, tid);  // the staged K and H block -> bf16 planes
