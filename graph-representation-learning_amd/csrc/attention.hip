@@ -970,7 +970,15 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_x6_kernel(AttnArgs a) {
       pd = v ? a.Drow[b * N + qq] : 0.0f;
     }
   };
-  if constexpr (PRE) {
+  // dH (WANT_H) has the VGPR room for precomputed DMA addresses; dK does not
+  DmaRows<32, PL_PLAIN> qd;
+  DmaRows<128, PL_SWZ128> od;
+  if constexpr (PRE && WANT_H) {
+    qd.init(Qpb, qps, wave, lane);
+    od.init(Opb, ops, wave, lane);
+    qd.issue(q_lo, N, Qp_s, wave, lane);
+    od.issue(q_lo, N, Op_s, wave, lane);
+  } else if constexpr (PRE) {
     dma_block<32, PL_PLAIN>(Qpb, qps, q_lo, N, Qp_s, wave, lane);
     dma_block<128, PL_SWZ128>(Opb, ops, q_lo, N, Op_s, wave, lane);
   } else {
@@ -999,7 +1007,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_x6_kernel(AttnArgs a) {
     if constexpr (PRE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (q0 + 32 < q_hi) {
-      if constexpr (PRE) {
+      if constexpr (PRE && WANT_H) {
+        qd.issue(q0 + 32, N, Qp_s + (stg ^ 1) * 3 * 1024, wave, lane);
+        od.issue(q0 + 32, N, Op_s + (stg ^ 1) * 3 * 4096, wave, lane);
+      } else if constexpr (PRE) {
         dma_block<32, PL_PLAIN>(Qpb, qps, q0 + 32, N, Qp_s + (stg ^ 1) * 3 * 1024, wave, lane);
         dma_block<128, PL_SWZ128>(Opb, ops, q0 + 32, N, Op_s + (stg ^ 1) * 3 * 4096, wave, lane);
       } else {
