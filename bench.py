@@ -3,16 +3,23 @@
 MI355X -- BASELINE.json metric "aggregated edges/sec + SpMM HBM GB/s vs
 roofline, d=256, 1/2/4/8 GPU".
 
-    python bench.py [--gpus N --steps K --warmup W]
+    python bench.py [--gpus N --steps K --warmup W] [--workload C3|C4|C5|C2|weak]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
 
-Workload: per GPU a node-range shard of 1M nodes of a
-seeded Erdos-Renyi typed graph (avg total out-degree 32 over L=6 edge
-types, dedupe), d=256 fp32 features -- config C3 at N=1, the C4 shape
-(4M nodes) at N=4.  A step = one GraphConv aggregation forward over the
-rank's rows (N>1: preceded by the halo exchange -- RCCL all-to-all-v of the
-remote feature rows the shard's edges reference, grl/dist.py).  Inputs are resident in HBM before timing.
-Prints ONE JSON line on rank 0.
+Workloads (BASELINE.json configs):
+  C3 (default at N=1)  seeded Erdos-Renyi typed graph, N=1M, avg total
+                       out-degree 32 over L=6 edge types (dedupe), d=256.
+  C4 (default at N>1)  the same generator at a FIXED N=4M, node-range shards
+                       over the N ranks (strong scaling), halo over RCCL.
+  C5                   R-MAT scale 23 (N=8,388,608), avg_deg 64, d=512,
+                       DropEdge p=0.2 fused, edge-balanced shards.
+  C2                   ER N=100k, avg_deg 16, d=256.
+  weak                 1M nodes per GPU (weak scaling; the round-1 N>1 line).
+A step = one GraphConv aggregation forward over the rank's rows; at N>1 it
+includes the halo exchange, pipelined with the aggregation over column slices
+(grl.dist.HaloPipeline: slice c's rows travel while slice c-1 is
+aggregated; bitwise equal to the unsliced result).  Inputs are resident in HBM
+before timing.  Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
 
@@ -34,17 +41,31 @@ HBM_PEAK_GBS = 8000.0     # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
 F32_MFMA_PEAK_TFS = 157.3  # dense fp32 MFMA (v_mfma_f32_32x32x2_f32)
 
 
+WORKLOADS = {  # name: (graph, nodes_total (None: per GPU), avg_deg, d, dropedge p)
+    "C2": ("er", 100_000, 16.0, 256, 0.0),
+    "C3": ("er", 1_000_000, 32.0, 256, 0.0),
+    "C4": ("er", 4_000_000, 32.0, 256, 0.0),
+    "C5": ("rmat", 1 << 23, 64.0, 512, 0.2),
+    "weak": ("er", None, 32.0, 256, 0.0),
+}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--nodes-per-gpu", type=int, default=1_000_000)
-    ap.add_argument("--avg-deg", type=float, default=32.0)
+    ap.add_argument("--workload", choices=["auto"] + list(WORKLOADS), default="auto",
+                    help="auto: C3 on one GPU, C4 (fixed 4M nodes, strong scaling) on several")
+    ap.add_argument("--nodes-per-gpu", type=int, default=None,
+                    help="custom workload: nodes per GPU (overrides --workload's node count)")
+    ap.add_argument("--avg-deg", type=float, default=None)
     ap.add_argument("--types", type=int, default=6)
-    ap.add_argument("--dim", type=int, default=256)
-    ap.add_argument("--p", type=float, default=0.0, help="DropEdge rate inside the timed step (0 = eval)")
-    ap.add_argument("--graph", choices=["er", "rmat"], default="er")
+    ap.add_argument("--dim", type=int, default=None)
+    ap.add_argument("--p", type=float, default=None, help="DropEdge rate inside the timed step (0 = eval)")
+    ap.add_argument("--graph", choices=["er", "rmat"], default=None)
+    ap.add_argument("--chunks", type=int, default=0,
+                    help="N>1: column slices of the pipelined halo exchange (0 = d/128; 1 = serial)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 disables)")
     ap.add_argument("--extras", action="store_true",
                     help="also time fused-DropEdge fwd, backward, MFMA linear and a full layer (not the headline)")
@@ -60,10 +81,37 @@ def parse():
     return ap.parse_args()
 
 
+def resolve_workload(args, world):
+    """Fill graph / nodes / avg_deg / dim / p from --workload, then apply the
+    explicit overrides.  Returns (name, nodes_total, scaling)."""
+    name = args.workload if args.workload != "auto" else ("C3" if world == 1 else "C4")
+    graph, nodes, deg, dim, p = WORKLOADS[name]
+    if nodes is None:
+        nodes = 1_000_000 * world
+    custom = args.nodes_per_gpu is not None or any(
+        v is not None and v != d for v, d in ((args.avg_deg, deg), (args.dim, dim), (args.p, p), (args.graph, graph)))
+    args.graph = args.graph or graph
+    args.avg_deg = deg if args.avg_deg is None else args.avg_deg
+    args.dim = dim if args.dim is None else args.dim
+    args.p = p if args.p is None else args.p
+    if args.nodes_per_gpu is not None:
+        nodes = args.nodes_per_gpu * world
+    if args.graph == "rmat":
+        nodes = 1 << (nodes - 1).bit_length()
+    scaling = "weak" if (name == "weak" or args.nodes_per_gpu is not None) else "strong"
+    if world == 1:
+        scaling = "weak"  # one GPU: nothing to scale; the driver's N=1 line
+    return (name if not custom else name + "-shape (custom)"), nodes, scaling
+
+
 def spmm_bytes(E, N, L, F, p, idx_bytes=4, ptr_bytes=4):
     """Algorithmic HBM bytes of one unfused typed-SpMM forward."""
     keep = 1.0 - p
     return keep * E * F * 4 + idx_bytes * E + ptr_bytes * (N * L + 1) + keep * N * F * 4 + N * (L + 1) * F * 4
+
+
+def _events(n):
+    return [torch.cuda.Event(enable_timing=True) for _ in range(n)]
 
 
 def main():
@@ -91,15 +139,11 @@ def main():
         return
 
     from grl import DropEdge
-    from grl.dist import ShardedGraph, halo_exchange_into
+    from grl.dist import HaloPipeline, ShardedGraph
     from grl.ops import spmm_forward
 
+    wname, N, scaling = resolve_workload(args, world)
     L, F = args.types, args.dim
-    n_loc = args.nodes_per_gpu
-    N = n_loc * world
-    if args.graph == "rmat":
-        N = 1 << (N - 1).bit_length()
-        n_loc = N // world
     t0 = time.time()
     sg = ShardedGraph.synthetic(N, args.avg_deg, L, kind=args.graph, seed=0, device=dev, halo=args.halo)
     graph, plan = sg.graph, sg.plan
@@ -107,103 +151,106 @@ def main():
     E_loc, E_tot = graph.nnz, plan.num_edges_total
     gen = torch.Generator(device=dev)
     gen.manual_seed(1 + rank)
-    # [own rows | halo rows]: own rows are written once, halo rows by the exchange
-    X_full = torch.empty(plan.n_loc + plan.n_halo, F, device=dev)
-    X_full[n_loc:plan.stride].zero_()  # dense plans: shard padding rows (never read by the kernel)
-    X_loc = X_full[:n_loc]
-    X_loc.copy_(torch.randn(n_loc, F, generator=gen, device=dev, dtype=torch.float32))
-    send_buf = torch.empty(plan.send_index.numel(), F, device=dev)
-    build_s = time.time() - t0
-
+    X_loc = torch.randn(n_loc, F, generator=gen, device=dev, dtype=torch.float32)
     de = DropEdge(args.p, 2, 0, True) if args.p > 0 else None
     g_step = graph.with_dropedge(de)
     stream = torch.cuda.current_stream(dev)
     Z = torch.empty(graph.num_rows, graph.segments * F, device=dev)  # preallocated: no allocation in the step
+    chunks = args.chunks or max(1, F // 128)
+    pipe = X_full = None
+    if world > 1:
+        pipe = HaloPipeline(sg, F, chunks=chunks, device=dev)
 
-    def gather():
-        halo_exchange_into(X_loc, X_full, send_buf, plan)
+        def step():
+            pipe.run(X_loc, Z, de)
+    else:
+        X_full = X_loc
 
-    def spmm():
-        return spmm_forward(X_full, g_step, out=Z)
+        def step():
+            spmm_forward(X_full, g_step, out=Z)
+    build_s = time.time() - t0
 
     if args.only is not None:
-        run_only(args, graph, X_full, gather, spmm, L, F)
+        if world > 1:
+            raise SystemExit("--only profiles one GPU")
+        run_only(args, graph, X_full, step, L, F)
         return
 
     for _ in range(args.warmup):
-        gather()
-        spmm()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
-    ev_h = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+        step()
+    ev_s, ev_e = _events(args.steps), _events(args.steps)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     for i in range(args.steps):
-        ev_h[i].record(stream)
-        gather()
-        ev[i][0].record(stream)
-        spmm()
-        ev[i][1].record(stream)
+        ev_s[i].record(stream)
+        step()
+        ev_e[i].record(stream)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t_start
-    per_step = [a.elapsed_time(b) for a, b in ev]
-    kern_ms = float(np.mean(per_step))
-    halo_ms = float(np.mean([h.elapsed_time(a) for h, (a, _) in zip(ev_h, ev)]))
+    per_step = [a.elapsed_time(b) for a, b in zip(ev_s, ev_e)]
+    step_ev_ms = float(np.mean(per_step))
+    halo = None
     if world > 1:
-        tt = torch.tensor([wall, kern_ms, halo_ms], dtype=torch.float64,
+        halo = halo_breakdown(args, pipe, X_loc, Z, de, g_step, dev)
+        kern_ms = halo["spmm_only_ms"]
+        tt = torch.tensor([wall, kern_ms, step_ev_ms], dtype=torch.float64,
                           device=dev if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        wall, kern_ms, halo_ms = float(tt[0]), float(tt[1]), float(tt[2])
+        wall, kern_ms, step_ev_ms = float(tt[0]), float(tt[1]), float(tt[2])
+    else:
+        kern_ms = step_ev_ms
     ms_step = wall / args.steps * 1e3
     value = E_tot / (wall / args.steps)
 
     bytes_launch = spmm_bytes(E_loc, n_loc, L, F, args.p)
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
     traffic = load_traffic(args, n_loc, world)
+    gname = "Erdos-Renyi" if args.graph == "er" else "R-MAT (a,b,c,d = 0.57,0.19,0.19,0.05)"
     out = {
         "metric": METRIC, "value": value, "unit": "edges/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True, "scaling": "weak",
+        "warmup": args.warmup, "ms_per_step": ms_step, "higher_is_better": True, "scaling": scaling,
         "vs_baseline": None, "dtype": "f32",
-        "data": f"synthetic: seeded {'Erdos-Renyi' if args.graph == 'er' else 'R-MAT'} typed graph (graph seed 0), "
-                "X ~ N(0,1) fp32 (seed 1+rank)",
-        "config": {"workload": workload_name(args, world, n_loc) + f": {args.graph.upper()} typed graph, "
-                   f"{n_loc} nodes/GPU, avg_deg {args.avg_deg:g} over L={L} edge types, d={F}, typed-SpMM "
-                   f"forward (GraphConv aggregation){' + DropEdge p=%g' % args.p if args.p else ''}",
-                   "nodes_total": N, "edges_total": E_tot, "nodes_per_gpu": n_loc, "avg_deg": args.avg_deg,
+        "data": f"synthetic: seeded {gname} typed graph (graph seed 0), X ~ N(0,1) fp32 (seed 1+rank)",
+        "config": {"workload": wname, "description": f"{args.graph.upper()} typed graph, {N} nodes "
+                   f"({'one GPU' if world == 1 else f'{world} node-range shards'}), avg_deg {args.avg_deg:g} over "
+                   f"L={L} edge types, d={F}, typed-SpMM forward (GraphConv aggregation)"
+                   f"{' + DropEdge p=%g' % args.p if args.p else ''}",
+                   "nodes_total": N, "edges_total": E_tot, "nodes_per_gpu_rank0": n_loc, "avg_deg": args.avg_deg,
                    "num_types": L, "d": F, "dropedge_p": args.p, "graph": args.graph,
                    "parallelism": "single GPU" if world == 1 else
                    f"node-range shards x{world}, "
                    + ("RCCL" if args.dist_backend == "nccl" else f"{args.dist_backend} (host-staged)") + " "
                    + ("all-gather (dense halo)" if plan.mode == "dense" else "all-to-all-v (sparse halo)")
-                   + f", rank {rank} references {plan.referenced_halo_rows} of {N - n_loc} remote rows"},
+                   + f" pipelined over {chunks} column slices, rank 0 references {plan.referenced_halo_rows} of "
+                   f"{N - n_loc} remote rows"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "spmm_kernel<4,1,8,false,false> (grl_typed_spmm_fwd)",
-                     "kernel_ms": kern_ms, "kernel_ms_min_max": [min(per_step), max(per_step)],
+                     "kernel": "spmm_kernel<4,1,8,false,false> (grl_typed_spmm_fwd)" if world == 1 else
+                     f"spmm_kernel (grl_typed_spmm_fwd_slice, {chunks} slices of {F // chunks} columns)",
+                     "kernel_ms": kern_ms, "kernel_ms_min_max": [min(per_step), max(per_step)] if world == 1 else None,
                      "algorithmic_bytes_per_launch": bytes_launch},
         "build_s": build_s,
     }
-    if world > 1:
-        rows_in = (world - 1) * plan.stride if plan.mode == "dense" else sum(plan.recv_counts)
-        out["halo"] = {"mode": plan.mode, "ms_max_over_ranks": halo_ms, "rows_received_rank0": rows_in,
-                       "GB_received_rank0": rows_in * F * 4 / 1e9,
-                       "GBps_rank0": rows_in * F * 4 / 1e9 / (halo_ms * 1e-3) if halo_ms > 0 else None}
+    if halo is not None:
+        out["halo"] = halo
     if args.graph == "rmat":
         out["config"]["split"] = graph.split_stats()
         out["config"]["max_row_edges"] = int((graph.rowptr[L::L] - graph.rowptr[:-1:L]).max())
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         out["cpu_baseline"], out["parity"] = cpu_baseline(args, g_step, X_loc, Z, L, F)
-    if args.extras:
-        out["extras"] = extras(args, graph, X_full, gather, L, F, dev, E_loc, n_loc)
-        if rank == 0:
-            del X_full, Z
-            torch.cuda.empty_cache()  # C1 is a small-graph workload: time it without C3's 8 GB resident
-            out["extras"]["c1_debug_json"] = c1_extras(dev)
-            out["extras"]["model_one_graph_100k"] = model_extras(dev)
-            out["extras"]["model_dense_A_mid_n"] = model_mid_extras(dev)
+    if world == 1 and wname.startswith("C3"):
+        out["dropedge_train_p0.3"] = dropedge_train(graph, X_loc, E_loc, max(3, min(10, args.steps)))
+    if args.extras and world == 1:
+        out["extras"] = extras(args, graph, X_loc, L, F, dev, E_loc, n_loc)
+        del X_loc, X_full, Z
+        torch.cuda.empty_cache()  # C1 is a small-graph workload: time it without C3's 8 GB resident
+        out["extras"]["c1_debug_json"] = c1_extras(dev)
+        out["extras"]["model_one_graph_100k"] = model_extras(dev)
+        out["extras"]["model_dense_A_mid_n"] = model_mid_extras(dev)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -211,17 +258,55 @@ def main():
         dist.destroy_process_group()
 
 
-def workload_name(args, world, n_loc):
-    """Which SURVEY.md §8(d) config this run is (or is shaped like)."""
-    if args.graph == "rmat":
-        return "C5" if (n_loc * world == 1 << 23 and args.dim == 512) else "C5-shape"
-    if args.dim == 256 and args.avg_deg == 32 and n_loc == 1_000_000:
-        return {1: "C3", 4: "C4"}.get(world, "C4-shape (1M nodes/GPU)")
-    if args.dim == 256 and args.avg_deg == 32 and n_loc * world == 4_000_000:
-        return "C4"
-    if args.dim == 256 and args.avg_deg == 16 and n_loc * world == 100_000:
-        return "C2"
-    return "custom"
+def halo_breakdown(args, pipe, X_loc, Z, de, g_step, dev, iters=None):
+    """Where an N>1 step goes (this rank; the caller takes the max over ranks
+    of the aggregation alone): the exchange alone, the aggregation alone (all
+    slices, tables resident), and the serial sum -- next to the pipelined step
+    the headline times."""
+    from grl.ops import spmm_forward_slice
+
+    iters = iters or max(3, min(10, args.steps))
+    g = g_step
+
+    def exchange_only():
+        pipe._pack(X_loc)
+        for c in range(pipe.K):
+            pipe._exchange(c) if pipe.side is None else _wait(pipe._exchange(c))
+
+    def aggregate_only():
+        for c in range(pipe.K):
+            spmm_forward_slice(pipe.tables[c], g, Z, c * pipe.Fc)
+
+    def _wait(w):
+        if w is not None:
+            w.wait()
+
+    ex = _time(exchange_only, iters)
+    ag = _time(aggregate_only, iters)
+    plan = pipe.plan
+    world = len(plan.bounds) - 1
+    rows_in = (world - 1) * plan.stride if plan.mode == "dense" else sum(plan.recv_counts)
+    return {"mode": plan.mode, "chunks": pipe.K, "exchange_only_ms": ex, "spmm_only_ms": ag,
+            "serial_sum_ms": ex + ag, "rows_received_rank0": rows_in,
+            "GB_received_rank0": rows_in * pipe.F * 4 / 1e9,
+            "GBps_received_rank0": rows_in * pipe.F * 4 / 1e9 / (ex * 1e-3) if ex > 0 else None}
+
+
+def dropedge_train(graph, X, E, iters):
+    """The training-mode aggregation next to the headline: fused DropEdge
+    p=0.3 forward and its backward (CSC gather, same regenerated mask)."""
+    from grl import DropEdge
+    from grl.ops import spmm_backward, spmm_forward
+
+    g = graph.with_dropedge(DropEdge(0.3, 2, 7, True))
+    graph.csc()  # built once per graph, cached (not part of the step)
+    Zd = spmm_forward(X, g)
+    dZ = torch.randn_like(Zd)
+    fwd = _time(lambda: spmm_forward(X, g, out=Zd), iters)
+    bwd = _time(lambda: spmm_backward(dZ, g, X.shape[1]), iters)
+    del Zd, dZ
+    return {"fwd_ms": fwd, "bwd_ms": bwd, "fwd_bwd_edges_per_s": E / ((fwd + bwd) * 1e-3),
+            "note": "fused DropEdge p=0.3 (seed 2, call 7): forward SpMM + CSC-gather backward"}
 
 
 def load_traffic(args, n_loc, world):
@@ -239,22 +324,53 @@ def load_traffic(args, n_loc, world):
         return None
 
 
+def host_cpu_info():
+    """The host the CPU baseline runs on: model name, logical CPUs the OS
+    reports, the CPUs this process may run on, and the cgroup CPU quota."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = os.cpu_count()
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            quota = None if q == "max" else float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    return {"cpu_model": model, "os_cpu_count": os.cpu_count(), "affinity_cpus": affinity, "cgroup_cpu_quota": quota}
+
+
+def cpu_threads(info):
+    """every core the process can use -- os.cpu_count()
+    unless the affinity mask or the cgroup quota grants fewer (threads beyond
+    those only time-slice the same cores)."""
+    n = info["os_cpu_count"] or 1
+    n = min(n, info["affinity_cpus"] or n)
+    if info["cgroup_cpu_quota"]:
+        n = min(n, max(1, int(info["cgroup_cpu_quota"])))
+    return n
+
+
 def cpu_baseline(args, graph, X, Z, L, F):
-    """Oracle (grl_oracle.c, OpenMP) on a bounded row sample of the SAME
-    graph and features; also checks the GPU rows of that sample bitwise."""
+    """Oracle (grl_oracle.c, OpenMP) over the WHOLE graph and the same
+    features, with every usable host core; also checks every GPU row of Z
+    bitwise against it."""
     from oracle import c_oracle
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0")) or min(16, os.cpu_count() or 1)
-    # a contiguous row range from the middle of the graph holding ~3.2M edges
-    # (= 100k rows of C3; on R-MAT the bulk of rows, not the hub head)
-    node_ptr = graph.rowptr[::L].contiguous()
-    r0 = graph.num_rows // 2
-    target = torch.tensor([int(node_ptr[r0]) + 3_200_000], dtype=torch.int32, device=node_ptr.device)
-    r1 = max(r0 + 1, min(graph.num_rows, int(torch.searchsorted(node_ptr, target))))
-    rows = r1 - r0
-    e0 = int(node_ptr[r0])
-    rowptr = (graph.rowptr[r0 * L: r1 * L + 1] - e0).cpu().numpy()
-    colidx = graph.colidx[e0: e0 + int(rowptr[-1])].cpu().numpy()
+    info = host_cpu_info()
+    threads = cpu_threads(info)
+    rowptr = graph.rowptr.cpu().numpy()
+    colidx = graph.colidx.cpu().numpy()
     Xh = X.cpu().numpy()
     E = int(rowptr[-1])
     d = None if args.p <= 0 else c_oracle.drop(args.p, 2, 0, True)  # the timed step's DropEdge stream
@@ -263,19 +379,19 @@ def cpu_baseline(args, graph, X, Z, L, F):
     passes = 0
     while True:
         Zc = c_oracle.spmm_fwd(rowptr, colidx, Xh, L, True, d=d, nthreads=threads, split=split,
-                               edge_base=graph.edge_id_base + e0, self_base=graph.self_id_base + r0,
-                               X_self=Xh[r0:])
+                               edge_base=graph.edge_id_base, self_base=graph.self_id_base)
         passes += 1
         if time.perf_counter() - t0 >= args.cpu_seconds:
             break
     dt = time.perf_counter() - t0
-    Zg = Z[r0:r1].cpu().numpy()
-    diff = float(np.abs(Zg.astype(np.float64) - Zc).max())
+    Zg = Z.cpu().numpy()
+    equal = bool(np.array_equal(Zg, Zc))
+    diff = 0.0 if equal else float(np.abs(Zg.astype(np.float64) - Zc).max())
     cpu = {"value": E * passes / dt, "unit": "edges/s", "cores": threads, "kind": "port",
-           "sample": f"nodes [{r0}, {r1}) ({E} typed edges) of the same graph and X, {passes} passes in {dt:.1f}s; "
-                     f"oracle/grl_oracle.c OpenMP typed-CSR SpMM"}
-    parity = {"rows_checked": rows, "max_abs_diff": diff, "bitwise_equal": bool(np.array_equal(Zg, Zc)),
-              "tolerance": 1e-4}
+           "sample": f"the whole graph ({graph.num_rows} nodes, {E} typed edges) and X, {passes} pass(es) in "
+                     f"{dt:.1f}s; oracle/grl_oracle.c OpenMP typed-CSR SpMM, {threads} threads",
+           **info}
+    parity = {"rows_checked": int(graph.num_rows), "max_abs_diff": diff, "bitwise_equal": equal, "tolerance": 1e-4}
     return cpu, parity
 
 
@@ -292,7 +408,7 @@ def _time(fn, iters, warm=1):
     return s.elapsed_time(e) / iters
 
 
-def extras(args, graph, X_full, gather, L, F, dev, E_loc, n_loc):
+def extras(args, graph, X_full, L, F, dev, E_loc, n_loc):
     """Secondary numbers (not the headline): fused DropEdge forward, backward
     (transposed gather), MFMA linear, full GraphConv layer fwd+bwd."""
     from grl import DropEdge
@@ -496,7 +612,7 @@ def model_mid_extras(dev, sizes=(512, 2048, 4096), iters=5):
     return out
 
 
-def run_only(args, graph, X_full, gather, spmm, L, F):
+def run_only(args, graph, X_full, spmm, L, F):
     """Kernel-isolated loop for rocprofv3 (kernel trace / PMC passes)."""
     from grl.ops import linear_fwd, typed_aggregate
 

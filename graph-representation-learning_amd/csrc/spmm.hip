@@ -89,6 +89,13 @@ __device__ __forceinline__ void vstore(float* p, const float& v) {
 #endif
 }
 
+// GRL_SPMM_PAIR=0 (read on every launch) sends narrow forward rows to the
+// whole-row kernel instead of spmm_pair_kernel (A/B aid and tests).
+bool pair_rows_enabled() {
+  const char* e = getenv("GRL_SPMM_PAIR");
+  return !(e && e[0] == '0');
+}
+
 // Persistent-grid size: 16 four-wave blocks per CU (tuned on C3).  The
 // GRL_SPMM_BLOCKS_PER_CU environment variable overrides it (tuning aid, e.g.
 // to leave room for a concurrent GEMM on another stream).
@@ -123,7 +130,9 @@ __global__ __launch_bounds__(256) void spmm_kernel(
     const float* __restrict__ vals, uint64_t edge_base, uint64_t self_base,
     int64_t self_row0,  // fwd: X row of item row 0's self term (row-range launches)
     const float* __restrict__ src, int64_t lds,  // gathered matrix + row stride
-    int F, float* __restrict__ out, int64_t ldo, DropDev de, SplitDev sp) {
+    int F, float* __restrict__ out, int64_t ldo,
+    int zseg,  // fwd: floats between output segments (F, or the full width for a column slice)
+    DropDev de, SplitDev sp) {
   using vec_t = typename VecT<VEC>::type;
   const int lane = threadIdx.x & 63;
   const int cbase = blockIdx.y * (64 * VEC * NV);
@@ -180,7 +189,7 @@ __global__ __launch_bounds__(256) void spmm_kernel(
         }
       }
       if (heavy) continue;  // typed segments come from the chunk partials (fixup)
-      obase = BWD ? orow : orow + hs * F;
+      obase = BWD ? orow : orow + hs * zseg;
     }
 
     // ---- gather-accumulate over the item's edges ------------------------
@@ -237,7 +246,7 @@ __global__ __launch_bounds__(256) void spmm_kernel(
               while (e >= seg_end) {  // flush finished segments (wave-uniform)
 #pragma unroll
                 for (int k = 0; k < NV; ++k) {
-                  if (cval[k]) vstore(obase + t * F + coff[k], acc[k]);
+                  if (cval[k]) vstore(obase + t * zseg + coff[k], acc[k]);
                   vzero(acc[k]);
                 }
                 ++t;
@@ -255,9 +264,138 @@ __global__ __launch_bounds__(256) void spmm_kernel(
     for (; t < nseg; ++t) {
 #pragma unroll
       for (int k = 0; k < NV; ++k) {
-        if (cval[k]) vstore(obase + t * F + coff[k], acc[k]);
+        if (cval[k]) vstore(obase + t * zseg + coff[k], acc[k]);
         vzero(acc[k]);
       }
+    }
+  }
+}
+
+// Narrow rows (forward, F <= 128 in float4 columns: the column slices of a
+// pipelined halo exchange).  A whole-row wave would leave half its lanes idle
+// and move 512 B per gather instruction; here every gather instruction
+// fetches two edges' rows -- lanes 0-31 edge j, lanes 32-63 edge j+1 -- and
+// v_permlane32_swap hands edge j+1's row to lanes 0-31, which accumulate the
+// two in CSR order (fmaf chain identical to spmm_kernel: bitwise equal).
+// Lanes 32-63 only fetch; stores and the self term are lanes 0-31's.
+__device__ __forceinline__ float swap_halves(float x) {
+  return __uint_as_float(__builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false)[1]);
+}
+
+template <int U, bool VALS>
+__global__ __launch_bounds__(256) void spmm_pair_kernel(
+    int64_t num_rows, int S, int hs, const int32_t* __restrict__ ptr, const int32_t* __restrict__ idx,
+    const float* __restrict__ vals, uint64_t edge_base, uint64_t self_base, int64_t self_row0,
+    const float* __restrict__ src, int64_t lds, int F, float* __restrict__ out, int64_t ldo, int zseg, DropDev de,
+    SplitDev sp) {
+  const int lane = threadIdx.x & 63;
+  const int half = lane >> 5;
+  const int coff = (lane & 31) * 4;
+  const bool ld_ok = coff < F;
+  const bool own = half == 0 && ld_ok;
+  const int64_t wave0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + uniform_i(threadIdx.x >> 6);
+  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const int64_t num_items = sp.num_chunks + num_rows;
+
+  for (int64_t item = wave0; item < num_items; item += nwaves) {
+    float4 acc;
+    vzero(acc);
+    int pv, nseg;
+    float* obase;
+    if (item < sp.num_chunks) {
+      const int64_t c = item;
+      pv = lane == 0 ? sp.chunk_begin[c] : (lane == 1 ? sp.chunk_end[c] : 0);
+      nseg = 1;
+      obase = sp.partials + c * F;
+    } else {
+      const int64_t n = item - sp.num_chunks;
+      float* orow = out + n * ldo;
+      pv = lane <= S ? ptr[n * S + lane] : 0;
+      nseg = S;
+      const bool heavy = readlane_i(pv, nseg) - readlane_i(pv, 0) > sp.threshold;
+      if (hs) {
+        float w = 1.0f;
+        if (de.active && de.drop_self) w = dropedge_weight(de, 1.0f, self_base + (uint64_t)n);
+        if (own) {
+          float4 x;
+          if (w != 0.0f)
+            x = vmul(w, *reinterpret_cast<const float4*>(src + (n + self_row0) * lds + coff));
+          else
+            vzero(x);
+          vstore(orow + coff, x);
+        }
+      }
+      if (heavy) continue;
+      obase = orow + hs * zseg;
+    }
+
+    const int e_begin = readlane_i(pv, 0);
+    const int e_end = readlane_i(pv, nseg);
+    int t = 0;
+    int seg_end = readlane_i(pv, 1);
+    for (int c0 = e_begin; c0 < e_end; c0 += 64) {
+      const int cnt = min(64, e_end - c0);
+      int sidx = 0;
+      float w = 0.0f;
+      if (lane < cnt) {
+        sidx = idx[c0 + lane];
+        const float v = VALS ? vals[c0 + lane] : 1.0f;
+        w = de.active ? dropedge_weight(de, v, edge_base + (uint64_t)(c0 + lane)) : v;
+      }
+      uint64_t kept = __ballot(w != 0.0f);
+      while (kept) {
+        int jj[2 * U];
+#pragma unroll
+        for (int u = 0; u < 2 * U; ++u) {
+          if (kept) {
+            jj[u] = __builtin_ctzll(kept);
+            kept &= kept - 1;
+          } else {
+            jj[u] = -1;
+          }
+        }
+        float4 xv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int ja = jj[2 * u], jb = jj[2 * u + 1];
+          if (ja >= 0) {
+            const int ra = readlane_i(sidx, ja);
+            const int rb = jb >= 0 ? readlane_i(sidx, jb) : ra;
+            const int r = half ? rb : ra;
+            if (ld_ok && (half == 0 || jb >= 0))
+              xv[u] = *reinterpret_cast<const float4*>(src + (int64_t)r * lds + coff);
+            else
+              vzero(xv[u]);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int j = jj[2 * u + h];
+            if (j < 0) continue;
+            const int e = c0 + j;
+            while (e >= seg_end) {  // flush finished segments (wave-uniform)
+              if (own) vstore(obase + t * zseg + coff, acc);
+              vzero(acc);
+              ++t;
+              seg_end = readlane_i(pv, t + 1);
+            }
+            const float wj = readlane_f(w, j);
+            if (h == 0) {
+              vfma(acc, wj, xv[u]);
+            } else {
+              const float4 y = make_float4(swap_halves(xv[u].x), swap_halves(xv[u].y), swap_halves(xv[u].z),
+                                           swap_halves(xv[u].w));
+              vfma(acc, wj, y);
+            }
+          }
+        }
+      }
+    }
+    for (; t < nseg; ++t) {
+      if (own) vstore(obase + t * zseg + coff, acc);
+      vzero(acc);
     }
   }
 }
@@ -268,7 +406,7 @@ template <int VEC, int NV, bool BWD>
 __global__ __launch_bounds__(256) void spmm_fixup_kernel(
     int64_t num_heavy, const int32_t* __restrict__ heavy_seg, const int32_t* __restrict__ heavy_cptr,
     const float* __restrict__ partials, int nseg, int S, int hs, int64_t self_rows, uint64_t self_base,
-    const float* __restrict__ dZ, int F, float* __restrict__ out, int64_t ldo, DropDev de) {
+    const float* __restrict__ dZ, int F, float* __restrict__ out, int64_t ldo, int zseg, DropDev de) {
   using vec_t = typename VecT<VEC>::type;
   const int lane = threadIdx.x & 63;
   const int cbase = blockIdx.y * (64 * VEC * NV);
@@ -284,7 +422,7 @@ __global__ __launch_bounds__(256) void spmm_fixup_kernel(
       w_self = 1.0f;
       if (de.active && de.drop_self) w_self = dropedge_weight(de, 1.0f, self_base + (uint64_t)n);
     }
-    float* orow = BWD ? out + n * ldo : out + n * ldo + (hs + t) * F;
+    float* orow = BWD ? out + n * ldo : out + n * ldo + (hs + t) * zseg;
 #pragma unroll
     for (int k = 0; k < NV; ++k) {
       const int col = cbase + (k * 64 + lane) * VEC;
@@ -397,9 +535,10 @@ int64_t wide_table_bytes() {
   return (int64_t)12 << 30;
 }
 
-LaunchShape pick_shape(const float* a, const float* b, int64_t lda, int64_t ldb, int F, int64_t table_bytes) {
+LaunchShape pick_shape(const float* a, const float* b, int64_t lda, int64_t ldb, int F, int64_t table_bytes,
+                       int zseg) {
   const bool al = (reinterpret_cast<uintptr_t>(a) % 16 == 0) && (reinterpret_cast<uintptr_t>(b) % 16 == 0) &&
-                  (lda % 4 == 0) && (ldb % 4 == 0) && (F % 4 == 0);
+                  (lda % 4 == 0) && (ldb % 4 == 0) && (F % 4 == 0) && (zseg % 4 == 0);
   if (al) {
     // One float4 per lane, 256 columns per wave: wider rows go to more waves
     // along grid.y (each re-reads the row's indices) instead of more
@@ -439,7 +578,9 @@ template <bool BWD>
 int launch_spmm(int64_t num_rows, int64_t self_rows, int S, int hs, const int32_t* ptr, const int32_t* idx,
                 const int32_t* eid, const float* vals, uint64_t edge_base, uint64_t self_base, const float* src,
                 int64_t lds, int F, float* out, int64_t ldo, const DropDev& de, const GrlSplitPlan* plan,
-                hipStream_t stream, const float* align_probe, int64_t self_row0 = 0, int64_t table_rows = -1) {
+                hipStream_t stream, const float* align_probe, int64_t self_row0 = 0, int64_t table_rows = -1,
+                int zseg = 0) {
+  if (zseg <= 0) zseg = F;
   if (num_rows == 0) return GRL_OK;
   SplitDev sp;
   int rc = to_split_dev(plan, F, sp);
@@ -447,7 +588,7 @@ int launch_spmm(int64_t num_rows, int64_t self_rows, int S, int hs, const int32_
   // gathered table: X (~num_rows rows of lds floats) forward, dZ rows (S per node) backward
   if (table_rows < 0) table_rows = num_rows;
   const int64_t table_bytes = BWD ? table_rows * (int64_t)S * F * 4 : table_rows * lds * 4;
-  const LaunchShape sh = pick_shape(src, align_probe, lds, ldo, F, table_bytes);
+  const LaunchShape sh = pick_shape(src, align_probe, lds, ldo, F, table_bytes, zseg);
   const int64_t items = num_rows + sp.num_chunks;
   const int64_t cap = (int64_t)device_cu_count() * spmm_blocks_per_cu();  // 4-wave blocks per CU in flight
   const int64_t gx = std::min<int64_t>(ceil_div(items, 4), cap);
@@ -456,9 +597,17 @@ int launch_spmm(int64_t num_rows, int64_t self_rows, int S, int hs, const int32_
   const bool v = vals != nullptr;
 #define GRL_SPMM_LAUNCH(VEC, NV, U, VALS)                                                                  \
   hipLaunchKernelGGL((spmm_kernel<VEC, NV, U, VALS, BWD>), grid, block, 0, stream, num_rows, self_rows, S, \
-                     hs, ptr, idx, eid, vals, edge_base, self_base, self_row0, src, lds, F, out, ldo, de, sp)
+                     hs, ptr, idx, eid, vals, edge_base, self_base, self_row0, src, lds, F, out, ldo, zseg, de, sp)
   if (sh.vec == 4) {
-    if (sh.nv == 1) {
+    if (sh.nv == 1 && F <= 128 && !BWD && pair_rows_enabled()) {
+      // narrow rows (column slices of a pipelined halo): two edges per gather instruction
+      if (v)
+        hipLaunchKernelGGL((spmm_pair_kernel<8, true>), grid, block, 0, stream, num_rows, S, hs, ptr, idx, vals,
+                           edge_base, self_base, self_row0, src, lds, F, out, ldo, zseg, de, sp);
+      else
+        hipLaunchKernelGGL((spmm_pair_kernel<8, false>), grid, block, 0, stream, num_rows, S, hs, ptr, idx, vals,
+                           edge_base, self_base, self_row0, src, lds, F, out, ldo, zseg, de, sp);
+    } else if (sh.nv == 1) {
       if (v) GRL_SPMM_LAUNCH(4, 1, 8, true); else GRL_SPMM_LAUNCH(4, 1, 8, false);
     } else {
       if (v) GRL_SPMM_LAUNCH(4, 2, 4, true); else GRL_SPMM_LAUNCH(4, 2, 4, false);
@@ -480,7 +629,7 @@ int launch_spmm(int64_t num_rows, int64_t self_rows, int S, int hs, const int32_
 #define GRL_FIXUP_LAUNCH(VEC, NV)                                                                            \
   hipLaunchKernelGGL((spmm_fixup_kernel<VEC, NV, BWD>), fgrid, block, 0, stream, plan->num_heavy,            \
                      plan->heavy_seg, plan->heavy_cptr, plan->partials, nseg, S, hs, self_rows, self_base, src, \
-                     F, out, ldo, de)
+                     F, out, ldo, zseg, de)
     if (sh.vec == 4) {
       if (sh.nv == 1) GRL_FIXUP_LAUNCH(4, 1); else GRL_FIXUP_LAUNCH(4, 2);
     } else {
@@ -562,6 +711,27 @@ extern "C" int grl_typed_spmm_fwd(const GrlTypedCsr* g, const float* X, int64_t 
   return launch_spmm<false>(g->num_rows, g->num_rows, g->num_types, hs, g->rowptr, g->colidx, nullptr, g->vals,
                             g->edge_id_base, g->self_id_base, X, ldx, F, Z, ldz, to_dev(de), g->split,
                             as_stream(stream), Z);
+}
+
+extern "C" int grl_typed_spmm_fwd_slice(const GrlTypedCsr* g, const float* X, int64_t ldx, int32_t F,
+                                        int64_t self_col0, float* Z, int64_t ldz, int32_t zseg,
+                                        const GrlDropEdge* de, grl_stream_t stream) {
+  GRL_CHECK_ARG(g != nullptr, "grl_typed_spmm_fwd_slice: graph is NULL");
+  GRL_CHECK_ARG(g->num_rows >= 0 && g->num_types >= 1 && g->num_types <= 63,
+                "grl_typed_spmm_fwd_slice: num_types must be in [1, 63] (got %d)", g->num_types);
+  GRL_CHECK_ARG(F > 0 && ldx >= F && zseg >= F && self_col0 >= 0,
+                "grl_typed_spmm_fwd_slice: need F > 0, ldx >= F, zseg >= F, self_col0 >= 0 (F=%d ldx=%lld zseg=%d)",
+                F, (long long)ldx, zseg, (long long)self_col0);
+  const int hs = g->has_self ? 1 : 0;
+  GRL_CHECK_ARG(ldz >= (int64_t)(g->num_types + hs - 1) * zseg + F,
+                "grl_typed_spmm_fwd_slice: ldz %lld too small for %d segments of stride %d", (long long)ldz,
+                g->num_types + hs, zseg);
+  if (g->num_rows == 0) return GRL_OK;
+  GRL_CHECK_ARG(X && Z && g->rowptr && (g->nnz == 0 || g->colidx), "grl_typed_spmm_fwd_slice: NULL pointer");
+  GRL_CHECK_ARG(g->nnz < 2147483647LL, "grl_typed_spmm_fwd_slice: nnz %lld exceeds int32", (long long)g->nnz);
+  return launch_spmm<false>(g->num_rows, g->num_rows, g->num_types, hs, g->rowptr, g->colidx, nullptr, g->vals,
+                            g->edge_id_base, g->self_id_base, X, ldx, F, Z, ldz, to_dev(de), g->split,
+                            as_stream(stream), Z, self_col0, -1, zseg);
 }
 
 extern "C" int grl_typed_spmm_bwd(const GrlTypedCsc* g, const float* dZ, int32_t F, float* dX, int64_t lddx,

@@ -64,9 +64,16 @@ class BaseDataLoader:
             batch_size = data_config.get("batch_size", 1)
             sampler = None
             if distributed:
-                batch_size = max(1, batch_size // self.config.num_gpus)  # the reference can reach 0 here
-                sampler = DistributedSampler(dataset, num_replicas=self.config.num_gpus,
-                                             rank=self.config.local_rank, shuffle=bool(data_config.get("shuffle")))
+                # the initialised process group is the truth for replicas and rank (config.num_gpus /
+                # local_rank only stand in before it exists); a different count would overlap or
+                # skip documents
+                if torch.distributed.is_available() and torch.distributed.is_initialized():
+                    replicas, rank = torch.distributed.get_world_size(), torch.distributed.get_rank()
+                else:
+                    replicas, rank = int(self.config.num_gpus), int(self.config.local_rank)
+                batch_size = max(1, batch_size // replicas)  # the reference can reach 0 here
+                sampler = DistributedSampler(dataset, num_replicas=replicas, rank=rank,
+                                             shuffle=bool(data_config.get("shuffle")))
             return DataLoader(dataset, batch_size=batch_size, num_workers=data_config.get("num_workers", 0),
                               drop_last=bool(data_config.get("drop_last")),
                               pin_memory=bool(data_config.get("pin_memory")) and torch.cuda.is_available(),

@@ -74,6 +74,10 @@ class EdgeDropout(nn.Dropout):
         return A.with_dropedge(DropEdge(p=float(self.p), seed=seed, call=call, drop_self=drop_self))
 
 
+# grl_bag_linear_fwd keeps one output row per wave in registers (include/grl.h)
+BAG_LINEAR_MAX_C = 512
+
+
 class GraphCNNDropEdge(BaseNetwork):
     def __init__(self, input_dim: int, output_dim: int, num_edges: int, net_size: int = 256,
                  use_attention: bool = True, dropedge_seed: Optional[int] = None):
@@ -107,10 +111,10 @@ class GraphCNNDropEdge(BaseNetwork):
 
     def _embed(self, V: torch.Tensor) -> torch.Tensor:
         """emb1 (drop_robust_gcn.py:36,64): Linear + ReLU, same parameters."""
-        if self.sparse_emb1 and V.is_cuda:
-            lin = self.emb1[0]
+        lin = self.emb1[0]
+        if self.sparse_emb1 and V.is_cuda and lin.out_features <= BAG_LINEAR_MAX_C:
             return bag_linear(V.float(), lin.weight, lin.bias, relu=True)
-        return self.emb1(V)
+        return self.emb1(V)  # net_size > 512: one output row no longer fits a wave's registers
 
     def forward(self, inputs, efficient_mode: bool = True):
         V, A = inputs

@@ -112,6 +112,9 @@ class KVProcedure(BaseProcedure):
         from sklearn.metrics import classification_report
 
         train = Dictlist()
+        sampler = getattr(self.train_loader, "sampler", None)
+        if hasattr(sampler, "set_epoch"):  # DistributedSampler: a new shuffle every epoch, same on every rank
+            sampler.set_epoch(epoch)
         for batch in self.train_loader:
             scores, _ = self._run_train_step(batch)
             train._update(scores)

@@ -1,12 +1,42 @@
 """Checkpoint save/restore (the reference's CheckpointHandler,
 gnn/utils/checkpoint_handler.py:9-60): `<dir>/model_latest.pt` holding
 {"epoch", "config", "meta_data", "state_dict"}.  Configs are stored as plain
-dicts so checkpoints load with torch.load(weights_only=True)."""
+dicts so checkpoints load with torch.load(weights_only=True).
+
+Checkpoints written by the reference load too, still weights-only: its
+KVProcedure saves `dict(munch_config)` (kv_procedure.py:364-368, config from
+munch.munchify at cl_warper.py:72), so nested config values are pickled as
+`munch.Munch`, and its metrics come from sklearn as numpy float64 scalars.
+Those globals -- munch.Munch rebuilt as an OrderedDict, and numpy's scalar /
+dtype reconstructors -- are allow-listed for the load; nothing else is.
+"""
 import logging
 import os
+from collections import OrderedDict
 from typing import Any, Dict
 
+import numpy as np
 import torch
+
+
+def _reference_globals():
+    """(object, pickled name) pairs a reference checkpoint may reference."""
+    # munch.Munch (a dict subclass pickled as NEWOBJ + SETITEMS + BUILD(items)) is
+    # rebuilt as an OrderedDict: the weights-only unpickler fills only exact
+    # dict / OrderedDict instances, and an OrderedDict's BUILD puts the items
+    # in its __dict__ as well, so attribute access (cfg.model.type) keeps working.
+    out = [(OrderedDict, "munch.Munch"), (OrderedDict, "munch.DefaultMunch"), (OrderedDict, "munch.AutoMunch")]
+    try:
+        from numpy._core.multiarray import scalar
+    except ImportError:  # numpy < 2
+        from numpy.core.multiarray import scalar
+    out += [(scalar, "numpy.core.multiarray.scalar"), (scalar, "numpy._core.multiarray.scalar"),
+            (np.dtype, "numpy.dtype")]
+    for name in ("Float64DType", "Float32DType", "Int64DType", "Int32DType", "BoolDType"):
+        cls = getattr(getattr(np, "dtypes", None), name, None)
+        if cls is not None:
+            out.append((cls, f"numpy.dtypes.{name}"))
+    return out
 
 
 class CheckpointHandler:
@@ -29,6 +59,7 @@ class CheckpointHandler:
         return path
 
     def restore_checkpoint(self, checkpoint_path: str) -> Dict[str, Any]:
-        ckpt = torch.load(checkpoint_path, map_location=self.device, weights_only=True)
+        with torch.serialization.safe_globals(_reference_globals()):
+            ckpt = torch.load(checkpoint_path, map_location=self.device, weights_only=True)
         self.logger.info("Loading checkpoint success!")
         return ckpt

@@ -124,6 +124,8 @@ SIGNATURES = {
     "grl_dropedge_init": (_c_i32, [_P(GrlDropEdge), ctypes.c_float, _c_u64, _c_u64, _c_i32]),
     "grl_dropedge_mask": (_c_i32, [_P(GrlDropEdge), _c_u64, _c_i64, _c_vp, _c_vp]),
     "grl_typed_spmm_fwd": (_c_i32, [_P(GrlTypedCsr), _c_vp, _c_i64, _c_i32, _c_vp, _P(GrlDropEdge), _c_vp]),
+    "grl_typed_spmm_fwd_slice": (_c_i32, [_P(GrlTypedCsr), _c_vp, _c_i64, _c_i32, _c_i64, _c_vp, _c_i64, _c_i32,
+                                          _P(GrlDropEdge), _c_vp]),
     "grl_typed_spmm_bwd": (_c_i32, [_P(GrlTypedCsc), _c_vp, _c_i32, _c_vp, _c_i64, _P(GrlDropEdge), _c_vp]),
     "grl_graphconv_fwd_workspace_size": (_c_size, [_c_i64, _c_i32, _c_i32, _c_i32, _c_i32]),
     "grl_graphconv_fwd": (_c_i32, [_P(GrlTypedCsr), _c_vp, _c_i64, _c_i32, _c_vp, _c_vp, _c_i32, _c_i32, _c_vp,

@@ -232,6 +232,97 @@ def halo_exchange_into(X_loc: torch.Tensor, X_ext: torch.Tensor, send_buf: torch
     all_to_all_v(X_ext[plan.n_loc:], send_buf, plan.recv_counts, plan.send_counts, group)
 
 
+class HaloPipeline:
+    """Halo exchange overlapped with the aggregation (forward, no autograd).
+
+    The feature columns are cut into `chunks` slices of F/chunks columns.
+    Slice c's halo rows travel (RCCL all-gather or all-to-all-v on a side
+    stream, in slice order) while the compute stream aggregates slice c-1
+    with grl_typed_spmm_fwd_slice into Z's columns of that slice.  Every Z
+    element is the same edges in the same order as the unsliced aggregation,
+    so the result is bitwise equal to it (and to the single-GPU run); what
+    changes is that after the first slice the exchange runs under the
+    gather.  chunks=1 is the serial exchange-then-aggregate step.
+
+    Tables (HBM, per slice c, rows as the plan's X_ext, F/chunks columns):
+      dense:  [own rows padded to stride | every rank's rows]
+      sparse: [own rows | referenced halo rows in owner order]
+    """
+
+    def __init__(self, sg: "ShardedGraph", F: int, chunks: int = 2, device=None):
+        plan = sg.plan
+        if chunks < 1 or F % chunks:
+            raise ValueError(f"chunks must divide F={F} (got {chunks}); slices of a multiple of 4 columns take "
+                             "the vector path")
+        self.sg, self.plan, self.F, self.K, self.Fc = sg, plan, F, chunks, F // chunks
+        self.group = sg.group
+        self.world = _world(self.group)
+        dev = torch.device(device) if device is not None else sg.graph.device
+        rows = plan.n_loc + plan.n_halo
+        self.tables = torch.empty(chunks, rows, self.Fc, device=dev)
+        if plan.mode == "dense":
+            self.tables[:, plan.n_loc:plan.stride].zero_()  # shard padding rows: travel, never read
+        self.send = None
+        if plan.mode == "sparse" and self.world > 1:
+            self.send = torch.empty(chunks, plan.send_index.numel(), self.Fc, device=dev)
+        self.side = torch.cuda.Stream(dev) if dev.type == "cuda" and not _host_staged(self.group) else None
+
+    def _slices(self, X: torch.Tensor) -> torch.Tensor:
+        """[rows, F] -> [chunks, rows, Fc] view (no copy)."""
+        return X.view(X.shape[0], self.K, self.Fc).permute(1, 0, 2)
+
+    def _pack(self, X_loc: torch.Tensor) -> None:
+        p = self.plan
+        self.tables[:, :p.n_loc].copy_(self._slices(X_loc))
+        if self.send is not None:
+            self.send.copy_(self._slices(X_loc.index_select(0, p.send_index)))
+
+    def _exchange(self, c: int):
+        """Start slice c's exchange; returns a work handle (or None if done)."""
+        p, t = self.plan, self.tables[c]
+        if self.world == 1:
+            return None
+        if p.mode == "dense":
+            if self.side is None:
+                all_gather_into(t[p.stride:], t[:p.stride], self.group)
+                return None
+            return dist.all_gather_into_tensor(t[p.stride:], t[:p.stride], group=self.group, async_op=True)
+        if self.side is None:
+            all_to_all_v(t[p.n_loc:], self.send[c], p.recv_counts, p.send_counts, self.group)
+            return None
+        return dist.all_to_all_single(t[p.n_loc:], self.send[c], p.recv_counts, p.send_counts, group=self.group,
+                                      async_op=True)
+
+    def run(self, X_loc: torch.Tensor, Z: torch.Tensor, dropedge: Optional[DropEdge] = None,
+            aggregate_slice=None) -> torch.Tensor:
+        """Z[:, s*F + c*Fc : s*F + (c+1)*Fc] for every slice c (Z contiguous
+        [n_loc, segments*F]).  aggregate_slice(table, graph, Z, col0) replaces
+        the HIP slice aggregation (CPU tests only)."""
+        from .ops import spmm_forward_slice
+
+        agg = aggregate_slice or (lambda table, g, out, col0: spmm_forward_slice(table, g, out, col0))
+        graph = self.sg.graph.with_dropedge(dropedge)
+        if self.side is None:  # host-staged (gloo) or single rank: in order, no overlap
+            self._pack(X_loc)
+            for c in range(self.K):
+                self._exchange(c)
+                agg(self.tables[c], graph, Z, c * self.Fc)
+            return Z
+        main = torch.cuda.current_stream(X_loc.device)
+        self.side.wait_stream(main)  # X_loc is final on the compute stream
+        with torch.cuda.stream(self.side):
+            self._pack(X_loc)
+            works = [self._exchange(c) for c in range(self.K)]
+        for c in range(self.K):
+            if works[c] is not None:
+                works[c].wait()  # the compute stream waits for slice c only
+            else:
+                main.wait_stream(self.side)
+            agg(self.tables[c], graph, Z, c * self.Fc)
+        main.wait_stream(self.side)  # buffers are reused by the next call
+        return Z
+
+
 def broadcast_module(module: torch.nn.Module, src: int = 0, group=None) -> None:
     """Copy `src`'s parameters and buffers to every rank (replica start)."""
     if _world(group) == 1:

@@ -50,6 +50,35 @@ def spmm_forward(X: torch.Tensor, graph: TypedGraph, out: torch.Tensor = None) -
     return out
 
 
+def spmm_forward_slice(X: torch.Tensor, graph: TypedGraph, out: torch.Tensor, col0: int,
+                       self_col0: int = 0) -> torch.Tensor:
+    """Columns [col0, col0 + F) of Z = A_drop X into `out` (contiguous
+    [num_rows, segments * F_total]), where X is that column slice's table
+    ([graph.num_cols, F], any row stride) and row n's self term reads X row
+    self_col0 + n (grl_typed_spmm_fwd_slice).  Bitwise equal, per element,
+    to the whole-width spmm_forward: the pipelined halo exchange of grl.dist
+    aggregates one slice while the next is in flight."""
+    _require_device(X, "node features")
+    if X.dtype != torch.float32 or X.dim() != 2 or X.stride(1) != 1:
+        raise _lib.GrlError("slice table must be a 2-D float32 tensor with unit column stride")
+    if X.shape[0] != graph.num_cols:
+        raise _lib.GrlError(f"slice table has {X.shape[0]} rows, graph gathers from {graph.num_cols}")
+    F = X.shape[1]
+    S = graph.segments
+    if out.dtype != torch.float32 or not out.is_contiguous() or out.shape[0] != graph.num_rows \
+            or out.shape[1] % S or out.device != X.device:
+        raise _lib.GrlError(f"out must be a contiguous float32 [{graph.num_rows}, {S} x F_total] tensor")
+    zseg = out.shape[1] // S
+    if col0 < 0 or col0 + F > zseg:
+        raise _lib.GrlError(f"columns [{col0}, {col0 + F}) outside the {zseg}-column segments")
+    csr = graph.csr_c(F)
+    de = graph.dropedge.to_c() if graph.dropedge is not None else None
+    call("grl_typed_spmm_fwd_slice", ctypes.byref(csr), X.data_ptr(), X.stride(0), F, int(self_col0),
+         out.data_ptr() + 4 * col0, out.stride(0), zseg, ctypes.byref(de) if de is not None else None,
+         current_stream_handle(X.device))
+    return out
+
+
 def spmm_backward(dZ: torch.Tensor, graph: TypedGraph, F: int) -> torch.Tensor:
     """dX = A_drop^T dZ (grl_typed_spmm_bwd over the cached CSC, same mask)."""
     dZ = dZ.contiguous().float()

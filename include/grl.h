@@ -165,6 +165,21 @@ int grl_typed_spmm_fwd(const GrlTypedCsr* g, const float* X, int64_t ldx,
                        int32_t F, float* Z, const GrlDropEdge* de,
                        grl_stream_t stream);
 
+/* Column slice of Z = A_drop X, for the pipelined halo exchange of a
+ * node-range shard (grl/dist.py): the aggregation of
+ * robust_gcn.py:45-47 restricted to F feature columns, so columns whose halo
+ * rows have arrived are aggregated while the next slice is still in flight.
+ *   Z[n*ldz + s*zseg + j] = segment s of row n, column j < F
+ *   (s < has_self+num_types; Z points at the slice's first column),
+ * the self term of row n reads X row self_col0 + n (the shard's own rows
+ * inside a gathered table).  X: the slice's table, row stride ldx >= F.
+ * Per element the same edges in the same order as grl_typed_spmm_fwd, so a
+ * sliced aggregation is bitwise equal to the whole one.                     */
+int grl_typed_spmm_fwd_slice(const GrlTypedCsr* g, const float* X, int64_t ldx,
+                             int32_t F, int64_t self_col0, float* Z,
+                             int64_t ldz, int32_t zseg, const GrlDropEdge* de,
+                             grl_stream_t stream);
+
 /* dX = A_drop^T dZ.  Replaces autograd's BmmBackward0 for robust_gcn.py:45
  * (grad of V through the aggregation), with the same DropEdge mask as the
  * forward call that used `de`.  dZ: contiguous [*, (has_self+num_types)*F];

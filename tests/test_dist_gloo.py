@@ -86,8 +86,43 @@ def _worker(rank, world, port, bounds, mode):
         np.testing.assert_array_equal(Z.detach().numpy(), Zref[rb:re])  # bitwise: same rows, same edge order
         Z.backward(torch.from_numpy(dZ[rb:re].copy()))
         np.testing.assert_allclose(X_loc.grad.numpy(), dXref[rb:re], rtol=0, atol=1e-5)
+        _check_pipeline(plan, lr, X[rb:re], Zref[rb:re], rb, d)
     finally:
         dist.destroy_process_group()
+
+
+class _HostGraph:
+    """Test double for the TypedGraph a ShardedGraph carries (the real one
+    lives on the GPU); HaloPipeline only asks it for with_dropedge."""
+
+    def __init__(self):
+        self.device = torch.device("cpu")
+
+    def with_dropedge(self, de):
+        return self
+
+
+def _check_pipeline(plan, lr, X_loc, Zref, rb, d):
+    """grl.dist.HaloPipeline's slice tables and exchanges (product code),
+    each slice aggregated by the oracle: Z bitwise equal to one process."""
+    import types
+
+    from grl.dist import HaloPipeline
+
+    sg = types.SimpleNamespace(plan=plan, graph=_HostGraph(), group=None)
+    n = plan.n_loc
+    for K in (1, 2, 3):
+        pipe = HaloPipeline(sg, F, chunks=K, device="cpu")
+        assert pipe.side is None and pipe.tables.shape == (K, plan.n_loc + plan.n_halo, F // K)
+        Z = torch.full((n, (L + 1) * F), float("nan"))
+
+        def agg(table, graph, out, col0):
+            Zc = c_oracle.spmm_fwd(lr, plan.colidx_local.numpy(), table.numpy(), L, True, d=d,
+                                   edge_base=plan.edge_id_base, self_base=plan.num_edges_total + rb)
+            out.view(n, L + 1, F)[:, :, col0:col0 + table.shape[1]] = torch.from_numpy(Zc).view(n, L + 1, table.shape[1])
+
+        pipe.run(torch.from_numpy(X_loc.copy()), Z, None, aggregate_slice=agg)
+        np.testing.assert_array_equal(Z.numpy(), Zref)
 
 
 @pytest.mark.parametrize("mode", ["auto", "sparse", "dense"])

@@ -29,6 +29,35 @@ def test_world1_shard_equals_plain_graph():
     assert torch.equal(out, Z2)
 
 
+@pytest.mark.parametrize("kind,F,slices", [("er", 256, (128, 128)), ("er", 256, (64, 64, 128)),
+                                           ("rmat", 512, (128, 256, 128)), ("er", 100, (52, 48)),
+                                           ("er", 100, (50, 50))])
+def test_column_slices_equal_whole_aggregation(kind, F, slices):
+    """grl_typed_spmm_fwd_slice: each column slice of Z from its own slice
+    table (row stride = slice width), self rows at an offset, bitwise equal
+    to the whole-width aggregation -- DropEdge on, R-MAT hub rows split."""
+    from grl.ops import spmm_forward_slice
+
+    N = 1 << 13
+    g = TypedGraph.synthetic(N, 48.0, 6, kind=kind, seed=8, device=DEV)
+    g.split_threshold, g.split_chunk = 256, 128  # force the hub-chunk path at this size
+    de = DropEdge(0.3, 4, 2)
+    X = torch.randn(N, F, device=DEV)
+    Zw = spmm_forward(X, g.with_dropedge(de))
+    Zs = torch.full_like(Zw, float("nan"))
+    c0 = 0
+    for w in slices:
+        table = torch.zeros(N + 7, w, device=DEV)  # self rows at offset 7 (a gathered table's own slot)
+        table[7:] = X[:, c0:c0 + w]
+        gs = TypedGraph(g.rowptr, (g.colidx + 7).to(torch.int32), 6, num_cols=N + 7, edge_id_base=g.edge_id_base,
+                        self_id_base=g.self_id_base, self_rows=N)
+        gs.split_threshold, gs.split_chunk = 256, 128
+        spmm_forward_slice(table, gs.with_dropedge(de), Zs, c0, self_col0=7)
+        c0 += w
+    assert c0 == F
+    assert torch.equal(Zs, Zw)
+
+
 def _free_port():
     import socket
 
@@ -78,6 +107,15 @@ def _shard_worker(rank, world, port, mode, kind):
         out = torch.empty_like(Z)
         spmm_forward(X_ext, sg.graph.with_dropedge(de), out=out)
         assert torch.equal(out, Zg[rb:re].detach())
+        # the pipelined exchange (column slices in flight while the previous slice aggregates)
+        from grl.dist import HaloPipeline
+
+        for K in (1, 2, 4):
+            pipe = HaloPipeline(sg, F, chunks=K, device=DEV)
+            outp = torch.full_like(out, float("nan"))
+            pipe.run(X[rb:re].contiguous(), outp, de)
+            torch.cuda.synchronize()
+            assert torch.equal(outp, Zg[rb:re].detach()), K
         # a whole sharded GraphConv layer: weight grads summed over ranks equal one GPU's
         from gnn.models import GraphConv
         from grl.dist import allreduce_gradients
@@ -106,11 +144,7 @@ def test_two_ranks_on_one_gpu_match_single_gpu(mode, kind):
     mp.spawn(_shard_worker, args=(2, _free_port(), mode, kind), nprocs=2, join=True)
 
 
-def test_bench_two_ranks_contract():
-    """The driver's N>1 launch (torch.distributed.run, one rank per GPU) of
-    bench.py, rehearsed with two gloo ranks sharing the box's GPU: exactly
-    one JSON line from rank 0 with the contract's fields, weak scaling and
-    the halo report."""
+def _bench_two_ranks(extra):
     import json
     import os
     import subprocess
@@ -119,9 +153,8 @@ def test_bench_two_ranks_contract():
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
-           "--dist-backend", "gloo", "--nodes-per-gpu", "20000", "--steps", "2", "--warmup", "1",
-           "--cpu-seconds", "0"]
-    r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=300)
+           "--dist-backend", "gloo", "--steps", "2", "--warmup", "1", "--cpu-seconds", "0"] + extra
+    r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=280)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, r.stdout[-2000:]
@@ -129,5 +162,25 @@ def test_bench_two_ranks_contract():
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
               "vs_baseline", "dtype", "data", "config", "roofline", "halo"):
         assert k in out, k
-    assert out["n_gpus"] == 2 and out["scaling"] == "weak" and out["value"] > 0
-    assert out["config"]["nodes_total"] == 40000 and out["halo"]["mode"] in ("dense", "sparse")
+    assert out["n_gpus"] == 2 and out["value"] > 0
+    return out
+
+
+def test_bench_two_ranks_contract():
+    """The driver's N>1 launch (torch.distributed.run, one rank per GPU) of
+    bench.py, rehearsed with two gloo ranks sharing the box's GPU: exactly
+    one JSON line from rank 0 with the contract's fields; with no workload
+    flag N>1 is BASELINE's C4 (a fixed 4M-node graph, strong scaling)."""
+    out = _bench_two_ranks([])
+    assert out["config"]["workload"] == "C4" and out["config"]["nodes_total"] == 4_000_000
+    assert out["scaling"] == "strong" and out["config"]["d"] == 256
+    assert out["halo"]["mode"] == "dense" and out["halo"]["chunks"] == 2
+
+
+def test_bench_two_ranks_weak_and_c5_shape():
+    """The weak-scaling extra and a small R-MAT d=512 DropEdge shard pair."""
+    out = _bench_two_ranks(["--workload", "weak", "--nodes-per-gpu", "20000"])
+    assert out["scaling"] == "weak" and out["config"]["nodes_total"] == 40000
+    out = _bench_two_ranks(["--workload", "C5", "--nodes-per-gpu", "65536", "--chunks", "4"])
+    assert out["config"]["graph"] == "rmat" and out["config"]["d"] == 512 and out["config"]["dropedge_p"] == 0.2
+    assert out["config"]["nodes_total"] == 131072 and out["halo"]["chunks"] == 4

@@ -1,0 +1,104 @@
+"""GPU: data parallelism across documents (the reference's
+declared DP at cl_warper.py:73-75 / base_dataloader.py:91-106) against a
+single process.  Two gloo ranks share the box's GPU; each runs the product's
+training step (KVProcedure._run_train_step, kv_procedure.py:143-164 in the
+reference: forward, loss, backward, then the procedure's averaged bucketed
+gradient all-reduce, clip, Adam) on its half of the batch.  A single-process
+procedure runs the same steps on the union batch.  With equal-size graphs
+the union mean loss is the mean of the two halves' losses, so:
+  * the averaged gradients equal the union batch's gradients (1e-4),
+  * the loss curve over three Adam steps matches (1e-4).
+Feature dropout and DropEdge are off (p = 0) so both runs draw nothing."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+B, N, L, F_IN, C_OUT, NET = 4, 24, 6, 64, 15, 32
+STEPS = 3
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _batches():
+    """Three union batches of B equal-size graphs (every node labelled)."""
+    rng = np.random.default_rng(42)
+    out = []
+    for _ in range(STEPS):
+        V = (rng.random((B, N, F_IN)) < 0.1).astype(np.float32)
+        A = (rng.random((B, N, L, N)) < 3.0 / (L * N)).astype(np.float32)
+        y = rng.integers(0, C_OUT, (B, N)).astype(np.int64)
+        out.append({"textline_encoding": torch.from_numpy(V), "adjacency_matrix": torch.from_numpy(A),
+                    "node_label": torch.from_numpy(y)})
+    return out
+
+
+def _half(batch, rank, world):
+    per = B // world
+    return {k: v[rank * per:(rank + 1) * per] for k, v in batch.items()}
+
+
+def _procedure(cfg, distributed):
+    from gnn.models import GraphCNNDropEdge
+    from gnn.trainer.training_procedures import KVProcedure
+
+    torch.manual_seed(0)
+    model = GraphCNNDropEdge(F_IN, C_OUT, L, net_size=NET)
+    model.dropout.p = 0.0
+    model.edge_dropout.p = 0.0
+    c = type(cfg)(dict(cfg))
+    c.distributed = distributed
+    return KVProcedure(model, c)
+
+
+def _worker(rank, world, port, cfg):
+    import torch.distributed as dist
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        cfg.num_gpus, cfg.local_rank = world, rank
+        dp = _procedure(cfg, True)
+        single = _procedure(cfg, False)
+        assert dp.distributed and not single.distributed
+        for step, batch in enumerate(_batches()):
+            s_dp, _ = dp._run_train_step(_half(batch, rank, world))
+            s_one, _ = single._run_train_step(batch)
+            losses = [None] * world
+            dist.all_gather_object(losses, s_dp["loss"])
+            assert abs(np.mean(losses) - s_one["loss"]) <= 1e-4 * max(1.0, abs(s_one["loss"])), (step, losses, s_one)
+            if step == 0:  # the (clipped) gradients each optimizer stepped with
+                for (name, p_dp), (_, p_one) in zip(dp.model.named_parameters(), single.model.named_parameters()):
+                    if p_one.grad is None:
+                        assert p_dp.grad is None, name
+                        continue
+                    torch.testing.assert_close(p_dp.grad, p_one.grad, rtol=1e-4, atol=1e-6, msg=name)
+        # the replicas stayed identical to each other
+        flat = torch.cat([p.detach().reshape(-1).cpu() for p in dp.model.parameters()])
+        gathered = [torch.empty_like(flat) for _ in range(world)]
+        dist.all_gather(gathered, flat)
+        assert torch.equal(gathered[0], gathered[1])
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_step_equals_single_process_on_union_batch(tmp_path):
+    import torch.multiprocessing as mp
+
+    from test_data_pipeline import make_config
+
+    cfg = make_config(str(tmp_path), epochs=1)
+    cfg.dist_backend = "gloo"
+    mp.spawn(_worker, args=(2, _free_port(), cfg), nprocs=2, join=True)

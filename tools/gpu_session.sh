@@ -26,7 +26,7 @@ run() {  # name seconds cmd...
 
 for step in "$@"; do
   case $step in
-    tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -rf ;;
+    tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py ;;
     bench_extras) run bench_extras 600 python bench.py --extras --cpu-seconds 0 ;;
@@ -75,6 +75,9 @@ for step in "$@"; do
                   SQ_LDS_CMD_FIFO_FULL SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY SQ_INSTS_VALU_MFMA_MOPS_BF16 \
                   --kernel-trace -d "$OUT/pmc_x6_b" -o run --output-format csv \
                   -- python bench.py --only linear --steps 5 --warmup 1 ;;
+    probe_slices) run probe_slices 300 python tools/probe_slices.py ;;
+    tests_dist) run pytest_gpu_dist 600 python -u -m pytest tests/test_gpu_dist.py -m gpu -v -rf --timeout 300 \
+                  --timeout-method thread ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -1,0 +1,60 @@
+"""Diagnostic: cost of aggregating in column slices (the pipelined halo
+exchange, grl.dist.HaloPipeline) on one GPU.  The C3 / C4 graphs; each slice
+table is contiguous [rows, F/K] (as the pipeline holds it); times the K slice
+launches back to back against one whole-width launch, and checks bitwise
+equality.  PROBE_NODES (default 1M), PROBE_DIM (256)."""
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "graph-representation-learning_amd"))
+import torch  # noqa: E402
+
+from grl import TypedGraph  # noqa: E402
+from grl.ops import spmm_forward, spmm_forward_slice  # noqa: E402
+
+
+def timeit(fn, n=10):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(n):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / n
+
+
+def main():
+    F = int(os.environ.get("PROBE_DIM", "256"))
+    dev = torch.device("cuda:0")
+    for N in [int(x) for x in os.environ.get("PROBE_NODES", "1000000,4000000").split(",")]:
+        g = TypedGraph.synthetic(N, 32.0, 6, seed=0, device=dev)
+        X = torch.randn(N, F, device=dev)
+        Zw = torch.empty(N, 7 * F, device=dev)
+        whole = timeit(lambda: spmm_forward(X, g, out=Zw))
+        print(f"N={N} F={F} whole {whole:7.3f} ms", flush=True)
+        Zs = torch.empty_like(Zw)
+        for K in (2, 4):
+            w = F // K
+            tables = [X[:, c * w:(c + 1) * w].contiguous() for c in range(K)]
+
+            def sliced():
+                for c in range(K):
+                    spmm_forward_slice(tables[c], g, Zs, c * w)
+
+            for pair in ("1", "0"):
+                os.environ["GRL_SPMM_PAIR"] = pair  # read per launch: pair-row kernel vs whole-row kernel
+                Zs.zero_()
+                t = timeit(sliced)
+                one = timeit(lambda: spmm_forward_slice(tables[0], g, Zs, 0))
+                print(f"N={N} K={K} slices of {w} pair={pair}: total {t:7.3f} ms ({t / whole:.2f}x whole), "
+                      f"one slice {one:.3f} ms, bitwise {torch.equal(Zs, Zw)}", flush=True)
+            os.environ.pop("GRL_SPMM_PAIR")
+            del tables
+        del g, X, Zw, Zs
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
