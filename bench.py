@@ -517,15 +517,38 @@ def c1_extras(dev, iters=20):
         except Exception as err:  # report, never fall back silently
             res["eval_ms_hip_graph"] = None
             res["hip_graph_error"] = repr(err)[:200]
-    # CPU baseline (before the train steps below change the weights): the oracle's float64 restatement of the same forward
-    P = {k: v.detach().double().cpu().numpy() for k, v in model.state_dict().items()}
+    # parity (before the train steps below change the weights): the oracle's float64 restatement
+    sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    P = {k: v.double().numpy() for k, v in sd.items()}
     Vh, Ah = V.cpu().numpy(), A.cpu().numpy()
     ref = dense_ref.graph_cnn_dropedge_forward(P, Vh, Ah)
-    t0, n = time.perf_counter(), 0
-    while time.perf_counter() - t0 < 2.0 or n < 3:
-        dense_ref.graph_cnn_dropedge_forward(P, Vh, Ah)
-        n += 1
-    res["cpu_eval_ms"] = (time.perf_counter() - t0) / n * 1e3
+    # CPU baseline: the reference's own math in fp32 torch on every usable host core
+    # (oracle/dense_torch.py: dense A_pre, dense Bernoulli masks in training)
+    from oracle import dense_torch
+
+    info = host_cpu_info()
+    threads_before = torch.get_num_threads()
+    torch.set_num_threads(cpu_threads(info))
+    Pf = {k: v.float() for k, v in sd.items()}
+    Vc, Ac = V.cpu(), A.cpu()
+
+    def cpu_time(fn, budget=2.0):
+        fn()
+        t0, n = time.perf_counter(), 0
+        while time.perf_counter() - t0 < budget or n < 3:
+            fn()
+            n += 1
+        return (time.perf_counter() - t0) / n * 1e3
+
+    with torch.no_grad():
+        res["cpu_eval_ms"] = cpu_time(lambda: dense_torch.forward(Pf, Vc, Ac))
+    cpu_step = dense_torch.TrainStep(sd)
+    V4c, A4c = Vc.expand(4, -1, -1).contiguous(), Ac.expand(4, -1, -1, -1).contiguous()
+    y4c = torch.randint(0, 53, (4, V.shape[1]), generator=torch.Generator().manual_seed(5))
+    res["cpu_train_step_ms_B4"] = cpu_time(lambda: cpu_step(V4c, A4c, y4c))
+    res["cpu_threads"] = torch.get_num_threads()
+    res["cpu_model"] = info["cpu_model"]
+    torch.set_num_threads(threads_before)
     # train step, B=4 (the reference's training batch), Adam as BuitlinOptimizer builds it
     model.train()
     V4, A4 = V.expand(4, -1, -1).contiguous(), A.expand(4, -1, -1, -1).contiguous()
@@ -540,7 +563,39 @@ def c1_extras(dev, iters=20):
         opt.step()
 
     res["train_step_ms_B4"] = _time(step, iters)
-    res["cpu_kind"] = "port: oracle/dense_ref.py float64 numpy dense model (A_pre materialised like the reference)"
+    # the same step with the batch graph prebuilt, eager and as ONE HIP graph (device-seeded DropEdge
+    # and feature dropout redraw on every replay; capturable Adam)
+    g4 = model.to_graph(A4)
+    opt_c = torch.optim.Adam(model.parameters(), lr=1e-3, capturable=True)
+
+    def step_c():
+        loss = lossf(model.forward([V4, g4]).reshape(-1, 53), y4.reshape(-1))
+        loss.backward()
+        opt_c.step()
+        return loss
+
+    def step_c_eager():
+        opt_c.zero_grad(set_to_none=True)
+        step_c()
+
+    res["train_step_ms_B4_graph_prebuilt"] = _time(step_c_eager, iters)
+    try:
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            for _ in range(3):
+                step_c_eager()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        hg = torch.cuda.CUDAGraph()
+        opt_c.zero_grad(set_to_none=True)
+        with torch.cuda.graph(hg):
+            step_c()
+        res["train_step_ms_B4_hip_graph"] = _time(hg.replay, iters)
+    except Exception as err:  # report, never fall back silently
+        res["train_step_ms_B4_hip_graph"] = None
+        res["train_hip_graph_error"] = repr(err)[:200]
+    res["cpu_kind"] = ("port: oracle/dense_torch.py, the reference's dense fp32 torch math on CPU (A_pre "
+                       "materialised, Bernoulli masks over it in training, Adam)")
     res["logits_max_abs_diff_vs_oracle"] = float(np.abs(logits - ref).max())
     res["tolerance"] = 1e-4
     return res

@@ -74,17 +74,29 @@ struct DropDev {
   float scale;
   int32_t active;
   int32_t drop_self;
+  const uint64_t* seed_dev;  // non-null: key = dropedge_key(*seed_dev, call) (resolve_key)
+  uint64_t call;
 };
 
 inline DropDev to_dev(const GrlDropEdge* de) {
-  DropDev d{0, 0, 1.0f, 0, 0};
+  DropDev d{0, 0, 1.0f, 0, 0, nullptr, 0};
   if (de && de->active) {
     d.key = de->key;
     d.threshold = de->threshold;
     d.scale = de->scale;
     d.active = 1;
     d.drop_self = de->drop_self;
+    d.seed_dev = de->seed_dev;
+    d.call = de->call_id;
   }
+  return d;
+}
+
+// Device-resident seed: every kernel taking a DropDev resolves its key once
+// at entry (one uniform 8-byte load; a graph replay sees the seed written
+// before it on the same stream).
+__device__ __forceinline__ DropDev resolve_key(DropDev d) {
+  if (d.active && d.seed_dev) d.key = dropedge_key(*d.seed_dev, d.call);
   return d;
 }
 

@@ -134,6 +134,7 @@ __global__ __launch_bounds__(256) void spmm_kernel(
     int zseg,  // fwd: floats between output segments (F, or the full width for a column slice)
     DropDev de, SplitDev sp) {
   using vec_t = typename VecT<VEC>::type;
+  de = resolve_key(de);
   const int lane = threadIdx.x & 63;
   const int cbase = blockIdx.y * (64 * VEC * NV);
   int coff[NV];
@@ -288,6 +289,7 @@ __global__ __launch_bounds__(256) void spmm_pair_kernel(
     const float* __restrict__ vals, uint64_t edge_base, uint64_t self_base, int64_t self_row0,
     const float* __restrict__ src, int64_t lds, int F, float* __restrict__ out, int64_t ldo, int zseg, DropDev de,
     SplitDev sp) {
+  de = resolve_key(de);
   const int lane = threadIdx.x & 63;
   const int half = lane >> 5;
   const int coff = (lane & 31) * 4;
@@ -408,6 +410,7 @@ __global__ __launch_bounds__(256) void spmm_fixup_kernel(
     const float* __restrict__ partials, int nseg, int S, int hs, int64_t self_rows, uint64_t self_base,
     const float* __restrict__ dZ, int F, float* __restrict__ out, int64_t ldo, int zseg, DropDev de) {
   using vec_t = typename VecT<VEC>::type;
+  de = resolve_key(de);
   const int lane = threadIdx.x & 63;
   const int cbase = blockIdx.y * (64 * VEC * NV);
   const int64_t zstride = (int64_t)(S + hs) * F;
@@ -437,6 +440,7 @@ __global__ __launch_bounds__(256) void spmm_fixup_kernel(
 }
 
 __global__ void mask_kernel(DropDev de, uint64_t id_base, int64_t count, uint8_t* __restrict__ keep) {
+  de = resolve_key(de);
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count;
        i += (int64_t)gridDim.x * blockDim.x) {
     keep[i] = dropedge_weight(de, 1.0f, id_base + (uint64_t)i) != 0.0f ? 1 : 0;
@@ -665,6 +669,8 @@ extern "C" int grl_dropedge_init(GrlDropEdge* de, float p, uint64_t seed, uint64
   GRL_CHECK_ARG(p >= 0.0f && p == p, "grl_dropedge_init: p must be >= 0 (got %f)", (double)p);
   de->key = dropedge_key(seed, call_id);
   de->drop_self = drop_self ? 1 : 0;
+  de->seed_dev = nullptr;
+  de->call_id = call_id;
   if (p <= 0.0f) {
     de->active = 0;
     de->threshold = 0;
@@ -681,6 +687,15 @@ extern "C" int grl_dropedge_init(GrlDropEdge* de, float p, uint64_t seed, uint64
   de->threshold = thr >= 4294967295.0 ? 0xFFFFFFFFu : (uint32_t)thr;
   // torch native_dropout: scale = 1/(1-p) computed in double, applied as float.
   de->scale = (float)(1.0 / (1.0 - (double)p));
+  return GRL_OK;
+}
+
+extern "C" int grl_dropedge_init_device(GrlDropEdge* de, float p, const uint64_t* seed_dev, uint64_t call_id,
+                                        int32_t drop_self) {
+  GRL_CHECK_ARG(seed_dev != nullptr, "grl_dropedge_init_device: seed_dev is NULL");
+  const int rc = grl_dropedge_init(de, p, 0, call_id, drop_self);
+  if (rc) return rc;
+  de->seed_dev = seed_dev;
   return GRL_OK;
 }
 

@@ -47,9 +47,12 @@ class EdgeDropout(nn.Dropout):
     On a TypedGraph it returns the graph tagged with a fresh DropEdge draw
     (training) or untagged (eval / p == 0): the mask is generated inside the
     aggregation kernels from (seed, call, edge id).  `seed=None` draws each
-    call's seed from torch's default CPU generator, so torch.manual_seed
-    makes runs reproducible; a fixed `seed` numbers calls 0, 1, 2, ...
-    (reset_calls()) for parity tests.  Dense tensors get plain nn.Dropout.
+    call's seed on the graph's device (torch's CUDA generator, so
+    torch.manual_seed makes runs reproducible) into a 1-element tensor the
+    kernels read at launch: no host round trip, and a training step captured
+    in a HIP graph redraws every mask on each replay.  A fixed `seed` numbers
+    calls 0, 1, 2, ... (reset_calls()) for parity tests.  Dense tensors get
+    plain nn.Dropout.
     """
 
     def __init__(self, p: float = 0.5, seed: Optional[int] = None):
@@ -66,8 +69,8 @@ class EdgeDropout(nn.Dropout):
         if not self.training or self.p == 0.0:
             return A.with_dropedge(None)
         if self.seed is None:
-            seed = int(torch.randint(0, 2**62, (1,)).item())
-            call = 0
+            seed_t = torch.randint(0, 2**62, (1,), dtype=torch.int64, device=A.device)
+            return A.with_dropedge(DropEdge(p=float(self.p), seed=0, call=0, drop_self=drop_self, seed_tensor=seed_t))
         else:
             seed, call = self.seed, self._calls
             self._calls += 1

@@ -90,6 +90,8 @@ class GrlDropEdge(ctypes.Structure):
         ("scale", ctypes.c_float),
         ("active", _c_i32),
         ("drop_self", _c_i32),
+        ("seed_dev", _c_vp),
+        ("call_id", _c_u64),
     ]
 
 
@@ -122,6 +124,7 @@ SIGNATURES = {
     "grl_version": (ctypes.c_char_p, []),
     "grl_last_error": (ctypes.c_char_p, []),
     "grl_dropedge_init": (_c_i32, [_P(GrlDropEdge), ctypes.c_float, _c_u64, _c_u64, _c_i32]),
+    "grl_dropedge_init_device": (_c_i32, [_P(GrlDropEdge), ctypes.c_float, _c_vp, _c_u64, _c_i32]),
     "grl_dropedge_mask": (_c_i32, [_P(GrlDropEdge), _c_u64, _c_i64, _c_vp, _c_vp]),
     "grl_typed_spmm_fwd": (_c_i32, [_P(GrlTypedCsr), _c_vp, _c_i64, _c_i32, _c_vp, _P(GrlDropEdge), _c_vp]),
     "grl_typed_spmm_fwd_slice": (_c_i32, [_P(GrlTypedCsr), _c_vp, _c_i64, _c_i32, _c_i64, _c_vp, _c_i64, _c_i32,

@@ -16,7 +16,7 @@ Layout in HBM (int32 indices, fp32 values):
 from __future__ import annotations
 
 import ctypes
-from dataclasses import dataclass
+from dataclasses import dataclass, field
 from typing import Optional, Tuple
 
 import torch
@@ -42,15 +42,28 @@ def _require_device(t: torch.Tensor, what: str) -> None:
 
 @dataclass(frozen=True)
 class DropEdge:
-    """One edge_dropout draw: nn.Dropout(p) over A_pre (drop_robust_gcn.py:38)."""
+    """One edge_dropout draw: nn.Dropout(p) over A_pre (drop_robust_gcn.py:38).
+
+    seed_tensor: optional 1-element int64 device tensor holding the seed; the
+    kernels read it at launch (grl_dropedge_init_device), so a HIP graph that
+    captured the seed's producer (a device RNG kernel) redraws the mask on
+    every replay.  `seed` is then unused."""
 
     p: float
     seed: int
     call: int = 0
     drop_self: bool = True  # efficient_mode=True masks the identity block too
+    seed_tensor: Optional[torch.Tensor] = field(default=None, compare=False, repr=False)
 
     def to_c(self) -> GrlDropEdge:
         de = GrlDropEdge()
+        if self.seed_tensor is not None:
+            t = self.seed_tensor
+            if not t.is_cuda or t.dtype != torch.int64 or t.numel() != 1:
+                raise _lib.GrlError("DropEdge.seed_tensor must be a 1-element int64 device tensor")
+            call("grl_dropedge_init_device", ctypes.byref(de), float(self.p), t.data_ptr(),
+                 int(self.call) & (2**64 - 1), int(self.drop_self))
+            return de
         call("grl_dropedge_init", ctypes.byref(de), float(self.p), int(self.seed) & (2**64 - 1),
              int(self.call) & (2**64 - 1), int(self.drop_self))
         return de

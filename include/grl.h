@@ -131,6 +131,13 @@ typedef struct GrlDropEdge {
   float scale;        /* 1/(1-p) (0 when p >= 1); 1 when p == 0                */
   int32_t active;     /* 0: identity (eval mode / p == 0)                      */
   int32_t drop_self;  /* 1: the identity block is masked too (efficient_mode)  */
+  /* Device-resident stream (HIP-graph replays): when seed_dev != NULL every
+   * kernel derives key = grl_dropedge_key(*seed_dev, call_id) at launch
+   * instead of using `key`, so a captured training step draws a fresh mask
+   * on each replay from a seed written on the device (e.g. by the RNG kernel
+   * captured with it).  NULL for grl_dropedge_init.                        */
+  const uint64_t* seed_dev;
+  uint64_t call_id;
 } GrlDropEdge;
 
 /* Library identity / errors. */
@@ -144,6 +151,12 @@ const char* grl_last_error(void);
  * Host-only, no device work.  Replaces nn.Dropout.__init__/bernoulli_ setup. */
 int grl_dropedge_init(GrlDropEdge* de, float p, uint64_t seed, uint64_t call_id,
                       int32_t drop_self);
+
+/* As grl_dropedge_init, with the seed read on the device at each launch
+ * from *seed_dev (device memory, 8 bytes; must stay valid while `de` is used,
+ * including by graph replays).  Host-only, no device work.                 */
+int grl_dropedge_init_device(GrlDropEdge* de, float p, const uint64_t* seed_dev,
+                             uint64_t call_id, int32_t drop_self);
 
 /* keep[i] = 1 if id_base + i survives DropEdge `de`, else 0 (i < count).
  * Exposes the fused mask for parity checks against the dense reference

@@ -282,13 +282,21 @@ int64_t oracle_synth(int32_t kind, int32_t L, int64_t N, int64_t C, uint64_t see
     while ((1LL << scale) < N) ++scale;
   uint64_t* keys = (uint64_t*)malloc(sizeof(uint64_t) * (size_t)(cap > 0 ? cap : 1));
   int64_t cnt = 0;
+  /* the candidate scan runs in parallel; the keys are sorted afterwards, so
+     the insertion order (and hence the thread count) cannot matter */
+#pragma omp parallel for schedule(static)
   for (int64_t k = 0; k < C; ++k) {
     int64_t s, d;
     int t;
     o_synth_edge(kind, L, N, scale, seed, (uint64_t)k, &s, &d, &t);
-    if (s >= rb && s < re && cnt < cap)
-      keys[cnt++] = ((uint64_t)(s - rb) * (uint64_t)L + (uint64_t)t) * (uint64_t)N + (uint64_t)d;
+    if (s >= rb && s < re) {
+      int64_t slot;
+#pragma omp atomic capture
+      slot = cnt++;
+      if (slot < cap) keys[slot] = ((uint64_t)(s - rb) * (uint64_t)L + (uint64_t)t) * (uint64_t)N + (uint64_t)d;
+    }
   }
+  if (cnt > cap) cnt = cap;
   qsort(keys, (size_t)cnt, sizeof(uint64_t), o_cmp_u64);
   int64_t nnz = 0;
   const int64_t nseg = (re - rb) * L;
@@ -309,6 +317,7 @@ int64_t oracle_synth_count(int32_t kind, int32_t L, int64_t N, int64_t C, uint64
   if (kind == 1)
     while ((1LL << scale) < N) ++scale;
   int64_t cnt = 0;
+#pragma omp parallel for schedule(static) reduction(+ : cnt)
   for (int64_t k = 0; k < C; ++k) {
     int64_t s, d;
     int t;

@@ -174,6 +174,32 @@ def test_oracle_model_matches_reference_eval(golden):
     _close(logits, g["logits"], 1e-5)
 
 
+def test_torch_fp32_restatement_matches_reference_eval(golden):
+    """oracle/dense_torch.py (the fp32 torch-CPU restatement timed as the C1
+    CPU baseline) reproduces the reference's eval logits on debug.json, and
+    its train step runs (dense Bernoulli masks over A_pre, Adam)."""
+    import torch
+
+    from gnn.models import GraphCNNDropEdge
+    from oracle import dense_torch
+
+    g = golden("model_debug.npz")
+    torch.manual_seed(0)
+    model = GraphCNNDropEdge(4369, 53, 6, 256)
+    P = {k: v.detach().float() for k, v in model.state_dict().items()}
+    V = np.zeros(tuple(g["V_shape"]), dtype=np.float32)
+    V[g["V_rows"], g["V_cols"]] = g["V_vals"]
+    A = np.unpackbits(g["A_bits"])[: int(np.prod(g["A_shape"]))].reshape(tuple(g["A_shape"])).astype(np.float32)
+    with torch.no_grad():
+        logits = dense_torch.forward(P, torch.from_numpy(V)[None], torch.from_numpy(A)[None])[0].double().numpy()
+    _close(logits, g["logits"], 1e-4)
+    step = dense_torch.TrainStep(model.state_dict())
+    y = torch.randint(0, 53, (2, V.shape[0]), generator=torch.Generator().manual_seed(1))
+    V2, A2 = torch.from_numpy(V)[None].expand(2, -1, -1), torch.from_numpy(A)[None].expand(2, -1, -1, -1)
+    l0 = step(V2, A2, y)
+    assert np.isfinite(l0)
+
+
 def test_oracle_model_matches_reference_train_masks(golden):
     g = golden("model_small_train.npz")
     P = {k[len("init::"):]: v.astype(np.float64) for k, v in g.items() if k.startswith("init::")}

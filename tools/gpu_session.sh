@@ -78,6 +78,13 @@ for step in "$@"; do
     probe_slices) run probe_slices 300 python tools/probe_slices.py ;;
     tests_dist) run pytest_gpu_dist 600 python -u -m pytest tests/test_gpu_dist.py -m gpu -v -rf --timeout 300 \
                   --timeout-method thread ;;
+    tests_configs) run pytest_gpu_configs 1000 python -u -m pytest tests/test_gpu_configs.py -m gpu -v -s -rf \
+                  --timeout 600 --timeout-method thread ;;
+    tests_dp) run pytest_gpu_dp 300 python -u -m pytest tests/test_gpu_dp.py -m gpu -v -s -rf --timeout 240 \
+                  --timeout-method thread ;;
+    tests_capture) run pytest_gpu_capture 300 python -u -m pytest tests/test_gpu_graph_capture.py -m gpu -v -s -rf \
+                  --timeout 240 --timeout-method thread ;;
+    c1) run c1 300 python bench.py --only c1 --steps 20 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
