@@ -1295,6 +1295,7 @@ extern "C" int grl_node_attention_fwd(const float* Q, const float* K, const floa
                                       const float* gamma, float* out, float* o_norm, float* row_max, float* row_sum,
                                       int64_t B, int64_t N, int32_t dk, int32_t dv, void* workspace,
                                       size_t workspace_bytes, grl_stream_t stream) {
+  TraceRange trace_("grl_node_attention_fwd");
   int rc = check_dims("grl_node_attention_fwd", B, N, dk, dv);
   if (rc) return rc;
   if (B == 0 || N == 0) return GRL_OK;
@@ -1343,6 +1344,7 @@ extern "C" int grl_node_attention_bwd(const float* Q, const float* K, const floa
                                       const float* row_max, const float* row_sum, const float* D, float* dQ,
                                       float* dK, float* dH, int64_t B, int64_t N, int32_t dk, int32_t dv,
                                       void* workspace, size_t workspace_bytes, grl_stream_t stream) {
+  TraceRange trace_("grl_node_attention_bwd");
   int rc = check_dims("grl_node_attention_bwd", B, N, dk, dv);
   if (rc) return rc;
   if (B == 0 || N == 0) return GRL_OK;

@@ -120,6 +120,7 @@ using namespace grl;
 
 extern "C" int grl_bag_linear_fwd(const float* V, int64_t ldv, int64_t M, int32_t K, const float* Wt, int32_t C,
                                   const float* bias, int32_t relu, float* out, grl_stream_t stream) {
+  TraceRange trace_("grl_bag_linear_fwd");
   GRL_CHECK_ARG(M >= 0 && K >= 0 && ldv >= K, "grl_bag_linear_fwd: bad sizes (M %lld, K %d, ldv %lld)", (long long)M,
                 K, (long long)ldv);
   GRL_CHECK_ARG(C >= 1 && C <= 512, "grl_bag_linear_fwd: output width %d outside [1, 512]", C);

@@ -9,6 +9,8 @@
 
 #include "grl.h"
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 namespace grl {
 
 // ---- thread-local error string (grl_last_error) --------------------------
@@ -113,6 +115,15 @@ __device__ __forceinline__ float readlane_f(float v, int lane) {
 __device__ __forceinline__ int uniform_i(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+// roctx range around a C-ABI entry point: `rocprofv3 --marker-trace` shows
+// where host time goes between kernels (a no-op call without a profiler).
+struct TraceRange {
+  explicit TraceRange(const char* name) { roctxRangePushA(name); }
+  ~TraceRange() { roctxRangePop(); }
+  TraceRange(const TraceRange&) = delete;
+  TraceRange& operator=(const TraceRange&) = delete;
+};
 
 // Number of CUs of the current device (cached per process).
 int device_cu_count();

@@ -1145,6 +1145,7 @@ extern "C" size_t grl_linear_fwd_workspace_size(int64_t M, int32_t K, int32_t C)
 extern "C" int grl_linear_fwd(const float* Z, int64_t ldz, const float* W, const float* bias, float* out, int64_t M,
                               int32_t K, int32_t C, int32_t relu, void* workspace, size_t workspace_bytes,
                               grl_stream_t stream) {
+  TraceRange trace_("grl_linear_fwd");
   GRL_CHECK_ARG(M >= 0 && K >= 0 && C >= 0, "grl_linear_fwd: negative size");
   GRL_CHECK_ARG(ldz >= K, "grl_linear_fwd: ldz (%lld) < K (%d)", (long long)ldz, K);
   if (M == 0 || C == 0) return GRL_OK;
@@ -1178,6 +1179,7 @@ extern "C" size_t grl_graphconv_fwd_workspace_size(int64_t num_rows, int32_t num
 extern "C" int grl_graphconv_fwd(const GrlTypedCsr* g, const float* X, int64_t ldx, int32_t F, const float* W,
                                  const float* bias, int32_t C, int32_t relu, float* out, const GrlDropEdge* de,
                                  void* workspace, size_t workspace_bytes, grl_stream_t stream) {
+  TraceRange trace_("grl_graphconv_fwd");
   GRL_CHECK_ARG(g != nullptr, "grl_graphconv_fwd: graph is NULL");
   GRL_CHECK_ARG(g->num_rows >= 0 && g->num_types >= 1 && g->num_types <= 63,
                 "grl_graphconv_fwd: num_types must be in [1, 63] (got %d)", g->num_types);
@@ -1246,6 +1248,7 @@ extern "C" size_t grl_linear_bwd_data_workspace_size(int64_t M, int32_t K, int32
 extern "C" int grl_linear_bwd_data(const float* g, const float* relu_out, const float* W, float* dZ, int64_t lddz,
                                    int64_t M, int32_t K, int32_t C, void* workspace, size_t workspace_bytes,
                                    grl_stream_t stream) {
+  TraceRange trace_("grl_linear_bwd_data");
   GRL_CHECK_ARG(M >= 0 && K >= 0 && C >= 0 && lddz >= K, "grl_linear_bwd_data: bad sizes");
   if (M == 0 || K == 0) return GRL_OK;
   GRL_CHECK_ARG(g && W && dZ, "grl_linear_bwd_data: NULL pointer");
@@ -1302,6 +1305,7 @@ extern "C" size_t grl_linear_bwd_weight_workspace_size(int64_t M, int32_t K, int
 extern "C" int grl_linear_bwd_weight(const float* Z, int64_t ldz, const float* g, const float* relu_out, float* dW,
                                      float* db, int64_t M, int32_t K, int32_t C, void* workspace,
                                      size_t workspace_bytes, grl_stream_t stream) {
+  TraceRange trace_("grl_linear_bwd_weight");
   GRL_CHECK_ARG(M >= 0 && K >= 0 && C >= 0 && ldz >= K, "grl_linear_bwd_weight: bad sizes");
   if (K == 0 || C == 0) return GRL_OK;
   GRL_CHECK_ARG(Z && g && dW, "grl_linear_bwd_weight: NULL pointer");

@@ -664,6 +664,9 @@ int spmm_fwd_rows(const GrlTypedCsr* g, int64_t r0, int64_t rows, const float* X
 
 using namespace grl;
 
+extern "C" void grl_trace_push(const char* name) { roctxRangePushA(name ? name : "grl"); }
+extern "C" void grl_trace_pop(void) { roctxRangePop(); }
+
 extern "C" int grl_dropedge_init(GrlDropEdge* de, float p, uint64_t seed, uint64_t call_id, int32_t drop_self) {
   GRL_CHECK_ARG(de != nullptr, "grl_dropedge_init: de is NULL");
   GRL_CHECK_ARG(p >= 0.0f && p == p, "grl_dropedge_init: p must be >= 0 (got %f)", (double)p);
@@ -713,6 +716,7 @@ extern "C" int grl_dropedge_mask(const GrlDropEdge* de, uint64_t id_base, int64_
 
 extern "C" int grl_typed_spmm_fwd(const GrlTypedCsr* g, const float* X, int64_t ldx, int32_t F, float* Z,
                                   const GrlDropEdge* de, grl_stream_t stream) {
+  TraceRange trace_("grl_typed_spmm_fwd");
   GRL_CHECK_ARG(g != nullptr, "grl_typed_spmm_fwd: graph is NULL");
   GRL_CHECK_ARG(g->num_rows >= 0 && g->num_types >= 1 && g->num_types <= 63,
                 "grl_typed_spmm_fwd: num_types must be in [1, 63] (got %d)", g->num_types);
@@ -731,6 +735,7 @@ extern "C" int grl_typed_spmm_fwd(const GrlTypedCsr* g, const float* X, int64_t 
 extern "C" int grl_typed_spmm_fwd_slice(const GrlTypedCsr* g, const float* X, int64_t ldx, int32_t F,
                                         int64_t self_col0, float* Z, int64_t ldz, int32_t zseg,
                                         const GrlDropEdge* de, grl_stream_t stream) {
+  TraceRange trace_("grl_typed_spmm_fwd_slice");
   GRL_CHECK_ARG(g != nullptr, "grl_typed_spmm_fwd_slice: graph is NULL");
   GRL_CHECK_ARG(g->num_rows >= 0 && g->num_types >= 1 && g->num_types <= 63,
                 "grl_typed_spmm_fwd_slice: num_types must be in [1, 63] (got %d)", g->num_types);
@@ -751,6 +756,7 @@ extern "C" int grl_typed_spmm_fwd_slice(const GrlTypedCsr* g, const float* X, in
 
 extern "C" int grl_typed_spmm_bwd(const GrlTypedCsc* g, const float* dZ, int32_t F, float* dX, int64_t lddx,
                                   const GrlDropEdge* de, grl_stream_t stream) {
+  TraceRange trace_("grl_typed_spmm_bwd");
   GRL_CHECK_ARG(g != nullptr, "grl_typed_spmm_bwd: graph is NULL");
   GRL_CHECK_ARG(g->num_rows >= 0 && g->self_rows >= 0 && g->self_rows <= g->num_rows,
                 "grl_typed_spmm_bwd: bad num_rows/self_rows");

@@ -10,6 +10,7 @@ e.g. gnn/models/base_network.py:34-47; we keep that convention).
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 import threading
@@ -123,6 +124,8 @@ _P = ctypes.POINTER
 SIGNATURES = {
     "grl_version": (ctypes.c_char_p, []),
     "grl_last_error": (ctypes.c_char_p, []),
+    "grl_trace_push": (None, [ctypes.c_char_p]),
+    "grl_trace_pop": (None, []),
     "grl_dropedge_init": (_c_i32, [_P(GrlDropEdge), ctypes.c_float, _c_u64, _c_u64, _c_i32]),
     "grl_dropedge_init_device": (_c_i32, [_P(GrlDropEdge), ctypes.c_float, _c_vp, _c_u64, _c_i32]),
     "grl_dropedge_mask": (_c_i32, [_P(GrlDropEdge), _c_u64, _c_i64, _c_vp, _c_vp]),
@@ -197,6 +200,17 @@ def check(rc: int, what: str) -> None:
 
 def call(name: str, *args) -> None:
     check(getattr(lib(), name)(*args), name)
+
+
+@contextlib.contextmanager
+def trace(name: str):
+    """roctx range (grl_trace_push / grl_trace_pop) around host-side steps,
+    e.g. the halo exchange; shown by `rocprofv3 --marker-trace`."""
+    lib().grl_trace_push(name.encode())
+    try:
+        yield
+    finally:
+        lib().grl_trace_pop()
 
 
 def version() -> str:

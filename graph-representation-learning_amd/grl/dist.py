@@ -37,6 +37,7 @@ from typing import List, Optional
 import torch
 import torch.distributed as dist
 
+from ._lib import trace
 from .graph import DropEdge, TypedGraph
 from .ops import graph_linear, typed_aggregate
 
@@ -174,6 +175,11 @@ def build_halo_plan(colidx: torch.Tensor, row_begin: int, row_end: int, group=No
 class _HaloExchange(torch.autograd.Function):
     @staticmethod
     def forward(ctx, X_loc: torch.Tensor, plan: HaloPlan, group):
+        with trace("grl.halo_exchange"):
+            return _HaloExchange._forward(ctx, X_loc, plan, group)
+
+    @staticmethod
+    def _forward(ctx, X_loc: torch.Tensor, plan: HaloPlan, group):
         F = X_loc.shape[1]
         X_ext = X_loc.new_empty(plan.n_loc + plan.n_halo, F)
         X_ext[: plan.n_loc].copy_(X_loc)
@@ -279,9 +285,13 @@ class HaloPipeline:
 
     def _exchange(self, c: int):
         """Start slice c's exchange; returns a work handle (or None if done)."""
-        p, t = self.plan, self.tables[c]
         if self.world == 1:
             return None
+        with trace(f"grl.halo_slice{c}"):
+            return self._exchange_slice(c)
+
+    def _exchange_slice(self, c: int):
+        p, t = self.plan, self.tables[c]
         if p.mode == "dense":
             if self.side is None:
                 all_gather_into(t[p.stride:], t[:p.stride], self.group)

@@ -144,6 +144,12 @@ typedef struct GrlDropEdge {
 const char* grl_version(void);
 const char* grl_last_error(void);
 
+/* roctx ranges (rocprofv3 --marker-trace): the hot entry points push their
+ * own; these let a host layer bracket its steps, e.g. the halo exchange of a
+ * node-range shard (grl/dist.py).  Pop closes the innermost open range.   */
+void grl_trace_push(const char* name);
+void grl_trace_pop(void);
+
 /* Fills *de for drop probability p, RNG stream (seed, call_id).
  * drop_self = 1 reproduces efficient_mode=True (drop_robust_gcn.py:69,76):
  * the mask covers the identity block; 0 reproduces efficient_mode=False,

@@ -12,7 +12,8 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libgrl_oracle.so")
+# GRL_ORACLE_LIB: another build of grl_oracle.c (the ASan build of tests/test_asan.py)
+LIB_PATH = os.environ.get("GRL_ORACLE_LIB", os.path.join(_HERE, "libgrl_oracle.so"))
 
 
 class ODrop(ctypes.Structure):
