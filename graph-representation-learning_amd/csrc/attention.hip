@@ -244,7 +244,10 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(AttnArgs a) {
   const float mq = qv ? a.smax[b * N + q] : 0.0f;
   const float il = qv ? 1.0f / a.ssum[b * N + q] : 0.0f;
   const float Dq = qv ? a.Drow[b * N + q] : 0.0f;
-  f32x16 dq = zero16();
+  constexpr int DT = (DKP + 31) / 32;  // 32-wide dQ tiles (dk up to 64)
+  f32x16 dq[DT];
+#pragma unroll
+  for (int j = 0; j < DT; ++j) dq[j] = zero16();
   Stager<DKP, LDK> sk;
   Stager<DV, DV> sh;
   const bool vk = vec_ok(Kb, a.dk), vh = vec_ok(Hb, a.dv);
@@ -271,18 +274,22 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(AttnArgs a) {
       s[r] = p * (dp[r] - Dq);  // dS
     }
 #pragma unroll
-    for (int st = 0; st < 16; ++st) {
-      const float kv = l32 < DKP ? Ks[kappa(st, h) * LDK + l32] : 0.0f;
-      dq = MFMA(kv, s[st], dq);
-    }
+    for (int j = 0; j < DT; ++j)
+#pragma unroll
+      for (int st = 0; st < 16; ++st) {
+        const float kv = 32 * j + l32 < DKP ? Ks[kappa(st, h) * LDK + 32 * j + l32] : 0.0f;
+        dq[j] = MFMA(kv, s[st], dq[j]);
+      }
     __syncthreads();
   }
   if (qv) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int d = kappa(r, h);
-      if (d < a.dk) a.dQ[(b * N + q) * a.dk + d] = dq[r];
-    }
+    for (int j = 0; j < DT; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int d = 32 * j + kappa(r, h);
+        if (d < a.dk) a.dQ[(b * N + q) * a.dk + d] = dq[j][r];
+      }
   }
 }
 
@@ -315,7 +322,10 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(AttnArgs a) {
   f32x16 dh[NT];
 #pragma unroll
   for (int t = 0; t < NT; ++t) dh[t] = zero16();
-  f32x16 dk = zero16();
+  constexpr int DT = (DKP + 31) / 32;  // 32-wide dK tiles (dk up to 64)
+  f32x16 dk[DT];
+#pragma unroll
+  for (int j = 0; j < DT; ++j) dk[j] = zero16();
 
   Stager<DKP, LDK> sq;
   Stager<DV, DV> so;
@@ -368,10 +378,12 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(AttnArgs a) {
 #pragma unroll
       for (int st = 0; st < 16; ++st) dh[t] = MFMA(Os[kappa(st, h) * DV + t * 32 + l32], s[st], dh[t]);
 #pragma unroll
-    for (int st = 0; st < 16; ++st) {
-      const float qv = l32 < DKP ? Qs[kappa(st, h) * LDK + l32] : 0.0f;
-      dk = MFMA(qv, ds[st], dk);
-    }
+    for (int j = 0; j < DT; ++j)
+#pragma unroll
+      for (int st = 0; st < 16; ++st) {
+        const float qv = 32 * j + l32 < DKP ? Qs[kappa(st, h) * LDK + 32 * j + l32] : 0.0f;
+        dk[j] = MFMA(qv, ds[st], dk[j]);
+      }
     __syncthreads();
   }
   if (kv) {
@@ -384,10 +396,12 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(AttnArgs a) {
         if (f < a.dv) a.dH[rowv + f] = dh[t][r];
       }
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int d = kappa(r, h);
-      if (d < a.dk) a.dK[rowk + d] = dk[r];
-    }
+    for (int j = 0; j < DT; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int d = 32 * j + kappa(r, h);
+        if (d < a.dk) a.dK[rowk + d] = dk[j][r];
+      }
   }
 }
 
@@ -1152,7 +1166,8 @@ bool attn_x6_enabled() {
 template <int DKP, int NT>
 int launch_attn(AttnPass pass, const AttnArgs& a0, int64_t B, int S, hipStream_t st) {
   AttnArgs a = a0;
-  const bool x6 = attn_x6_enabled() && (pass == PASS_FWD || NT == 4);
+  // dk in (32, 64] (NodeSelfAtten of input_dim > 256): the fp32-MFMA kernels only
+  const bool x6 = DKP <= 32 && attn_x6_enabled() && (pass == PASS_FWD || NT == 4);
   if (!x6 || !a.part) S = 1;
   if (S == 1) {
     a.part = a.part2 = nullptr;
@@ -1173,7 +1188,14 @@ int launch_attn(AttnPass pass, const AttnArgs& a0, int64_t B, int S, hipStream_t
     else                                                                                            \
       hipLaunchKernelGGL((KERNEL<__VA_ARGS__, false, false>), grid, dim3(256), 0, st, a);           \
   } while (0)
-  if (pass == PASS_FWD && x6) {
+  if constexpr (DKP > 32) {
+    if (pass == PASS_FWD)
+      hipLaunchKernelGGL((attn_fwd_kernel<DKP, NT>), grid, dim3(256), 0, st, a);
+    else if (pass == PASS_BWD_Q)
+      hipLaunchKernelGGL((attn_bwd_q_kernel<DKP, NT>), grid, dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL((attn_bwd_kv_kernel<DKP, NT>), grid, dim3(256), 0, st, a);
+  } else if (pass == PASS_FWD && x6) {
     GRL_X6L(attn_fwd_x6_kernel, DKP, NT);
     if (S > 1) {
       GRL_LAUNCH_CHECK();
@@ -1241,7 +1263,9 @@ int dispatch_nt(AttnPass pass, const AttnArgs& a, int64_t B, int S, hipStream_t 
 
 int dispatch(AttnPass pass, const AttnArgs& a, int64_t B, int S, hipStream_t st) {
   if (a.N == 0 || B == 0) return GRL_OK;
-  return a.dk <= 16 ? dispatch_nt<16>(pass, a, B, S, st) : dispatch_nt<32>(pass, a, B, S, st);
+  if (a.dk <= 16) return dispatch_nt<16>(pass, a, B, S, st);
+  if (a.dk <= 32) return dispatch_nt<32>(pass, a, B, S, st);
+  return dispatch_nt<64>(pass, a, B, S, st);
 }
 
 constexpr int64_t kAttnPlaneMinRows = 4096;
@@ -1269,7 +1293,7 @@ int check_dims(const char* who, int64_t B, int64_t N, int dk, int dv) {
   GRL_CHECK_ARG(B >= 0 && N >= 0, "%s: negative size", who);
   // dk = 0 is legal (input_dim < 8 gives Linear(F, 0) in the reference): all
   // scores are 0 and the attention is uniform, which the kernels compute as is.
-  GRL_CHECK_ARG(dk >= 0 && dk <= 32, "%s: key width %d outside [0, 32] (NodeSelfAtten: input_dim // 8)", who, dk);
+  GRL_CHECK_ARG(dk >= 0 && dk <= 64, "%s: key width %d outside [0, 64] (NodeSelfAtten: input_dim // 8)", who, dk);
   GRL_CHECK_ARG(dv >= 1 && dv <= 256, "%s: value width %d outside [1, 256]", who, dv);
   GRL_CHECK_ARG(B * ceil_div(N, 128) < 2147483647LL && B < 65536, "%s: grid too large", who);
   return GRL_OK;
@@ -1281,7 +1305,7 @@ int check_dims(const char* who, int64_t B, int64_t N, int dk, int dv) {
 using namespace grl;
 
 extern "C" size_t grl_node_attention_workspace_size(int64_t B, int64_t N, int32_t dk, int32_t dv) {
-  if (B <= 0 || N <= 0 || dk < 0 || dk > 32 || dv < 1 || dv > 256) return 0;
+  if (B <= 0 || N <= 0 || dk < 0 || dk > 32 || dv < 1 || dv > 256) return 0;  // dk > 32: fp32 kernels, no workspace
   const int64_t rows = B * N;
   int64_t kr;
   const int S = attn_splits(B, N, &kr);
@@ -1318,7 +1342,7 @@ extern "C" int grl_node_attention_fwd(const float* Q, const float* K, const floa
   int S = 1;
   // below ~4k rows the per-call split launches cost more than the in-kernel
   // splits they save (a 74-node page: 2 extra launches per call)
-  if (workspace && attn_x6_enabled()) {  // split K and H once for every query block
+  if (workspace && attn_x6_enabled() && dk <= 32) {  // split K and H once for every query block
     unsigned char* cur = reinterpret_cast<unsigned char*>((reinterpret_cast<uintptr_t>(workspace) + 255) & ~(uintptr_t)255);
     const unsigned char* end = static_cast<unsigned char*>(workspace) + workspace_bytes;
     const uint16_t *kp = nullptr, *hp = nullptr;
@@ -1366,7 +1390,7 @@ extern "C" int grl_node_attention_bwd(const float* Q, const float* K, const floa
   a.dv = dv;
   hipStream_t st = as_stream(stream);
   int S = 1;
-  if (workspace && attn_x6_enabled() && attn_dvp(dv) == 128) {  // the x6 backward's operands, split once
+  if (workspace && attn_x6_enabled() && attn_dvp(dv) == 128 && dk <= 32) {  // the x6 backward's operands
     unsigned char* cur = reinterpret_cast<unsigned char*>((reinterpret_cast<uintptr_t>(workspace) + 255) & ~(uintptr_t)255);
     const unsigned char* end = static_cast<unsigned char*>(workspace) + workspace_bytes;
     const uint16_t *kp = nullptr, *hp = nullptr, *qp = nullptr, *op = nullptr;

@@ -121,7 +121,11 @@ struct SplitDev {
 //               sources are X rows (index = colidx), ids = edge_base + e.
 // BWD = true : backward, rows are source nodes with one segment (CSC column),
 //               sources are dZ rows (index = zrow), ids = edge_base + eid[e].
-template <int VEC, int NV, int U, bool VALS, bool BWD>
+// ACCUM (backward only): continue each column's sum from the value already in
+// dX instead of starting from the self term -- the later edge blocks of a
+// graph with >= 2^31 edges (grl_typed_spmm_bwd_accum), whose CSC positions all
+// follow the earlier blocks', so the fmaf chain equals the one-CSC chain.
+template <int VEC, int NV, int U, bool VALS, bool BWD, bool ACCUM = false>
 __global__ __launch_bounds__(256) void spmm_kernel(
     int64_t num_rows, int64_t self_rows, int S, int hs,
     const int32_t* __restrict__ ptr,   // fwd: rowptr [rows*S+1]; bwd: colptr [rows+1]
@@ -169,8 +173,13 @@ __global__ __launch_bounds__(256) void spmm_kernel(
       pv = lane <= nseg_row ? ptr[n * nseg_row + lane] : 0;
       nseg = nseg_row;
       const bool heavy = readlane_i(pv, nseg) - readlane_i(pv, 0) > sp.threshold;
+      if (ACCUM && !heavy) {
+#pragma unroll
+        for (int k = 0; k < NV; ++k)
+          if (cval[k]) acc[k] = *reinterpret_cast<const vec_t*>(orow + coff[k]);
+      }
       // ---- self term (identity block of A_pre, robust_gcn.py:58-65) ------
-      if (hs && (!BWD || (n < self_rows && !heavy))) {
+      if (!ACCUM && hs && (!BWD || (n < self_rows && !heavy))) {
         float w = 1.0f;
         if (de.active && de.drop_self) w = dropedge_weight(de, 1.0f, self_base + (uint64_t)n);
         const float* srow = BWD ? (src + n * zstride) : (src + (n + self_row0) * lds);
@@ -404,7 +413,7 @@ __global__ __launch_bounds__(256) void spmm_pair_kernel(
 
 // Heavy segment h: out = [self term (bwd)] + sum of its chunk partials in
 // chunk order.  One wavefront per heavy segment.
-template <int VEC, int NV, bool BWD>
+template <int VEC, int NV, bool BWD, bool ACCUM = false>
 __global__ __launch_bounds__(256) void spmm_fixup_kernel(
     int64_t num_heavy, const int32_t* __restrict__ heavy_seg, const int32_t* __restrict__ heavy_cptr,
     const float* __restrict__ partials, int nseg, int S, int hs, int64_t self_rows, uint64_t self_base,
@@ -421,7 +430,7 @@ __global__ __launch_bounds__(256) void spmm_fixup_kernel(
     const int64_t n = s / nseg, t = s % nseg;
     const int c_begin = heavy_cptr[h], c_end = heavy_cptr[h + 1];
     float w_self = 0.0f;
-    if (BWD && hs && n < self_rows) {
+    if (!ACCUM && BWD && hs && n < self_rows) {
       w_self = 1.0f;
       if (de.active && de.drop_self) w_self = dropedge_weight(de, 1.0f, self_base + (uint64_t)n);
     }
@@ -432,6 +441,7 @@ __global__ __launch_bounds__(256) void spmm_fixup_kernel(
       if (col >= F) continue;
       vec_t acc;
       vzero(acc);
+      if (ACCUM) acc = *reinterpret_cast<const vec_t*>(orow + col);
       if (BWD && w_self != 0.0f) acc = vmul(w_self, *reinterpret_cast<const vec_t*>(dZ + n * zstride + col));
       for (int c = c_begin; c < c_end; ++c) vadd(acc, *reinterpret_cast<const vec_t*>(partials + (int64_t)c * F + col));
       *reinterpret_cast<vec_t*>(orow + col) = acc;
@@ -583,7 +593,7 @@ int launch_spmm(int64_t num_rows, int64_t self_rows, int S, int hs, const int32_
                 const int32_t* eid, const float* vals, uint64_t edge_base, uint64_t self_base, const float* src,
                 int64_t lds, int F, float* out, int64_t ldo, const DropDev& de, const GrlSplitPlan* plan,
                 hipStream_t stream, const float* align_probe, int64_t self_row0 = 0, int64_t table_rows = -1,
-                int zseg = 0) {
+                int zseg = 0, bool accum = false) {
   if (zseg <= 0) zseg = F;
   if (num_rows == 0) return GRL_OK;
   SplitDev sp;
@@ -600,8 +610,16 @@ int launch_spmm(int64_t num_rows, int64_t self_rows, int S, int hs, const int32_
   const dim3 block(256);
   const bool v = vals != nullptr;
 #define GRL_SPMM_LAUNCH(VEC, NV, U, VALS)                                                                  \
-  hipLaunchKernelGGL((spmm_kernel<VEC, NV, U, VALS, BWD>), grid, block, 0, stream, num_rows, self_rows, S, \
-                     hs, ptr, idx, eid, vals, edge_base, self_base, self_row0, src, lds, F, out, ldo, zseg, de, sp)
+  do {                                                                                                     \
+    if (BWD && accum)                                                                                      \
+      hipLaunchKernelGGL((spmm_kernel<VEC, NV, U, VALS, BWD, true>), grid, block, 0, stream, num_rows,      \
+                         self_rows, S, hs, ptr, idx, eid, vals, edge_base, self_base, self_row0, src, lds, F, \
+                         out, ldo, zseg, de, sp);                                                          \
+    else                                                                                                   \
+      hipLaunchKernelGGL((spmm_kernel<VEC, NV, U, VALS, BWD>), grid, block, 0, stream, num_rows, self_rows, \
+                         S, hs, ptr, idx, eid, vals, edge_base, self_base, self_row0, src, lds, F, out, ldo, \
+                         zseg, de, sp);                                                                    \
+  } while (0)
   if (sh.vec == 4) {
     if (sh.nv == 1 && F <= 128 && !BWD && pair_rows_enabled()) {
       // narrow rows (column slices of a pipelined halo): two edges per gather instruction
@@ -631,9 +649,16 @@ int launch_spmm(int64_t num_rows, int64_t self_rows, int S, int hs, const int32_
     const dim3 fgrid((unsigned)std::min<int64_t>(ceil_div(plan->num_heavy, 4), cap), grid.y);
     const int nseg = BWD ? 1 : S;
 #define GRL_FIXUP_LAUNCH(VEC, NV)                                                                            \
-  hipLaunchKernelGGL((spmm_fixup_kernel<VEC, NV, BWD>), fgrid, block, 0, stream, plan->num_heavy,            \
-                     plan->heavy_seg, plan->heavy_cptr, plan->partials, nseg, S, hs, self_rows, self_base, src, \
-                     F, out, ldo, zseg, de)
+  do {                                                                                                       \
+    if (BWD && accum)                                                                                        \
+      hipLaunchKernelGGL((spmm_fixup_kernel<VEC, NV, BWD, true>), fgrid, block, 0, stream, plan->num_heavy,  \
+                         plan->heavy_seg, plan->heavy_cptr, plan->partials, nseg, S, hs, self_rows, self_base, \
+                         src, F, out, ldo, zseg, de);                                                        \
+    else                                                                                                     \
+      hipLaunchKernelGGL((spmm_fixup_kernel<VEC, NV, BWD>), fgrid, block, 0, stream, plan->num_heavy,        \
+                         plan->heavy_seg, plan->heavy_cptr, plan->partials, nseg, S, hs, self_rows, self_base, \
+                         src, F, out, ldo, zseg, de);                                                        \
+  } while (0)
     if (sh.vec == 4) {
       if (sh.nv == 1) GRL_FIXUP_LAUNCH(4, 1); else GRL_FIXUP_LAUNCH(4, 2);
     } else {
@@ -754,20 +779,31 @@ extern "C" int grl_typed_spmm_fwd_slice(const GrlTypedCsr* g, const float* X, in
                             as_stream(stream), Z, self_col0, -1, zseg);
 }
 
-extern "C" int grl_typed_spmm_bwd(const GrlTypedCsc* g, const float* dZ, int32_t F, float* dX, int64_t lddx,
-                                  const GrlDropEdge* de, grl_stream_t stream) {
-  TraceRange trace_("grl_typed_spmm_bwd");
-  GRL_CHECK_ARG(g != nullptr, "grl_typed_spmm_bwd: graph is NULL");
-  GRL_CHECK_ARG(g->num_rows >= 0 && g->self_rows >= 0 && g->self_rows <= g->num_rows,
-                "grl_typed_spmm_bwd: bad num_rows/self_rows");
-  GRL_CHECK_ARG(g->num_types >= 1 && g->num_types <= 63, "grl_typed_spmm_bwd: num_types must be in [1, 63]");
-  GRL_CHECK_ARG(F > 0 && lddx >= F, "grl_typed_spmm_bwd: need F > 0 and lddx >= F");
+static int spmm_bwd_entry(const char* who, const GrlTypedCsc* g, const float* dZ, int32_t F, float* dX,
+                          int64_t lddx, const GrlDropEdge* de, grl_stream_t stream, bool accum) {
+  GRL_CHECK_ARG(g != nullptr, "%s: graph is NULL", who);
+  GRL_CHECK_ARG(g->num_rows >= 0 && g->self_rows >= 0 && g->self_rows <= g->num_rows, "%s: bad num_rows/self_rows",
+                who);
+  GRL_CHECK_ARG(g->num_types >= 1 && g->num_types <= 63, "%s: num_types must be in [1, 63]", who);
+  GRL_CHECK_ARG(F > 0 && lddx >= F, "%s: need F > 0 and lddx >= F", who);
   if (g->num_rows == 0) return GRL_OK;
-  GRL_CHECK_ARG(dZ && dX && g->colptr && (g->nnz == 0 || (g->zrow && g->eid)), "grl_typed_spmm_bwd: NULL pointer");
+  GRL_CHECK_ARG(dZ && dX && g->colptr && (g->nnz == 0 || (g->zrow && g->eid)), "%s: NULL pointer", who);
   const int hs = g->has_self ? 1 : 0;
   return launch_spmm<true>(g->num_rows, g->self_rows, g->num_types, hs, g->colptr, g->zrow, g->eid, g->vals,
                            g->edge_id_base, g->self_id_base, dZ, (int64_t)F, F, dX, lddx, to_dev(de), g->split,
-                           as_stream(stream), dX);
+                           as_stream(stream), dX, 0, -1, 0, accum);
+}
+
+extern "C" int grl_typed_spmm_bwd_accum(const GrlTypedCsc* g, const float* dZ, int32_t F, float* dX, int64_t lddx,
+                                        const GrlDropEdge* de, grl_stream_t stream) {
+  TraceRange trace_("grl_typed_spmm_bwd_accum");
+  return spmm_bwd_entry("grl_typed_spmm_bwd_accum", g, dZ, F, dX, lddx, de, stream, true);
+}
+
+extern "C" int grl_typed_spmm_bwd(const GrlTypedCsc* g, const float* dZ, int32_t F, float* dX, int64_t lddx,
+                                  const GrlDropEdge* de, grl_stream_t stream) {
+  TraceRange trace_("grl_typed_spmm_bwd");
+  return spmm_bwd_entry("grl_typed_spmm_bwd", g, dZ, F, dX, lddx, de, stream, false);
 }
 
 extern "C" size_t grl_split_plan_workspace_size(int64_t rows) {

@@ -40,6 +40,10 @@ class GraphConv(nn.Module):
         self.L = num_edges
         self.F = input_dim
         self.gpu = torch.cuda.is_available()
+        # training memory: None = keep Z = A_pre V for the weight gradient unless it
+        # exceeds grl.ops.RECOMPUTE_Z_BYTES, True = always re-aggregate it in the
+        # backward (saves (L+1)F floats per node), False = always keep it
+        self.recompute_aggregation: Optional[bool] = None
         # Same allocation + init sequence as robust_gcn.py:22-30 (xavier_normal_
         # on h_weights, then normal_(1e-4, 5e-5) on bias): identical RNG draws.
         self.h_weights = nn.Parameter(torch.empty(self.F * (self.L + 1), self.C))
@@ -75,7 +79,7 @@ class GraphConv(nn.Module):
         """Aggregate + linear (+ fused ReLU) on a ready TypedGraph."""
         B, N = V.shape[0], V.shape[1]
         # new_V = A_pre V (B*N, (L+1)F) then new_V h_weights + bias, one autograd node
-        out = graph_conv(V, graph, self.h_weights, self.bias, relu=relu)
+        out = graph_conv(V, graph, self.h_weights, self.bias, relu=relu, recompute=self.recompute_aggregation)
         return out.view(B, N, self.C)
 
     def forward(self, V: torch.Tensor, A: AdjLike, preprocess_A: bool = True) -> torch.Tensor:

@@ -367,3 +367,110 @@ class TypedGraph:
         call("grl_dropedge_mask", ctypes.byref(c), id_base, count, keep.data_ptr(),
              current_stream_handle(self.device))
         return keep[:count]
+
+
+# Edges per block of an EdgeBlockedGraph: the kernels index edges with 32-bit
+# positions (4-byte rowptr, cheap address arithmetic on the hot path).
+MAX_BLOCK_EDGES = 2**31 - 1
+
+
+class EdgeBlockedGraph:
+    """A typed graph with 2^31 or more edges (SURVEY.md §8(b) Dtypes row:
+    "int64 rowptr when E >= 2^31"), held as consecutive row blocks of fewer
+    than MAX_BLOCK_EDGES edges each.  Every block is a TypedGraph over rows
+    [row0, row1) with an int32 rowptr relative to its first edge, global column
+    ids, and edge_id_base = the block's first global CSR position, so DropEdge
+    ids are the 64-bit global positions of one big CSR.  The forward runs one
+    aggregation per block (grl_typed_spmm_fwd_slice, self rows at row0, Z
+    rows at row0); the backward runs the blocks' CSCs in block order, the
+    first with grl_typed_spmm_bwd, the rest with grl_typed_spmm_bwd_accum --
+    the same fmaf chain per element as a single int64 CSR (heavy-row chunks
+    are cut per block)."""
+
+    def __init__(self, blocks, row_bounds, num_cols: int):
+        self.blocks = list(blocks)
+        self.row_bounds = list(row_bounds)  # [0, r1, r2, ..., num_rows]
+        b0 = self.blocks[0]
+        self.num_types, self.has_self = b0.num_types, b0.has_self
+        self.num_rows = self.row_bounds[-1]
+        self.num_cols = int(num_cols)
+        self.nnz = sum(b.nnz for b in self.blocks)
+        self.dropedge: Optional[DropEdge] = None
+
+    @property
+    def device(self) -> torch.device:
+        return self.blocks[0].device
+
+    @property
+    def segments(self) -> int:
+        return self.num_types + (1 if self.has_self else 0)
+
+    def with_dropedge(self, de: Optional[DropEdge]) -> "EdgeBlockedGraph":
+        g = EdgeBlockedGraph.__new__(EdgeBlockedGraph)
+        g.__dict__.update(self.__dict__)
+        g.blocks = [b.with_dropedge(de) for b in self.blocks]
+        g.dropedge = de
+        return g
+
+    def __repr__(self) -> str:
+        return (f"EdgeBlockedGraph(rows={self.num_rows}, cols={self.num_cols}, types={self.num_types}, "
+                f"nnz={self.nnz}, blocks={len(self.blocks)}, dropedge={self.dropedge})")
+
+    @classmethod
+    def from_csr64(cls, rowptr: torch.Tensor, colidx: torch.Tensor, num_types: int, *, num_cols: Optional[int] = None,
+                   has_self: bool = True, max_block_edges: int = MAX_BLOCK_EDGES) -> "EdgeBlockedGraph":
+        """One typed CSR with an int64 rowptr [num_rows*num_types + 1] and
+        int32 colidx, cut into row blocks of <= max_block_edges edges (a row
+        with more edges than that is refused)."""
+        _require_device(rowptr, "rowptr")
+        if rowptr.dtype != torch.int64 or colidx.dtype != torch.int32:
+            raise _lib.GrlError("from_csr64: rowptr must be int64 and colidx int32")
+        L = int(num_types)
+        num_rows = (rowptr.numel() - 1) // L
+        node_ptr = rowptr[::L].contiguous()  # [num_rows + 1]
+        nnz = int(node_ptr[-1])
+        E_total = nnz
+        bounds = [0]
+        while bounds[-1] < num_rows:
+            r0 = bounds[-1]
+            limit = torch.tensor([int(node_ptr[r0]) + max_block_edges], dtype=torch.int64, device=rowptr.device)
+            r1 = int(torch.searchsorted(node_ptr, limit, right=True)) - 1
+            r1 = min(max(r1, r0), num_rows)
+            if r1 == r0:
+                raise _lib.GrlError(f"row {r0} alone holds more than {max_block_edges} edges")
+            bounds.append(r1)
+        blocks = []
+        ncols = num_rows if num_cols is None else int(num_cols)
+        for r0, r1 in zip(bounds[:-1], bounds[1:]):
+            e0, e1 = int(node_ptr[r0]), int(node_ptr[r1])
+            rp = (rowptr[r0 * L: r1 * L + 1] - e0).to(torch.int32)
+            blocks.append(TypedGraph(rp, colidx[e0:e1], L, has_self=has_self, num_cols=ncols, edge_id_base=e0,
+                                     self_id_base=E_total + r0, self_rows=r1 - r0))
+        return cls(blocks, bounds, ncols)
+
+    @classmethod
+    def synthetic(cls, num_nodes: int, avg_deg: float, num_types: int = 6, *, kind: str = "er", seed: int = 0,
+                  device="cuda", max_block_edges: int = MAX_BLOCK_EDGES) -> "EdgeBlockedGraph":
+        """TypedGraph.synthetic's graph (same edges, same global order) built
+        as row blocks, for edge counts beyond one int32 CSR: the blocks are
+        row ranges holding <= max_block_edges candidate edges each."""
+        deg = TypedGraph.synthetic_degrees(num_nodes, avg_deg, num_types, kind=kind, seed=seed, device=device)
+        cum = torch.cumsum(deg.to(torch.int64), 0)
+        bounds = [0]
+        while bounds[-1] < num_nodes:
+            r0 = bounds[-1]
+            base = int(cum[r0 - 1]) if r0 else 0
+            limit = torch.tensor([base + max_block_edges], dtype=torch.int64, device=cum.device)
+            r1 = min(num_nodes, int(torch.searchsorted(cum, limit, right=True)))
+            if r1 == r0:
+                raise _lib.GrlError(f"node {r0} alone has more than {max_block_edges} candidate edges")
+            bounds.append(r1)
+        parts = [TypedGraph.synthetic(num_nodes, avg_deg, num_types, kind=kind, seed=seed, row_range=(a, b),
+                                      device=device) for a, b in zip(bounds[:-1], bounds[1:])]
+        E_total = sum(p.nnz for p in parts)
+        blocks, e0 = [], 0
+        for (a, b), p in zip(zip(bounds[:-1], bounds[1:]), parts):
+            blocks.append(TypedGraph(p.rowptr, p.colidx, num_types, num_cols=num_nodes, edge_id_base=e0,
+                                     self_id_base=E_total + a, self_rows=b - a))
+            e0 += p.nnz
+        return cls(blocks, bounds, num_nodes)

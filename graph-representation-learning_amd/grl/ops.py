@@ -16,7 +16,7 @@ import torch
 
 from . import _lib
 from ._lib import call
-from .graph import TypedGraph, _require_device, current_stream_handle
+from .graph import EdgeBlockedGraph, TypedGraph, _require_device, current_stream_handle
 
 
 def _rows_view(X: torch.Tensor) -> torch.Tensor:
@@ -30,6 +30,8 @@ def _rows_view(X: torch.Tensor) -> torch.Tensor:
 def spmm_forward(X: torch.Tensor, graph: TypedGraph, out: torch.Tensor = None) -> torch.Tensor:
     """Z = A_drop X without autograd bookkeeping, optionally into `out`
     (contiguous [num_rows, segments*F] fp32): the inference / benchmark form."""
+    if isinstance(graph, EdgeBlockedGraph):
+        return _blocked_forward(X, graph, out)
     _require_device(X, "node features")
     if X.dtype != torch.float32:
         raise _lib.GrlError(f"node features must be float32 (got {X.dtype})")
@@ -79,8 +81,45 @@ def spmm_forward_slice(X: torch.Tensor, graph: TypedGraph, out: torch.Tensor, co
     return out
 
 
+def _blocked_forward(X: torch.Tensor, graph: EdgeBlockedGraph, out: torch.Tensor = None) -> torch.Tensor:
+    """Z of a graph with >= 2^31 edges: one aggregation per row block (self
+    rows at the block's first row, Z rows likewise)."""
+    X2 = _rows_view(X)
+    if X2.shape[0] != graph.num_cols:
+        raise _lib.GrlError(f"features have {X2.shape[0]} rows, graph gathers from {graph.num_cols}")
+    F = X2.shape[1]
+    shape = (graph.num_rows, graph.segments * F)
+    if out is None:
+        out = torch.empty(shape, dtype=torch.float32, device=X.device)
+    elif tuple(out.shape) != shape or not out.is_contiguous() or out.dtype != torch.float32:
+        raise _lib.GrlError(f"out must be a contiguous float32 {shape} tensor")
+    for blk, r0, r1 in zip(graph.blocks, graph.row_bounds[:-1], graph.row_bounds[1:]):
+        spmm_forward_slice(X2, blk, out[r0:r1], 0, self_col0=r0)
+    return out
+
+
+def _blocked_backward(dZ: torch.Tensor, graph: EdgeBlockedGraph, F: int) -> torch.Tensor:
+    """dX of a graph with >= 2^31 edges: the blocks' CSCs in block order --
+    the first with the self term over every row, the rest continuing each
+    column's sum (grl_typed_spmm_bwd_accum)."""
+    dZ = dZ.contiguous().float()
+    dX = torch.empty(graph.num_cols, F, dtype=torch.float32, device=dZ.device)
+    stream = current_stream_handle(dZ.device)
+    ldz = graph.segments * F
+    for i, (blk, r0) in enumerate(zip(graph.blocks, graph.row_bounds[:-1])):
+        csc = blk.csc_c(F)
+        if i == 0:
+            csc.self_rows = min(graph.num_rows, graph.num_cols)  # every node's self loop, dZ rows from 0
+        de = blk.dropedge.to_c() if blk.dropedge is not None else None
+        call("grl_typed_spmm_bwd" if i == 0 else "grl_typed_spmm_bwd_accum", ctypes.byref(csc),
+             dZ.data_ptr() + 4 * r0 * ldz, F, dX.data_ptr(), F, ctypes.byref(de) if de is not None else None, stream)
+    return dX
+
+
 def spmm_backward(dZ: torch.Tensor, graph: TypedGraph, F: int) -> torch.Tensor:
     """dX = A_drop^T dZ (grl_typed_spmm_bwd over the cached CSC, same mask)."""
+    if isinstance(graph, EdgeBlockedGraph):
+        return _blocked_backward(dZ, graph, F)
     dZ = dZ.contiguous().float()
     dX = torch.empty(graph.num_cols, F, dtype=torch.float32, device=dZ.device)
     csc = graph.csc_c(F)
@@ -199,17 +238,22 @@ class _GraphConv(torch.autograd.Function):
     39-41 ms per C3 layer either way, each kernel already fills the chip.)"""
 
     @staticmethod
-    def forward(ctx, X: torch.Tensor, graph: TypedGraph, W: torch.Tensor, b, relu: bool):
+    def forward(ctx, X: torch.Tensor, graph: TypedGraph, W: torch.Tensor, b, relu: bool, recompute: bool):
         Z = spmm_forward(X, graph)
         Wc = W.contiguous()
         out = linear_fwd(Z, Wc, b.contiguous() if b is not None else None, relu)
         ctx.graph, ctx.relu, ctx.has_b, ctx.xshape = graph, relu, b is not None, X.shape
-        ctx.save_for_backward(Z, Wc, out if relu else None)
+        ctx.recompute = recompute
+        # recompute: keep X (F wide) instead of Z ((L+1)F wide); the backward
+        # regenerates Z with the same DropEdge record, so it is the same bits
+        ctx.save_for_backward(X if recompute else Z, Wc, out if relu else None)
         return out
 
     @staticmethod
     def backward(ctx, g: torch.Tensor):
         Z, W, out = ctx.saved_tensors
+        if ctx.recompute and (ctx.needs_input_grad[2] or (ctx.has_b and ctx.needs_input_grad[3])):
+            Z = spmm_forward(Z, ctx.graph)
         g, mask = relu_grad(g.contiguous().float(), out if ctx.relu else None)
         want_w = ctx.needs_input_grad[2]
         want_b = ctx.has_b and ctx.needs_input_grad[3]
@@ -220,7 +264,7 @@ class _GraphConv(torch.autograd.Function):
             del dZ
         if want_w or want_b:
             dW, db = linear_bwd_weight(Z, g, mask, want_b)
-        return dX, None, dW if want_w else None, db, None
+        return dX, None, dW if want_w else None, db, None, None
 
 
 def graph_conv_infer(X: torch.Tensor, graph: TypedGraph, W: torch.Tensor, b=None, relu: bool = False,
@@ -254,14 +298,29 @@ def graph_conv_infer(X: torch.Tensor, graph: TypedGraph, W: torch.Tensor, b=None
     return out
 
 
-def graph_conv(X: torch.Tensor, graph: TypedGraph, W: torch.Tensor, b=None, relu: bool = False) -> torch.Tensor:
+# Z bytes above which a training GraphConv keeps X and recomputes Z in the
+# backward instead of holding Z between the passes (recompute=None): at C5
+# scale (2^23 nodes, d=512) Z is 120 GB per layer, X 17 GB.
+RECOMPUTE_Z_BYTES = 8 << 30
+
+
+def graph_conv(X: torch.Tensor, graph: TypedGraph, W: torch.Tensor, b=None, relu: bool = False,
+               recompute: bool = None) -> torch.Tensor:
     """GraphConv forward (aggregation + linear [+ReLU]) as one autograd node;
     X: [num_cols, F] (or [B, N, F] for a batch graph).  When no gradient is
     wanted (eval, torch.no_grad) it is one grl_graphconv_fwd call instead:
-    the same kernels, so the same bits."""
+    the same kernels, so the same bits.
+    recompute: True keeps X and re-aggregates Z in the backward (one more
+    SpMM pass for (L+1)x less saved memory); None decides by Z's size
+    (RECOMPUTE_Z_BYTES); both give the same gradients bit for bit."""
     if not (torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in (X, W, b))):
+        if isinstance(graph, EdgeBlockedGraph):  # one int32 CSR per call: aggregate by blocks, then the linear
+            return linear_fwd(spmm_forward(X, graph), W.contiguous(), b.contiguous() if b is not None else None,
+                              relu)
         return graph_conv_infer(X, graph, W, b, relu)
-    return _GraphConv.apply(X, graph, W, b, relu)
+    if recompute is None:
+        recompute = graph.num_rows * graph.segments * X.shape[-1] * 4 > RECOMPUTE_Z_BYTES
+    return _GraphConv.apply(X, graph, W, b, relu, bool(recompute))
 
 
 def graph_linear(Z: torch.Tensor, W: torch.Tensor, b=None, relu: bool = False) -> torch.Tensor:
@@ -288,6 +347,20 @@ def _attn_workspace(B, N, dk, dv, device):
     return (torch.empty(n, dtype=torch.uint8, device=device), n) if n else (None, 0)
 
 
+# Value columns per kernel call: the kernels hold one query's output row in
+# registers (dv <= 256; 128 when dk > 32, where the fp32 kernels also carry
+# 64-wide Q/K rows).  Wider values run as column blocks of one softmax: each
+# block recomputes S = Q K^T (same bits, so the same P), and the backward's
+# dS = P o (dP - D) is linear in the per-block dP_b and D_b, so dQ and dK are
+# the block sums (robust_gcn.py:78-96 for any input_dim up to 512).
+def _dv_blocks(dk: int, dv: int):
+    width = 256 if dk <= 32 else 128
+    n = -(-dv // width)
+    step = -(-dv // n)
+    step = -(-step // 32) * 32
+    return [(c0, min(dv, c0 + step)) for c0 in range(0, dv, step)]
+
+
 def node_attention_forward(Q, K, H, V, gamma, stats: bool = False):
     """out = gamma * softmax(Q K^T) H + V (robust_gcn.py:90-96), fused.
     stats=True also returns (o_norm, row_max, row_sum) for the backward."""
@@ -295,6 +368,15 @@ def node_attention_forward(Q, K, H, V, gamma, stats: bool = False):
     Q, K, H, V, gamma = (t.contiguous() for t in (Q, K, H, V, gamma))
     B, N, dk = Q.shape
     dv = H.shape[2]
+    blocks = _dv_blocks(dk, dv)
+    if len(blocks) > 1:
+        parts = [node_attention_forward(Q, K, H[..., a:b].contiguous(), V[..., a:b].contiguous(),
+                                        gamma[a:b].contiguous(), stats=stats) for a, b in blocks]
+        if not stats:
+            return torch.cat(parts, -1)
+        out = torch.cat([p[0] for p in parts], -1)
+        onorm = torch.cat([p[1] for p in parts], -1)
+        return out, onorm, parts[0][2], parts[0][3]
     out = torch.empty_like(V)
     onorm = torch.empty_like(V) if stats else None
     rmax = torch.empty(B, N, device=V.device) if stats else None
@@ -321,12 +403,23 @@ class _NodeAttention(torch.autograd.Function):
         B, N, dk = Q.shape
         dv = H.shape[2]
         dO = dout * gamma
-        D = (dO * onorm).sum(-1).contiguous()
-        dQ, dK, dH = torch.empty_like(Q), torch.empty_like(K), torch.empty_like(H)
-        ws, ws_bytes = _attn_workspace(B, N, dk, dv, Q.device)
-        call("grl_node_attention_bwd", Q.data_ptr(), K.data_ptr(), H.data_ptr(), dO.data_ptr(), rmax.data_ptr(),
-             rsum.data_ptr(), D.data_ptr(), dQ.data_ptr(), dK.data_ptr(), dH.data_ptr(), B, N, dk, dv,
-             ws.data_ptr() if ws is not None else None, ws_bytes, current_stream_handle(Q.device))
+        dQ = dK = None
+        dHs = []
+        for a, b in _dv_blocks(dk, dv):  # one block unless dv exceeds a call's width
+            dO_b = dO[..., a:b].contiguous()
+            D = (dO_b * onorm[..., a:b]).sum(-1).contiguous()
+            dQ_b, dK_b = torch.empty_like(Q), torch.empty_like(K)
+            dH_b = torch.empty(B, N, b - a, dtype=H.dtype, device=H.device)
+            H_b = H[..., a:b].contiguous()
+            ws, ws_bytes = _attn_workspace(B, N, dk, b - a, Q.device)
+            call("grl_node_attention_bwd", Q.data_ptr(), K.data_ptr(), H_b.data_ptr(), dO_b.data_ptr(),
+                 rmax.data_ptr(), rsum.data_ptr(), D.data_ptr(), dQ_b.data_ptr(), dK_b.data_ptr(), dH_b.data_ptr(),
+                 B, N, dk, b - a, ws.data_ptr() if ws is not None else None, ws_bytes,
+                 current_stream_handle(Q.device))
+            dQ = dQ_b if dQ is None else dQ + dQ_b
+            dK = dK_b if dK is None else dK + dK_b
+            dHs.append(dH_b)
+        dH = dHs[0] if len(dHs) == 1 else torch.cat(dHs, -1)
         dgamma = (dout * onorm).sum((0, 1))
         return dQ, dK, dH, dout, dgamma
 

@@ -207,6 +207,17 @@ int grl_typed_spmm_bwd(const GrlTypedCsc* g, const float* dZ, int32_t F,
                        float* dX, int64_t lddx, const GrlDropEdge* de,
                        grl_stream_t stream);
 
+/* dX += A_drop^T dZ over this CSC's edges, continuing every column's sum
+ * from the value dX already holds (no self term).  Graphs with >= 2^31 typed
+ * edges run as row blocks of < 2^31 edges (int32 positions inside a block,
+ * 64-bit global edge ids via edge_id_base): the first block's CSC goes
+ * through grl_typed_spmm_bwd, the later ones through this call, in block
+ * order -- their CSC positions all follow the earlier blocks', so each
+ * column's fmaf chain is the one a single CSC over all edges would run.   */
+int grl_typed_spmm_bwd_accum(const GrlTypedCsc* g, const float* dZ, int32_t F,
+                             float* dX, int64_t lddx, const GrlDropEdge* de,
+                             grl_stream_t stream);
+
 /* out = Z W + bias (optionally ReLU), fp32-accurate on the matrix cores.
  * Replaces torch.matmul(new_V, self.h_weights) + self.bias
  * (robust_gcn.py:50) and, with relu = 1, the F.relu around the layer

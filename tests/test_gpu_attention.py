@@ -31,7 +31,9 @@ def _ref(Q, K, H, V, gamma):
 SHAPES = [(1, 74, 16, 128), (4, 74, 16, 128), (2, 33, 4, 32), (1, 1, 2, 16), (3, 130, 16, 128), (2, 300, 32, 256),
           (2, 64, 5, 40), (1, 500, 16, 100), (2, 9, 0, 4),  # dk = 0: net_size 8 (4 // 8), uniform attention
           (1, 2048, 16, 128), (2, 1000, 5, 100), (1, 777, 32, 128),  # small-N key / query splits (S = 8, 3, 3)
-          (64, 1024, 16, 128), (4, 1100, 16, 128)]  # >= 4096 rows: LDS-DMA planes, unsplit / split (S = 4)
+          (64, 1024, 16, 128), (4, 1100, 16, 128),  # >= 4096 rows: LDS-DMA planes, unsplit / split (S = 4)
+          (2, 200, 64, 512), (1, 150, 40, 300), (2, 96, 33, 64), (1, 300, 20, 640)]  # net_size 1024 (dk 64,
+          # dv 512) and other widths beyond one call: fp32 kernels with 64-wide Q/K, dv in column blocks
 
 
 MODES = ["x6", "x6-no-workspace", "f32"]
@@ -109,7 +111,7 @@ def test_deterministic():
 
 
 def test_bad_widths_raise():
-    Q, K, H, V, gamma = _inputs(1, 8, 40, 16, seed=0)
+    Q, K, H, V, gamma = _inputs(1, 8, 72, 16, seed=0)  # input_dim > 512: dk > 64
     with pytest.raises(_lib.GrlError, match="key width"):
         node_attention_forward(Q, K, H, V, gamma)
     with pytest.raises(_lib.GrlError, match="attention shapes"):

@@ -85,6 +85,8 @@ for step in "$@"; do
     tests_capture) run pytest_gpu_capture 300 python -u -m pytest tests/test_gpu_graph_capture.py -m gpu -v -s -rf \
                   --timeout 240 --timeout-method thread ;;
     c1) run c1 300 python bench.py --only c1 --steps 20 ;;
+    tests_new) run pytest_gpu_new 900 python -u -m pytest tests/test_gpu_blocked.py tests/test_gpu_graphconv.py \
+                  -m gpu -v -s -rf --timeout 600 --timeout-method thread ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
