@@ -54,10 +54,11 @@ def test_blocks_equal_one_csr(kind, block, threshold):
     dX = spmm_backward(dZ, g.with_dropedge(de), F)
     for graph in (gb, g64):
         dXb = spmm_backward(dZ, graph.with_dropedge(de), F)
-        if threshold is None or kind == "er":
+        if kind == "er":
             assert torch.equal(dXb, dX)  # no heavy columns: the one-CSC chain exactly
-        else:  # heavy columns are chunked per block: the same terms, chunk sums grouped differently
-            torch.testing.assert_close(dXb, dX, rtol=1e-5, atol=1e-5)
+        else:  # R-MAT hub columns are chunked per block: the same terms, chunk sums grouped
+            # differently (hubs sum thousands of terms: the north-star fp32 tolerance)
+            torch.testing.assert_close(dXb, dX, rtol=1e-5, atol=1e-4)
     if threshold is not None:
         return
     # a whole GraphConv (autograd) on the blocked graph
@@ -71,8 +72,11 @@ def test_blocks_equal_one_csr(kind, block, threshold):
         out = graph_conv(Xg, graph.with_dropedge(DropEdge(0.3, 6, 0)), W, b, relu=True)
         out.square().sum().backward()
         res.append((out.detach(), Xg.grad, W.grad.clone(), b.grad.clone()))
-    for a, c in zip(*res):
-        assert torch.equal(a, c)
+    for i, (a, c) in enumerate(zip(*res)):
+        if i == 1 and kind == "rmat":  # dX: hub columns chunked per block (as above)
+            torch.testing.assert_close(a, c, rtol=1e-5, atol=1e-4)
+        else:  # out, dW, db: the same Z, so the same bits
+            assert torch.equal(a, c)
 
 
 def test_two_billion_edges():
