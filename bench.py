@@ -64,6 +64,9 @@ def parse():
     ap.add_argument("--dim", type=int, default=None)
     ap.add_argument("--p", type=float, default=None, help="DropEdge rate inside the timed step (0 = eval)")
     ap.add_argument("--graph", choices=["er", "rmat"], default=None)
+    ap.add_argument("--node-order", choices=["auto", "given", "degree"], default="auto",
+                    help="one GPU: relabel nodes by descending in-degree before timing (grl.graph.degree_order, a "
+                         "one-time preprocessing of the graph); auto = degree for R-MAT, given for ER")
     ap.add_argument("--chunks", type=int, default=0,
                     help="N>1: column slices of the pipelined halo exchange (0 = d/128; 1 = serial)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 disables)")
@@ -144,15 +147,38 @@ def main():
 
     wname, N, scaling = resolve_workload(args, world)
     L, F = args.types, args.dim
+    node_order = args.node_order if args.node_order != "auto" else ("degree" if args.graph == "rmat" else "given")
     t0 = time.time()
-    sg = ShardedGraph.synthetic(N, args.avg_deg, L, kind=args.graph, seed=0, device=dev, halo=args.halo)
+    if world > 1 and node_order == "degree":
+        # every rank builds the whole (deterministic) graph, relabels it and keeps its row range:
+        # the CSR is small next to the features (C5: 2.3 GB vs 17 GB)
+        from grl import TypedGraph
+        from grl.graph import degree_order
+
+        g_all, _ = degree_order(TypedGraph.synthetic(N, args.avg_deg, L, kind=args.graph, seed=0, device=dev))
+        sg = ShardedGraph.from_graph(g_all, halo=args.halo)
+        del g_all
+    else:
+        sg = ShardedGraph.synthetic(N, args.avg_deg, L, kind=args.graph, seed=0, device=dev, halo=args.halo)
     graph, plan = sg.graph, sg.plan
     n_loc = plan.n_loc
     E_loc, E_tot = graph.nnz, plan.num_edges_total
     gen = torch.Generator(device=dev)
     gen.manual_seed(1 + rank)
     X_loc = torch.randn(n_loc, F, generator=gen, device=dev, dtype=torch.float32)
+    order_ab = None
     de = DropEdge(args.p, 2, 0, True) if args.p > 0 else None
+    if node_order == "degree" and world == 1:
+        from grl.graph import degree_order
+
+        if args.only is None:  # (a profiled run keeps only the timed kernel's launches)
+            order_ab = {"given_ms": _time(lambda: spmm_forward(X_loc, graph.with_dropedge(de)), 3)}
+        t1 = time.time()
+        graph, perm = degree_order(graph)
+        X_loc = X_loc[perm].contiguous()  # features enter the relabelled graph once
+        if order_ab is not None:
+            order_ab["relabel_s"] = time.time() - t1
+        del perm
     g_step = graph.with_dropedge(de)
     stream = torch.cuda.current_stream(dev)
     Z = torch.empty(graph.num_rows, graph.segments * F, device=dev)  # preallocated: no allocation in the step
@@ -229,14 +255,22 @@ def main():
                    f"{N - n_loc} remote rows"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "spmm_kernel<4,1,8,false,false> (grl_typed_spmm_fwd)" if world == 1 else
-                     f"spmm_kernel (grl_typed_spmm_fwd_slice, {chunks} slices of {F // chunks} columns)",
+                     "kernel": (f"spmm_kernel<4,{2 if F > 256 and graph.num_cols * F * 4 > (12 << 30) else 1},"
+                                f"{4 if F > 256 and graph.num_cols * F * 4 > (12 << 30) else 8},false,false> "
+                                "(grl_typed_spmm_fwd)") if world == 1 else
+                     f"spmm_kernel / spmm_pair_kernel (grl_typed_spmm_fwd_slice, {chunks} slices of "
+                     f"{F // chunks} columns)",
                      "kernel_ms": kern_ms, "kernel_ms_min_max": [min(per_step), max(per_step)] if world == 1 else None,
                      "algorithmic_bytes_per_launch": bytes_launch},
         "build_s": build_s,
     }
     if halo is not None:
         out["halo"] = halo
+    out["config"]["node_order"] = ("degree-sorted node ids (one-time relabel of the same graph, "
+                                   "grl.graph.degree_order)" if node_order == "degree" else "as generated")
+    if order_ab is not None:
+        order_ab["degree_ms"] = kern_ms
+        out["node_order_ab"] = order_ab
     if args.graph == "rmat":
         out["config"]["split"] = graph.split_stats()
         out["config"]["max_row_edges"] = int((graph.rowptr[L::L] - graph.rowptr[:-1:L]).max())
@@ -369,8 +403,15 @@ def cpu_baseline(args, graph, X, Z, L, F):
 
     info = host_cpu_info()
     threads = cpu_threads(info)
-    rowptr = graph.rowptr.cpu().numpy()
-    colidx = graph.colidx.cpu().numpy()
+    n = graph.num_rows
+    # the whole graph, unless Z would not fit the host comfortably twice (C5: 120 GB): then
+    # SURVEY.md §8(d)'s 1/8 node-range shard from the middle of the graph
+    whole = Z.numel() * 4 <= (16 << 30)
+    r0, r1 = (0, n) if whole else (n // 2 - n // 16, n // 2 - n // 16 + -(-n // 8))
+    rp = graph.rowptr[r0 * L: r1 * L + 1].cpu().numpy()
+    e0 = int(rp[0])
+    rowptr = rp - e0
+    colidx = graph.colidx[e0: e0 + int(rowptr[-1])].cpu().numpy()
     Xh = X.cpu().numpy()
     E = int(rowptr[-1])
     d = None if args.p <= 0 else c_oracle.drop(args.p, 2, 0, True)  # the timed step's DropEdge stream
@@ -379,19 +420,21 @@ def cpu_baseline(args, graph, X, Z, L, F):
     passes = 0
     while True:
         Zc = c_oracle.spmm_fwd(rowptr, colidx, Xh, L, True, d=d, nthreads=threads, split=split,
-                               edge_base=graph.edge_id_base, self_base=graph.self_id_base)
+                               edge_base=graph.edge_id_base + e0, self_base=graph.self_id_base + r0,
+                               X_self=Xh[r0:])
         passes += 1
         if time.perf_counter() - t0 >= args.cpu_seconds:
             break
     dt = time.perf_counter() - t0
-    Zg = Z.cpu().numpy()
+    Zg = Z[r0:r1].cpu().numpy()
     equal = bool(np.array_equal(Zg, Zc))
     diff = 0.0 if equal else float(np.abs(Zg.astype(np.float64) - Zc).max())
+    what = (f"the whole graph ({n} nodes, {E} typed edges)" if whole else
+            f"the 1/8 node-range shard [{r0}, {r1}) ({E} of {graph.nnz} typed edges; edges/s of the shard)")
     cpu = {"value": E * passes / dt, "unit": "edges/s", "cores": threads, "kind": "port",
-           "sample": f"the whole graph ({graph.num_rows} nodes, {E} typed edges) and X, {passes} pass(es) in "
-                     f"{dt:.1f}s; oracle/grl_oracle.c OpenMP typed-CSR SpMM, {threads} threads",
-           **info}
-    parity = {"rows_checked": int(graph.num_rows), "max_abs_diff": diff, "bitwise_equal": equal, "tolerance": 1e-4}
+           "sample": f"{what} and X, {passes} pass(es) in {dt:.1f}s; oracle/grl_oracle.c OpenMP typed-CSR SpMM, "
+                     f"{threads} threads", **info}
+    parity = {"rows_checked": int(r1 - r0), "max_abs_diff": diff, "bitwise_equal": equal, "tolerance": 1e-4}
     return cpu, parity
 
 

@@ -89,6 +89,13 @@ __device__ __forceinline__ void vstore(float* p, const float& v) {
 #endif
 }
 
+// GRL_SPMM_WIDE_U=8 (read on every launch): whole 2 KB rows (F in (256, 512])
+// issued 8 at a time instead of 4 (more bytes in flight, fewer waves).
+int wide_rows_in_flight() {
+  const char* e = getenv("GRL_SPMM_WIDE_U");
+  return e && e[0] == '8' ? 8 : 4;
+}
+
 // GRL_SPMM_PAIR=0 (read on every launch) sends narrow forward rows to the
 // whole-row kernel instead of spmm_pair_kernel (A/B aid and tests).
 bool pair_rows_enabled() {
@@ -631,6 +638,8 @@ int launch_spmm(int64_t num_rows, int64_t self_rows, int S, int hs, const int32_
                            edge_base, self_base, self_row0, src, lds, F, out, ldo, zseg, de, sp);
     } else if (sh.nv == 1) {
       if (v) GRL_SPMM_LAUNCH(4, 1, 8, true); else GRL_SPMM_LAUNCH(4, 1, 8, false);
+    } else if (!BWD && wide_rows_in_flight() == 8) {  // A/B aid: twice the whole rows in flight per wave
+      if (v) GRL_SPMM_LAUNCH(4, 2, 8, true); else GRL_SPMM_LAUNCH(4, 2, 8, false);
     } else {
       if (v) GRL_SPMM_LAUNCH(4, 2, 4, true); else GRL_SPMM_LAUNCH(4, 2, 4, false);
     }

@@ -434,6 +434,28 @@ class ShardedGraph:
                                  device=device)
         return cls(g.rowptr, g.colidx, num_types, rb, re, group=group, halo=halo)
 
+    @classmethod
+    def from_graph(cls, graph: TypedGraph, *, group=None, balance: str = "edges", halo: str = "auto") -> "ShardedGraph":
+        """This rank's node-range shard of a global typed graph every rank
+        holds (e.g. a generated graph after grl.graph.degree_order: C5's
+        528M-edge CSR is 2.3 GB, small next to its 17 GB of features).
+        balance "edges": ranges holding ~E/P edges each; "nodes": equal ranges."""
+        if graph.num_cols != graph.num_rows:
+            raise ValueError("from_graph needs a square graph (rows and sources are the same nodes)")
+        world, rank = _world(group), _rank(group)
+        L, n = graph.num_types, graph.num_rows
+        if balance == "edges":
+            bounds = edge_balanced_bounds((graph.rowptr[L::L] - graph.rowptr[:-1:L]).to(torch.int64), world)
+        else:
+            per = -(-n // world)
+            bounds = [min(n, r * per) for r in range(world + 1)]
+        rb, re = bounds[rank], bounds[rank + 1]
+        e0, e1 = int(graph.rowptr[rb * L]), int(graph.rowptr[re * L])
+        sg = cls((graph.rowptr[rb * L: re * L + 1] - e0).contiguous(), graph.colidx[e0:e1], L, rb, re,
+                 vals=None if graph.vals is None else graph.vals[e0:e1], group=group, halo=halo)
+        sg.graph.split_threshold, sg.graph.split_chunk = graph.split_threshold, graph.split_chunk
+        return sg
+
     @property
     def halo_rows(self) -> int:
         return self.plan.n_halo

@@ -474,3 +474,41 @@ class EdgeBlockedGraph:
                                      self_id_base=E_total + a, self_rows=b - a))
             e0 += p.nnz
         return cls(blocks, bounds, num_nodes)
+
+
+def degree_order(graph: TypedGraph) -> Tuple[TypedGraph, torch.Tensor]:
+    """Relabel the nodes of a square typed graph by descending in-degree (how
+    often a node is gathered as a source), keeping every row's edges in their
+    order: returns (G', perm) with node i of G' = node perm[i] of G.
+
+    For power-law graphs (R-MAT) the rows most often gathered then sit in one
+    contiguous head of X (C5: the 43.5k sources behind half of all edges span
+    85 MiB instead of pages all over a 17 GB table), which the Infinity Cache
+    and the address-translation caches cover.  A one-time preprocessing step
+    of the graph, like the CSC and the split plan: features go in permuted
+    once (X' = X[perm]) and outputs come back once (Z[perm] = Z'); every layer
+    in between runs on G'.  Z' rows are the same fmaf chains as G's rows
+    (bitwise equal without DropEdge); DropEdge ids are G' CSR positions."""
+    if graph.num_cols != graph.num_rows or graph.self_rows != graph.num_rows:
+        raise _lib.GrlError("degree_order needs a square graph (one node set for rows and sources)")
+    dev, L, N = graph.device, graph.num_types, graph.num_rows
+    col = graph.colidx.long()
+    indeg = torch.bincount(col, minlength=N)
+    perm = torch.sort(indeg, descending=True, stable=True).indices
+    rank = torch.empty_like(perm)
+    rank[perm] = torch.arange(N, device=dev)
+    rp = graph.rowptr.long()
+    seglen = (rp[1:] - rp[:-1]).view(N, L)[perm]                      # new row i = old row perm[i]
+    new_rp = torch.zeros(N * L + 1, dtype=torch.int64, device=dev)
+    torch.cumsum(seglen.reshape(-1), 0, out=new_rp[1:])
+    row_len = seglen.sum(1)
+    old_start = rp[perm * L]
+    new_start = new_rp[:-1:L]
+    pos = torch.arange(graph.nnz, dtype=torch.int64, device=dev)
+    pos += torch.repeat_interleave(old_start - new_start, row_len, output_size=graph.nnz)
+    colidx = rank[col[pos]].to(torch.int32)
+    vals = None if graph.vals is None else graph.vals[pos]
+    del pos
+    g2 = TypedGraph(new_rp.to(torch.int32), colidx, L, vals=vals, has_self=graph.has_self, num_cols=N)
+    g2.split_threshold, g2.split_chunk = graph.split_threshold, graph.split_chunk
+    return g2, perm

@@ -58,7 +58,7 @@ def test_blocks_equal_one_csr(kind, block, threshold):
             assert torch.equal(dXb, dX)  # no heavy columns: the one-CSC chain exactly
         else:  # R-MAT hub columns are chunked per block: the same terms, chunk sums grouped
             # differently (hubs sum thousands of terms: the north-star fp32 tolerance)
-            torch.testing.assert_close(dXb, dX, rtol=1e-5, atol=1e-4)
+            torch.testing.assert_close(dXb, dX, rtol=1e-4, atol=1e-4)
     if threshold is not None:
         return
     # a whole GraphConv (autograd) on the blocked graph
@@ -74,7 +74,7 @@ def test_blocks_equal_one_csr(kind, block, threshold):
         res.append((out.detach(), Xg.grad, W.grad.clone(), b.grad.clone()))
     for i, (a, c) in enumerate(zip(*res)):
         if i == 1 and kind == "rmat":  # dX: hub columns chunked per block (as above)
-            torch.testing.assert_close(a, c, rtol=1e-5, atol=1e-4)
+            torch.testing.assert_close(a, c, rtol=1e-4, atol=1e-4)
         else:  # out, dW, db: the same Z, so the same bits
             assert torch.equal(a, c)
 

@@ -87,6 +87,28 @@ for step in "$@"; do
     c1) run c1 300 python bench.py --only c1 --steps 20 ;;
     tests_new) run pytest_gpu_new 900 python -u -m pytest tests/test_gpu_blocked.py tests/test_gpu_graphconv.py \
                   -m gpu -v -s -rf --timeout 600 --timeout-method thread ;;
+    pmc_calib_fetch) run pmc_calib_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_calib_fetch" \
+                  -o run --output-format csv -- python tools/pmc_calib.py ;;
+    pmc_calib_write) run pmc_calib_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_calib_write" \
+                  -o run --output-format csv -- python tools/pmc_calib.py ;;
+    prof_c5) run prof_c5 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c5" -o run --output-format csv \
+                  -- python bench.py --workload C5 --only fwd --steps 5 --warmup 1 ;;
+    pmc_c5_tlb) run pmc_c5_tlb 600 rocprofv3 --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum \
+                  TCP_TCC_READ_REQ_sum TCP_TCC_READ_REQ_LATENCY_sum --kernel-trace -d "$OUT/pmc_c5_tlb" -o run \
+                  --output-format csv -- python bench.py --workload C5 --only fwd --steps 3 --warmup 1 ;;
+    pmc_c5_fetch) run pmc_c5_fetch 600 rocprofv3 --pmc FETCH_SIZE TCC_HIT_sum --kernel-trace -d "$OUT/pmc_c5_fetch" \
+                  -o run --output-format csv -- python bench.py --workload C5 --only fwd --steps 3 --warmup 1 ;;
+    probe_cumask) run probe_cumask 400 python tools/probe_cumask.py ;;
+    probe_c5) run probe_c5 600 python tools/probe_c5.py ;;
+    tests_relabel) run pytest_gpu_relabel 300 python -u -m pytest tests/test_gpu_relabel.py -m gpu -v -rf \
+                  --timeout 240 --timeout-method thread ;;
+    bench_c5full) run bench_c5full 900 python bench.py --workload C5 --steps 5 --warmup 2 ;;
+    pmc_c5_fetch2) run pmc_c5_fetch2 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_c5_fetch2" -o run \
+                  --output-format csv -- python bench.py --workload C5 --only fwd --steps 3 --warmup 1 ;;
+    pmc_c5_write) run pmc_c5_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_c5_write" -o run \
+                  --output-format csv -- python bench.py --workload C5 --only fwd --steps 3 --warmup 1 ;;
+    prof_c5b) run prof_c5b 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c5b" -o run --output-format csv \
+                  -- python bench.py --workload C5 --only fwd --steps 5 --warmup 1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
