@@ -624,6 +624,12 @@ __global__ void split_planes_kernel(const float* __restrict__ B, int64_t ldb, in
   }
 }
 
+// GRL_X6_STAGGER (read per call): 1 = the staggered x6 forward / dZ kernel
+bool x6_stagger() {
+  const char* e = getenv("GRL_X6_STAGGER");
+  return e && e[0] == '1';
+}
+
 // global -> LDS DMA of one 16 B chunk per lane (lane l lands at lds_base + 16 l).
 // Issued from asm so that hipcc's waitcnt pass neither sees nor waits on it;
 // completion is ordered by the kernel's counted `s_waitcnt vmcnt`.
@@ -650,7 +656,14 @@ __device__ __forceinline__ void dma16(const void* src, const void* lds_base) {
 // A's loads get two compute phases to land, B's (L2-resident planes) one.
 constexpr int X6_SLOT = 512 * 8;  // floats per landing slot (16 KB)
 
-template <int EPI>
+// STAGGER: the two waves sharing a SIMD (w and w + 4) take the step's two
+// non-MFMA phases in opposite order -- waves 0-3 multiply then split A(t+1)
+// into the next stage, waves 4-7 split first and multiply after -- so one
+// partner's split (VALU + LDS writes, its DMA wait) runs under the other's
+// MFMAs instead of both splitting while the matrix core idles
+// (MI355X_MICROARCH.md, two waves per SIMD: stagger).  Same arithmetic,
+// same bits.
+template <int EPI, bool STAGGER = false>
 __global__ __launch_bounds__(512) void gemm_x6_kernel(GemmArgs p, const uint16_t* __restrict__ Bp, int64_t Np) {
   __shared__ __attribute__((aligned(16))) uint16_t smem[2 * X6_STAGE];  // 2 plane stages x 48 KB
   __shared__ __attribute__((aligned(16))) float land[3 * X6_SLOT];      // 3 landing slots x 16 KB
@@ -749,6 +762,14 @@ __global__ __launch_bounds__(512) void gemm_x6_kernel(GemmArgs p, const uint16_t
 #pragma unroll
         for (int q = 0; q < 3; ++q)
           b_[j][q] = *reinterpret_cast<const bf16x8_t*>(cur + (3 + q) * X6_PLANE + sw(wn * 64 + j * 32 + l32, h * 8));
+      if (STAGGER && wm == 1 && t + 1 < nk) {  // the late half: split A(t+1) before its MFMAs
+        // B(t+1) (3 DMAs) and A(t+2) (2) were just issued and may stay in flight; A(t+1) is older
+        if (t + 2 < nk)
+          asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+        stash_a(t + 1, nxt);
+      }
       // small terms first (i + j = 2, then 1, then the leading product)
 #if GRL_X6_PRIO
       __builtin_amdgcn_s_setprio(1);
@@ -785,7 +806,7 @@ __global__ __launch_bounds__(512) void gemm_x6_kernel(GemmArgs p, const uint16_t
         asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // A(t+2) may stay in flight
       else
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      stash_a(t + 1, nxt);
+      if (!STAGGER || wm == 0) stash_a(t + 1, nxt);
     }
   }
   float* Cz = p.C;
@@ -1080,9 +1101,15 @@ int launch_x6_gemm(GemmArgs a, const uint16_t* planes, hipStream_t st) {
   GRL_CHECK_ARG(a.mt * a.nt < 2147483647LL, "gemm: grid too large");
   const dim3 grid((unsigned)(a.mt * a.nt));
   if (a.bias || a.relu)
-    hipLaunchKernelGGL(gemm_x6_kernel<EPI_BIAS>, grid, dim3(512), 0, st, a, planes, Np);
+    if (x6_stagger())
+      hipLaunchKernelGGL((gemm_x6_kernel<EPI_BIAS, true>), grid, dim3(512), 0, st, a, planes, Np);
+    else
+      hipLaunchKernelGGL(gemm_x6_kernel<EPI_BIAS>, grid, dim3(512), 0, st, a, planes, Np);
   else
-    hipLaunchKernelGGL(gemm_x6_kernel<EPI_STORE>, grid, dim3(512), 0, st, a, planes, Np);
+    if (x6_stagger())
+      hipLaunchKernelGGL((gemm_x6_kernel<EPI_STORE, true>), grid, dim3(512), 0, st, a, planes, Np);
+    else
+      hipLaunchKernelGGL(gemm_x6_kernel<EPI_STORE>, grid, dim3(512), 0, st, a, planes, Np);
   GRL_LAUNCH_CHECK();
   return GRL_OK;
 }

@@ -109,6 +109,10 @@ for step in "$@"; do
                   --output-format csv -- python bench.py --workload C5 --only fwd --steps 3 --warmup 1 ;;
     prof_c5b) run prof_c5b 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c5b" -o run --output-format csv \
                   -- python bench.py --workload C5 --only fwd --steps 5 --warmup 1 ;;
+    probe_stagger) run probe_stagger 400 python tools/probe_stagger.py ;;
+    pmc_x6_stagger) export GRL_X6_STAGGER=1; run pmc_x6_stagger 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES \
+                  GRBM_GUI_ACTIVE SQ_BUSY_CU_CYCLES --kernel-trace -d "$OUT/pmc_x6_stagger" -o run --output-format csv \
+                  -- python bench.py --only linear --steps 5 --warmup 1; unset GRL_X6_STAGGER ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
