@@ -113,6 +113,7 @@ for step in "$@"; do
     pmc_x6_stagger) export GRL_X6_STAGGER=1; run pmc_x6_stagger 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES \
                   GRBM_GUI_ACTIVE SQ_BUSY_CU_CYCLES --kernel-trace -d "$OUT/pmc_x6_stagger" -o run --output-format csv \
                   -- python bench.py --only linear --steps 5 --warmup 1; unset GRL_X6_STAGGER ;;
+    probe_contig) run probe_contig 300 python tools/probe_contig.py ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
