@@ -69,6 +69,13 @@ __host__ __device__ __forceinline__ uint64_t synth_bits(uint64_t seed, uint64_t 
 int spmm_fwd_rows(const GrlTypedCsr* g, int64_t r0, int64_t rows, const float* X, int64_t ldx, int F, float* Z,
                   const GrlDropEdge* de, hipStream_t st);
 
+// Fused one-kernel GraphConv forward (graphconv.hip), used by grl_graphconv_fwd.
+bool graphconv_fused_enabled();
+bool graphconv_fused_shape_ok(int F, int C);
+size_t graphconv_fused_ws_bytes(int64_t K);
+int graphconv_fused_fwd(const GrlTypedCsr* g, const float* X, int64_t ldx, int F, const float* W, const float* bias,
+                        int C, int relu, float* out, const GrlDropEdge* de, void* ws, hipStream_t st);
+
 // Plain-data copy of GrlDropEdge passed by value to kernels.
 struct DropDev {
   uint64_t key;

@@ -1195,6 +1195,26 @@ extern "C" int grl_linear_fwd(const float* Z, int64_t ldz, const float* W, const
 
 static size_t ws_align(size_t b) { return (b + 255) & ~(size_t)255; }
 
+// grl_graphconv_fwd takes the fused kernel when its arithmetic equals the
+// two-kernel path's (the linear on the x6 GEMM: large graphs, 16-B aligned W,
+// C % 4 == 0), the shapes fit it (F in {64, 128, 256}, C <= 256), X rows are
+// float4-aligned and no heavy row is split (the split path sums chunk
+// partials, a different order).
+static bool fused_path(const GrlTypedCsr* g, const float* X, int64_t ldx, int F, const float* W, int C) {
+  const int64_t K = (int64_t)(g->num_types + (g->has_self ? 1 : 0)) * F;
+  return graphconv_fused_enabled() && graphconv_fused_shape_ok(F, C) && x6_shape_ok(g->num_rows, C, K) &&
+         al16(W) && C % 4 == 0 && al16(X) && ldx % 4 == 0 && (!g->split || g->split->num_heavy == 0);
+}
+
+extern "C" size_t grl_graphconv_fwd_workspace_query(const GrlTypedCsr* g, const float* X, int64_t ldx, int32_t F,
+                                                   const float* W, int32_t C) {
+  if (!g || g->num_rows <= 0 || g->num_types < 1 || F <= 0 || C <= 0) return 0;
+  const int64_t K = (int64_t)(g->num_types + (g->has_self ? 1 : 0)) * F;
+  if (K > 2147483647LL) return 0;
+  if (fused_path(g, X, ldx, F, W, C)) return graphconv_fused_ws_bytes(K);
+  return grl_graphconv_fwd_workspace_size(g->num_rows, g->num_types, g->has_self, F, C);
+}
+
 extern "C" size_t grl_graphconv_fwd_workspace_size(int64_t num_rows, int32_t num_types, int32_t has_self, int32_t F,
                                                    int32_t C) {
   if (num_rows <= 0 || num_types < 1 || F <= 0 || C <= 0) return 0;
@@ -1222,6 +1242,11 @@ extern "C" int grl_graphconv_fwd(const GrlTypedCsr* g, const float* X, int64_t l
   char* ws = static_cast<char*>(workspace);
   GRL_CHECK_ARG(ws == nullptr || al16(ws), "grl_graphconv_fwd: workspace must be 16-B aligned");
   const size_t zfull = ws_align((size_t)M * (size_t)K * 4);
+  if (fused_path(g, X, ldx, F, W, C) && ws && workspace_bytes >= graphconv_fused_ws_bytes(K)) {
+    // one kernel: Z never leaves the CU (graphconv.hip)
+    GRL_CHECK_ARG(g->nnz < 2147483647LL, "grl_graphconv_fwd: nnz %lld exceeds int32", (long long)g->nnz);
+    return graphconv_fused_fwd(g, X, ldx, F, W, bias, C, relu, out, de, ws, st);
+  }
   if (ws && workspace_bytes >= grl_graphconv_fwd_workspace_size(M, g->num_types, hs, F, C)) {
     // whole graph: Z in the workspace, then the linear (its workspace behind Z)
     float* Z = reinterpret_cast<float*>(ws);

@@ -270,9 +270,10 @@ class _GraphConv(torch.autograd.Function):
 def graph_conv_infer(X: torch.Tensor, graph: TypedGraph, W: torch.Tensor, b=None, relu: bool = False,
                      max_workspace_bytes: int = None) -> torch.Tensor:
     """GraphConv forward for inference through one grl_graphconv_fwd call
-    (aggregation + linear [+ReLU]).  Z lives only in the call's workspace;
-    max_workspace_bytes bounds it (the call then works in row chunks, bitwise
-    equal to the whole-graph result)."""
+    (aggregation + linear [+ReLU]).  On large graphs this is one fused kernel
+    and Z never reaches HBM; otherwise Z lives only in the call's workspace
+    and max_workspace_bytes bounds it (the call then works in row chunks,
+    bitwise equal to the whole-graph result)."""
     _require_device(X, "node features")
     if X.dtype != torch.float32 or W.dtype != torch.float32:
         raise _lib.GrlError("graph_conv_infer: features and weights must be float32")
@@ -286,10 +287,12 @@ def graph_conv_infer(X: torch.Tensor, graph: TypedGraph, W: torch.Tensor, b=None
         raise _lib.GrlError(f"weights have {Wc.shape[0]} rows, expected {graph.segments} x {F}")
     bc = b.contiguous() if b is not None else None
     out = torch.empty(graph.num_rows, C, dtype=torch.float32, device=X.device)
-    full = _lib.lib().grl_graphconv_fwd_workspace_size(graph.num_rows, graph.num_types, int(graph.has_self), F, C)
+    csr = graph.csr_c(F)
+    # the fused one-kernel path needs only W's planes; else Z whole
+    full = _lib.lib().grl_graphconv_fwd_workspace_query(ctypes.byref(csr), X2.data_ptr(), X2.stride(0), F,
+                                                         Wc.data_ptr(), C)
     ws_bytes = full if max_workspace_bytes is None else min(full, int(max_workspace_bytes))
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=X.device) if ws_bytes else None
-    csr = graph.csr_c(F)
     de = graph.dropedge.to_c() if graph.dropedge is not None else None
     call("grl_graphconv_fwd", ctypes.byref(csr), X2.data_ptr(), X2.stride(0), F, Wc.data_ptr(),
          bc.data_ptr() if bc is not None else None, C, int(relu), out.data_ptr(),

@@ -260,6 +260,18 @@ int grl_graphconv_fwd(const GrlTypedCsr* g, const float* X, int64_t ldx,
                       void* workspace, size_t workspace_bytes,
                       grl_stream_t stream);
 
+/* Workspace grl_graphconv_fwd uses for THIS graph, X and W (0 on bad
+ * arguments).  Large graphs without a heavy-row split plan, F in {64, 128,
+ * 256}, C <= 256, float4-aligned X rows and W run as ONE kernel
+ * (graphconv.hip): Z = A_drop X stays on chip (32-row tiles in LDS as x6
+ * bf16 planes, MFMA against W's planes) and the workspace holds only W's
+ * planes (2.75 MB at K = 1792, C = 256) -- bitwise the two-kernel result.
+ * Otherwise this is grl_graphconv_fwd_workspace_size().
+ * GRL_GRAPHCONV_FUSED=0 forces the two-kernel path.                      */
+size_t grl_graphconv_fwd_workspace_query(const GrlTypedCsr* g, const float* X,
+                                         int64_t ldx, int32_t F,
+                                         const float* W, int32_t C);
+
 /* Backward of grl_linear_fwd (autograd MmBackward0 of robust_gcn.py:50, with
  * the ReLU of drop_robust_gcn.py:76 folded in when relu_out != NULL):
  *   dZ = (g * [relu_out > 0]) W^T           grl_linear_bwd_data,  dZ [M, K] (ld lddz)

@@ -54,10 +54,12 @@ def test_graphconv_small_matches_two_ops_and_oracle(N, L, deg, F, C, has_self, r
 
 
 @pytest.mark.parametrize("di,strided", [(0, False), (1, False), (2, True)])
-def test_graphconv_row_chunks_bitwise(di, strided):
-    """Bounded workspace: rows in chunks (here 12 chunks, the last partial)
-    give the whole-graph bits, which are the two-op bits (also with X a
-    column slice of a wider matrix, and DropEdge sparing the self loops)."""
+def test_graphconv_row_chunks_bitwise(di, strided, monkeypatch):
+    """Bounded workspace on the two-kernel path: rows in chunks (here 12
+    chunks, the last partial) give the whole-graph bits, which are the
+    two-op bits (also with X a column slice of a wider matrix, and DropEdge
+    sparing the self loops)."""
+    monkeypatch.setenv("GRL_GRAPHCONV_FUSED", "0")
     N, L, F, C = 100_003, 6, 256, 256
     de = [None, DropEdge(0.3, 2, 0, True), DropEdge(0.2, 5, 3, False)][di]
     g = TypedGraph.synthetic(N, 16.0, L, seed=0, device=DEV).with_dropedge(de)
@@ -127,3 +129,71 @@ def test_recompute_z_gives_the_same_gradients_with_less_memory(relu):
     from grl import ops
 
     assert z_bytes < ops.RECOMPUTE_Z_BYTES
+
+
+def _ws_query(X, g, W, C):
+    csr = g.csr_c(X.shape[1])
+    import ctypes
+    return _lib.lib().grl_graphconv_fwd_workspace_query(ctypes.byref(csr), X.data_ptr(), X.stride(0), X.shape[1],
+                                                        W.data_ptr(), C)
+
+
+# sizes just above the x6 GEMM's 1.6e10-flop threshold (below it the linear,
+# hence the two-kernel reference, is the fp32-MFMA kernel and no fusion runs)
+@pytest.mark.parametrize("N,L,F,C,has_self,deg", [(20_011, 6, 256, 256, True, 16.0), (50_000, 6, 256, 96, True, 9.0),
+                                                  (40_007, 6, 128, 256, True, 16.0), (70_001, 6, 64, 256, True, 12.0),
+                                                  (60_001, 3, 256, 200, False, 20.0)])
+@pytest.mark.parametrize("variant", ["plain", "drop_bias_relu", "drop_spare_self", "strided_relu"])
+def test_fused_graphconv_bitwise_equals_two_kernels(N, L, F, C, has_self, deg, variant, monkeypatch):
+    """The one-kernel GraphConv (graphconv.hip) gives the two-kernel bits
+    (typed SpMM, then the x6 GEMM): the same fmaf chain per Z element, the
+    same split, K order and product order; and it runs in a workspace of
+    only W's planes (Z never reaches HBM)."""
+    de = {"plain": None, "drop_bias_relu": DropEdge(0.3, 3, 2, True), "drop_spare_self": DropEdge(0.25, 9, 0, False),
+          "strided_relu": None}[variant]
+    bias = variant == "drop_bias_relu"
+    relu = variant in ("drop_bias_relu", "strided_relu")
+    g = TypedGraph.synthetic(N, deg, L, seed=N % 7, device=DEV)
+    if not has_self:
+        g = TypedGraph(g.rowptr, g.colidx, L, has_self=False, num_cols=N)
+    g = g.with_dropedge(de)
+    gen = torch.Generator(device=DEV).manual_seed(N + F)
+    wide = F + 64 if variant == "strided_relu" else F
+    X = torch.randn(N, wide, device=DEV, generator=gen)[:, :F]
+    K = (L + (1 if has_self else 0)) * F
+    W = torch.randn(K, C, device=DEV, generator=gen) / K ** 0.5
+    b = torch.randn(C, device=DEV, generator=gen) if bias else None
+    ws = _ws_query(X, g, W, C)
+    assert ws < 3 * 256 * K * 2 + 4096 < N * K * 4, ws  # W planes only: the fused path
+    out = graph_conv_infer(X, g, W, b, relu)
+    ref = _two_op(X, g, W, b, relu)
+    assert torch.equal(out, ref)
+    monkeypatch.setenv("GRL_GRAPHCONV_FUSED", "0")
+    assert _ws_query(X, g, W, C) >= N * K * 4
+    assert torch.equal(graph_conv_infer(X, g, W, b, relu), out)
+
+
+def test_fused_graphconv_edge_values_and_oracle():
+    """fc_similarity-style edge values (vals != NULL) through the fused
+    kernel: bitwise the two-kernel result, and within 1e-5 sum|terms| of the
+    oracle's Z times W in fp64 on sampled rows."""
+    N, L, F, C = 20_480, 6, 256, 256
+    rowptr, colidx = ohash.synth_csr(0, L, N, N * 12, 5)
+    rng = np.random.default_rng(3)
+    vals = rng.random(len(colidx)).astype(np.float32)
+    g = TypedGraph.from_csr_host(rowptr, colidx, L, DEV, vals=vals).with_dropedge(DropEdge(0.3, 1, 4, True))
+    X = rng.standard_normal((N, F)).astype(np.float32)
+    K = 7 * F
+    W = (rng.standard_normal((K, C)) / np.sqrt(K)).astype(np.float32)
+    b = rng.standard_normal(C).astype(np.float32)
+    Xt, Wt, bt = (torch.from_numpy(a).to(DEV) for a in (X, W, b))
+    assert _ws_query(Xt, g, Wt, C) < N * K * 4
+    out = graph_conv_infer(Xt, g, Wt, bt, True)
+    assert torch.equal(out, _two_op(Xt, g, Wt, bt, True))
+    de = g.dropedge
+    Z = c_oracle.spmm_fwd(rowptr, colidx, X, L, True, vals=vals,
+                          d=c_oracle.drop(de.p, de.seed, de.call, de.drop_self)).astype(np.float64)
+    rows = np.r_[0:64, N - 64:N, rng.integers(0, N, 512)]
+    o = np.maximum(Z[rows] @ W.astype(np.float64) + b, 0.0)
+    scale = np.abs(Z[rows]) @ np.abs(W.astype(np.float64)) + np.abs(b)
+    assert np.all(np.abs(out.cpu().numpy()[rows] - o) <= 1e-5 * scale + 1e-6)

@@ -1,0 +1,11 @@
+#!/bin/bash
+# A/B of the fused GraphConv kernel between the default libgrl and diag builds
+# (tools/build_diag.sh NAME "-D..." graphconv), interleaved, two rounds:
+#   tools/ab_fused_lib.sh NAME...
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
+L=graph-representation-learning_amd/grl
+for rep in 1 2; do
+  for lib in $L/libgrl.so $(for n in "$@"; do echo $L/diag/libgrl_$n.so; done); do
+    GRL_LIB_PATH=$lib timeout -k 10 200 python tools/probe_fused.py >> gpurun_out/ab_fused_lib.log 2>&1 || exit 1
+  done
+done
