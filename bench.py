@@ -78,7 +78,7 @@ def parse():
     ap.add_argument("--halo", choices=["auto", "sparse", "dense"], default="auto",
                     help="halo exchange layout for N>1 (grl/dist.py): sparse all-to-all-v of the referenced rows, "
                          "dense all-gather of every shard; auto picks dense when >=75%% of remote rows are referenced")
-    ap.add_argument("--only", choices=["fwd", "bwd", "linear", "layer", "c1", "model"], default=None,
+    ap.add_argument("--only", choices=["fwd", "bwd", "linear", "layer", "infer", "c1", "model"], default=None,
                     help="profiling aid: run just that kernel K times (no JSON line); c1: print the C1 "
                          "(debug.json model) timings alone")
     return ap.parse_args()
@@ -507,12 +507,25 @@ def extras(args, graph, X_full, L, F, dev, E_loc, n_loc):
     res["graphconv_layer_fwd_bwd_p0.3"] = {"ms": _time(layer, max(3, iters // 2), warm=3)}
     res["graphconv_layer_fwd_bwd_p0.3_two_ops"] = {"ms": _time(layer_two_ops, max(3, iters // 2), warm=2)}
     del Z, dZ, Zd
-    # inference: one grl_graphconv_fwd call, Z whole (7.2 GB) or in 1 GiB row chunks
+    # inference: one grl_graphconv_fwd call -- the one-kernel form (Z stays on
+    # chip, graphconv.hip), and the two-kernel form (Z whole, 7.2 GB, or in
+    # 1 GiB row chunks) for comparison; all bitwise equal
     from grl.ops import graph_conv_infer
     Xe = X_full.detach()[: graph.num_cols]
-    res["graphconv_infer_fwd"] = {"ms": _time(lambda: graph_conv_infer(Xe, graph, W, b, True), iters, warm=2)}
-    res["graphconv_infer_fwd_z_chunks_1GiB"] = {
-        "ms": _time(lambda: graph_conv_infer(Xe, graph, W, b, True, max_workspace_bytes=1 << 30), iters, warm=2)}
+    fused = graph_conv_infer(Xe, graph, W, b, True)
+    res["graphconv_infer_fwd"] = {"ms": _time(lambda: graph_conv_infer(Xe, graph, W, b, True), iters, warm=2),
+                                  "path": "one kernel (graphconv_ws_kernel): gather waves + MFMA waves, Z in LDS"}
+    os.environ["GRL_GRAPHCONV_FUSED"] = "0"
+    try:
+        two = graph_conv_infer(Xe, graph, W, b, True)
+        res["graphconv_infer_fwd_two_kernels"] = {
+            "ms": _time(lambda: graph_conv_infer(Xe, graph, W, b, True), iters, warm=2),
+            "bitwise_equal_to_one_kernel": bool(torch.equal(two, fused))}
+        res["graphconv_infer_fwd_two_kernels_z_chunks_1GiB"] = {
+            "ms": _time(lambda: graph_conv_infer(Xe, graph, W, b, True, max_workspace_bytes=1 << 30), iters,
+                        warm=2)}
+    finally:
+        del os.environ["GRL_GRAPHCONV_FUSED"]
     return res
 
 
@@ -722,6 +735,13 @@ def run_only(args, graph, X_full, spmm, L, F):
         dZ = torch.randn_like(Z)
         graph.csc()
         fn = lambda: torch.autograd.grad(Z, Xg, dZ, retain_graph=True)  # noqa: E731
+    elif args.only == "infer":  # one-call GraphConv inference (the fused kernel by default)
+        from grl.ops import graph_conv_infer
+
+        W = torch.randn((L + 1) * F, F, device=X_full.device) / np.sqrt((L + 1) * F)
+        b = torch.randn(F, device=X_full.device)
+        Xe = X_full.detach()[: graph.num_cols]
+        fn = lambda: graph_conv_infer(Xe, graph, W, b, True)  # noqa: E731
     elif args.only == "linear":
         Z = typed_aggregate(X_full, graph)
         W = torch.randn((L + 1) * F, F, device=X_full.device) / np.sqrt((L + 1) * F)

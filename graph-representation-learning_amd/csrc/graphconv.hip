@@ -6,23 +6,19 @@
 //
 // The two-kernel path (grl_typed_spmm_fwd, then the x6 GEMM) writes Z =
 // A_drop X to HBM and reads it back: 7.2 GB each way at C3 (N = 1M, L = 6,
-// F = 256).  Here Z never leaves the CU:
-//  * a workgroup (4 waves) owns a tile of 32 destination rows and walks the
-//    K dimension one typed segment (F columns of Z) at a time:
-//      gather:  each wave sums its 8 rows' segment-t neighbour rows (one
-//               float4 per lane, one 1 KB row per wave-instruction, 8 rows
-//               in flight, the rows' edge lists streamed as one list with
-//               flushes at row boundaries), splits each finished Z row into
-//               three bf16 planes (the exact x6 split) and stores it in LDS;
-//      multiply: each wave owns 64 output columns and multiplies the 32 x F
-//               Z tile with its W slice on v_mfma_f32_32x32x16_bf16, six
-//               plane products per K16 step into fp32 accumulators; W comes
-//               pre-split in MFMA fragment order straight from L2 into
-//               registers (one coalesced 1 KB load per fragment), the next
-//               step's fragments in flight during the current step's MFMAs;
-//  * 48 KB of LDS per workgroup, so three workgroups share a CU and one's
-//    gather overlaps another's MFMAs;
-//  * bias + ReLU in the epilogue; only out (N x C) is written.
+// F = 256).  Here Z never leaves the CU.  Two kernels share the pieces:
+//  * graphconv_ws_kernel (default): persistent, one workgroup per CU, gather
+//    waves and MFMA waves specialised and coupled by an LDS ring of Z tiles
+//    (64 rows x 128 columns); see its comment below;
+//  * graphconv_fused_kernel (GRL_FG_WS=0): 32-row tiles, every wave
+//    alternates gather and multiply phases, three workgroups per CU.
+// Shared pieces: the gather sums a wave's rows' segment-t neighbour rows
+// (one float4 per lane, one 1 KB row per wave-instruction, the rows' edge
+// lists streamed as one list with flushes at row boundaries); the multiply
+// runs v_mfma_f32_32x32x16_bf16 six plane products per K16 step into fp32
+// accumulators with W pre-split (fused_w_planes_kernel) in MFMA fragment
+// order, fetched from L2 straight into registers (one coalesced 1 KB load
+// per fragment); bias + ReLU in the epilogue; only out (N x C) is written.
 // Arithmetic: each Z element is the same fmaf chain as spmm_kernel (CSR
 // order, the same DropEdge weights), split and multiplied in the same K16
 // order and product order as gemm_x6_kernel, so the result is bitwise that
@@ -42,10 +38,19 @@ typedef float f32x2_t __attribute__((ext_vector_type(2)));
 constexpr int FG_R = 32;                  // destination rows per tile
 constexpr int FG_WAVES = 4;               // waves per workgroup
 constexpr int FG_RW = FG_R / FG_WAVES;    // rows per wave in the gather
-constexpr int FG_LD = 256;                // bf16 per Z-tile plane row (F <= 256)
+constexpr int FG_LD = 256 + 8;            // bf16 per Z-tile plane row (F <= 256) + one 16-B pad chunk
 constexpr int FG_PLANE = FG_R * FG_LD;    // bf16 per plane
 #ifndef GRL_FG_U
 #define GRL_FG_U 8
+#endif
+// GRL_FG_PIPE_IDX=1: segment t+1's edge list and first 64 source rows /
+// weights are loaded before segment t is gathered (their latency hidden)
+#ifndef GRL_FG_PIPE_IDX
+#define GRL_FG_PIPE_IDX 1
+#endif
+// GRL_FG_BDEPTH: register stages of W fragments in the multiply (2 or 3)
+#ifndef GRL_FG_BDEPTH
+#define GRL_FG_BDEPTH 2
 #endif
 #ifndef GRL_FG_WPE
 #define GRL_FG_WPE 3
@@ -107,10 +112,12 @@ __global__ void fused_w_planes_kernel(const float* __restrict__ W, int64_t K, in
   }
 }
 
-// 16-B chunk c of Z-tile row r sits at chunk c ^ (r & 15): the fragment reads
-// (ds_read_b128: lane groups of 16 rows at one chunk) and the row stores
-// (ds_write_b64) are both conflict-free.
-__device__ __forceinline__ int zoff(int r, int chunk) { return r * FG_LD + ((chunk ^ (r & 15)) << 3); }
+// Z-tile plane rows are 528 B apart (33 chunks of 16 B): row r's chunk c
+// sits in bank slot (r + c) mod 16, so the fragment reads (ds_read_b128: lane
+// groups of 16 rows at one chunk) and the row stores (ds_write_b64, 16 lanes
+// on 128 contiguous bytes) are conflict-free, and a fragment's address is a
+// per-lane base plus a compile-time offset per K16 step.
+__device__ __forceinline__ int zoff(int r, int chunk) { return r * FG_LD + (chunk << 3); }
 
 template <int KS, bool VALS>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GRL_FG_WPE, GRL_FG_WPE))) void graphconv_fused_kernel(
@@ -128,7 +135,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GRL_FG_WPE,
   const int64_t rw0 = m0 + wave * FG_RW;
   const int col = lane * 4;
   const bool col_ok = col < F;
-  const int S = L + hs;
 
   f32x16 acc[2];
 #pragma unroll
@@ -149,135 +155,196 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GRL_FG_WPE,
     }
   };
 
-  for (int s = 0; s < S; ++s) {
-    // ---------------- gather: Z segment s of this wave's rows ----------------
-    if (s < hs) {
-      // identity block of A_pre (robust_gcn.py:58-65): the node's own row
-      float4 xv[FG_RW];
+  // ---------------- multiply: acc += Zs(32 x F) W_s(F x 64 cols of this wave) ----------------
+  auto multiply = [&](int s) {
+    const uint16_t* wk = Wf + ((int64_t)s * KS * FG_CB + wave * 2) * 3 * FG_FRAG + lane * 8;
+    constexpr int WSTEP = FG_CB * 3 * FG_FRAG;  // bf16 between K16 steps
+    auto load_b = [&](bf16x8_t (&bb)[2][3], int ks) {
+      const uint16_t* w = wk + ks * WSTEP;
 #pragma unroll
-      for (int i = 0; i < FG_RW; ++i)
-        xv[i] = (rw0 + i < M && col_ok) ? *reinterpret_cast<const float4*>(X + (rw0 + i) * ldx + col) : zero4();
+      for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int i = 0; i < FG_RW; ++i) {
-        float w = 1.0f;
-        if (de.active && de.drop_self) w = dropedge_weight(de, 1.0f, self_base + (uint64_t)(rw0 + i));
-        const float4 x = w != 0.0f ? make_float4(w * xv[i].x, w * xv[i].y, w * xv[i].z, w * xv[i].w) : zero4();
-        flush(i, x);
+        for (int q = 0; q < 3; ++q) bb[j][q] = *reinterpret_cast<const bf16x8_t*>(w + (j * 3 + q) * FG_FRAG);
+    };
+    auto step = [&](const bf16x8_t (&bb)[2][3], int ks) {
+      bf16x8_t a[3];
+      const int ao = zoff(l32, 2 * ks + h);
+#pragma unroll
+      for (int q = 0; q < 3; ++q) a[q] = *reinterpret_cast<const bf16x8_t*>(zs + q * FG_PLANE + ao);
+      // gemm_x6_kernel's product order: small terms first, the leading product last
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], bb[j][0], acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], bb[j][1], acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bb[j][2], acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], bb[j][0], acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bb[j][1], acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bb[j][0], acc[j], 0, 0, 0);
       }
-    } else {
-      const int t = s - hs;
-      // lanes < FG_RW: edge range of row rw0 + lane in segment t
-      int b = 0, cnt = 0;
-      if (lane < FG_RW && rw0 + lane < M) {
-        const int64_t q = (rw0 + lane) * L + t;
-        b = rowptr[q];
-        cnt = rowptr[q + 1] - b;
-      }
-      int incl = cnt;
-#pragma unroll
-      for (int d = 1; d < FG_RW; d <<= 1) {
-        const int v = __shfl_up(incl, d);
-        if (lane >= d) incl += v;
-      }
-      const int exc = incl - cnt;
-      const int total = readlane_i(incl, FG_RW - 1);
-      int slot = 0;
-      int bound = readlane_i(incl, 0);  // end position of row `slot` in the combined list
-      float4 a4 = zero4();
-      for (int c0 = 0; c0 < total; c0 += 64) {
-        const int p = c0 + lane;
-        int sl = 0;
-#pragma unroll
-        for (int i = 0; i < FG_RW - 1; ++i) sl += p >= readlane_i(incl, i) ? 1 : 0;
-        const int e = __shfl(b, sl) + (p - __shfl(exc, sl));  // CSR position of list entry p
-        int sidx = 0;
-        float w = 0.0f;
-        if (p < total) {
-          sidx = colidx[e];
-          const float v = VALS ? vals[e] : 1.0f;
-          w = de.active ? dropedge_weight(de, v, edge_base + (uint64_t)e) : v;
-        }
-        uint64_t kept = __ballot(w != 0.0f);
-        while (kept) {
-          int jj[FG_U];
-#pragma unroll
-          for (int u = 0; u < FG_U; ++u) {
-            if (kept) {
-              jj[u] = __builtin_ctzll(kept);
-              kept &= kept - 1;
-            } else {
-              jj[u] = -1;
-            }
-          }
-          float4 xv[FG_U];
-#pragma unroll
-          for (int u = 0; u < FG_U; ++u) {
-            if (jj[u] >= 0) {
-              const int r = readlane_i(sidx, jj[u]);
-              xv[u] = col_ok ? *reinterpret_cast<const float4*>(X + (int64_t)r * ldx + col) : zero4();
-            }
-          }
-#pragma unroll
-          for (int u = 0; u < FG_U; ++u) {
-            if (jj[u] >= 0) {
-              const int pos = c0 + jj[u];
-              while (pos >= bound) {  // rows finished before this entry (wave-uniform)
-                flush(slot, a4);
-                a4 = zero4();
-                ++slot;
-                bound = readlane_i(incl, slot);
-              }
-              fma4(a4, readlane_f(w, jj[u]), xv[u]);
-            }
-          }
-        }
-      }
-      for (; slot < FG_RW; ++slot) {
-        flush(slot, a4);
-        a4 = zero4();
-      }
-    }
-    __syncthreads();
-
-    // ---------------- multiply: acc += Zs(32 x F) W_s(F x 64 cols of this wave) ----------------
-    {
-      const uint16_t* wk = Wf + ((int64_t)s * KS * FG_CB + wave * 2) * 3 * FG_FRAG + lane * 8;
-      constexpr int WSTEP = FG_CB * 3 * FG_FRAG;  // bf16 between K16 steps
-      auto load_b = [&](bf16x8_t (&bb)[2][3], int ks) {
-        const uint16_t* w = wk + ks * WSTEP;
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int q = 0; q < 3; ++q) bb[j][q] = *reinterpret_cast<const bf16x8_t*>(w + (j * 3 + q) * FG_FRAG);
-      };
-      auto step = [&](const bf16x8_t (&bb)[2][3], int ks) {
-        bf16x8_t a[3];
-        const int ao = zoff(l32, 2 * ks + h);
-#pragma unroll
-        for (int q = 0; q < 3; ++q) a[q] = *reinterpret_cast<const bf16x8_t*>(zs + q * FG_PLANE + ao);
-        // gemm_x6_kernel's product order: small terms first, the leading product last
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], bb[j][0], acc[j], 0, 0, 0);
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], bb[j][1], acc[j], 0, 0, 0);
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bb[j][2], acc[j], 0, 0, 0);
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], bb[j][0], acc[j], 0, 0, 0);
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bb[j][1], acc[j], 0, 0, 0);
-          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bb[j][0], acc[j], 0, 0, 0);
-        }
-      };
-      // ping-pong: the next step's W fragments are in flight during this step's MFMAs
-      bf16x8_t b0[2][3], b1[2][3];
-      load_b(b0, 0);
+    };
+#if GRL_FG_BDEPTH == 2
+    // ping-pong: the next step's W fragments are in flight during this step's MFMAs
+    bf16x8_t b0[2][3], b1[2][3];
+    load_b(b0, 0);
 #pragma unroll 1
-      for (int ks = 0; ks < KS; ks += 2) {
-        load_b(b1, ks + 1);  // KS is even
-        step(b0, ks);
-        if (ks + 2 < KS) load_b(b0, ks + 2);
-        step(b1, ks + 1);
-      }
+    for (int ks = 0; ks < KS; ks += 2) {
+      load_b(b1, ks + 1);  // KS is even
+      step(b0, ks);
+      if (ks + 2 < KS) load_b(b0, ks + 2);
+      step(b1, ks + 1);
+    }
+#else
+    // three register stages: step ks's fragments were issued two steps
+    // earlier (an L2 hit under load takes longer than one step's 12 MFMAs)
+    bf16x8_t bb[3][2][3];
+    load_b(bb[0], 0);
+    load_b(bb[1], 1);
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      if (ks + 2 < KS) load_b(bb[(ks + 2) % 3], ks + 2);
+      // keep the scheduler from sinking the loads into the MFMA stream (its
+      // vmcnt waits would then stop on fragments issued a few MFMAs earlier)
+      __builtin_amdgcn_sched_barrier(0);
+      step(bb[ks % 3], ks);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#endif
+  };
+
+  // ---------------- edge lists, one typed segment ahead ----------------
+  // rowptr window of this wave's rows (lane l: rowptr[rw0 L + l], l <= FG_RW L;
+  // rows past M read as empty), loaded once per tile
+  const int nvalid = (int)max<int64_t>(0, min<int64_t>(FG_RW, M - rw0));
+  const int rp = lane <= FG_RW * L ? rowptr[min<int64_t>(rw0 * L + min(lane, nvalid * L), M * L)] : 0;
+  struct SegList {
+    int b, exc, incl, total;
+  };
+  // the wave's rows' segment-t edge ranges as one list (lanes < FG_RW: row lane)
+  auto seg_list = [&](int t) {
+    const int r = min(lane, FG_RW - 1);
+    SegList sg;
+    sg.b = __shfl(rp, r * L + t);
+    const int e1 = __shfl(rp, r * L + t + 1);  // all lanes: ds_bpermute reads only active lanes
+    const int cnt = lane < FG_RW ? e1 - sg.b : 0;
+    int incl = cnt;
+#pragma unroll
+    for (int d = 1; d < FG_RW; d <<= 1) {
+      const int v = __shfl_up(incl, d);
+      if (lane >= d) incl += v;
+    }
+    sg.incl = incl;
+    sg.exc = incl - cnt;
+    sg.total = readlane_i(incl, FG_RW - 1);
+    return sg;
+  };
+  // list entries [c0, c0 + 64): source row and DropEdge weight (0 = dropped / past the end)
+  auto fetch = [&](const SegList& sg, int c0, int& sidx, float& w) {
+    const int p = c0 + lane;
+    int sl = 0;
+#pragma unroll
+    for (int i = 0; i < FG_RW - 1; ++i) sl += p >= readlane_i(sg.incl, i) ? 1 : 0;
+    const int e = __shfl(sg.b, sl) + (p - __shfl(sg.exc, sl));  // CSR position of entry p
+    sidx = 0;
+    w = 0.0f;
+    if (p < sg.total) {
+      sidx = colidx[e];
+      const float v = VALS ? vals[e] : 1.0f;
+      w = de.active ? dropedge_weight(de, v, edge_base + (uint64_t)e) : v;
+    }
+  };
+  SegList cur = seg_list(0);
+  int sidx_c;
+  float w_c;
+  fetch(cur, 0, sidx_c, w_c);  // in flight during segment 0
+
+  // ---------------- segment 0: the identity block of A_pre (robust_gcn.py:58-65) ----------------
+  if (hs) {
+    float4 xv[FG_RW];
+#pragma unroll
+    for (int i = 0; i < FG_RW; ++i)
+      xv[i] = (rw0 + i < M && col_ok) ? *reinterpret_cast<const float4*>(X + (rw0 + i) * ldx + col) : zero4();
+#pragma unroll
+    for (int i = 0; i < FG_RW; ++i) {
+      float w = 1.0f;
+      if (de.active && de.drop_self) w = dropedge_weight(de, 1.0f, self_base + (uint64_t)(rw0 + i));
+      const float4 x = w != 0.0f ? make_float4(w * xv[i].x, w * xv[i].y, w * xv[i].z, w * xv[i].w) : zero4();
+      flush(i, x);
     }
     __syncthreads();
+    multiply(0);
+    __syncthreads();
+  }
+
+  // ---------------- typed segments: gather Z segment t of this wave's rows, then multiply ----------------
+  for (int t = 0; t < L; ++t) {
+    // the next segment's list and first 64 entries load while this one gathers and multiplies
+    SegList nxt = cur;
+    int sidx_n = 0;
+    float w_n = 0.0f;
+#if GRL_FG_PIPE_IDX
+    if (t + 1 < L) {
+      nxt = seg_list(t + 1);
+      fetch(nxt, 0, sidx_n, w_n);
+    }
+#else
+    if (t > 0) {
+      cur = seg_list(t);
+      fetch(cur, 0, sidx_c, w_c);
+    }
+#endif
+    const int total = cur.total;
+    int slot = 0;
+    int bound = readlane_i(cur.incl, 0);  // end position of row `slot` in the combined list
+    float4 a4 = zero4();
+    for (int c0 = 0; c0 < total; c0 += 64) {
+      int sidx = sidx_c;
+      float w = w_c;
+      if (c0 > 0) fetch(cur, c0, sidx, w);  // rows with more than 64 segment edges together
+      uint64_t kept = __ballot(w != 0.0f);
+      while (kept) {
+        int jj[FG_U];
+#pragma unroll
+        for (int u = 0; u < FG_U; ++u) {
+          if (kept) {
+            jj[u] = __builtin_ctzll(kept);
+            kept &= kept - 1;
+          } else {
+            jj[u] = -1;
+          }
+        }
+        float4 xv[FG_U];
+#pragma unroll
+        for (int u = 0; u < FG_U; ++u) {
+          if (jj[u] >= 0) {
+            const int r = readlane_i(sidx, jj[u]);
+            xv[u] = col_ok ? *reinterpret_cast<const float4*>(X + (int64_t)r * ldx + col) : zero4();
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < FG_U; ++u) {
+          if (jj[u] >= 0) {
+            const int pos = c0 + jj[u];
+            while (pos >= bound) {  // rows finished before this entry (wave-uniform)
+              flush(slot, a4);
+              a4 = zero4();
+              ++slot;
+              bound = readlane_i(cur.incl, slot);
+            }
+            fma4(a4, readlane_f(w, jj[u]), xv[u]);
+          }
+        }
+      }
+    }
+    for (; slot < FG_RW; ++slot) {
+      flush(slot, a4);
+      a4 = zero4();
+    }
+    __syncthreads();
+    multiply(hs + t);
+    __syncthreads();
+    cur = nxt;
+    sidx_c = sidx_n;
+    w_c = w_n;
   }
 
   // ---------------- epilogue: bias + ReLU, as gemm_x6_kernel ----------------
@@ -302,7 +369,400 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GRL_FG_WPE,
   }
 }
 
+
+// ---------------------------------------------------------------------------
+// Warp-specialized persistent form (the default).  One workgroup per CU, 12
+// waves: 8 gather waves produce Z tiles into a 4-slot LDS ring, 4 MFMA waves
+// consume them, so the HBM-bound gather and the matrix cores run at the same
+// time instead of in alternating phases.
+//  * a tile is 64 destination rows; a ring unit is a 128-column part of one
+//    segment of it, kept fp32 (64 x 128 floats + a pad chunk per row, 33
+//    KB): every W fragment fetched from L2 feeds 64 rows (at 32 rows W's
+//    re-read stream alone exceeded what L2 delivers to a CU), and the MFMA
+//    waves split their A fragments into the x6 planes as they read them;
+//  * the unit stream: tile it of this workgroup (tile = blockIdx.x + it *
+//    gridDim.x), segment s, part hh -> unit u = (it * S + s) * NH + hh, ring
+//    slot u % 4, generation u / 4;
+//  * gather wave p owns rows 8p..8p+7 of each tile: it streams its rows'
+//    segment-s edges as one list (flushes at row boundaries), gathering
+//    whole rows (one float4 per lane, 1 KB per wave-instruction, up to
+//    WS_U rows in flight), and a finished row goes to the segment's NH
+//    units at once; the next segment's list and first 64 sources load while
+//    this one gathers.  Before its first store to a segment's units it waits
+//    until the MFMA waves released their slots' previous generation
+//    (consumed[slot] >= 4 g); after its last it adds 1 to produced[slot]
+//    (release); gather waves never wait for each other;
+//  * MFMA wave c owns output columns 64c..64c+63 for all 64 rows (2 x 2
+//    MFMA blocks): it waits for produced[slot] >= 8 (g + 1) (acquire), runs
+//    the unit's K16 steps (24 MFMAs each) with the next step's W fragments
+//    in flight (the W stream crosses unit and tile boundaries: it is
+//    periodic in the segment order), then adds 1 to consumed[slot]; after a
+//    tile's last unit it stores the tile.
+// Every wave walks the same unit sequence and units complete in order, so
+// the waits cannot form a cycle; each spin is bounded anyway (a kernel that
+// could hang the GPU is not an option), and a wave that gives up stops.
+// Arithmetic per element is the same as graphconv_fused_kernel's (same
+// chains, split, K order, product order): bitwise the two-kernel result.
+// GRL_WS_PLANES=1: the gather waves store x6 bf16 planes (the MFMA waves only
+// read fragments; 3 ring slots of 52 KB); 0: the ring holds fp32 and each
+// MFMA wave splits the fragments it reads (4 slots of 33 KB)
+#ifndef GRL_WS_PLANES
+#define GRL_WS_PLANES 0
+#endif
+constexpr int WS_R = 64;                   // rows per tile
+constexpr int WS_KC = 128;                 // Z columns per ring unit (F > 128: F / 128 units per segment)
+#if GRL_WS_PLANES
+constexpr int WS_LDF = WS_KC + 8;          // bf16 per plane row (+ one 16-B pad chunk: conflict-free)
+constexpr int WS_PLANE = WS_R * WS_LDF;    // bf16 per plane
+constexpr int WS_SLOT = 3 * WS_PLANE / 2;  // ring slot in floats (the ring is declared as float)
+#else
+constexpr int WS_LDF = WS_KC + 4;          // floats per ring row (+ one 16-B pad chunk: conflict-free)
+constexpr int WS_SLOT = WS_R * WS_LDF;     // floats per ring slot
+#endif
+constexpr int WS_PROD = 8;                 // gather waves
+constexpr int WS_CONS = 4;                 // MFMA waves (64 output columns each)
+constexpr int WS_RW = WS_R / WS_PROD;      // rows per gather wave
+constexpr int WS_NB = GRL_WS_PLANES ? 3 : 4;  // ring slots
+#ifndef GRL_WS_U
+#define GRL_WS_U 12
+#endif
+constexpr int WS_U = GRL_WS_U;             // neighbour rows in flight per gather wave
+constexpr int WS_SPIN = 1 << 24;           // bounded waits (~ seconds)
+
+// GRL_WS_STAMP=1 (diagnostic builds only): every wave adds up the cycles it
+// spent waiting on the ring and its total, read back with grl_debug_ws_stats
+#ifndef GRL_WS_STAMP
+#define GRL_WS_STAMP 0
+#endif
+#if GRL_WS_STAMP
+__device__ unsigned long long g_ws_dbg[1024 * 12 * 2];
+#endif
+
+__device__ __forceinline__ int lds_load_acq(int* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+__device__ __forceinline__ void lds_add_rel(int* p, int v) {
+  __hip_atomic_fetch_add(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+// wait until *p >= target (wave-uniform); false if the bound ran out
+__device__ __forceinline__ bool wait_ge(int* p, int target, unsigned long long* waited) {
+#if GRL_WS_STAMP
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+#endif
+  for (int spin = 0; spin < WS_SPIN; ++spin) {
+    if (lds_load_acq(p) >= target) {
+#if GRL_WS_STAMP
+      *waited += __builtin_amdgcn_s_memtime() - t0;
+#endif
+      return true;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+  return false;
+}
+
+template <int KS, bool VALS>
+__global__ __launch_bounds__(64 * (WS_PROD + WS_CONS)) void graphconv_ws_kernel(
+    int64_t M, int L, int hs, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ colidx,
+    const float* __restrict__ vals, uint64_t edge_base, uint64_t self_base, const float* __restrict__ X,
+    int64_t ldx, const uint16_t* __restrict__ Wf, const float* __restrict__ bias, int relu,
+    float* __restrict__ out, int C, DropDev de, int64_t num_tiles) {
+  constexpr int F = KS * 16;
+  constexpr int KC = F < WS_KC ? F : WS_KC;  // Z columns per unit
+  constexpr int NH = F / KC;                  // units per segment
+  constexpr int KSU = KC / 16;                // K16 steps per unit
+  static_assert(NH <= 2 && NH < WS_NB, "a segment's units are distinct ring slots");
+  __shared__ __attribute__((aligned(16))) float ring[WS_NB * WS_SLOT];
+  __shared__ int produced[WS_NB], consumed[WS_NB];
+  if (threadIdx.x < WS_NB) {
+    produced[threadIdx.x] = 0;
+    consumed[threadIdx.x] = 0;
+  }
+  __syncthreads();
+  de = resolve_key(de);
+  const int lane = threadIdx.x & 63;
+  const int wave = uniform_i(threadIdx.x >> 6);
+  const int S = L + hs;
+  unsigned long long waited = 0;
+#if GRL_WS_STAMP
+  const unsigned long long t_start = __builtin_amdgcn_s_memtime();
+  auto stamp_out = [&]() {
+    if (lane == 0 && blockIdx.x < 1024) {
+      g_ws_dbg[(blockIdx.x * 12 + wave) * 2] = waited;
+      g_ws_dbg[(blockIdx.x * 12 + wave) * 2 + 1] = __builtin_amdgcn_s_memtime() - t_start;
+    }
+  };
+#else
+  auto stamp_out = [&]() {};
+#endif
+
+  if (wave < WS_PROD) {
+    // =========================== gather waves ===========================
+    const int col = lane * 4;            // this lane's 4 columns of the row
+    const bool col_ok = col < F;
+    const int part = col / KC;           // the unit (part of the segment) they belong to
+    const int ucol = col - part * KC;    // column within that unit
+    int u = 0;                           // first unit of the current segment
+    // segment lists: lanes < WS_RW hold row lane's range start b and the
+    // inclusive count incl; the first 64 entries' source rows / weights are
+    // fetched one segment ahead
+    struct List {
+      int b, incl, exc, total, sidx;
+      float w;
+    };
+    auto make_list = [&](int rp, int t) {
+      List ls;
+      const int r = min(lane, WS_RW - 1);
+      ls.b = __shfl(rp, r * L + t);
+      const int e1 = __shfl(rp, r * L + t + 1);  // all lanes: ds_bpermute reads active lanes only
+      const int cnt = lane < WS_RW ? e1 - ls.b : 0;
+      int incl = cnt;
+#pragma unroll
+      for (int d = 1; d < WS_RW; d <<= 1) {
+        const int v = __shfl_up(incl, d);
+        if (lane >= d) incl += v;
+      }
+      ls.incl = incl;
+      ls.exc = incl - cnt;
+      ls.total = readlane_i(incl, WS_RW - 1);
+      return ls;
+    };
+    // list entries [c0, c0 + 64): source row and DropEdge weight (0 = dropped / past the end)
+    auto fetch = [&](const List& ls, int c0, int& sidx, float& w) {
+      const int pp = c0 + lane;
+      int sl = 0;
+#pragma unroll
+      for (int i = 0; i < WS_RW - 1; ++i) sl += pp >= readlane_i(ls.incl, i) ? 1 : 0;
+      const int e = __shfl(ls.b, sl) + (pp - __shfl(ls.exc, sl));  // CSR position of entry pp
+      sidx = 0;
+      w = 0.0f;
+      if (pp < ls.total) {
+        sidx = colidx[e];
+        const float v = VALS ? vals[e] : 1.0f;
+        w = de.active ? dropedge_weight(de, v, edge_base + (uint64_t)e) : v;
+      }
+    };
+    for (int64_t tile = blockIdx.x; tile < num_tiles; tile += gridDim.x) {
+      const int64_t rw0 = tile * WS_R + wave * WS_RW;
+      const int nvalid = (int)max<int64_t>(0, min<int64_t>(WS_RW, M - rw0));
+      const int rp = lane <= WS_RW * L ? rowptr[min<int64_t>(rw0 * L + min(lane, nvalid * L), M * L)] : 0;
+      List cur = make_list(rp, 0);
+      fetch(cur, 0, cur.sidx, cur.w);
+      for (int s = 0; s < S; ++s, u += NH) {
+        // claim the segment's NH slots (this wave's rows only), once, before the first store
+        bool have = false;
+        auto claim = [&]() -> bool {
+          if (have) return true;
+#pragma unroll
+          for (int q = 0; q < NH; ++q)
+            if (!wait_ge(&consumed[(u + q) % WS_NB], WS_CONS * ((u + q) / WS_NB), &waited)) return false;
+          have = true;
+          return true;
+        };
+#if GRL_WS_PLANES
+        uint16_t* const dst = reinterpret_cast<uint16_t*>(ring + ((u + part) % WS_NB) * WS_SLOT) + ucol;
+        auto flush = [&](int r, const float4& v) {
+          if (col_ok) {
+            uint2 q0, q1, q2;
+            split3(v, q0, q1, q2);
+            uint16_t* d = dst + (wave * WS_RW + r) * WS_LDF;
+            *reinterpret_cast<uint2*>(d) = q0;
+            *reinterpret_cast<uint2*>(d + WS_PLANE) = q1;
+            *reinterpret_cast<uint2*>(d + 2 * WS_PLANE) = q2;
+          }
+        };
+#else
+        float* const dst = ring + ((u + part) % WS_NB) * WS_SLOT + ucol;
+        auto flush = [&](int r, const float4& v) {
+          if (col_ok) *reinterpret_cast<float4*>(dst + (wave * WS_RW + r) * WS_LDF) = v;
+        };
+#endif
+        if (s < hs) {
+          // identity block of A_pre (robust_gcn.py:58-65): the rows' own features
+          float4 xv[WS_RW];
+#pragma unroll
+          for (int i = 0; i < WS_RW; ++i)
+            xv[i] = (i < nvalid && col_ok) ? *reinterpret_cast<const float4*>(X + (rw0 + i) * ldx + col) : zero4();
+          if (!claim()) return;
+#pragma unroll
+          for (int i = 0; i < WS_RW; ++i) {
+            float w = 1.0f;
+            if (de.active && de.drop_self) w = dropedge_weight(de, 1.0f, self_base + (uint64_t)(rw0 + i));
+            flush(i, w != 0.0f ? make_float4(w * xv[i].x, w * xv[i].y, w * xv[i].z, w * xv[i].w) : zero4());
+          }
+        } else {
+          // the next segment's list and first 64 entries load while this one gathers
+          List nxt = cur;
+          if (s + 1 < S) {
+            nxt = make_list(rp, s + 1 - hs);
+            fetch(nxt, 0, nxt.sidx, nxt.w);
+          }
+          int row = 0;
+          int bound = readlane_i(cur.incl, 0);
+          float4 a4 = zero4();
+          for (int c0 = 0; c0 < cur.total; c0 += 64) {
+            int sidx = cur.sidx;
+            float w = cur.w;
+            if (c0 > 0) fetch(cur, c0, sidx, w);  // rows with more than 64 segment edges together
+            uint64_t kept = __ballot(w != 0.0f);
+            while (kept) {
+              int jj[WS_U];
+#pragma unroll
+              for (int q = 0; q < WS_U; ++q) {
+                if (kept) {
+                  jj[q] = __builtin_ctzll(kept);
+                  kept &= kept - 1;
+                } else {
+                  jj[q] = -1;
+                }
+              }
+              float4 xv[WS_U];
+#pragma unroll
+              for (int q = 0; q < WS_U; ++q) {
+                if (jj[q] >= 0) {
+                  const int src = readlane_i(sidx, jj[q]);
+                  xv[q] = col_ok ? *reinterpret_cast<const float4*>(X + (int64_t)src * ldx + col) : zero4();
+                }
+              }
+#pragma unroll
+              for (int q = 0; q < WS_U; ++q) {
+                if (jj[q] >= 0) {
+                  const int pos = c0 + jj[q];
+                  while (pos >= bound) {  // rows finished before this entry (wave-uniform)
+                    if (!claim()) return;
+                    flush(row, a4);
+                    a4 = zero4();
+                    ++row;
+                    bound = readlane_i(cur.incl, row);
+                  }
+                  fma4(a4, readlane_f(w, jj[q]), xv[q]);
+                }
+              }
+            }
+          }
+          if (!claim()) return;
+          for (; row < WS_RW; ++row) {
+            flush(row, a4);
+            a4 = zero4();
+          }
+          cur = nxt;
+        }
+        if (lane == 0)
+#pragma unroll
+          for (int q = 0; q < NH; ++q) lds_add_rel(&produced[(u + q) % WS_NB], 1);
+      }
+    }
+    stamp_out();
+  } else {
+    // =========================== MFMA waves ===========================
+    const int c = wave - WS_PROD;
+    const int l32 = lane & 31, h = lane >> 5;
+    constexpr int WSTEP = FG_CB * 3 * FG_FRAG;  // bf16 between K16 steps of W
+    const int nsteps = S * KS;                   // one tile's K16 steps (the W stream's period)
+    // uniform base (SGPRs) + the lane's 16 B: saddr loads
+    const uint16_t* wbase = Wf + (int64_t)(c * 2) * 3 * FG_FRAG;
+    const int loff = lane * 8;
+    auto load_b = [&](bf16x8_t (&bb)[2][3], int gstep) {
+      const uint16_t* w = wbase + (int64_t)gstep * WSTEP;
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) bb[j][q] = *reinterpret_cast<const bf16x8_t*>(w + (j * 3 + q) * FG_FRAG + loff);
+    };
+    f32x16 acc[2][2];  // [row block][column block]
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+    bf16x8_t bb[2][2][3];
+    int nxt = 0;  // K16 step (within the tile) of the next W fragments to load
+    load_b(bb[0], nxt);
+    nxt = nxt + 1 == nsteps ? 0 : nxt + 1;
+    int u = 0;
+    for (int64_t tile = blockIdx.x; tile < num_tiles; tile += gridDim.x) {
+      for (int su = 0; su < S * NH; ++su, ++u) {
+        const int slot = u % WS_NB, g = u / WS_NB;
+        const float* zs = ring + slot * WS_SLOT;
+        if (!wait_ge(&produced[slot], WS_PROD * (g + 1), &waited)) return;
+#pragma unroll
+        for (int ks = 0; ks < KSU; ++ks) {  // KSU is even: the stage of step ks is ks & 1
+          load_b(bb[(ks + 1) & 1], nxt);
+          nxt = nxt + 1 == nsteps ? 0 : nxt + 1;
+          __builtin_amdgcn_sched_barrier(0);
+          const int st = ks & 1;
+#pragma unroll
+          for (int i = 0; i < 2; ++i) {
+            bf16x8_t a[3];
+#if GRL_WS_PLANES
+            const uint16_t* ar = reinterpret_cast<const uint16_t*>(zs) + (i * 32 + l32) * WS_LDF + ks * 16 + h * 8;
+#pragma unroll
+            for (int q = 0; q < 3; ++q) a[q] = *reinterpret_cast<const bf16x8_t*>(ar + q * WS_PLANE);
+#else
+            // this lane's 8 k of row i*32 + l32, split into the three bf16 planes
+            const float* ar = zs + (i * 32 + l32) * WS_LDF + ks * 16 + h * 8;
+            const float4 v0 = *reinterpret_cast<const float4*>(ar);
+            const float4 v1 = *reinterpret_cast<const float4*>(ar + 4);
+            uint2 p0, p1, p2, r0, r1, r2;
+            split3(v0, p0, p1, p2);
+            split3(v1, r0, r1, r2);
+            a[0] = __builtin_bit_cast(bf16x8_t, make_uint4(p0.x, p0.y, r0.x, r0.y));
+            a[1] = __builtin_bit_cast(bf16x8_t, make_uint4(p1.x, p1.y, r1.x, r1.y));
+            a[2] = __builtin_bit_cast(bf16x8_t, make_uint4(p2.x, p2.y, r2.x, r2.y));
+#endif
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {  // gemm_x6_kernel's product order
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], bb[st][j][0], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], bb[st][j][1], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bb[st][j][2], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], bb[st][j][0], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bb[st][j][1], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bb[st][j][0], acc[i][j], 0, 0, 0);
+            }
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+        // the slot's A fragments are in registers once their reads returned
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) lds_add_rel(&consumed[slot], 1);
+      }
+      // tile done: bias + ReLU, as gemm_x6_kernel
+      const int64_t m0 = tile * WS_R;
+      const bool epi = bias != nullptr || relu;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int n = (c * 2 + j) * 32 + l32;
+        const float bv = (bias && n < C) ? bias[n] : 0.0f;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int64_t m = m0 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            if (m < M && n < C) {
+              float v = acc[i][j][r];
+              if (epi) {
+                v = v + bv;
+                if (relu) v = v > 0.0f ? v : 0.0f;
+              }
+              out[m * C + n] = v;
+            }
+            acc[i][j][r] = 0.0f;
+          }
+      }
+    }
+    stamp_out();
+  }
+}
+
 }  // namespace
+
+#if GRL_WS_STAMP
+extern "C" int grl_debug_ws_stats(unsigned long long* host, int64_t n) {
+  GRL_HIP(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_ws_dbg), (size_t)n * 8));
+  return GRL_OK;
+}
+#endif
 
 // GRL_GRAPHCONV_FUSED=0 (read on every call) keeps grl_graphconv_fwd on the
 // two-kernel path (A/B aid and tests).
@@ -311,7 +771,11 @@ bool graphconv_fused_enabled() {
   return !(e && e[0] == '0');
 }
 
-bool graphconv_fused_shape_ok(int F, int C) { return (F == 256 || F == 128 || F == 64) && C >= 1 && C <= 256; }
+// F in {64, 128, 256}, C <= 256, and one wave register holds a wave's rowptr
+// window (FG_RW * L + 1 <= 64: L <= 7)
+bool graphconv_fused_shape_ok(int F, int C, int L) {
+  return (F == 256 || F == 128 || F == 64) && C >= 1 && C <= 256 && L >= 1 && FG_RW * L < 64;
+}
 
 size_t graphconv_fused_ws_bytes(int64_t K) { return (size_t)K * FG_CB * 32 * 3 * 2 + 256; }
 
@@ -329,6 +793,31 @@ int graphconv_fused_fwd(const GrlTypedCsr* g, const float* X, int64_t ldx, int F
   GRL_CHECK_ARG(tiles < 2147483647LL, "grl_graphconv_fwd: too many row tiles");
   const DropDev d = to_dev(de);
   const bool v = g->vals != nullptr;
+  const char* wse = getenv("GRL_FG_WS");
+  if (!(wse && wse[0] == '0')) {
+    const int64_t ws_tiles = ceil_div(M, WS_R);
+    const int64_t grid = std::min<int64_t>(ws_tiles, (int64_t)device_cu_count());
+#define GRL_WS_LAUNCH(KS_)                                                                                           \
+  do {                                                                                                               \
+    if (v)                                                                                                           \
+      hipLaunchKernelGGL((graphconv_ws_kernel<KS_, true>), dim3((unsigned)grid), dim3(64 * (WS_PROD + WS_CONS)), 0,  \
+                         st, M, g->num_types, hs, g->rowptr, g->colidx, g->vals, g->edge_id_base, g->self_id_base, X, \
+                         ldx, Wf, bias, relu, out, C, d, ws_tiles);                                                  \
+    else                                                                                                             \
+      hipLaunchKernelGGL((graphconv_ws_kernel<KS_, false>), dim3((unsigned)grid), dim3(64 * (WS_PROD + WS_CONS)), 0, \
+                         st, M, g->num_types, hs, g->rowptr, g->colidx, g->vals, g->edge_id_base, g->self_id_base, X, \
+                         ldx, Wf, bias, relu, out, C, d, ws_tiles);                                                  \
+  } while (0)
+    if (F == 256)
+      GRL_WS_LAUNCH(16);
+    else if (F == 128)
+      GRL_WS_LAUNCH(8);
+    else
+      GRL_WS_LAUNCH(4);
+#undef GRL_WS_LAUNCH
+    GRL_LAUNCH_CHECK();
+    return GRL_OK;
+  }
 #define GRL_FUSED_LAUNCH(KS_)                                                                                        \
   do {                                                                                                               \
     if (v)                                                                                                           \

@@ -1202,7 +1202,7 @@ static size_t ws_align(size_t b) { return (b + 255) & ~(size_t)255; }
 // partials, a different order).
 static bool fused_path(const GrlTypedCsr* g, const float* X, int64_t ldx, int F, const float* W, int C) {
   const int64_t K = (int64_t)(g->num_types + (g->has_self ? 1 : 0)) * F;
-  return graphconv_fused_enabled() && graphconv_fused_shape_ok(F, C) && x6_shape_ok(g->num_rows, C, K) &&
+  return graphconv_fused_enabled() && graphconv_fused_shape_ok(F, C, g->num_types) && x6_shape_ok(g->num_rows, C, K) &&
          al16(W) && C % 4 == 0 && al16(X) && ldx % 4 == 0 && (!g->split || g->split->num_heavy == 0);
 }
 

@@ -144,11 +144,14 @@ def _ws_query(X, g, W, C):
                                                   (40_007, 6, 128, 256, True, 16.0), (70_001, 6, 64, 256, True, 12.0),
                                                   (60_001, 3, 256, 200, False, 20.0)])
 @pytest.mark.parametrize("variant", ["plain", "drop_bias_relu", "drop_spare_self", "strided_relu"])
-def test_fused_graphconv_bitwise_equals_two_kernels(N, L, F, C, has_self, deg, variant, monkeypatch):
-    """The one-kernel GraphConv (graphconv.hip) gives the two-kernel bits
-    (typed SpMM, then the x6 GEMM): the same fmaf chain per Z element, the
-    same split, K order and product order; and it runs in a workspace of
-    only W's planes (Z never reaches HBM)."""
+@pytest.mark.parametrize("kernel", ["ws", "phases"])
+def test_fused_graphconv_bitwise_equals_two_kernels(N, L, F, C, has_self, deg, variant, kernel, monkeypatch):
+    """The one-kernel GraphConv (graphconv.hip; both kernels: the
+    warp-specialized default and the phase-alternating GRL_FG_WS=0 one)
+    gives the two-kernel bits (typed SpMM, then the x6 GEMM): the same fmaf
+    chain per Z element, the same split, K order and product order; and it
+    runs in a workspace of only W's planes (Z never reaches HBM)."""
+    monkeypatch.setenv("GRL_FG_WS", "1" if kernel == "ws" else "0")
     de = {"plain": None, "drop_bias_relu": DropEdge(0.3, 3, 2, True), "drop_spare_self": DropEdge(0.25, 9, 0, False),
           "strided_relu": None}[variant]
     bias = variant == "drop_bias_relu"

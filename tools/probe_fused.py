@@ -42,6 +42,13 @@ def main():
         t_f = timeit(lambda: graph_conv_infer(X, g, W, b, True))
         if os.environ.get("PROBE_ONLY_FUSED"):  # profiler runs: the fused kernel only
             print(f"{lib} p={p}: fused {t_f:.3f} ms", flush=True)
+            if os.environ.get("PROBE_SIMPLE"):  # the phase-alternating kernel (GRL_FG_WS=0) beside it
+                os.environ["GRL_FG_WS"] = "0"
+                simple = graph_conv_infer(X, g, W, b, True)
+                t_s = timeit(lambda: graph_conv_infer(X, g, W, b, True))
+                os.environ["GRL_FG_WS"] = "1"
+                print(f"{lib} p={p}: simple {t_s:.3f} ms, bitwise equal to ws: {bool(torch.equal(simple, fused))}",
+                      flush=True)
             continue
         os.environ["GRL_GRAPHCONV_FUSED"] = "0"
         two = graph_conv_infer(X, g, W, b, True)
