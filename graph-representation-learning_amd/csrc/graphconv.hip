@@ -434,6 +434,11 @@ constexpr int WS_SPIN = 1 << 24;           // bounded waits (~ seconds)
 #ifndef GRL_WS_STAMP
 #define GRL_WS_STAMP 0
 #endif
+// GRL_WS_ONLY_ROLE (register-use diagnostics only, never a working build):
+// 1 = compile the gather role alone, 2 = the MFMA role alone
+#ifndef GRL_WS_ONLY_ROLE
+#define GRL_WS_ONLY_ROLE 0
+#endif
 #if GRL_WS_STAMP
 __device__ unsigned long long g_ws_dbg[1024 * 12 * 2];
 #endif
@@ -496,7 +501,11 @@ __global__ __launch_bounds__(64 * (WS_PROD + WS_CONS)) void graphconv_ws_kernel(
   auto stamp_out = [&]() {};
 #endif
 
+#if GRL_WS_ONLY_ROLE == 2
+  if (false) {
+#else
   if (wave < WS_PROD) {
+#endif
     // =========================== gather waves ===========================
     const int col = lane * 4;            // this lane's 4 columns of the row
     const bool col_ok = col < F;
@@ -654,6 +663,9 @@ __global__ __launch_bounds__(64 * (WS_PROD + WS_CONS)) void graphconv_ws_kernel(
     }
     stamp_out();
   } else {
+#if GRL_WS_ONLY_ROLE == 1
+    return;
+#endif
     // =========================== MFMA waves ===========================
     const int c = wave - WS_PROD;
     const int l32 = lane & 31, h = lane >> 5;
@@ -676,6 +688,43 @@ __global__ __launch_bounds__(64 * (WS_PROD + WS_CONS)) void graphconv_ws_kernel(
       for (int j = 0; j < 2; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+    // 12 MFMAs of row block i against both column blocks, gemm_x6_kernel's product order
+    auto mma = [&](int i, const bf16x8_t (&b)[2][3], const bf16x8_t (&a)[3]) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[j][0], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[j][1], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[j][2], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[j][0], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[j][1], acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[j][0], acc[i][j], 0, 0, 0);
+      }
+    };
+#if !GRL_WS_PLANES
+    // this lane's 8 k (step ks) of row i*32 + l32 of a fp32 ring unit
+    auto read_a = [&](const float* zs, int ks, int i, float4& v0, float4& v1) {
+      const float* ar = zs + (i * 32 + l32) * WS_LDF + ks * 16 + h * 8;
+      v0 = *reinterpret_cast<const float4*>(ar);
+      v1 = *reinterpret_cast<const float4*>(ar + 4);
+    };
+    auto split_a = [&](const float4& v0, const float4& v1, bf16x8_t (&a)[3]) {
+      uint2 p0, p1, p2, r0, r1, r2;
+      split3(v0, p0, p1, p2);
+      split3(v1, r0, r1, r2);
+      a[0] = __builtin_bit_cast(bf16x8_t, make_uint4(p0.x, p0.y, r0.x, r0.y));
+      a[1] = __builtin_bit_cast(bf16x8_t, make_uint4(p1.x, p1.y, r1.x, r1.y));
+      a[2] = __builtin_bit_cast(bf16x8_t, make_uint4(p2.x, p2.y, r2.x, r2.y));
+    };
+    // scheduling hint for the region just written: 2 MFMAs, then 3 VALU / 1 MFMA
+    auto interleave = [&]() {
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+#pragma unroll
+      for (int q = 0; q < 10; ++q) {
+        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+      }
+    };
+#endif
     bf16x8_t bb[2][2][3];
     int nxt = 0;  // K16 step (within the tile) of the next W fragments to load
     load_b(bb[0], nxt);
@@ -686,6 +735,7 @@ __global__ __launch_bounds__(64 * (WS_PROD + WS_CONS)) void graphconv_ws_kernel(
         const int slot = u % WS_NB, g = u / WS_NB;
         const float* zs = ring + slot * WS_SLOT;
         if (!wait_ge(&produced[slot], WS_PROD * (g + 1), &waited)) return;
+#if GRL_WS_PLANES
 #pragma unroll
         for (int ks = 0; ks < KSU; ++ks) {  // KSU is even: the stage of step ks is ks & 1
           load_b(bb[(ks + 1) & 1], nxt);
@@ -695,34 +745,44 @@ __global__ __launch_bounds__(64 * (WS_PROD + WS_CONS)) void graphconv_ws_kernel(
 #pragma unroll
           for (int i = 0; i < 2; ++i) {
             bf16x8_t a[3];
-#if GRL_WS_PLANES
             const uint16_t* ar = reinterpret_cast<const uint16_t*>(zs) + (i * 32 + l32) * WS_LDF + ks * 16 + h * 8;
 #pragma unroll
             for (int q = 0; q < 3; ++q) a[q] = *reinterpret_cast<const bf16x8_t*>(ar + q * WS_PLANE);
-#else
-            // this lane's 8 k of row i*32 + l32, split into the three bf16 planes
-            const float* ar = zs + (i * 32 + l32) * WS_LDF + ks * 16 + h * 8;
-            const float4 v0 = *reinterpret_cast<const float4*>(ar);
-            const float4 v1 = *reinterpret_cast<const float4*>(ar + 4);
-            uint2 p0, p1, p2, r0, r1, r2;
-            split3(v0, p0, p1, p2);
-            split3(v1, r0, r1, r2);
-            a[0] = __builtin_bit_cast(bf16x8_t, make_uint4(p0.x, p0.y, r0.x, r0.y));
-            a[1] = __builtin_bit_cast(bf16x8_t, make_uint4(p1.x, p1.y, r1.x, r1.y));
-            a[2] = __builtin_bit_cast(bf16x8_t, make_uint4(p2.x, p2.y, r2.x, r2.y));
-#endif
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {  // gemm_x6_kernel's product order
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], bb[st][j][0], acc[i][j], 0, 0, 0);
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], bb[st][j][1], acc[i][j], 0, 0, 0);
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bb[st][j][2], acc[i][j], 0, 0, 0);
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], bb[st][j][0], acc[i][j], 0, 0, 0);
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bb[st][j][1], acc[i][j], 0, 0, 0);
-              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], bb[st][j][0], acc[i][j], 0, 0, 0);
-            }
+            mma(i, bb[st], a);
           }
           __builtin_amdgcn_sched_barrier(0);
         }
+#else
+        // Software-pipelined by row block: the split of the next row block's
+        // A fragments (VALU) is interleaved with the current row block's 12
+        // MFMAs (an MFMA holds the SIMD's issue for 8 of its 32 cycles; the
+        // VALU fits in the rest), instead of running between them.
+        bf16x8_t pa[2][3];
+        {
+          float4 v0, v1;
+          read_a(zs, 0, 0, v0, v1);
+          split_a(v0, v1, pa[0]);
+        }
+#pragma unroll
+        for (int ks = 0; ks < KSU; ++ks) {  // KSU is even: the stage of step ks is ks & 1
+          load_b(bb[(ks + 1) & 1], nxt);
+          nxt = nxt + 1 == nsteps ? 0 : nxt + 1;
+          const int st = ks & 1;
+          float4 v0, v1;
+          read_a(zs, ks, 1, v0, v1);
+          __builtin_amdgcn_sched_barrier(0);
+          mma(0, bb[st], pa[0]);
+          split_a(v0, v1, pa[1]);
+          interleave();
+          __builtin_amdgcn_sched_barrier(0);
+          if (ks + 1 < KSU) read_a(zs, ks + 1, 0, v0, v1);
+          __builtin_amdgcn_sched_barrier(0);
+          mma(1, bb[st], pa[1]);
+          if (ks + 1 < KSU) split_a(v0, v1, pa[0]);
+          interleave();
+          __builtin_amdgcn_sched_barrier(0);
+        }
+#endif
         // the slot's A fragments are in registers once their reads returned
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (lane == 0) lds_add_rel(&consumed[slot], 1);

@@ -630,6 +630,12 @@ bool x6_stagger() {
   return e && e[0] == '1';
 }
 
+// GRL_X6_INTERLEAVE (read per call): 1 = the A split interleaved with the MFMAs
+bool x6_interleave() {
+  const char* e = getenv("GRL_X6_INTERLEAVE");
+  return e && e[0] == '1';
+}
+
 // global -> LDS DMA of one 16 B chunk per lane (lane l lands at lds_base + 16 l).
 // Issued from asm so that hipcc's waitcnt pass neither sees nor waits on it;
 // completion is ordered by the kernel's counted `s_waitcnt vmcnt`.
@@ -663,7 +669,13 @@ constexpr int X6_SLOT = 512 * 8;  // floats per landing slot (16 KB)
 // MFMAs instead of both splitting while the matrix core idles
 // (MI355X_MICROARCH.md, two waves per SIMD: stagger).  Same arithmetic,
 // same bits.
-template <int EPI, bool STAGGER = false>
+// INTERLEAVE: the split of A(t+1) into the next stage (2 landing-slot reads,
+// ~44 VALU, 6 LDS writes per wave) is scheduled between step t's 48 MFMAs
+// (sched_group_barrier) instead of after them: an MFMA holds the SIMD's issue
+// for 8 of its 32 cycles and the split fits in the rest.  A(t+1) landed one
+// step earlier, so its wait moves before the MFMAs; B(t+1)'s DMA is waited
+// for at the end of the step, before the next barrier.  Same bits.
+template <int EPI, bool STAGGER = false, bool INTERLEAVE = false>
 __global__ __launch_bounds__(512) void gemm_x6_kernel(GemmArgs p, const uint16_t* __restrict__ Bp, int64_t Np) {
   __shared__ __attribute__((aligned(16))) uint16_t smem[2 * X6_STAGE];  // 2 plane stages x 48 KB
   __shared__ __attribute__((aligned(16))) float land[3 * X6_SLOT];      // 3 landing slots x 16 KB
@@ -762,6 +774,12 @@ __global__ __launch_bounds__(512) void gemm_x6_kernel(GemmArgs p, const uint16_t
 #pragma unroll
         for (int q = 0; q < 3; ++q)
           b_[j][q] = *reinterpret_cast<const bf16x8_t*>(cur + (3 + q) * X6_PLANE + sw(wn * 64 + j * 32 + l32, h * 8));
+      if (INTERLEAVE && t + 1 < nk) {  // A(t+1) is older than B(t+1) (3 DMAs) and A(t+2) (2)
+        if (t + 2 < nk)
+          asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      }
       if (STAGGER && wm == 1 && t + 1 < nk) {  // the late half: split A(t+1) before its MFMAs
         // B(t+1) (3 DMAs) and A(t+2) (2) were just issued and may stay in flight; A(t+1) is older
         if (t + 2 < nk)
@@ -800,8 +818,30 @@ __global__ __launch_bounds__(512) void gemm_x6_kernel(GemmArgs p, const uint16_t
 #if GRL_X6_PRIO
       __builtin_amdgcn_s_setprio(0);
 #endif
+      if (INTERLEAVE && t + 1 < nk) {
+        stash_a(t + 1, nxt);
+        // fragment and landing reads first, then 2 MFMAs / 2 VALU, the stores last
+        __builtin_amdgcn_sched_group_barrier(0x100, 20, 0);
+#pragma unroll
+        for (int q = 0; q < 22; ++q) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+          __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x200, 2, 0);
+        }
+      }
     }
-    if (t + 1 < nk) {
+    if (INTERLEAVE) {
+      if (t + 1 < nk) {  // B(t+1) landed before the next barrier
+        if (t + 2 < nk)
+          asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    } else if (t + 1 < nk) {
       if (t + 2 < nk)
         asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // A(t+2) may stay in flight
       else
@@ -1100,14 +1140,19 @@ int launch_x6_gemm(GemmArgs a, const uint16_t* planes, hipStream_t st) {
   a.k_per_split = a.K;
   GRL_CHECK_ARG(a.mt * a.nt < 2147483647LL, "gemm: grid too large");
   const dim3 grid((unsigned)(a.mt * a.nt));
+  const bool il = x6_interleave();
   if (a.bias || a.relu)
     if (x6_stagger())
       hipLaunchKernelGGL((gemm_x6_kernel<EPI_BIAS, true>), grid, dim3(512), 0, st, a, planes, Np);
+    else if (il)
+      hipLaunchKernelGGL((gemm_x6_kernel<EPI_BIAS, false, true>), grid, dim3(512), 0, st, a, planes, Np);
     else
       hipLaunchKernelGGL(gemm_x6_kernel<EPI_BIAS>, grid, dim3(512), 0, st, a, planes, Np);
   else
     if (x6_stagger())
       hipLaunchKernelGGL((gemm_x6_kernel<EPI_STORE, true>), grid, dim3(512), 0, st, a, planes, Np);
+    else if (il)
+      hipLaunchKernelGGL((gemm_x6_kernel<EPI_STORE, false, true>), grid, dim3(512), 0, st, a, planes, Np);
     else
       hipLaunchKernelGGL(gemm_x6_kernel<EPI_STORE>, grid, dim3(512), 0, st, a, planes, Np);
   GRL_LAUNCH_CHECK();
