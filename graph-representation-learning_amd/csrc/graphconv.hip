@@ -34,6 +34,7 @@ using f32x16 = __attribute__((ext_vector_type(16))) float;
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
 constexpr int FG_R = 32;                  // destination rows per tile
 constexpr int FG_WAVES = 4;               // waves per workgroup
@@ -420,7 +421,11 @@ constexpr int WS_LDF = WS_KC + 4;          // floats per ring row (+ one 16-B pa
 constexpr int WS_SLOT = WS_R * WS_LDF;     // floats per ring slot
 #endif
 constexpr int WS_PROD = 8;                 // gather waves
-constexpr int WS_CONS = 4;                 // MFMA waves (64 output columns each)
+#ifndef GRL_WS_CONS
+#define GRL_WS_CONS 4
+#endif
+constexpr int WS_CONS = GRL_WS_CONS;       // MFMA waves (4: 64 output columns each; 8: 32, two per SIMD)
+constexpr int WS_CB = FG_CB / WS_CONS;     // 32-column blocks per MFMA wave
 constexpr int WS_RW = WS_R / WS_PROD;      // rows per gather wave
 constexpr int WS_NB = GRL_WS_PLANES ? 3 : 4;  // ring slots
 #ifndef GRL_WS_U
@@ -471,7 +476,7 @@ __global__ __launch_bounds__(64 * (WS_PROD + WS_CONS)) void graphconv_ws_kernel(
     int64_t M, int L, int hs, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ colidx,
     const float* __restrict__ vals, uint64_t edge_base, uint64_t self_base, const float* __restrict__ X,
     int64_t ldx, const uint16_t* __restrict__ Wf, const float* __restrict__ bias, int relu,
-    float* __restrict__ out, int C, DropDev de, int64_t num_tiles) {
+    float* __restrict__ out, int C, DropDev de, int64_t num_tiles, float* __restrict__ Zout, int64_t ldz) {
   constexpr int F = KS * 16;
   constexpr int KC = F < WS_KC ? F : WS_KC;  // Z columns per unit
   constexpr int NH = F / KC;                  // units per segment
@@ -582,8 +587,17 @@ __global__ __launch_bounds__(64 * (WS_PROD + WS_CONS)) void graphconv_ws_kernel(
         };
 #else
         float* const dst = ring + ((u + part) % WS_NB) * WS_SLOT + ucol;
+        // training forward (Zout): the row also goes to HBM for the weight
+        // gradient, with non-temporal stores as spmm_kernel's
+        float* const zrow = Zout ? Zout + rw0 * ldz + (int64_t)s * F + col : nullptr;
         auto flush = [&](int r, const float4& v) {
-          if (col_ok) *reinterpret_cast<float4*>(dst + (wave * WS_RW + r) * WS_LDF) = v;
+          if (col_ok) {
+            *reinterpret_cast<float4*>(dst + (wave * WS_RW + r) * WS_LDF) = v;
+            if (zrow && r < nvalid) {
+              f32x4_t t = {v.x, v.y, v.z, v.w};
+              __builtin_nontemporal_store(t, reinterpret_cast<f32x4_t*>(zrow + (int64_t)r * ldz));
+            }
+          }
         };
 #endif
         if (s < hs) {
@@ -672,26 +686,26 @@ __global__ __launch_bounds__(64 * (WS_PROD + WS_CONS)) void graphconv_ws_kernel(
     constexpr int WSTEP = FG_CB * 3 * FG_FRAG;  // bf16 between K16 steps of W
     const int nsteps = S * KS;                   // one tile's K16 steps (the W stream's period)
     // uniform base (SGPRs) + the lane's 16 B: saddr loads
-    const uint16_t* wbase = Wf + (int64_t)(c * 2) * 3 * FG_FRAG;
+    const uint16_t* wbase = Wf + (int64_t)(c * WS_CB) * 3 * FG_FRAG;
     const int loff = lane * 8;
-    auto load_b = [&](bf16x8_t (&bb)[2][3], int gstep) {
+    auto load_b = [&](bf16x8_t (&bb)[WS_CB][3], int gstep) {
       const uint16_t* w = wbase + (int64_t)gstep * WSTEP;
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < WS_CB; ++j)
 #pragma unroll
         for (int q = 0; q < 3; ++q) bb[j][q] = *reinterpret_cast<const bf16x8_t*>(w + (j * 3 + q) * FG_FRAG + loff);
     };
-    f32x16 acc[2][2];  // [row block][column block]
+    f32x16 acc[2][WS_CB];  // [row block][column block]
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < WS_CB; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
     // 12 MFMAs of row block i against both column blocks, gemm_x6_kernel's product order
-    auto mma = [&](int i, const bf16x8_t (&b)[2][3], const bf16x8_t (&a)[3]) {
+    auto mma = [&](int i, const bf16x8_t (&b)[WS_CB][3], const bf16x8_t (&a)[3]) {
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < WS_CB; ++j) {
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2], b[j][0], acc[i][j], 0, 0, 0);
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1], b[j][1], acc[i][j], 0, 0, 0);
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[j][2], acc[i][j], 0, 0, 0);
@@ -725,7 +739,7 @@ __global__ __launch_bounds__(64 * (WS_PROD + WS_CONS)) void graphconv_ws_kernel(
       }
     };
 #endif
-    bf16x8_t bb[2][2][3];
+    bf16x8_t bb[2][WS_CB][3];
     int nxt = 0;  // K16 step (within the tile) of the next W fragments to load
     load_b(bb[0], nxt);
     nxt = nxt + 1 == nsteps ? 0 : nxt + 1;
@@ -791,8 +805,8 @@ __global__ __launch_bounds__(64 * (WS_PROD + WS_CONS)) void graphconv_ws_kernel(
       const int64_t m0 = tile * WS_R;
       const bool epi = bias != nullptr || relu;
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int n = (c * 2 + j) * 32 + l32;
+      for (int j = 0; j < WS_CB; ++j) {
+        const int n = (c * WS_CB + j) * 32 + l32;
         const float bv = (bias && n < C) ? bias[n] : 0.0f;
 #pragma unroll
         for (int i = 0; i < 2; ++i)
@@ -840,7 +854,7 @@ bool graphconv_fused_shape_ok(int F, int C, int L) {
 size_t graphconv_fused_ws_bytes(int64_t K) { return (size_t)K * FG_CB * 32 * 3 * 2 + 256; }
 
 int graphconv_fused_fwd(const GrlTypedCsr* g, const float* X, int64_t ldx, int F, const float* W, const float* bias,
-                        int C, int relu, float* out, const GrlDropEdge* de, void* ws, hipStream_t st) {
+                        int C, int relu, float* out, const GrlDropEdge* de, void* ws, hipStream_t st, float* Z) {
   const int hs = g->has_self ? 1 : 0;
   const int64_t K = (int64_t)(g->num_types + hs) * F;
   uint16_t* Wf = static_cast<uint16_t*>(ws);
@@ -854,7 +868,8 @@ int graphconv_fused_fwd(const GrlTypedCsr* g, const float* X, int64_t ldx, int F
   const DropDev d = to_dev(de);
   const bool v = g->vals != nullptr;
   const char* wse = getenv("GRL_FG_WS");
-  if (!(wse && wse[0] == '0')) {
+  if (!(wse && wse[0] == '0') || Z) {  // Z out: the warp-specialized kernel only
+    const int64_t ldz = K;
     const int64_t ws_tiles = ceil_div(M, WS_R);
     const int64_t grid = std::min<int64_t>(ws_tiles, (int64_t)device_cu_count());
 #define GRL_WS_LAUNCH(KS_)                                                                                           \
@@ -862,11 +877,11 @@ int graphconv_fused_fwd(const GrlTypedCsr* g, const float* X, int64_t ldx, int F
     if (v)                                                                                                           \
       hipLaunchKernelGGL((graphconv_ws_kernel<KS_, true>), dim3((unsigned)grid), dim3(64 * (WS_PROD + WS_CONS)), 0,  \
                          st, M, g->num_types, hs, g->rowptr, g->colidx, g->vals, g->edge_id_base, g->self_id_base, X, \
-                         ldx, Wf, bias, relu, out, C, d, ws_tiles);                                                  \
+                         ldx, Wf, bias, relu, out, C, d, ws_tiles, Z, ldz);                                          \
     else                                                                                                             \
       hipLaunchKernelGGL((graphconv_ws_kernel<KS_, false>), dim3((unsigned)grid), dim3(64 * (WS_PROD + WS_CONS)), 0, \
                          st, M, g->num_types, hs, g->rowptr, g->colidx, g->vals, g->edge_id_base, g->self_id_base, X, \
-                         ldx, Wf, bias, relu, out, C, d, ws_tiles);                                                  \
+                         ldx, Wf, bias, relu, out, C, d, ws_tiles, Z, ldz);                                          \
   } while (0)
     if (F == 256)
       GRL_WS_LAUNCH(16);

@@ -74,7 +74,8 @@ bool graphconv_fused_enabled();
 bool graphconv_fused_shape_ok(int F, int C, int L);
 size_t graphconv_fused_ws_bytes(int64_t K);
 int graphconv_fused_fwd(const GrlTypedCsr* g, const float* X, int64_t ldx, int F, const float* W, const float* bias,
-                        int C, int relu, float* out, const GrlDropEdge* de, void* ws, hipStream_t st);
+                        int C, int relu, float* out, const GrlDropEdge* de, void* ws, hipStream_t st,
+                        float* Z = nullptr);
 
 // Plain-data copy of GrlDropEdge passed by value to kernels.
 struct DropDev {

@@ -1338,6 +1338,32 @@ extern "C" int grl_graphconv_fwd(const GrlTypedCsr* g, const float* X, int64_t l
   return GRL_OK;
 }
 
+extern "C" int grl_graphconv_fwd_train(const GrlTypedCsr* g, const float* X, int64_t ldx, int32_t F, const float* W,
+                                       const float* bias, int32_t C, int32_t relu, float* out, float* Z,
+                                       const GrlDropEdge* de, void* workspace, size_t workspace_bytes,
+                                       grl_stream_t stream) {
+  TraceRange trace_("grl_graphconv_fwd_train");
+  GRL_CHECK_ARG(g != nullptr, "grl_graphconv_fwd_train: graph is NULL");
+  GRL_CHECK_ARG(g->num_rows >= 0 && g->num_types >= 1 && g->num_types <= 63,
+                "grl_graphconv_fwd_train: num_types must be in [1, 63] (got %d)", g->num_types);
+  GRL_CHECK_ARG(F > 0 && ldx >= F && C > 0, "grl_graphconv_fwd_train: need F > 0, ldx >= F, C > 0");
+  const int64_t M = g->num_rows;
+  if (M == 0) return GRL_OK;
+  GRL_CHECK_ARG(X && W && out && Z && g->rowptr && (g->nnz == 0 || g->colidx), "grl_graphconv_fwd_train: NULL pointer");
+  const int hs = g->has_self ? 1 : 0;
+  const int64_t K64 = (int64_t)(g->num_types + hs) * F;
+  GRL_CHECK_ARG(K64 <= 2147483647LL, "grl_graphconv_fwd_train: (has_self + num_types) * F exceeds int32");
+  const int32_t K = (int32_t)K64;
+  char* ws = static_cast<char*>(workspace);
+  GRL_CHECK_ARG(ws == nullptr || al16(ws), "grl_graphconv_fwd_train: workspace must be 16-B aligned");
+  if (fused_path(g, X, ldx, F, W, C) && al16(Z) && ws && workspace_bytes >= graphconv_fused_ws_bytes(K)) {
+    GRL_CHECK_ARG(g->nnz < 2147483647LL, "grl_graphconv_fwd_train: nnz %lld exceeds int32", (long long)g->nnz);
+    return graphconv_fused_fwd(g, X, ldx, F, W, bias, C, relu, out, de, ws, as_stream(stream), Z);
+  }
+  const int rc = grl_typed_spmm_fwd(g, X, ldx, F, Z, de, stream);
+  return rc ? rc : grl_linear_fwd(Z, K, W, bias, out, M, K, C, relu, workspace, workspace_bytes, stream);
+}
+
 extern "C" size_t grl_linear_bwd_data_workspace_size(int64_t M, int32_t K, int32_t C) {
   return M > 0 && K > 0 && C > 0 ? std::max(small_ws_bytes(M, K, C), x6_ws_bytes(M, K, C)) : 0;
 }

@@ -239,9 +239,16 @@ class _GraphConv(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, X: torch.Tensor, graph: TypedGraph, W: torch.Tensor, b, relu: bool, recompute: bool):
-        Z = spmm_forward(X, graph)
         Wc = W.contiguous()
-        out = linear_fwd(Z, Wc, b.contiguous() if b is not None else None, relu)
+        bc = b.contiguous() if b is not None else None
+        if isinstance(graph, EdgeBlockedGraph):
+            Z = spmm_forward(X, graph)
+            out = linear_fwd(Z, Wc, bc, relu)
+        elif recompute:  # Z is not kept: the one-kernel inference form (Z stays on chip)
+            Z = None
+            out = graph_conv_infer(X, graph, Wc, bc, relu)
+        else:  # one kernel that also writes Z where it applies (grl_graphconv_fwd_train)
+            out, Z = graph_conv_fwd_train(X, graph, Wc, bc, relu)
         ctx.graph, ctx.relu, ctx.has_b, ctx.xshape = graph, relu, b is not None, X.shape
         ctx.recompute = recompute
         # recompute: keep X (F wide) instead of Z ((L+1)F wide); the backward
@@ -265,6 +272,36 @@ class _GraphConv(torch.autograd.Function):
         if want_w or want_b:
             dW, db = linear_bwd_weight(Z, g, mask, want_b)
         return dX, None, dW if want_w else None, db, None, None
+
+
+def graph_conv_fwd_train(X: torch.Tensor, graph: TypedGraph, W: torch.Tensor, b=None, relu: bool = False):
+    """(out, Z) of one GraphConv layer through grl_graphconv_fwd_train: the
+    one-kernel path writes Z as a by-product (for the backward's dW); the
+    result is bitwise spmm_forward then linear_fwd."""
+    _require_device(X, "node features")
+    if X.dtype != torch.float32 or W.dtype != torch.float32:
+        raise _lib.GrlError("graph_conv_fwd_train: features and weights must be float32")
+    X2 = _rows_view(X)
+    if X2.shape[0] != graph.num_cols:
+        raise _lib.GrlError(f"features have {X2.shape[0]} rows, graph gathers from {graph.num_cols}")
+    F = X2.shape[1]
+    Wc = W.contiguous()
+    C = Wc.shape[1]
+    K = graph.segments * F
+    if Wc.shape[0] != K:
+        raise _lib.GrlError(f"weights have {Wc.shape[0]} rows, expected {graph.segments} x {F}")
+    bc = b.contiguous() if b is not None else None
+    out = torch.empty(graph.num_rows, C, dtype=torch.float32, device=X.device)
+    Z = torch.empty(graph.num_rows, K, dtype=torch.float32, device=X.device)
+    csr = graph.csr_c(F)
+    ws_bytes = _lib.lib().grl_linear_fwd_workspace_size(graph.num_rows, K, C)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=X.device) if ws_bytes else None
+    de = graph.dropedge.to_c() if graph.dropedge is not None else None
+    call("grl_graphconv_fwd_train", ctypes.byref(csr), X2.data_ptr(), X2.stride(0), F, Wc.data_ptr(),
+         bc.data_ptr() if bc is not None else None, C, int(relu), out.data_ptr(), Z.data_ptr(),
+         ctypes.byref(de) if de is not None else None, ws.data_ptr() if ws is not None else None, ws_bytes,
+         current_stream_handle(X.device))
+    return out, Z
 
 
 def graph_conv_infer(X: torch.Tensor, graph: TypedGraph, W: torch.Tensor, b=None, relu: bool = False,

@@ -272,6 +272,20 @@ size_t grl_graphconv_fwd_workspace_query(const GrlTypedCsr* g, const float* X,
                                          int64_t ldx, int32_t F,
                                          const float* W, int32_t C);
 
+/* Training forward of one GraphConv layer: out as grl_graphconv_fwd AND
+ * Z = A_drop X ([num_rows, (has_self+num_types)*F] contiguous, 16-B aligned),
+ * which the backward needs for dW (grl_linear_bwd_weight).  Where the
+ * one-kernel path applies, Z is written by the gather waves as they finish
+ * rows (its 7.2 GB write at C3 overlaps the MFMAs; the 7.2 GB read-back of
+ * the two-kernel path disappears); elsewhere grl_typed_spmm_fwd then
+ * grl_linear_fwd.  Bitwise the same out and Z either way.  Workspace:
+ * grl_linear_fwd_workspace_size(num_rows, K, C).                         */
+int grl_graphconv_fwd_train(const GrlTypedCsr* g, const float* X, int64_t ldx,
+                            int32_t F, const float* W, const float* bias,
+                            int32_t C, int32_t relu, float* out, float* Z,
+                            const GrlDropEdge* de, void* workspace,
+                            size_t workspace_bytes, grl_stream_t stream);
+
 /* Backward of grl_linear_fwd (autograd MmBackward0 of robust_gcn.py:50, with
  * the ReLU of drop_robust_gcn.py:76 folded in when relu_out != NULL):
  *   dZ = (g * [relu_out > 0]) W^T           grl_linear_bwd_data,  dZ [M, K] (ld lddz)

@@ -200,3 +200,33 @@ def test_fused_graphconv_edge_values_and_oracle():
     o = np.maximum(Z[rows] @ W.astype(np.float64) + b, 0.0)
     scale = np.abs(Z[rows]) @ np.abs(W.astype(np.float64)) + np.abs(b)
     assert np.all(np.abs(out.cpu().numpy()[rows] - o) <= 1e-5 * scale + 1e-6)
+
+
+@pytest.mark.parametrize("de", [None, DropEdge(0.3, 4, 2, True)])
+@pytest.mark.parametrize("recompute", [False, True])
+def test_training_forward_one_kernel_same_bits(de, recompute, monkeypatch):
+    """The training GraphConv (graph_conv with gradients) runs its forward as
+    one kernel that also writes Z for the backward (grl_graphconv_fwd_train),
+    or -- recompute=True -- as the inference kernel; out, Z and every
+    gradient are bitwise those of the two-kernel path (GRL_GRAPHCONV_FUSED=0)."""
+    from grl.ops import graph_conv_fwd_train, spmm_forward
+
+    N, L, F, C = 20_011, 6, 256, 256
+    g = TypedGraph.synthetic(N, 16.0, L, seed=3, device=DEV).with_dropedge(de)
+    gen = torch.Generator(device=DEV).manual_seed(5)
+    X0 = torch.randn(N, F, device=DEV, generator=gen)
+    W0 = torch.randn(7 * F, C, device=DEV, generator=gen) / 40
+    b0 = torch.randn(C, device=DEV, generator=gen)
+    R = torch.randn(N, C, device=DEV, generator=gen)
+    out_f, Z_f = graph_conv_fwd_train(X0, g, W0, b0, True)
+    assert torch.equal(Z_f, spmm_forward(X0, g))
+    res = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("GRL_GRAPHCONV_FUSED", fused)
+        X, W, b = (t.clone().requires_grad_(True) for t in (X0, W0, b0))
+        out = graph_conv(X, g, W, b, relu=True, recompute=recompute)
+        (out * R).sum().backward()
+        res[fused] = (out.detach(), X.grad, W.grad, b.grad)
+    assert torch.equal(res["1"][0], out_f)
+    for a, c in zip(res["1"], res["0"]):
+        assert torch.equal(a, c)
