@@ -444,6 +444,13 @@ constexpr int WS_SPIN = 1 << 24;           // bounded waits (~ seconds)
 #ifndef GRL_WS_ONLY_ROLE
 #define GRL_WS_ONLY_ROLE 0
 #endif
+// GRL_WS_WHATIF (timing diagnostics only, WRONG results): 1 = the MFMA waves
+// load W fragments once per unit instead of per step; 2 = they skip the A
+// split; 3 = the gather waves skip the neighbour rows (own row only); 4 = the
+// MFMA waves only release the slots (the gather alone)
+#ifndef GRL_WS_WHATIF
+#define GRL_WS_WHATIF 0
+#endif
 #if GRL_WS_STAMP
 __device__ unsigned long long g_ws_dbg[1024 * 12 * 2];
 #endif
@@ -628,6 +635,7 @@ __global__ __launch_bounds__(64 * (WS_PROD + WS_CONS)) void graphconv_ws_kernel(
             float w = cur.w;
             if (c0 > 0) fetch(cur, c0, sidx, w);  // rows with more than 64 segment edges together
             uint64_t kept = __ballot(w != 0.0f);
+            if (GRL_WS_WHATIF == 3) kept = 0;
             while (kept) {
               int jj[WS_U];
 #pragma unroll
@@ -722,6 +730,10 @@ __global__ __launch_bounds__(64 * (WS_PROD + WS_CONS)) void graphconv_ws_kernel(
       v1 = *reinterpret_cast<const float4*>(ar + 4);
     };
     auto split_a = [&](const float4& v0, const float4& v1, bf16x8_t (&a)[3]) {
+#if GRL_WS_WHATIF == 2
+      a[0] = a[1] = a[2] = __builtin_bit_cast(bf16x8_t, make_float4(v0.x, v0.y, v1.x, v1.y));
+      return;
+#endif
       uint2 p0, p1, p2, r0, r1, r2;
       split3(v0, p0, p1, p2);
       split3(v1, r0, r1, r2);
@@ -749,6 +761,10 @@ __global__ __launch_bounds__(64 * (WS_PROD + WS_CONS)) void graphconv_ws_kernel(
         const int slot = u % WS_NB, g = u / WS_NB;
         const float* zs = ring + slot * WS_SLOT;
         if (!wait_ge(&produced[slot], WS_PROD * (g + 1), &waited)) return;
+#if GRL_WS_WHATIF == 4
+        if (lane == 0) lds_add_rel(&consumed[slot], 1);
+        continue;
+#endif
 #if GRL_WS_PLANES
 #pragma unroll
         for (int ks = 0; ks < KSU; ++ks) {  // KSU is even: the stage of step ks is ks & 1
@@ -779,7 +795,7 @@ __global__ __launch_bounds__(64 * (WS_PROD + WS_CONS)) void graphconv_ws_kernel(
         }
 #pragma unroll
         for (int ks = 0; ks < KSU; ++ks) {  // KSU is even: the stage of step ks is ks & 1
-          load_b(bb[(ks + 1) & 1], nxt);
+          if (GRL_WS_WHATIF != 1 || ks == 0) load_b(bb[(ks + 1) & 1], nxt);
           nxt = nxt + 1 == nsteps ? 0 : nxt + 1;
           const int st = ks & 1;
           float4 v0, v1;
