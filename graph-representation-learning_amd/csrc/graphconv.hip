@@ -451,6 +451,10 @@ constexpr int WS_SPIN = 1 << 24;           // bounded waits (~ seconds)
 #ifndef GRL_WS_WHATIF
 #define GRL_WS_WHATIF 0
 #endif
+// GRL_WS_PRIO (A/B aid): 1 = MFMA waves issue at s_setprio 2, 2 = gather waves do
+#ifndef GRL_WS_PRIO
+#define GRL_WS_PRIO 0
+#endif
 #if GRL_WS_STAMP
 __device__ unsigned long long g_ws_dbg[1024 * 12 * 2];
 #endif
@@ -519,6 +523,9 @@ __global__ __launch_bounds__(64 * (WS_PROD + WS_CONS)) void graphconv_ws_kernel(
   if (wave < WS_PROD) {
 #endif
     // =========================== gather waves ===========================
+#if GRL_WS_PRIO == 2
+    __builtin_amdgcn_s_setprio(2);
+#endif
     const int col = lane * 4;            // this lane's 4 columns of the row
     const bool col_ok = col < F;
     const int part = col / KC;           // the unit (part of the segment) they belong to
@@ -689,6 +696,9 @@ __global__ __launch_bounds__(64 * (WS_PROD + WS_CONS)) void graphconv_ws_kernel(
     return;
 #endif
     // =========================== MFMA waves ===========================
+#if GRL_WS_PRIO == 1
+    __builtin_amdgcn_s_setprio(2);
+#endif
     const int c = wave - WS_PROD;
     const int l32 = lane & 31, h = lane >> 5;
     constexpr int WSTEP = FG_CB * 3 * FG_FRAG;  // bf16 between K16 steps of W

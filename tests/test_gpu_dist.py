@@ -184,3 +184,51 @@ def test_bench_two_ranks_weak_and_c5_shape():
     out = _bench_two_ranks(["--workload", "C5", "--nodes-per-gpu", "65536", "--chunks", "4"])
     assert out["config"]["graph"] == "rmat" and out["config"]["d"] == 512 and out["config"]["dropedge_p"] == 0.2
     assert out["config"]["nodes_total"] == 131072 and out["halo"]["chunks"] == 4
+
+
+def _fused_shard_worker(rank, world, port, mode):
+    """One rank of a 2-rank gloo world: the one-kernel GraphConv on this
+    rank's shard (local rows + halo slots, shard-offset DropEdge ids) equals
+    the one-GPU graph's rows, bitwise, and the two-kernel path on the shard."""
+    import os
+
+    import torch.distributed as dist
+
+    from grl.ops import graph_conv_infer
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        N, deg, L, F, C = 40_000, 16.0, 6, 256, 256  # shards of 20k rows: the x6 (hence fused) shape
+        sg = ShardedGraph.synthetic(N, deg, L, kind="er", seed=6, device=DEV, halo=mode)
+        g = TypedGraph.synthetic(N, deg, L, kind="er", seed=6, device=DEV)
+        rb, re = sg.plan.row_begin, sg.plan.row_end
+        gen = torch.Generator().manual_seed(31)
+        X = torch.randn(N, F, generator=gen).to(DEV)
+        W = (torch.randn(7 * F, C, generator=gen) / 40).to(DEV)
+        b = torch.randn(C, generator=gen).to(DEV)
+        de = DropEdge(0.3, 8, 1, True)
+        p = sg.plan
+        X_ext = torch.zeros(p.n_loc + p.n_halo, F, device=DEV)
+        X_ext[: p.n_loc] = X[rb:re]
+        send = torch.empty(p.send_index.numel(), F, device=DEV)
+        halo_exchange_into(X_ext[: p.n_loc], X_ext, send, p)
+        local = sg.graph.with_dropedge(de)
+        full = graph_conv_infer(X, g.with_dropedge(de), W, b, True)
+        out = graph_conv_infer(X_ext, local, W, b, True)
+        assert torch.equal(out, full[rb:re])
+        os.environ["GRL_GRAPHCONV_FUSED"] = "0"
+        try:
+            assert torch.equal(graph_conv_infer(X_ext, local, W, b, True), out)
+        finally:
+            del os.environ["GRL_GRAPHCONV_FUSED"]
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["sparse", "dense"])
+def test_two_ranks_fused_graphconv_on_shards(mode):
+    import torch.multiprocessing as mp
+
+    mp.spawn(_fused_shard_worker, args=(2, _free_port(), mode), nprocs=2, join=True)
