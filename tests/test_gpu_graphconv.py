@@ -139,10 +139,13 @@ def _ws_query(X, g, W, C):
 
 
 # sizes just above the x6 GEMM's 1.6e10-flop threshold (below it the linear,
-# hence the two-kernel reference, is the fp32-MFMA kernel and no fusion runs)
+# hence the two-kernel reference, is the fp32-MFMA kernel and no fusion runs);
+# avg_deg 120 puts ~160 edges in a gather wave's segment list (more than one
+# 64-entry fetch), L = 7 fills the wave's rowptr window (8 rows x 7 + 1)
 @pytest.mark.parametrize("N,L,F,C,has_self,deg", [(20_011, 6, 256, 256, True, 16.0), (50_000, 6, 256, 96, True, 9.0),
                                                   (40_007, 6, 128, 256, True, 16.0), (70_001, 6, 64, 256, True, 12.0),
-                                                  (60_001, 3, 256, 200, False, 20.0)])
+                                                  (60_001, 3, 256, 200, False, 20.0), (20_000, 6, 256, 256, True, 120.0),
+                                                  (18_001, 7, 256, 256, True, 14.0)])
 @pytest.mark.parametrize("variant", ["plain", "drop_bias_relu", "drop_spare_self", "strided_relu"])
 @pytest.mark.parametrize("kernel", ["ws", "phases"])
 def test_fused_graphconv_bitwise_equals_two_kernels(N, L, F, C, has_self, deg, variant, kernel, monkeypatch):
@@ -166,6 +169,8 @@ def test_fused_graphconv_bitwise_equals_two_kernels(N, L, F, C, has_self, deg, v
     K = (L + (1 if has_self else 0)) * F
     W = torch.randn(K, C, device=DEV, generator=gen) / K ** 0.5
     b = torch.randn(C, device=DEV, generator=gen) if bias else None
+    if deg > 64:  # no heavy-row split plan on this graph: the fused path applies
+        assert g.split_stats()["csr"]["heavy_segments"] == 0
     ws = _ws_query(X, g, W, C)
     assert ws < 3 * 256 * K * 2 + 4096 < N * K * 4, ws  # W planes only: the fused path
     out = graph_conv_infer(X, g, W, b, relu)
