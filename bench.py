@@ -320,10 +320,47 @@ def halo_breakdown(args, pipe, X_loc, Z, de, g_step, dev, iters=None):
     plan = pipe.plan
     world = len(plan.bounds) - 1
     rows_in = (world - 1) * plan.stride if plan.mode == "dense" else sum(plan.recv_counts)
-    return {"mode": plan.mode, "chunks": pipe.K, "exchange_only_ms": ex, "spmm_only_ms": ag,
-            "serial_sum_ms": ex + ag, "rows_received_rank0": rows_in,
-            "GB_received_rank0": rows_in * pipe.F * 4 / 1e9,
-            "GBps_received_rank0": rows_in * pipe.F * 4 / 1e9 / (ex * 1e-3) if ex > 0 else None}
+    out = {"mode": plan.mode, "chunks": pipe.K, "exchange_only_ms": ex, "spmm_only_ms": ag,
+           "serial_sum_ms": ex + ag, "rows_received_rank0": rows_in,
+           "GB_received_rank0": rows_in * pipe.F * 4 / 1e9,
+           "GBps_received_rank0": rows_in * pipe.F * 4 / 1e9 / (ex * 1e-3) if ex > 0 else None}
+    try:
+        out["backward"] = halo_backward_breakdown(pipe, g, dev, iters)
+    except Exception as err:  # reported, never hidden; the forward line stands on its own
+        out["backward"] = {"error": repr(err)[:300]}
+    return out
+
+
+def halo_backward_breakdown(pipe, g, dev, iters):
+    """The training-mode counterpart (not the headline): dX of the shard with
+    the reverse exchange pipelined with the column-slice gathers
+    (HaloPipeline.backward), next to its parts -- the slice gathers alone and
+    the reverse exchanges alone (CSC built once per graph, outside)."""
+    from grl.ops import spmm_backward_slice
+
+    F, K = pipe.F, pipe.K
+    g.csc()
+    dZ = torch.randn(pipe.plan.n_loc, g.segments * F, generator=torch.Generator(device=dev).manual_seed(5),
+                     device=dev)
+    gt, _ = pipe._grad_buffers(dev)
+    dX = pipe.backward(dZ, g.dropedge)  # warm: buffers, split plans
+    pipelined = _time(lambda: pipe.backward(dZ, g.dropedge), iters)
+
+    def gathers():
+        for c in range(K):
+            spmm_backward_slice(dZ, g, c * pipe.Fc, gt[c])
+
+    def exchanges():
+        for c in range(K):
+            w = pipe._exchange_back(c, async_op=pipe.side is not None)
+            if w is not None:
+                w.wait()
+
+    ga, ex = _time(gathers, iters), _time(exchanges, iters)
+    del dX, dZ
+    return {"pipelined_ms": pipelined, "gather_only_ms": ga, "exchange_only_ms": ex, "serial_sum_ms": ga + ex,
+            "note": "dX = A_drop^T dZ of the shard: grl_typed_spmm_bwd_slice per column slice, reverse halo "
+                    "all-to-all per slice in flight under the next gather, peer-order combine"}
 
 
 def dropedge_train(graph, X, E, iters):

@@ -142,7 +142,8 @@ __global__ __launch_bounds__(256) void spmm_kernel(
     int64_t self_row0,  // fwd: X row of item row 0's self term (row-range launches)
     const float* __restrict__ src, int64_t lds,  // gathered matrix + row stride
     int F, float* __restrict__ out, int64_t ldo,
-    int zseg,  // fwd: floats between output segments (F, or the full width for a column slice)
+    int zseg,  // fwd: floats between output segments (F, or the full width for a column slice);
+               // bwd: dZ segment width (F, or the full width for a column slice)
     DropDev de, SplitDev sp) {
   using vec_t = typename VecT<VEC>::type;
   de = resolve_key(de);
@@ -156,7 +157,7 @@ __global__ __launch_bounds__(256) void spmm_kernel(
     cval[k] = coff[k] < F;
   }
   const int nseg_row = BWD ? 1 : S;
-  const int64_t zstride = (int64_t)(S + hs) * F;  // dZ row stride (bwd self term)
+  const int64_t zstride = (int64_t)(S + hs) * (BWD ? zseg : F);  // bwd self term: dZ row stride
 
   const int64_t wave0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + uniform_i(threadIdx.x >> 6);
   const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
@@ -429,7 +430,7 @@ __global__ __launch_bounds__(256) void spmm_fixup_kernel(
   de = resolve_key(de);
   const int lane = threadIdx.x & 63;
   const int cbase = blockIdx.y * (64 * VEC * NV);
-  const int64_t zstride = (int64_t)(S + hs) * F;
+  const int64_t zstride = (int64_t)(S + hs) * zseg;  // bwd: dZ row stride
   const int64_t wave0 = (int64_t)blockIdx.x * (blockDim.x >> 6) + uniform_i(threadIdx.x >> 6);
   const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
   for (int64_t h = wave0; h < num_heavy; h += nwaves) {
@@ -788,31 +789,42 @@ extern "C" int grl_typed_spmm_fwd_slice(const GrlTypedCsr* g, const float* X, in
                             as_stream(stream), Z, self_col0, -1, zseg);
 }
 
-static int spmm_bwd_entry(const char* who, const GrlTypedCsc* g, const float* dZ, int32_t F, float* dX,
-                          int64_t lddx, const GrlDropEdge* de, grl_stream_t stream, bool accum) {
+// dX columns [0, F) = columns [col0, col0 + F) of A_drop^T dZ, dZ segments
+// F_total wide (F_total = F, col0 = 0: the whole gradient).
+static int spmm_bwd_entry(const char* who, const GrlTypedCsc* g, const float* dZ, int32_t F_total, int32_t col0,
+                          int32_t F, float* dX, int64_t lddx, const GrlDropEdge* de, grl_stream_t stream, bool accum) {
   GRL_CHECK_ARG(g != nullptr, "%s: graph is NULL", who);
   GRL_CHECK_ARG(g->num_rows >= 0 && g->self_rows >= 0 && g->self_rows <= g->num_rows, "%s: bad num_rows/self_rows",
                 who);
   GRL_CHECK_ARG(g->num_types >= 1 && g->num_types <= 63, "%s: num_types must be in [1, 63]", who);
   GRL_CHECK_ARG(F > 0 && lddx >= F, "%s: need F > 0 and lddx >= F", who);
+  GRL_CHECK_ARG(col0 >= 0 && (int64_t)col0 + F <= F_total, "%s: columns [%d, %d) outside the %d-column segments",
+                who, col0, col0 + F, F_total);
   if (g->num_rows == 0) return GRL_OK;
   GRL_CHECK_ARG(dZ && dX && g->colptr && (g->nnz == 0 || (g->zrow && g->eid)), "%s: NULL pointer", who);
   const int hs = g->has_self ? 1 : 0;
   return launch_spmm<true>(g->num_rows, g->self_rows, g->num_types, hs, g->colptr, g->zrow, g->eid, g->vals,
-                           g->edge_id_base, g->self_id_base, dZ, (int64_t)F, F, dX, lddx, to_dev(de), g->split,
-                           as_stream(stream), dX, 0, -1, 0, accum);
+                           g->edge_id_base, g->self_id_base, dZ + col0, (int64_t)F_total, F, dX, lddx, to_dev(de),
+                           g->split, as_stream(stream), dX, 0, -1, F_total, accum);
 }
 
 extern "C" int grl_typed_spmm_bwd_accum(const GrlTypedCsc* g, const float* dZ, int32_t F, float* dX, int64_t lddx,
                                         const GrlDropEdge* de, grl_stream_t stream) {
   TraceRange trace_("grl_typed_spmm_bwd_accum");
-  return spmm_bwd_entry("grl_typed_spmm_bwd_accum", g, dZ, F, dX, lddx, de, stream, true);
+  return spmm_bwd_entry("grl_typed_spmm_bwd_accum", g, dZ, F, 0, F, dX, lddx, de, stream, true);
 }
 
 extern "C" int grl_typed_spmm_bwd(const GrlTypedCsc* g, const float* dZ, int32_t F, float* dX, int64_t lddx,
                                   const GrlDropEdge* de, grl_stream_t stream) {
   TraceRange trace_("grl_typed_spmm_bwd");
-  return spmm_bwd_entry("grl_typed_spmm_bwd", g, dZ, F, dX, lddx, de, stream, false);
+  return spmm_bwd_entry("grl_typed_spmm_bwd", g, dZ, F, 0, F, dX, lddx, de, stream, false);
+}
+
+extern "C" int grl_typed_spmm_bwd_slice(const GrlTypedCsc* g, const float* dZ, int32_t F_total, int32_t col0,
+                                        int32_t F, float* dX, int64_t lddx, const GrlDropEdge* de,
+                                        grl_stream_t stream) {
+  TraceRange trace_("grl_typed_spmm_bwd_slice");
+  return spmm_bwd_entry("grl_typed_spmm_bwd_slice", g, dZ, F_total, col0, F, dX, lddx, de, stream, false);
 }
 
 extern "C" size_t grl_split_plan_workspace_size(int64_t rows) {

@@ -134,6 +134,8 @@ SIGNATURES = {
                                           _P(GrlDropEdge), _c_vp]),
     "grl_typed_spmm_bwd": (_c_i32, [_P(GrlTypedCsc), _c_vp, _c_i32, _c_vp, _c_i64, _P(GrlDropEdge), _c_vp]),
     "grl_typed_spmm_bwd_accum": (_c_i32, [_P(GrlTypedCsc), _c_vp, _c_i32, _c_vp, _c_i64, _P(GrlDropEdge), _c_vp]),
+    "grl_typed_spmm_bwd_slice": (_c_i32, [_P(GrlTypedCsc), _c_vp, _c_i32, _c_i32, _c_i32, _c_vp, _c_i64,
+                                          _P(GrlDropEdge), _c_vp]),
     "grl_graphconv_fwd_workspace_size": (_c_size, [_c_i64, _c_i32, _c_i32, _c_i32, _c_i32]),
     "grl_graphconv_fwd_workspace_query": (_c_size, [_P(GrlTypedCsr), _c_vp, _c_i64, _c_i32, _c_vp, _c_i32]),
     "grl_graphconv_fwd_train": (_c_i32, [_P(GrlTypedCsr), _c_vp, _c_i64, _c_i32, _c_vp, _c_vp, _c_i32, _c_i32, _c_vp,

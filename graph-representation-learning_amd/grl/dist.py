@@ -332,6 +332,110 @@ class HaloPipeline:
         main.wait_stream(self.side)  # buffers are reused by the next call
         return Z
 
+    # ------------------------------------------------------------- backward
+    def _grad_buffers(self, device):
+        """Slice tables of dX_ext ([chunks, rows, Fc], the forward tables'
+        shape) and the receive buffers of the reverse exchange (dense: every
+        peer's gradient of my rows, world * stride rows; sparse: the rows I
+        sent, sum(send_counts)); allocated on first use, then reused."""
+        if getattr(self, "gtables", None) is None:
+            p = self.plan
+            self.gtables = torch.empty_like(self.tables, device=device)
+            back_rows = self.world * p.stride if p.mode == "dense" else sum(p.send_counts)
+            self.gback = torch.empty(self.K, back_rows, self.Fc, device=device)
+        return self.gtables, self.gback
+
+    def _exchange_back(self, c: int, async_op: bool):
+        """Send slice c's halo-row gradients to their owners (the reverse of
+        the forward exchange); returns a work handle when async_op."""
+        if self.world == 1:
+            return None
+        p, g, back = self.plan, self.gtables[c], self.gback[c]
+        with trace(f"grl.halo_back_slice{c}"):
+            if p.mode == "dense":
+                splits = [p.stride] * self.world
+                if not async_op:
+                    all_to_all_v(back, g[p.stride:], splits, splits, self.group)
+                    return None
+                return dist.all_to_all_single(back, g[p.stride:], splits, splits, group=self.group, async_op=True)
+            if not async_op:
+                all_to_all_v(back, g[p.n_loc:], p.send_counts, p.recv_counts, self.group)
+                return None
+            return dist.all_to_all_single(back, g[p.n_loc:], p.send_counts, p.recv_counts, group=self.group,
+                                          async_op=True)
+
+    def _combine(self, c: int, dX_loc: torch.Tensor) -> None:
+        """dX_loc's columns of slice c = my own rows' gradient + every peer's
+        partial for them, in peer order (_HaloExchange.backward's order, so
+        the same bits)."""
+        p, g, back = self.plan, self.gtables[c], self.gback[c]
+        out = dX_loc[:, c * self.Fc:(c + 1) * self.Fc]
+        out.copy_(g[:p.n_loc])
+        if self.world == 1:
+            return
+        if p.mode == "dense":
+            st = p.stride
+            for q in range(self.world):
+                if q != p.rank:
+                    out += back[q * st: q * st + p.n_loc]
+            return
+        off = 0
+        for cnt in p.send_counts:  # indices unique within a peer -> deterministic
+            if cnt:
+                out.index_add_(0, p.send_index[off:off + cnt], back[off:off + cnt])
+            off += cnt
+
+    def backward(self, dZ: torch.Tensor, dropedge: Optional[DropEdge] = None, backward_slice=None) -> torch.Tensor:
+        """dX_loc = the shard's share of A_drop^T dZ, with the reverse halo
+        exchange overlapped with the gather: slice c's halo-row gradients
+        travel home (RCCL all-to-all, async on the collective's own stream)
+        while the compute stream gathers slice c+1 with
+        grl_typed_spmm_bwd_slice; the owner then adds the peers' partials in
+        peer order.  Per element the same operations as the unsliced
+        exchange + spmm_backward: bitwise equal to it.
+        backward_slice(dZ, graph, col0, out) replaces the HIP slice gather
+        (CPU tests only)."""
+        from .ops import spmm_backward_slice
+
+        gather = backward_slice or spmm_backward_slice
+        graph = self.sg.graph.with_dropedge(dropedge)
+        dZ = dZ.contiguous()
+        gt, _ = self._grad_buffers(dZ.device)
+        dX_loc = torch.empty(self.plan.n_loc, self.F, dtype=dZ.dtype, device=dZ.device)
+        if self.side is None:  # host-staged (gloo) or single rank: in order, no overlap
+            for c in range(self.K):
+                gather(dZ, graph, c * self.Fc, gt[c])
+                self._exchange_back(c, async_op=False)
+                self._combine(c, dX_loc)
+            return dX_loc
+        works = []
+        for c in range(self.K):
+            gather(dZ, graph, c * self.Fc, gt[c])
+            works.append(self._exchange_back(c, async_op=True))  # waits for slice c's gather only
+        for c in range(self.K):
+            if works[c] is not None:
+                works[c].wait()  # the compute stream waits for slice c's exchange only
+            self._combine(c, dX_loc)
+        return dX_loc
+
+
+class _PipelinedAggregate(torch.autograd.Function):
+    """Z = A_drop X_ext of a shard with both halo exchanges pipelined over
+    column slices (HaloPipeline.run forward, HaloPipeline.backward)."""
+
+    @staticmethod
+    def forward(ctx, X_loc: torch.Tensor, pipe: "HaloPipeline", dropedge):
+        with trace("grl.halo_pipeline_fwd"):
+            Z = X_loc.new_empty(pipe.plan.n_loc, pipe.sg.graph.segments * pipe.F)
+            pipe.run(X_loc.detach().contiguous(), Z, dropedge)
+        ctx.pipe, ctx.dropedge = pipe, dropedge
+        return Z
+
+    @staticmethod
+    def backward(ctx, dZ: torch.Tensor):
+        with trace("grl.halo_pipeline_bwd"):
+            return ctx.pipe.backward(dZ, ctx.dropedge), None, None
+
 
 def broadcast_module(module: torch.nn.Module, src: int = 0, group=None) -> None:
     """Copy `src`'s parameters and buffers to every rank (replica start)."""
@@ -463,15 +567,31 @@ class ShardedGraph:
     def exchange(self, X_loc: torch.Tensor) -> torch.Tensor:
         return halo_exchange(X_loc, self.plan, self.group)
 
-    def aggregate(self, X_loc: torch.Tensor, dropedge: Optional[DropEdge] = None) -> torch.Tensor:
-        """Z rows of this shard: halo exchange + typed SpMM (autograd through both)."""
-        return typed_aggregate(self.exchange(X_loc), self.graph.with_dropedge(dropedge))
+    def pipeline(self, F: int, chunks: int) -> HaloPipeline:
+        """The HaloPipeline of this shard for F-wide features in `chunks`
+        column slices (built once, buffers reused by every call)."""
+        cache = self.__dict__.setdefault("_pipelines", {})
+        key = (F, chunks)
+        if key not in cache:
+            cache[key] = HaloPipeline(self, F, chunks=chunks, device=self.graph.device)
+        return cache[key]
+
+    def aggregate(self, X_loc: torch.Tensor, dropedge: Optional[DropEdge] = None,
+                  chunks: Optional[int] = None) -> torch.Tensor:
+        """Z rows of this shard: halo exchange + typed SpMM (autograd through
+        both).  chunks=k pipelines both exchanges with the gathers over k
+        column slices (forward HaloPipeline.run, backward
+        HaloPipeline.backward); same bits as chunks=None."""
+        if chunks is None:
+            return typed_aggregate(self.exchange(X_loc), self.graph.with_dropedge(dropedge))
+        return _PipelinedAggregate.apply(X_loc, self.pipeline(X_loc.shape[1], chunks), dropedge)
 
     def graphconv(self, X_loc: torch.Tensor, layer, dropedge: Optional[DropEdge] = None,
-                  relu: bool = False) -> torch.Tensor:
+                  relu: bool = False, chunks: Optional[int] = None) -> torch.Tensor:
         """One GraphConv (gnn.models.GraphConv or anything with h_weights /
         bias) over this shard: halo exchange -> typed SpMM -> MFMA linear
         (+ fused ReLU).  Output rows = this rank's nodes.  After backward,
-        call allreduce_gradients(layer.parameters()) to complete dW / db."""
-        Z = self.aggregate(X_loc, dropedge)
+        call allreduce_gradients(layer.parameters()) to complete dW / db.
+        chunks: see aggregate."""
+        Z = self.aggregate(X_loc, dropedge, chunks)
         return graph_linear(Z, layer.h_weights, layer.bias, relu=relu)

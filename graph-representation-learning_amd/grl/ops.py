@@ -129,6 +129,30 @@ def spmm_backward(dZ: torch.Tensor, graph: TypedGraph, F: int) -> torch.Tensor:
     return dX
 
 
+def spmm_backward_slice(dZ: torch.Tensor, graph: TypedGraph, col0: int, out: torch.Tensor) -> torch.Tensor:
+    """Columns [col0, col0 + F) of dX = A_drop^T dZ into `out` ([graph.num_cols,
+    F] float32, unit column stride, any row stride), dZ contiguous
+    [num_rows, segments * F_total] (grl_typed_spmm_bwd_slice).  Bitwise equal,
+    per element, to spmm_backward: the pipelined backward of grl.dist sends
+    one slice's halo-row gradients home while the next slice gathers."""
+    if isinstance(graph, EdgeBlockedGraph):
+        raise _lib.GrlError("column-slice backward takes a TypedGraph (edge-blocked graphs: spmm_backward)")
+    _require_device(dZ, "dZ")
+    if dZ.dtype != torch.float32 or not dZ.is_contiguous() or dZ.dim() != 2 or dZ.shape[0] != graph.num_rows \
+            or dZ.shape[1] % graph.segments:
+        raise _lib.GrlError(f"dZ must be a contiguous float32 [{graph.num_rows}, {graph.segments} x F_total] tensor")
+    F_total = dZ.shape[1] // graph.segments
+    if out.dtype != torch.float32 or out.dim() != 2 or out.stride(1) != 1 or out.shape[0] != graph.num_cols \
+            or out.device != dZ.device:
+        raise _lib.GrlError(f"out must be a float32 [{graph.num_cols}, F] tensor with unit column stride")
+    F = out.shape[1]
+    csc = graph.csc_c(F)
+    de = graph.dropedge.to_c() if graph.dropedge is not None else None
+    call("grl_typed_spmm_bwd_slice", ctypes.byref(csc), dZ.data_ptr(), F_total, int(col0), F, out.data_ptr(),
+         out.stride(0), ctypes.byref(de) if de is not None else None, current_stream_handle(dZ.device))
+    return out
+
+
 class _TypedAggregate(torch.autograd.Function):
     @staticmethod
     def forward(ctx, X: torch.Tensor, graph: TypedGraph) -> torch.Tensor:

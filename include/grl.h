@@ -218,6 +218,19 @@ int grl_typed_spmm_bwd_accum(const GrlTypedCsc* g, const float* dZ, int32_t F,
                              float* dX, int64_t lddx, const GrlDropEdge* de,
                              grl_stream_t stream);
 
+/* Columns [col0, col0 + F) of dX = A_drop^T dZ into dX (row stride lddx,
+ * num_rows rows of F floats, fully overwritten), dZ contiguous
+ * [*, (has_self+num_types)*F_total].  Per element bitwise equal to
+ * grl_typed_spmm_bwd (same edges, same order): the multi-GPU backward
+ * (grl.dist.HaloPipeline.backward) gathers one column slice of the halo-row
+ * gradients while the previous slice travels back to its owners -- the
+ * reverse of the forward halo exchange that replaces the dense
+ * BmmBackward0 of robust_gcn.py:45 on a node-range shard.               */
+int grl_typed_spmm_bwd_slice(const GrlTypedCsc* g, const float* dZ,
+                             int32_t F_total, int32_t col0, int32_t F,
+                             float* dX, int64_t lddx, const GrlDropEdge* de,
+                             grl_stream_t stream);
+
 /* out = Z W + bias (optionally ReLU), fp32-accurate on the matrix cores.
  * Replaces torch.matmul(new_V, self.h_weights) + self.bias
  * (robust_gcn.py:50) and, with relu = 1, the F.relu around the layer

@@ -86,7 +86,7 @@ def _worker(rank, world, port, bounds, mode):
         np.testing.assert_array_equal(Z.detach().numpy(), Zref[rb:re])  # bitwise: same rows, same edge order
         Z.backward(torch.from_numpy(dZ[rb:re].copy()))
         np.testing.assert_allclose(X_loc.grad.numpy(), dXref[rb:re], rtol=0, atol=1e-5)
-        _check_pipeline(plan, lr, X[rb:re], Zref[rb:re], rb, d)
+        _check_pipeline(plan, lr, X[rb:re], Zref[rb:re], rb, d, dZ[rb:re], X_loc.grad)
     finally:
         dist.destroy_process_group()
 
@@ -102,9 +102,11 @@ class _HostGraph:
         return self
 
 
-def _check_pipeline(plan, lr, X_loc, Zref, rb, d):
+def _check_pipeline(plan, lr, X_loc, Zref, rb, d, dZ_loc, dX_sharded):
     """grl.dist.HaloPipeline's slice tables and exchanges (product code),
-    each slice aggregated by the oracle: Z bitwise equal to one process."""
+    each slice aggregated by the oracle: Z bitwise equal to one process; the
+    pipelined backward (slice gathers + reverse exchanges + peer-order
+    combine) bitwise equal to the unsliced sharded backward."""
     import types
 
     from grl.dist import HaloPipeline
@@ -123,6 +125,20 @@ def _check_pipeline(plan, lr, X_loc, Zref, rb, d):
 
         pipe.run(torch.from_numpy(X_loc.copy()), Z, None, aggregate_slice=agg)
         np.testing.assert_array_equal(Z.numpy(), Zref)
+
+        ncols = plan.n_loc + plan.n_halo
+        colptr, zrow, eid, _ = c_oracle.csr_to_csc(lr, plan.colidx_local.numpy(), L, ncols, True)
+
+        def bwd(dZ, graph, col0, out):
+            Fc = out.shape[1]
+            dZc = np.ascontiguousarray(dZ.numpy().reshape(n, L + 1, F)[:, :, col0:col0 + Fc]).reshape(n, (L + 1) * Fc)
+            out.copy_(torch.from_numpy(c_oracle.spmm_bwd(colptr, zrow, eid, dZc, L, Fc, n, True, d=d,
+                                                         edge_base=plan.edge_id_base,
+                                                         self_base=plan.num_edges_total + rb)))
+
+        for _ in range(2):  # the second call reuses the gradient buffers
+            dX = pipe.backward(torch.from_numpy(dZ_loc.copy()), None, backward_slice=bwd)
+            np.testing.assert_array_equal(dX.numpy(), dX_sharded.numpy())
 
 
 @pytest.mark.parametrize("mode", ["auto", "sparse", "dense"])

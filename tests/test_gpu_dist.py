@@ -58,6 +58,32 @@ def test_column_slices_equal_whole_aggregation(kind, F, slices):
     assert torch.equal(Zs, Zw)
 
 
+@pytest.mark.parametrize("kind,F,slices", [("er", 256, (128, 128)), ("er", 256, (64, 64, 128)),
+                                           ("rmat", 512, (128, 256, 128)), ("er", 100, (52, 48))])
+def test_column_slices_backward_equal_whole(kind, F, slices):
+    """grl_typed_spmm_bwd_slice: each column slice of dX (into its own table,
+    and into a strided, unaligned view) bitwise equal to the whole-width
+    backward -- DropEdge on, R-MAT hub columns split."""
+    from grl.ops import spmm_backward, spmm_backward_slice
+
+    N = 1 << 13
+    g = TypedGraph.synthetic(N, 48.0, 6, kind=kind, seed=8, device=DEV)
+    g.split_threshold, g.split_chunk = 256, 128  # force the hub-chunk path at this size
+    gd = g.with_dropedge(DropEdge(0.3, 4, 2))
+    dZ = torch.randn(N, 7 * F, device=DEV)
+    dXw = spmm_backward(dZ, gd, F)
+    c0 = 0
+    for w in slices:
+        table = torch.full((N, w), float("nan"), device=DEV)
+        spmm_backward_slice(dZ, gd, c0, table)
+        assert torch.equal(table, dXw[:, c0:c0 + w]), (c0, w)
+        buf = torch.full((N, w + 5), float("nan"), device=DEV)
+        spmm_backward_slice(dZ, gd, c0, buf[:, 3:3 + w])  # row stride w + 5, 12-B offset: scalar path
+        assert torch.equal(buf[:, 3:3 + w], dXw[:, c0:c0 + w]), (c0, w)
+        c0 += w
+    assert c0 == F
+
+
 def _free_port():
     import socket
 
@@ -116,6 +142,14 @@ def _shard_worker(rank, world, port, mode, kind):
             pipe.run(X[rb:re].contiguous(), outp, de)
             torch.cuda.synchronize()
             assert torch.equal(outp, Zg[rb:re].detach()), K
+        # both exchanges pipelined with the gathers (autograd): same Z, and dX bitwise equal to the
+        # unsliced sharded backward (the same partials, added in the same peer order)
+        for K in (1, 2, 4):
+            X_p = X[rb:re].clone().requires_grad_(True)
+            Zp = sg.aggregate(X_p, de, chunks=K)
+            assert torch.equal(Zp, Zg[rb:re].detach()), K
+            Zp.backward(dZ[rb:re])
+            assert torch.equal(X_p.grad, X_loc.grad), K
         # a whole sharded GraphConv layer: weight grads summed over ranks equal one GPU's
         from gnn.models import GraphConv
         from grl.dist import allreduce_gradients
@@ -131,6 +165,15 @@ def _shard_worker(rank, world, port, mode, kind):
         allreduce_gradients(layer.parameters())
         torch.testing.assert_close(layer.h_weights.grad, layer1.h_weights.grad, rtol=1e-4, atol=1e-4)
         torch.testing.assert_close(layer.bias.grad, layer1.bias.grad, rtol=1e-4, atol=1e-4)
+        # the same layer with the pipelined exchanges: bitwise the unpipelined layer's grads
+        grads = [t.grad.clone() for t in (layer.h_weights, layer.bias)]
+        layer.zero_grad()
+        X_a, X_b = X[rb:re].clone().requires_grad_(True), X[rb:re].clone().requires_grad_(True)
+        (sg.graphconv(X_a, layer, de, relu=True, chunks=2) * R[rb:re]).sum().backward()
+        allreduce_gradients(layer.parameters())
+        assert all(torch.equal(t.grad, g0) for t, g0 in zip((layer.h_weights, layer.bias), grads))
+        (sg.graphconv(X_b, layer, de, relu=True) * R[rb:re]).sum().backward()
+        assert torch.equal(X_a.grad, X_b.grad)
     finally:
         dist.destroy_process_group()
 
