@@ -296,17 +296,20 @@ __global__ __launch_bounds__(256) void spmm_kernel(
 // v_permlane32_swap hands edge j+1's row to lanes 0-31, which accumulate the
 // two in CSR order (fmaf chain identical to spmm_kernel: bitwise equal).
 // Lanes 32-63 only fetch; stores and the self term are lanes 0-31's.
+// BWD: the same over CSC columns (one segment, self term = dZ's own row
+// first, edge ids from eid): the column slices of the pipelined backward.
 __device__ __forceinline__ float swap_halves(float x) {
   return __uint_as_float(__builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false)[1]);
 }
 
-template <int U, bool VALS>
+template <int U, bool VALS, bool BWD = false>
 __global__ __launch_bounds__(256) void spmm_pair_kernel(
     int64_t num_rows, int S, int hs, const int32_t* __restrict__ ptr, const int32_t* __restrict__ idx,
     const float* __restrict__ vals, uint64_t edge_base, uint64_t self_base, int64_t self_row0,
     const float* __restrict__ src, int64_t lds, int F, float* __restrict__ out, int64_t ldo, int zseg, DropDev de,
-    SplitDev sp) {
+    SplitDev sp, const int32_t* __restrict__ eidv, int64_t self_rows) {
   de = resolve_key(de);
+  const int nseg_row = BWD ? 1 : S;
   const int lane = threadIdx.x & 63;
   const int half = lane >> 5;
   const int coff = (lane & 31) * 4;
@@ -329,23 +332,27 @@ __global__ __launch_bounds__(256) void spmm_pair_kernel(
     } else {
       const int64_t n = item - sp.num_chunks;
       float* orow = out + n * ldo;
-      pv = lane <= S ? ptr[n * S + lane] : 0;
-      nseg = S;
+      pv = lane <= nseg_row ? ptr[n * nseg_row + lane] : 0;
+      nseg = nseg_row;
       const bool heavy = readlane_i(pv, nseg) - readlane_i(pv, 0) > sp.threshold;
-      if (hs) {
+      if (hs && (!BWD || (n < self_rows && !heavy))) {
         float w = 1.0f;
         if (de.active && de.drop_self) w = dropedge_weight(de, 1.0f, self_base + (uint64_t)n);
         if (own) {
           float4 x;
+          const float* srow = BWD ? src + n * ((int64_t)(S + hs) * zseg) : src + (n + self_row0) * lds;
           if (w != 0.0f)
-            x = vmul(w, *reinterpret_cast<const float4*>(src + (n + self_row0) * lds + coff));
+            x = vmul(w, *reinterpret_cast<const float4*>(srow + coff));
           else
             vzero(x);
-          vstore(orow + coff, x);
+          if (BWD)
+            acc = x;
+          else
+            vstore(orow + coff, x);
         }
       }
       if (heavy) continue;
-      obase = orow + hs * zseg;
+      obase = BWD ? orow : orow + hs * zseg;
     }
 
     const int e_begin = readlane_i(pv, 0);
@@ -359,7 +366,11 @@ __global__ __launch_bounds__(256) void spmm_pair_kernel(
       if (lane < cnt) {
         sidx = idx[c0 + lane];
         const float v = VALS ? vals[c0 + lane] : 1.0f;
-        w = de.active ? dropedge_weight(de, v, edge_base + (uint64_t)(c0 + lane)) : v;
+        w = v;
+        if (de.active) {
+          const uint64_t id = BWD ? edge_base + (uint64_t)(uint32_t)eidv[c0 + lane] : edge_base + (uint64_t)(c0 + lane);
+          w = dropedge_weight(de, v, id);
+        }
       }
       uint64_t kept = __ballot(w != 0.0f);
       while (kept) {
@@ -394,7 +405,7 @@ __global__ __launch_bounds__(256) void spmm_pair_kernel(
             const int j = jj[2 * u + h];
             if (j < 0) continue;
             const int e = c0 + j;
-            while (e >= seg_end) {  // flush finished segments (wave-uniform)
+            while (!BWD && e >= seg_end) {  // flush finished segments (wave-uniform)
               if (own) vstore(obase + t * zseg + coff, acc);
               vzero(acc);
               ++t;
@@ -629,14 +640,15 @@ int launch_spmm(int64_t num_rows, int64_t self_rows, int S, int hs, const int32_
                          zseg, de, sp);                                                                    \
   } while (0)
   if (sh.vec == 4) {
-    if (sh.nv == 1 && F <= 128 && !BWD && pair_rows_enabled()) {
+    if (sh.nv == 1 && F <= 128 && !(BWD && accum) && pair_rows_enabled()) {
       // narrow rows (column slices of a pipelined halo): two edges per gather instruction
       if (v)
-        hipLaunchKernelGGL((spmm_pair_kernel<8, true>), grid, block, 0, stream, num_rows, S, hs, ptr, idx, vals,
-                           edge_base, self_base, self_row0, src, lds, F, out, ldo, zseg, de, sp);
+        hipLaunchKernelGGL((spmm_pair_kernel<8, true, BWD>), grid, block, 0, stream, num_rows, S, hs, ptr, idx, vals,
+                           edge_base, self_base, self_row0, src, lds, F, out, ldo, zseg, de, sp, eid, self_rows);
       else
-        hipLaunchKernelGGL((spmm_pair_kernel<8, false>), grid, block, 0, stream, num_rows, S, hs, ptr, idx, vals,
-                           edge_base, self_base, self_row0, src, lds, F, out, ldo, zseg, de, sp);
+        hipLaunchKernelGGL((spmm_pair_kernel<8, false, BWD>), grid, block, 0, stream, num_rows, S, hs, ptr, idx,
+                           vals, edge_base, self_base, self_row0, src, lds, F, out, ldo, zseg, de, sp, eid,
+                           self_rows);
     } else if (sh.nv == 1) {
       if (v) GRL_SPMM_LAUNCH(4, 1, 8, true); else GRL_SPMM_LAUNCH(4, 1, 8, false);
     } else if (!BWD && wide_rows_in_flight() == 8) {  // A/B aid: twice the whole rows in flight per wave

@@ -2,7 +2,8 @@
 exchange, grl.dist.HaloPipeline) on one GPU.  The C3 / C4 graphs; each slice
 table is contiguous [rows, F/K] (as the pipeline holds it); times the K slice
 launches back to back against one whole-width launch, and checks bitwise
-equality.  PROBE_NODES (default 1M), PROBE_DIM (256)."""
+equality; the same for the backward (grl_typed_spmm_bwd_slice, the pipelined
+multi-GPU backward).  PROBE_NODES (default 1M,4M), PROBE_DIM (256)."""
 import os
 import sys
 
@@ -10,7 +11,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 import torch  # noqa: E402
 
 from grl import TypedGraph  # noqa: E402
-from grl.ops import spmm_forward, spmm_forward_slice  # noqa: E402
+from grl.ops import spmm_backward, spmm_backward_slice, spmm_forward, spmm_forward_slice  # noqa: E402
 
 
 def timeit(fn, n=10):
@@ -52,7 +53,29 @@ def main():
                       f"one slice {one:.3f} ms, bitwise {torch.equal(Zs, Zw)}", flush=True)
             os.environ.pop("GRL_SPMM_PAIR")
             del tables
-        del g, X, Zw, Zs
+        del X, Zs
+        g.csc()
+        dZ = Zw.normal_()
+        dXw = spmm_backward(dZ, g, F)
+        bwhole = timeit(lambda: spmm_backward(dZ, g, F))
+        print(f"N={N} F={F} backward whole {bwhole:7.3f} ms", flush=True)
+        for K in (2, 4):
+            w = F // K
+            gts = [torch.empty(N, w, device=dev) for _ in range(K)]
+
+            def bsliced():
+                for c in range(K):
+                    spmm_backward_slice(dZ, g, c * w, gts[c])
+
+            for pair in ("1", "0"):
+                os.environ["GRL_SPMM_PAIR"] = pair
+                t = timeit(bsliced)
+                ok = all(torch.equal(gts[c], dXw[:, c * w:(c + 1) * w]) for c in range(K))
+                print(f"N={N} K={K} backward slices of {w} pair={pair}: total {t:7.3f} ms ({t / bwhole:.2f}x whole), "
+                      f"bitwise {ok}", flush=True)
+            os.environ.pop("GRL_SPMM_PAIR")
+            del gts
+        del g, Zw, dZ, dXw
         torch.cuda.empty_cache()
 
 
