@@ -218,6 +218,9 @@ def test_bench_two_ranks_contract():
     assert out["config"]["workload"] == "C4" and out["config"]["nodes_total"] == 4_000_000
     assert out["scaling"] == "strong" and out["config"]["d"] == 256
     assert out["halo"]["mode"] == "dense" and out["halo"]["chunks"] == 2
+    bwd = out["halo"]["backward"]
+    assert "error" not in bwd, bwd
+    assert bwd["pipelined_ms"] > 0 and bwd["gather_only_ms"] > 0 and bwd["exchange_only_ms"] > 0
 
 
 def test_bench_two_ranks_weak_and_c5_shape():
