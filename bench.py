@@ -541,8 +541,25 @@ def extras(args, graph, X_full, L, F, dev, E_loc, n_loc):
         graph_linear(typed_aggregate(Xl, gl), Wp, bp, relu=True).sum().backward()
 
     # 3 warm calls: the first builds the CSC and grows the caching allocator's pool
-    res["graphconv_layer_fwd_bwd_p0.3"] = {"ms": _time(layer, max(3, iters // 2), warm=3)}
+    res["graphconv_layer_fwd_bwd_p0.3"] = {"ms": _time(layer, max(3, iters // 2), warm=3),
+                                           "path": "fwd: one kernel writing Z; bwd: dX one kernel over the typed "
+                                                   "transpose (grl_graphconv_bwd_data) + dW/db GEMM"}
+    os.environ["GRL_GRAPHCONV_FUSED_BWD"] = "0"
+    try:
+        res["graphconv_layer_fwd_bwd_p0.3_chain_bwd"] = {
+            "ms": _time(layer, max(3, iters // 2), warm=2),
+            "path": "bwd dX as autograd's chain: dZ = g W^T (x6 GEMM), then the CSC gather"}
+    finally:
+        del os.environ["GRL_GRAPHCONV_FUSED_BWD"]
     res["graphconv_layer_fwd_bwd_p0.3_two_ops"] = {"ms": _time(layer_two_ops, max(3, iters // 2), warm=2)}
+    from grl.ops import graph_conv_bwd_data, linear_bwd_data, spmm_backward
+
+    gC = torch.randn(graph.num_rows, F, device=dev)
+    if graph_conv_bwd_data(gC, gl, W, F) is not None:  # builds the typed transpose once (cached per graph)
+        res["graphconv_bwd_data_p0.3"] = {
+            "one_kernel_ms": _time(lambda: graph_conv_bwd_data(gC, gl, W, F), iters),
+            "chain_ms": _time(lambda: spmm_backward(linear_bwd_data(gC, None, W), gl, F), iters)}
+    del gC
     del Z, dZ, Zd
     # inference: one grl_graphconv_fwd call -- the one-kernel form (Z stays on
     # chip, graphconv.hip), and the two-kernel form (Z whole, 7.2 GB, or in

@@ -91,7 +91,11 @@ __device__ __forceinline__ void fma4(float4& acc, float w, const float4& x) {
 // Wf[ks][cb][q][lane][e] = plane q of W(k = 16 ks + 8 (lane >> 5) + e,
 // n = 32 cb + (lane & 31)), zero for n >= C.  Scalar split as
 // split_planes_kernel (linear.hip).
-__global__ void fused_w_planes_kernel(const float* __restrict__ W, int64_t K, int C, uint16_t* __restrict__ Wf) {
+// t_cin > 0 (the data-gradient form, grl_graphconv_bwd_data): W(k, n) is the
+// block-transposed forward weight, W(s t_cin + c, n) = Wfwd[s C + n][c] for
+// the forward's [(L+1) C][t_cin] h_weights (block s of the result = W_s^T).
+__global__ void fused_w_planes_kernel(const float* __restrict__ W, int64_t K, int C, uint16_t* __restrict__ Wf,
+                                      int64_t t_cin) {
   const int64_t total = K * FG_CB * 32;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int e = (int)(i & 7), lane = (int)((i >> 3) & 63);
@@ -100,7 +104,7 @@ __global__ void fused_w_planes_kernel(const float* __restrict__ W, int64_t K, in
     const int64_t ks = rest / FG_CB;
     const int64_t k = ks * 16 + 8 * (lane >> 5) + e;
     const int n = cb * 32 + (lane & 31);
-    const float v = n < C ? W[k * C + n] : 0.0f;
+    const float v = n >= C ? 0.0f : (t_cin > 0 ? W[((k / t_cin) * C + n) * t_cin + k % t_cin] : W[k * C + n]);
     const uint32_t h0 = pack_bf16(v, 0.0f) & 0xFFFFu;
     const float r1 = v - lo_f(h0);
     const uint32_t h1 = pack_bf16(r1, 0.0f) & 0xFFFFu;
@@ -482,12 +486,15 @@ __device__ __forceinline__ bool wait_ge(int* p, int target, unsigned long long* 
   return false;
 }
 
-template <int KS, bool VALS>
+// EID (the data-gradient form over the typed transpose): entry e's DropEdge
+// id is edge_base + eid[e] (its forward CSR position) instead of edge_base + e.
+template <int KS, bool VALS, bool EID = false>
 __global__ __launch_bounds__(64 * (WS_PROD + WS_CONS)) void graphconv_ws_kernel(
     int64_t M, int L, int hs, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ colidx,
     const float* __restrict__ vals, uint64_t edge_base, uint64_t self_base, const float* __restrict__ X,
     int64_t ldx, const uint16_t* __restrict__ Wf, const float* __restrict__ bias, int relu,
-    float* __restrict__ out, int C, DropDev de, int64_t num_tiles, float* __restrict__ Zout, int64_t ldz) {
+    float* __restrict__ out, int C, DropDev de, int64_t num_tiles, float* __restrict__ Zout, int64_t ldz,
+    const int32_t* __restrict__ eid) {
   constexpr int F = KS * 16;
   constexpr int KC = F < WS_KC ? F : WS_KC;  // Z columns per unit
   constexpr int NH = F / KC;                  // units per segment
@@ -567,7 +574,10 @@ __global__ __launch_bounds__(64 * (WS_PROD + WS_CONS)) void graphconv_ws_kernel(
       if (pp < ls.total) {
         sidx = colidx[e];
         const float v = VALS ? vals[e] : 1.0f;
-        w = de.active ? dropedge_weight(de, v, edge_base + (uint64_t)e) : v;
+        if (EID)
+          w = de.active ? dropedge_weight(de, v, edge_base + (uint64_t)(uint32_t)eid[e]) : v;
+        else
+          w = de.active ? dropedge_weight(de, v, edge_base + (uint64_t)e) : v;
       }
     };
     for (int64_t tile = blockIdx.x; tile < num_tiles; tile += gridDim.x) {
@@ -886,7 +896,7 @@ int graphconv_fused_fwd(const GrlTypedCsr* g, const float* X, int64_t ldx, int F
   uint16_t* Wf = static_cast<uint16_t*>(ws);
   const int64_t n_el = K * FG_CB * 32;
   hipLaunchKernelGGL(fused_w_planes_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(n_el, 256), 4096)), dim3(256), 0,
-                     st, W, K, C, Wf);
+                     st, W, K, C, Wf, (int64_t)0);
   GRL_LAUNCH_CHECK();
   const int64_t M = g->num_rows;
   const int64_t tiles = ceil_div(M, FG_R);
@@ -903,11 +913,11 @@ int graphconv_fused_fwd(const GrlTypedCsr* g, const float* X, int64_t ldx, int F
     if (v)                                                                                                           \
       hipLaunchKernelGGL((graphconv_ws_kernel<KS_, true>), dim3((unsigned)grid), dim3(64 * (WS_PROD + WS_CONS)), 0,  \
                          st, M, g->num_types, hs, g->rowptr, g->colidx, g->vals, g->edge_id_base, g->self_id_base, X, \
-                         ldx, Wf, bias, relu, out, C, d, ws_tiles, Z, ldz);                                          \
+                         ldx, Wf, bias, relu, out, C, d, ws_tiles, Z, ldz, nullptr);                                 \
     else                                                                                                             \
       hipLaunchKernelGGL((graphconv_ws_kernel<KS_, false>), dim3((unsigned)grid), dim3(64 * (WS_PROD + WS_CONS)), 0, \
                          st, M, g->num_types, hs, g->rowptr, g->colidx, g->vals, g->edge_id_base, g->self_id_base, X, \
-                         ldx, Wf, bias, relu, out, C, d, ws_tiles, Z, ldz);                                          \
+                         ldx, Wf, bias, relu, out, C, d, ws_tiles, Z, ldz, nullptr);                                 \
   } while (0)
     if (F == 256)
       GRL_WS_LAUNCH(16);
@@ -937,6 +947,48 @@ int graphconv_fused_fwd(const GrlTypedCsr* g, const float* X, int64_t ldx, int F
   else
     GRL_FUSED_LAUNCH(4);
 #undef GRL_FUSED_LAUNCH
+  GRL_LAUNCH_CHECK();
+  return GRL_OK;
+}
+
+// dX = sum_s G_s W_s^T over the typed transpose gt (grl_graphconv_bwd_data):
+// graphconv_ws_kernel with the rows' CSC segments, DropEdge ids through eid,
+// and W's planes taken block-transposed.  Cin = G's width (the forward's C),
+// Cout = dX's width (the forward's F).
+int graphconv_fused_bwd_data(const GrlTypedCsr* gt, const int32_t* eid, const float* G, int64_t ldg, int Cin,
+                             const float* W, int Cout, float* dX, const GrlDropEdge* de, void* ws, hipStream_t st) {
+  const int hs = gt->has_self ? 1 : 0;
+  const int64_t K = (int64_t)(gt->num_types + hs) * Cin;
+  uint16_t* Wf = static_cast<uint16_t*>(ws);
+  const int64_t n_el = K * FG_CB * 32;
+  hipLaunchKernelGGL(fused_w_planes_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(n_el, 256), 4096)), dim3(256), 0,
+                     st, W, K, Cout, Wf, (int64_t)Cin);
+  GRL_LAUNCH_CHECK();
+  const int64_t M = gt->num_rows;
+  const int64_t ws_tiles = ceil_div(M, WS_R);
+  GRL_CHECK_ARG(ws_tiles < 2147483647LL, "grl_graphconv_bwd_data: too many row tiles");
+  const int64_t grid = std::min<int64_t>(ws_tiles, (int64_t)device_cu_count());
+  const DropDev d = to_dev(de);
+  const bool v = gt->vals != nullptr;
+#define GRL_WSB_LAUNCH(KS_)                                                                                          \
+  do {                                                                                                               \
+    if (v)                                                                                                           \
+      hipLaunchKernelGGL((graphconv_ws_kernel<KS_, true, true>), dim3((unsigned)grid), dim3(64 * (WS_PROD + WS_CONS)), \
+                         0, st, M, gt->num_types, hs, gt->rowptr, gt->colidx, gt->vals, gt->edge_id_base,             \
+                         gt->self_id_base, G, ldg, Wf, nullptr, 0, dX, Cout, d, ws_tiles, nullptr, 0, eid);           \
+    else                                                                                                             \
+      hipLaunchKernelGGL((graphconv_ws_kernel<KS_, false, true>), dim3((unsigned)grid),                              \
+                         dim3(64 * (WS_PROD + WS_CONS)), 0, st, M, gt->num_types, hs, gt->rowptr, gt->colidx,         \
+                         gt->vals, gt->edge_id_base, gt->self_id_base, G, ldg, Wf, nullptr, 0, dX, Cout, d, ws_tiles,  \
+                         nullptr, 0, eid);                                                                          \
+  } while (0)
+  if (Cin == 256)
+    GRL_WSB_LAUNCH(16);
+  else if (Cin == 128)
+    GRL_WSB_LAUNCH(8);
+  else
+    GRL_WSB_LAUNCH(4);
+#undef GRL_WSB_LAUNCH
   GRL_LAUNCH_CHECK();
   return GRL_OK;
 }

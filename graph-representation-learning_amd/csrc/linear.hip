@@ -1338,6 +1338,45 @@ extern "C" int grl_graphconv_fwd(const GrlTypedCsr* g, const float* X, int64_t l
   return GRL_OK;
 }
 
+// The data gradient of one GraphConv layer by reassociation (see grl.h):
+// dX = sum_s (A_drop,s^T G) W_s^T on the one-kernel GraphConv over the typed
+// transpose.  Eligible when the forward's x6 GEMM shape would be (large
+// graphs), C in {64, 128, 256}, F <= 256, L <= 7, G rows float4-aligned and no
+// heavy-row split plan on the transpose.
+static bool bwd_data_path(const GrlTypedCsr* gt, const float* G, int64_t ldg, int C, const float* W, int F) {
+  const int64_t K = (int64_t)(gt->num_types + (gt->has_self ? 1 : 0)) * C;
+  return graphconv_fused_enabled() && graphconv_fused_shape_ok(C, F, gt->num_types) && x6_shape_ok(gt->num_rows, F, K) &&
+         al16(W) && F % 4 == 0 && al16(G) && ldg % 4 == 0 && (!gt->split || gt->split->num_heavy == 0) &&
+         K <= 2147483647LL && gt->nnz < 2147483647LL;
+}
+
+extern "C" size_t grl_graphconv_bwd_data_workspace_query(const GrlTypedCsr* gt, const float* G, int64_t ldg, int32_t C,
+                                                        const float* W, int32_t F) {
+  if (!gt || gt->num_rows <= 0 || gt->num_types < 1 || C <= 0 || F <= 0) return 0;
+  if (!bwd_data_path(gt, G, ldg, C, W, F)) return 0;
+  return graphconv_fused_ws_bytes((int64_t)(gt->num_types + (gt->has_self ? 1 : 0)) * C);
+}
+
+extern "C" int grl_graphconv_bwd_data(const GrlTypedCsr* gt, const int32_t* eid, const float* G, int64_t ldg,
+                                      int32_t C, const float* W, int32_t F, float* dX, const GrlDropEdge* de,
+                                      void* workspace, size_t workspace_bytes, grl_stream_t stream) {
+  TraceRange trace_("grl_graphconv_bwd_data");
+  GRL_CHECK_ARG(gt != nullptr, "grl_graphconv_bwd_data: graph is NULL");
+  GRL_CHECK_ARG(gt->num_rows >= 0 && gt->num_types >= 1 && gt->num_types <= 63,
+                "grl_graphconv_bwd_data: num_types must be in [1, 63] (got %d)", gt->num_types);
+  GRL_CHECK_ARG(C > 0 && ldg >= C && F > 0, "grl_graphconv_bwd_data: need C > 0, ldg >= C, F > 0");
+  if (gt->num_rows == 0) return GRL_OK;
+  GRL_CHECK_ARG(G && W && dX && gt->rowptr && (gt->nnz == 0 || (gt->colidx && eid)),
+                "grl_graphconv_bwd_data: NULL pointer");
+  if (!bwd_data_path(gt, G, ldg, C, W, F))
+    GRL_FAIL(GRL_E_UNSUPPORTED, "grl_graphconv_bwd_data: shape outside the one-kernel path (C %d, F %d, L %d, rows "
+             "%lld; see grl_graphconv_bwd_data_workspace_query)", C, F, gt->num_types, (long long)gt->num_rows);
+  const size_t need = graphconv_fused_ws_bytes((int64_t)(gt->num_types + (gt->has_self ? 1 : 0)) * C);
+  if (!workspace || !al16(workspace) || workspace_bytes < need)
+    GRL_FAIL(GRL_E_WORKSPACE, "grl_graphconv_bwd_data: workspace %zu < %zu (16-B aligned)", workspace_bytes, need);
+  return graphconv_fused_bwd_data(gt, eid, G, ldg, C, W, F, dX, de, workspace, as_stream(stream));
+}
+
 extern "C" int grl_graphconv_fwd_train(const GrlTypedCsr* g, const float* X, int64_t ldx, int32_t F, const float* W,
                                        const float* bias, int32_t C, int32_t relu, float* out, float* Z,
                                        const GrlDropEdge* de, void* workspace, size_t workspace_bytes,

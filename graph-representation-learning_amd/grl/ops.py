@@ -11,6 +11,7 @@ mask from the graph's (p, seed, call) record, exactly like forward.
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -254,6 +255,45 @@ class _GraphLinear(torch.autograd.Function):
         return dZ, dW, db, None
 
 
+def _bwd_data_enabled() -> bool:
+    return os.environ.get("GRL_GRAPHCONV_FUSED_BWD", "1") != "0"
+
+
+def graph_conv_bwd_data(g: torch.Tensor, graph: TypedGraph, W: torch.Tensor, F: int, relu_out=None):
+    """dX of one GraphConv layer in one kernel (grl_graphconv_bwd_data):
+    dX = sum_s (A_drop,s^T g) W_s^T over the graph's typed transpose, for g
+    the output gradient ([num_rows, C]; through the ReLU's [relu_out > 0]
+    when relu_out is given).  None when the shape is outside the one-kernel
+    path (the caller then runs dZ = g W^T and the CSC gather).
+    GRL_GRAPHCONV_FUSED_BWD=0 disables it."""
+    if not _bwd_data_enabled() or isinstance(graph, EdgeBlockedGraph):
+        return None
+    M, C = g.shape
+    L = graph.num_types
+    # cheap pre-checks before the (cached, once per graph) transpose build; the library decides
+    if (C not in (64, 128, 256) or F > 256 or F % 4 or L > 7 or graph.num_rows != graph.num_cols
+            or graph.self_rows < graph.num_rows or 2.0 * M * graph.segments * C * F < 1.6e10
+            or g.dtype != torch.float32 or not g.is_contiguous() or W.dtype != torch.float32):
+        return None
+    if relu_out is not None:
+        g = torch.where(relu_out > 0, g, torch.zeros((), dtype=g.dtype, device=g.device))
+    gt, eid = graph.typed_transpose()
+    gt = gt.with_dropedge(graph.dropedge)
+    csr = gt.csr_c(C)
+    Wc = W.contiguous()
+    ws_bytes = _lib.lib().grl_graphconv_bwd_data_workspace_query(ctypes.byref(csr), g.data_ptr(), g.stride(0), C,
+                                                                 Wc.data_ptr(), F)
+    if ws_bytes == 0:
+        return None
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=g.device)
+    dX = torch.empty(M, F, dtype=torch.float32, device=g.device)
+    de = graph.dropedge.to_c() if graph.dropedge is not None else None
+    call("grl_graphconv_bwd_data", ctypes.byref(csr), eid.data_ptr(), g.data_ptr(), g.stride(0), C, Wc.data_ptr(), F,
+         dX.data_ptr(), ctypes.byref(de) if de is not None else None, ws.data_ptr(), ws_bytes,
+         current_stream_handle(g.device))
+    return dX
+
+
 class _GraphConv(torch.autograd.Function):
     """One GraphConv layer, X -> Z = A_drop X -> out = Z W + b [ReLU]
     (robust_gcn.py:45-51), as one autograd node: the same kernels and
@@ -290,9 +330,13 @@ class _GraphConv(torch.autograd.Function):
         want_b = ctx.has_b and ctx.needs_input_grad[3]
         dW = db = dX = None
         if ctx.needs_input_grad[0]:
-            dZ = linear_bwd_data(g, mask, W)
-            dX = spmm_backward(dZ, ctx.graph, ctx.xshape[-1]).view(ctx.xshape)
-            del dZ
+            F = ctx.xshape[-1]
+            dX = graph_conv_bwd_data(g, ctx.graph, W, F, mask)  # one kernel, no dZ (large graphs)
+            if dX is None:
+                dZ = linear_bwd_data(g, mask, W)
+                dX = spmm_backward(dZ, ctx.graph, F)
+                del dZ
+            dX = dX.view(ctx.xshape)
         if want_w or want_b:
             dW, db = linear_bwd_weight(Z, g, mask, want_b)
         return dX, None, dW if want_w else None, db, None, None

@@ -299,6 +299,33 @@ int grl_graphconv_fwd_train(const GrlTypedCsr* g, const float* X, int64_t ldx,
                             const GrlDropEdge* de, void* workspace,
                             size_t workspace_bytes, grl_stream_t stream);
 
+/* Data gradient of one GraphConv layer in ONE kernel.  Replaces the
+ * autograd chain MmBackward0 (dZ = G W^T, robust_gcn.py:50) then
+ * BmmBackward0 (dX = A_drop^T dZ, robust_gcn.py:45) by its reassociation
+ *   dX = sum_s (A_drop,s^T G) W_s^T     (W_s = rows [s F, (s+1) F) of W),
+ * i.e. the one-kernel GraphConv forward run over the typed transpose gt
+ * (rows = source nodes, segments (m, t) in forward-CSR order, colidx = the
+ * forward row n, vals = the CSC values; entry e's DropEdge id is
+ * gt->edge_id_base + eid[e], its forward CSR position, and row m's self id
+ * gt->self_id_base + m, so the mask is the forward's).  dZ (7.2 GB at C3)
+ * never exists.  G = the output gradient through the ReLU, [num_rows, C]
+ * (ldg); W the forward h_weights [(has_self+num_types)*F, C]; dX
+ * [num_rows, F] contiguous, overwritten.  Floating point: the same products
+ * summed in another order than the two-kernel chain (fp32-level difference,
+ * tests/test_gpu_graphconv.py).  Square graphs only (gt->num_rows rows of G
+ * hold the self terms).  Eligible shapes: a nonzero
+ * grl_graphconv_bwd_data_workspace_query(), which is also the workspace
+ * size; otherwise GRL_E_UNSUPPORTED and the caller runs the chain.       */
+size_t grl_graphconv_bwd_data_workspace_query(const GrlTypedCsr* gt,
+                                              const float* G, int64_t ldg,
+                                              int32_t C, const float* W,
+                                              int32_t F);
+int grl_graphconv_bwd_data(const GrlTypedCsr* gt, const int32_t* eid,
+                           const float* G, int64_t ldg, int32_t C,
+                           const float* W, int32_t F, float* dX,
+                           const GrlDropEdge* de, void* workspace,
+                           size_t workspace_bytes, grl_stream_t stream);
+
 /* Backward of grl_linear_fwd (autograd MmBackward0 of robust_gcn.py:50, with
  * the ReLU of drop_robust_gcn.py:76 folded in when relu_out != NULL):
  *   dZ = (g * [relu_out > 0]) W^T           grl_linear_bwd_data,  dZ [M, K] (ld lddz)

@@ -225,6 +225,7 @@ def test_training_forward_one_kernel_same_bits(de, recompute, monkeypatch):
     R = torch.randn(N, C, device=DEV, generator=gen)
     out_f, Z_f = graph_conv_fwd_train(X0, g, W0, b0, True)
     assert torch.equal(Z_f, spmm_forward(X0, g))
+    monkeypatch.setenv("GRL_GRAPHCONV_FUSED_BWD", "0")  # dX by the chain (the reassociated one: test below)
     res = {}
     for fused in ("1", "0"):
         monkeypatch.setenv("GRL_GRAPHCONV_FUSED", fused)
@@ -235,3 +236,75 @@ def test_training_forward_one_kernel_same_bits(de, recompute, monkeypatch):
     assert torch.equal(res["1"][0], out_f)
     for a, c in zip(res["1"], res["0"]):
         assert torch.equal(a, c)
+
+
+@pytest.mark.parametrize("N,L,F,C,has_self,deg", [(20_011, 6, 256, 256, True, 16.0), (100_003, 6, 96, 128, True, 9.0),
+                                                  (80_000, 6, 256, 64, True, 12.0), (60_001, 3, 200, 256, False, 20.0),
+                                                  (20_000, 6, 256, 256, True, 120.0), (18_001, 7, 256, 256, True, 14.0)])
+@pytest.mark.parametrize("variant", ["plain", "drop_self", "drop_spare_self_vals"])
+def test_bwd_data_one_kernel(N, L, F, C, has_self, deg, variant, monkeypatch):
+    """grl_graphconv_bwd_data: dX = sum_s (A_drop,s^T G) W_s^T in one kernel
+    over the typed transpose (DropEdge ids through eid, so the forward's
+    mask) against the autograd chain dZ = G W^T, dX = A_drop^T dZ: within
+    1e-5 of the chain run on |G|, |W| (fp32-level: the same products summed
+    in another order), deterministic, and what graph_conv's backward returns
+    (dW / db unchanged, bitwise)."""
+    from grl.ops import graph_conv_bwd_data, linear_bwd_data, spmm_backward
+
+    de = {"plain": None, "drop_self": DropEdge(0.3, 3, 2, True), "drop_spare_self_vals": DropEdge(0.25, 9, 0, False)}
+    de = de[variant]
+    g = TypedGraph.synthetic(N, deg, L, seed=N % 5, device=DEV)
+    if variant.endswith("vals"):
+        vals = torch.rand(g.nnz, generator=torch.Generator(device=DEV).manual_seed(2), device=DEV)
+        g = TypedGraph(g.rowptr, g.colidx, L, vals=vals, has_self=has_self, num_cols=N)
+    elif not has_self:
+        g = TypedGraph(g.rowptr, g.colidx, L, has_self=False, num_cols=N)
+    g = g.with_dropedge(de)
+    gen = torch.Generator(device=DEV).manual_seed(N + F)
+    K = g.segments * F
+    G = torch.randn(N, C, device=DEV, generator=gen)
+    W = torch.randn(K, C, device=DEV, generator=gen) / K ** 0.5
+    dX = graph_conv_bwd_data(G, g, W, F)
+    assert dX is not None, "shape should take the one-kernel path"
+    assert torch.equal(graph_conv_bwd_data(G, g, W, F), dX)  # deterministic
+    chain = spmm_backward(linear_bwd_data(G, None, W), g, F)
+    bound = spmm_backward(linear_bwd_data(G.abs(), None, W.abs()), g.with_dropedge(de), F)
+    err = (dX - chain).abs()
+    assert bool((err <= 1e-5 * bound + 1e-6).all()), float((err / (bound + 1e-30)).max())
+    # through autograd (ReLU on): X.grad is the one-kernel dX of g * [out > 0]; dW, db the chain's bits
+    X0 = torch.randn(N, F, device=DEV, generator=gen)
+    b0 = torch.randn(C, device=DEV, generator=gen)
+    res = {}
+    for fb in ("1", "0"):
+        monkeypatch.setenv("GRL_GRAPHCONV_FUSED_BWD", fb)
+        X, Wp, b = (t.clone().requires_grad_(True) for t in (X0, W, b0))
+        out = graph_conv(X, g, Wp, b, relu=True)
+        (out * G).sum().backward()
+        res[fb] = (out.detach(), X.grad, Wp.grad, b.grad)
+    monkeypatch.setenv("GRL_GRAPHCONV_FUSED_BWD", "1")
+    assert torch.equal(res["1"][1], graph_conv_bwd_data(G, g, W, F, res["1"][0]))
+    assert torch.equal(res["1"][0], res["0"][0]) and torch.equal(res["1"][2], res["0"][2])
+    assert torch.equal(res["1"][3], res["0"][3])
+    Gm = torch.where(res["1"][0] > 0, G, torch.zeros((), device=DEV))
+    bound = spmm_backward(linear_bwd_data(Gm.abs(), None, W.abs()), g, F)
+    assert bool(((res["1"][1] - res["0"][1]).abs() <= 1e-5 * bound + 1e-6).all())
+
+
+def test_bwd_data_falls_back_outside_its_shapes():
+    """Small graphs, C outside {64, 128, 256} or a non-square shard: None (the
+    caller runs the chain); the C entry refuses with GRL_E_UNSUPPORTED."""
+    import ctypes
+
+    from grl.ops import graph_conv_bwd_data
+
+    g = TypedGraph.synthetic(2000, 8.0, 6, seed=1, device=DEV)
+    assert graph_conv_bwd_data(torch.randn(2000, 256, device=DEV), g, torch.randn(7 * 256, 256, device=DEV), 256) is None
+    g = TypedGraph.synthetic(30_000, 8.0, 6, seed=1, device=DEV)
+    assert graph_conv_bwd_data(torch.randn(30_000, 96, device=DEV), g, torch.randn(7 * 256, 96, device=DEV), 256) is None
+    gt, eid = g.typed_transpose()
+    csr = gt.csr_c(96)
+    G = torch.randn(30_000, 96, device=DEV)
+    rc = _lib.lib().grl_graphconv_bwd_data(ctypes.byref(csr), eid.data_ptr(), G.data_ptr(), 96, 96,
+                                           torch.empty(7 * 256, 96, device=DEV).data_ptr(), 256,
+                                           torch.empty(30_000, 256, device=DEV).data_ptr(), None, None, 0, None)
+    assert rc == _lib.GRL_E_UNSUPPORTED
