@@ -220,34 +220,40 @@ class TypedGraph:
         return c
 
     def typed_transpose(self):
-        """(gt, eid): the typed transpose of a square graph, built once from
-        the CSC and cached -- gt's row m, segment t lists the forward rows n
-        with a type-t edge n <- m, in forward-CSR order; eid[e] = entry e's
-        forward CSR position (its DropEdge id minus edge_id_base); values are
-        the CSC's.  The one-kernel data gradient (grl_graphconv_bwd_data)
-        runs the GraphConv forward kernel over it."""
+        """(gt, eid): the typed transpose of a square graph, built once and
+        cached -- gt's row m, segment t lists the forward rows n with a type-t
+        edge n <- m, in forward-CSR order; eid[e] = entry e's forward CSR
+        position (its DropEdge id minus edge_id_base); values follow.  It is
+        the CSC builder (grl_csr_to_csc: a stable radix sort by column) run
+        with the column of edge (n, t, m) keyed as m * L + t.  The one-kernel
+        data gradient (grl_graphconv_bwd_data) runs the GraphConv forward
+        kernel over it."""
         tt = self._shared.get("typed_transpose")
         if tt is not None:
             return tt
         if self.num_rows != self.num_cols or self.self_rows < self.num_rows:
             raise _lib.GrlError("typed_transpose needs a square graph whose every row has its self loop")
-        c = self.csc()
-        L, S, hs = self.num_types, self.segments, 1 if self.has_self else 0
-        n_cols = self.num_cols
-        zrow = c["zrow"][: self.nnz].long()
-        m = torch.repeat_interleave(torch.arange(n_cols, device=self.device), c["colptr"].diff().long())
-        key = m * L + (zrow % S - hs)
-        key, perm = torch.sort(key, stable=True)  # (m, t) segments, forward-CSR order inside each
-        rowptr = torch.zeros(n_cols * L + 1, dtype=torch.int64, device=self.device)
-        rowptr[1:] = torch.cumsum(torch.bincount(key, minlength=n_cols * L), 0)
-        del key
-        colidx = (zrow[perm] // S).to(torch.int32)
-        eid = c["eid"][: self.nnz][perm].contiguous()
-        vals = None if c["cvals"] is None else c["cvals"][: self.nnz][perm]
-        gt = TypedGraph(rowptr.to(torch.int32), colidx, L, vals=vals, has_self=self.has_self, num_cols=self.num_rows,
-                        edge_id_base=self.edge_id_base, self_id_base=self.self_id_base, self_rows=self.num_rows)
+        L, S = self.num_types, self.segments
+        if self.num_cols * L >= 2 ** 31:
+            raise _lib.GrlError("typed_transpose: num_cols * num_types exceeds int32")
+        seg = torch.arange(self.num_rows * L, dtype=torch.int32, device=self.device) % L
+        t = torch.repeat_interleave(seg, self.rowptr.diff(), output_size=self.nnz)
+        keyed = TypedGraph(self.rowptr, self.colidx * L + t, L, vals=self.vals, has_self=self.has_self,
+                           num_cols=self.num_cols * L, edge_id_base=self.edge_id_base,
+                           self_id_base=self.self_id_base, self_rows=self.self_rows)
+        del seg, t
+        c = keyed.csc()
+        n = max(self.nnz, 1)
+        gt = TypedGraph(c["colptr"], (c["zrow"][:n] // S).contiguous(), L, vals=c["cvals"], has_self=self.has_self,
+                        num_cols=self.num_rows, edge_id_base=self.edge_id_base, self_id_base=self.self_id_base,
+                        self_rows=self.num_rows) if self.nnz else None
+        if gt is None:  # no edges: every segment empty
+            gt = TypedGraph(torch.zeros(self.num_cols * L + 1, dtype=torch.int32, device=self.device),
+                            torch.zeros(0, dtype=torch.int32, device=self.device), L, has_self=self.has_self,
+                            num_cols=self.num_rows, edge_id_base=self.edge_id_base, self_id_base=self.self_id_base,
+                            self_rows=self.num_rows)
         gt.split_threshold, gt.split_chunk = self.split_threshold, self.split_chunk
-        tt = (gt, eid)
+        tt = (gt, c["eid"])
         self._shared["typed_transpose"] = tt
         return tt
 
