@@ -129,6 +129,50 @@ def test_c3_full_graph_backward_vs_oracle(c3):
     _say("C3 backward: whole dX bitwise")
 
 
+def test_c3_full_graph_layer_data_gradient_one_kernel(c3):
+    """The layer's dX at C3 through the one-kernel reassociated backward
+    (grl_graphconv_bwd_data over the typed transpose, DropEdge p=0.3) against
+    the oracle in float64 on 2,048 sampled rows: dX[m] = w_self(m) G[m] W_0^T
+    + sum over the oracle CSC's entries (n, t) -> m of w_e G[n] W_{1+t}^T,
+    with the oracle's mask; within 1e-5 of the same sum over |terms|."""
+    from grl.ops import graph_conv_bwd_data
+    from oracle import hash as ohash
+
+    g, X, Xh = c3
+    N, F, C = g.num_rows, 256, 256
+    p, seed, call = 0.3, 2, 6
+    gd = g.with_dropedge(DropEdge(p, seed, call, True))
+    gen = torch.Generator(device=DEV).manual_seed(13)
+    G = torch.randn(N, C, generator=gen, device=DEV)
+    W = torch.randn(7 * F, C, generator=gen, device=DEV) / (7 * F) ** 0.5
+    dX = graph_conv_bwd_data(G, gd, W, F)
+    assert dX is not None
+    rows = np.unique(np.r_[0:64, N - 64:N, np.random.default_rng(4).integers(0, N, 1920)])
+    c = g.csc()
+    colptr, zrow, eid = (c[k].cpu().numpy() for k in ("colptr", "zrow", "eid"))
+    Gh, Wh = G.cpu().numpy().astype(np.float64), W.cpu().numpy().astype(np.float64)
+    Wt = Wh.reshape(7, F, C)  # W_s = rows [s F, (s+1) F)
+    _, _, scale = ohash.dropedge_params(p)
+    got = dX.cpu().numpy()[rows]
+    ref = np.zeros((len(rows), F))
+    mag = np.zeros((len(rows), F))
+    for i, m in enumerate(rows):
+        ids = [g.self_id_base + int(m)]
+        ns, ss = [int(m)], [0]
+        for e in range(colptr[m], colptr[m + 1]):
+            ns.append(int(zrow[e]) // 7)
+            ss.append(int(zrow[e]) % 7)
+            ids.append(int(eid[e]))
+        keep = ohash.dropedge_keep(p, seed, call, np.array(ids, dtype=np.uint64)).astype(np.float64) * float(scale)
+        for w, n, s_ in zip(keep, ns, ss):
+            if w:
+                ref[i] += w * (Wt[s_] @ Gh[n])
+                mag[i] += w * (np.abs(Wt[s_]) @ np.abs(Gh[n]))
+    err = np.abs(got - ref)
+    assert np.all(err <= 1e-5 * mag + 1e-6), float((err / (mag + 1e-30)).max())
+    _say(f"C3 one-kernel dX: {len(rows)} rows within {float((err / (mag + 1e-30)).max()):.2e} of sum|terms|")
+
+
 def test_c5_rmat_scale23_forward_vs_oracle():
     """C5 on one GPU: 2^23 nodes, ~528M typed edges, d=512, DropEdge p=0.2.
     Hub rows run as chunk items (default split threshold) and the table
