@@ -70,6 +70,8 @@ def parse():
     ap.add_argument("--chunks", type=int, default=0,
                     help="N>1: column slices of the pipelined halo exchange (0 = d/128; 1 = serial)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 disables)")
+    ap.add_argument("--no-c4-reference", dest="c4_reference", action="store_false",
+                    help="N=1 C3 line: skip timing BASELINE's C4 graph whole on the one GPU (the N>1 lines' baseline)")
     ap.add_argument("--extras", action="store_true",
                     help="also time fused-DropEdge fwd, backward, MFMA linear and a full layer (not the headline)")
     ap.add_argument("--dist-backend", default="nccl",
@@ -278,6 +280,8 @@ def main():
         out["cpu_baseline"], out["parity"] = cpu_baseline(args, g_step, X_loc, Z, L, F)
     if world == 1 and wname.startswith("C3"):
         out["dropedge_train_p0.3"] = dropedge_train(graph, X_loc, E_loc, max(3, min(10, args.steps)))
+        if args.c4_reference:
+            out["C4_one_gpu"] = c4_one_gpu(dev, max(3, min(10, args.steps)))
     if args.extras and world == 1:
         out["extras"] = extras(args, graph, X_loc, L, F, dev, E_loc, n_loc)
         del X_loc, X_full, Z
@@ -361,6 +365,27 @@ def halo_backward_breakdown(pipe, g, dev, iters):
     return {"pipelined_ms": pipelined, "gather_only_ms": ga, "exchange_only_ms": ex, "serial_sum_ms": ga + ex,
             "note": "dX = A_drop^T dZ of the shard: grl_typed_spmm_bwd_slice per column slice, reverse halo "
                     "all-to-all per slice in flight under the next gather, peer-order combine"}
+
+
+def c4_one_gpu(dev, iters):
+    """BASELINE's C4 graph (ER, N=4M, avg_deg 32, d=256) aggregated on ONE
+    GPU, next to the N=1 headline: the per-GPU reference the driver's N>1
+    lines (C4 sharded 2/4/8 ways, strong scaling) are measured against."""
+    from grl import TypedGraph
+    from grl.ops import spmm_forward
+
+    N, deg, L, F = WORKLOADS["C4"][1], WORKLOADS["C4"][2], 6, WORKLOADS["C4"][3]
+    g = TypedGraph.synthetic(N, deg, L, kind="er", seed=0, device=dev)
+    X = torch.randn(N, F, generator=torch.Generator(device=dev).manual_seed(1), device=dev)
+    Z = torch.empty(N, 7 * F, device=dev)
+    ms = _time(lambda: spmm_forward(X, g, out=Z), iters)
+    alg = spmm_bytes(g.nnz, N, L, F, 0.0)
+    res = {"nodes": N, "edges": g.nnz, "ms": ms, "edges_per_s": g.nnz / (ms * 1e-3),
+           "alg_GBps": alg / (ms * 1e-3) / 1e9, "frac_of_8TBps": alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+           "note": "C4's whole 4M-node graph on one GPU (same kernel as the headline); the N>1 lines shard it"}
+    del g, X, Z
+    torch.cuda.empty_cache()
+    return res
 
 
 def dropedge_train(graph, X, E, iters):
