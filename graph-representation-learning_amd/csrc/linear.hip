@@ -919,18 +919,23 @@ __global__ __launch_bounds__(512) void gemm_x6t_kernel(GemmArgs p) {
   const int st_off0 = kr0 * 256 + (col ^ ((kr0 & 3) << 5));
   const int st_off1 = kr1 * 256 + (col ^ ((kr1 & 3) << 5));
   float4 ra0, ra1, rb0, rb1;
+  bool in0 = true, in1 = true;  // the staged rows lie inside this split's K range
   const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  // Rows past the split's end are loaded clamped (from kbeg) and zeroed only
+  // when stashed, after the next step's MFMAs: zeroing right after the loads
+  // made hipcc branch on the loaded registers and wait vmcnt(0) for them
+  // there, exposing the whole load latency on every K16 step
+  // (cdna_hip_programming.md, "register or load" selects).
 #define X6T_LOAD(t)                                                                                       \
   do {                                                                                                    \
     const int64_t k_ = kbeg + (t) * X6_K;                                                                 \
-    const bool in0_ = k_ + kr0 < kend, in1_ = k_ + kr1 < kend;                                            \
-    const int64_t r0_ = in0_ ? k_ + kr0 : kbeg, r1_ = in1_ ? k_ + kr1 : kbeg;                             \
+    in0 = k_ + kr0 < kend;                                                                                \
+    in1 = k_ + kr1 < kend;                                                                                \
+    const int64_t r0_ = in0 ? k_ + kr0 : kbeg, r1_ = in1 ? k_ + kr1 : kbeg;                               \
     ra0 = *reinterpret_cast<const float4*>(a_base + r0_ * p.lda);                                         \
     ra1 = *reinterpret_cast<const float4*>(a_base + r1_ * p.lda);                                         \
     rb0 = *reinterpret_cast<const float4*>(b_base + r0_ * p.ldb);                                         \
     rb1 = *reinterpret_cast<const float4*>(b_base + r1_ * p.ldb);                                         \
-    if (!in0_) ra0 = rb0 = zero4;                                                                         \
-    if (!in1_) ra1 = rb1 = zero4;                                                                         \
   } while (0)
 #define X6T_SPLIT(v, base, off)                                                                           \
   do {                                                                                                    \
@@ -942,10 +947,10 @@ __global__ __launch_bounds__(512) void gemm_x6t_kernel(GemmArgs p) {
   } while (0)
 #define X6T_STASH(st)                                                                                     \
   do {                                                                                                    \
-    X6T_SPLIT(ra0, (st), st_off0);                                                                        \
-    X6T_SPLIT(ra1, (st), st_off1);                                                                        \
-    X6T_SPLIT(rb0, (st) + 3 * X6_PLANE, st_off0);                                                         \
-    X6T_SPLIT(rb1, (st) + 3 * X6_PLANE, st_off1);                                                         \
+    X6T_SPLIT(in0 ? ra0 : zero4, (st), st_off0);                                                          \
+    X6T_SPLIT(in1 ? ra1 : zero4, (st), st_off1);                                                          \
+    X6T_SPLIT(in0 ? rb0 : zero4, (st) + 3 * X6_PLANE, st_off0);                                           \
+    X6T_SPLIT(in1 ? rb1 : zero4, (st) + 3 * X6_PLANE, st_off1);                                           \
   } while (0)
 
   // this lane's transposed-read coordinates: k = 8h + ((lane & 15) >> 2),
