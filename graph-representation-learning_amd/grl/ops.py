@@ -263,34 +263,46 @@ def graph_conv_bwd_data(g: torch.Tensor, graph: TypedGraph, W: torch.Tensor, F: 
     """dX of one GraphConv layer in one kernel (grl_graphconv_bwd_data):
     dX = sum_s (A_drop,s^T g) W_s^T over the graph's typed transpose, for g
     the output gradient ([num_rows, C]; through the ReLU's [relu_out > 0]
-    when relu_out is given).  None when the shape is outside the one-kernel
-    path (the caller then runs dZ = g W^T and the CSC gather).
-    GRL_GRAPHCONV_FUSED_BWD=0 disables it."""
+    when relu_out is given).  F > 256 (gcn3's 2C-wide input) runs one call per
+    <= 256-column block of dX (the gather repeats per block; dZ still never
+    exists).  None when the shape is outside the one-kernel path (the caller
+    then runs dZ = g W^T and the CSC gather).  GRL_GRAPHCONV_FUSED_BWD=0
+    disables it."""
     if not _bwd_data_enabled() or isinstance(graph, EdgeBlockedGraph):
         return None
     M, C = g.shape
-    L = graph.num_types
+    L, S = graph.num_types, graph.segments
+    nblk = -(-F // 256)
+    wblk = (-(-F // nblk) + 3) // 4 * 4 if nblk > 1 else F  # block width, a multiple of 4
+    bounds = [(f0, min(F, f0 + wblk)) for f0 in range(0, F, wblk)]
     # cheap pre-checks before the (cached, once per graph) transpose build; the library decides
-    if (C not in (64, 128, 256) or F > 256 or F % 4 or L > 7 or graph.num_rows != graph.num_cols
-            or graph.self_rows < graph.num_rows or 2.0 * M * graph.segments * C * F < 1.6e10
-            or g.dtype != torch.float32 or not g.is_contiguous() or W.dtype != torch.float32):
+    if (C not in (64, 128, 256) or F % 4 or F > 1024 or L > 7 or graph.num_rows != graph.num_cols
+            or graph.self_rows < graph.num_rows or 2.0 * M * S * C * min(b - a for a, b in bounds) < 1.6e10
+            or g.dtype != torch.float32 or not g.is_contiguous() or W.dtype != torch.float32
+            or tuple(W.shape) != (S * F, C)):
         return None
-    if relu_out is not None:
-        g = torch.where(relu_out > 0, g, torch.zeros((), dtype=g.dtype, device=g.device))
     gt, eid = graph.typed_transpose()
     gt = gt.with_dropedge(graph.dropedge)
     csr = gt.csr_c(C)
-    Wc = W.contiguous()
     ws_bytes = _lib.lib().grl_graphconv_bwd_data_workspace_query(ctypes.byref(csr), g.data_ptr(), g.stride(0), C,
-                                                                 Wc.data_ptr(), F)
+                                                                 W.data_ptr(), bounds[0][1])
     if ws_bytes == 0:
         return None
+    if relu_out is not None:
+        g = torch.where(relu_out > 0, g, torch.zeros((), dtype=g.dtype, device=g.device))
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=g.device)
-    dX = torch.empty(M, F, dtype=torch.float32, device=g.device)
     de = graph.dropedge.to_c() if graph.dropedge is not None else None
-    call("grl_graphconv_bwd_data", ctypes.byref(csr), eid.data_ptr(), g.data_ptr(), g.stride(0), C, Wc.data_ptr(), F,
-         dX.data_ptr(), ctypes.byref(de) if de is not None else None, ws.data_ptr(), ws_bytes,
-         current_stream_handle(g.device))
+    stream = current_stream_handle(g.device)
+    dX = torch.empty(M, F, dtype=torch.float32, device=g.device)
+    for f0, f1 in bounds:
+        w = f1 - f0
+        Wb = W.contiguous() if len(bounds) == 1 else W.view(S, F, C)[:, f0:f1, :].reshape(S * w, C).contiguous()
+        out = dX if len(bounds) == 1 else torch.empty(M, w, dtype=torch.float32, device=g.device)
+        call("grl_graphconv_bwd_data", ctypes.byref(csr), eid.data_ptr(), g.data_ptr(), g.stride(0), C,
+             Wb.data_ptr(), w, out.data_ptr(), ctypes.byref(de) if de is not None else None, ws.data_ptr(), ws_bytes,
+             stream)
+        if len(bounds) > 1:
+            dX[:, f0:f1] = out
     return dX
 
 

@@ -240,7 +240,8 @@ def test_training_forward_one_kernel_same_bits(de, recompute, monkeypatch):
 
 @pytest.mark.parametrize("N,L,F,C,has_self,deg", [(20_011, 6, 256, 256, True, 16.0), (100_003, 6, 96, 128, True, 9.0),
                                                   (80_000, 6, 256, 64, True, 12.0), (60_001, 3, 200, 256, False, 20.0),
-                                                  (20_000, 6, 256, 256, True, 120.0), (18_001, 7, 256, 256, True, 14.0)])
+                                                  (20_000, 6, 256, 256, True, 120.0), (18_001, 7, 256, 256, True, 14.0),
+                                                  (20_011, 6, 512, 256, True, 10.0), (40_011, 6, 260, 256, True, 8.0)])
 @pytest.mark.parametrize("variant", ["plain", "drop_self", "drop_spare_self_vals"])
 def test_bwd_data_one_kernel(N, L, F, C, has_self, deg, variant, monkeypatch):
     """grl_graphconv_bwd_data: dX = sum_s (A_drop,s^T G) W_s^T in one kernel
