@@ -488,13 +488,15 @@ __device__ __forceinline__ bool wait_ge(int* p, int target, unsigned long long* 
 
 // EID (the data-gradient form over the typed transpose): entry e's DropEdge
 // id is edge_base + eid[e] (its forward CSR position) instead of edge_base + e.
+// Rows >= self_rows have no self term (a shard's transpose: its halo rows);
+// the forward passes M.
 template <int KS, bool VALS, bool EID = false>
 __global__ __launch_bounds__(64 * (WS_PROD + WS_CONS)) void graphconv_ws_kernel(
     int64_t M, int L, int hs, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ colidx,
     const float* __restrict__ vals, uint64_t edge_base, uint64_t self_base, const float* __restrict__ X,
     int64_t ldx, const uint16_t* __restrict__ Wf, const float* __restrict__ bias, int relu,
     float* __restrict__ out, int C, DropDev de, int64_t num_tiles, float* __restrict__ Zout, int64_t ldz,
-    const int32_t* __restrict__ eid) {
+    const int32_t* __restrict__ eid, int64_t self_rows) {
   constexpr int F = KS * 16;
   constexpr int KC = F < WS_KC ? F : WS_KC;  // Z columns per unit
   constexpr int NH = F / KC;                  // units per segment
@@ -629,7 +631,8 @@ __global__ __launch_bounds__(64 * (WS_PROD + WS_CONS)) void graphconv_ws_kernel(
           float4 xv[WS_RW];
 #pragma unroll
           for (int i = 0; i < WS_RW; ++i)
-            xv[i] = (i < nvalid && col_ok) ? *reinterpret_cast<const float4*>(X + (rw0 + i) * ldx + col) : zero4();
+            xv[i] = (i < nvalid && rw0 + i < self_rows && col_ok) ? *reinterpret_cast<const float4*>(X + (rw0 + i) * ldx + col)
+                                                                  : zero4();
           if (!claim()) return;
 #pragma unroll
           for (int i = 0; i < WS_RW; ++i) {
@@ -913,11 +916,11 @@ int graphconv_fused_fwd(const GrlTypedCsr* g, const float* X, int64_t ldx, int F
     if (v)                                                                                                           \
       hipLaunchKernelGGL((graphconv_ws_kernel<KS_, true>), dim3((unsigned)grid), dim3(64 * (WS_PROD + WS_CONS)), 0,  \
                          st, M, g->num_types, hs, g->rowptr, g->colidx, g->vals, g->edge_id_base, g->self_id_base, X, \
-                         ldx, Wf, bias, relu, out, C, d, ws_tiles, Z, ldz, nullptr);                                 \
+                         ldx, Wf, bias, relu, out, C, d, ws_tiles, Z, ldz, nullptr, M);                              \
     else                                                                                                             \
       hipLaunchKernelGGL((graphconv_ws_kernel<KS_, false>), dim3((unsigned)grid), dim3(64 * (WS_PROD + WS_CONS)), 0, \
                          st, M, g->num_types, hs, g->rowptr, g->colidx, g->vals, g->edge_id_base, g->self_id_base, X, \
-                         ldx, Wf, bias, relu, out, C, d, ws_tiles, Z, ldz, nullptr);                                 \
+                         ldx, Wf, bias, relu, out, C, d, ws_tiles, Z, ldz, nullptr, M);                              \
   } while (0)
     if (F == 256)
       GRL_WS_LAUNCH(16);
@@ -955,8 +958,9 @@ int graphconv_fused_fwd(const GrlTypedCsr* g, const float* X, int64_t ldx, int F
 // graphconv_ws_kernel with the rows' CSC segments, DropEdge ids through eid,
 // and W's planes taken block-transposed.  Cin = G's width (the forward's C),
 // Cout = dX's width (the forward's F).
-int graphconv_fused_bwd_data(const GrlTypedCsr* gt, const int32_t* eid, const float* G, int64_t ldg, int Cin,
-                             const float* W, int Cout, float* dX, const GrlDropEdge* de, void* ws, hipStream_t st) {
+int graphconv_fused_bwd_data(const GrlTypedCsr* gt, const int32_t* eid, const float* G, int64_t ldg, int64_t self_rows,
+                             int Cin, const float* W, int Cout, float* dX, const GrlDropEdge* de, void* ws,
+                             hipStream_t st) {
   const int hs = gt->has_self ? 1 : 0;
   const int64_t K = (int64_t)(gt->num_types + hs) * Cin;
   uint16_t* Wf = static_cast<uint16_t*>(ws);
@@ -975,12 +979,12 @@ int graphconv_fused_bwd_data(const GrlTypedCsr* gt, const int32_t* eid, const fl
     if (v)                                                                                                           \
       hipLaunchKernelGGL((graphconv_ws_kernel<KS_, true, true>), dim3((unsigned)grid), dim3(64 * (WS_PROD + WS_CONS)), \
                          0, st, M, gt->num_types, hs, gt->rowptr, gt->colidx, gt->vals, gt->edge_id_base,             \
-                         gt->self_id_base, G, ldg, Wf, nullptr, 0, dX, Cout, d, ws_tiles, nullptr, 0, eid);           \
+                         gt->self_id_base, G, ldg, Wf, nullptr, 0, dX, Cout, d, ws_tiles, nullptr, 0, eid, self_rows); \
     else                                                                                                             \
       hipLaunchKernelGGL((graphconv_ws_kernel<KS_, false, true>), dim3((unsigned)grid),                              \
                          dim3(64 * (WS_PROD + WS_CONS)), 0, st, M, gt->num_types, hs, gt->rowptr, gt->colidx,         \
                          gt->vals, gt->edge_id_base, gt->self_id_base, G, ldg, Wf, nullptr, 0, dX, Cout, d, ws_tiles,  \
-                         nullptr, 0, eid);                                                                          \
+                         nullptr, 0, eid, self_rows);                                                               \
   } while (0)
   if (Cin == 256)
     GRL_WSB_LAUNCH(16);

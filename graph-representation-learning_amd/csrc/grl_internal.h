@@ -76,8 +76,9 @@ size_t graphconv_fused_ws_bytes(int64_t K);
 int graphconv_fused_fwd(const GrlTypedCsr* g, const float* X, int64_t ldx, int F, const float* W, const float* bias,
                         int C, int relu, float* out, const GrlDropEdge* de, void* ws, hipStream_t st,
                         float* Z = nullptr);
-int graphconv_fused_bwd_data(const GrlTypedCsr* gt, const int32_t* eid, const float* G, int64_t ldg, int Cin,
-                             const float* W, int Cout, float* dX, const GrlDropEdge* de, void* ws, hipStream_t st);
+int graphconv_fused_bwd_data(const GrlTypedCsr* gt, const int32_t* eid, const float* G, int64_t ldg, int64_t self_rows,
+                             int Cin, const float* W, int Cout, float* dX, const GrlDropEdge* de, void* ws,
+                             hipStream_t st);
 
 // Plain-data copy of GrlDropEdge passed by value to kernels.
 struct DropDev {

@@ -39,7 +39,7 @@ import torch.distributed as dist
 
 from ._lib import trace
 from .graph import DropEdge, TypedGraph
-from .ops import graph_linear, typed_aggregate
+from .ops import graph_conv, graph_linear, typed_aggregate
 
 
 def _world(group) -> int:
@@ -592,6 +592,13 @@ class ShardedGraph:
         bias) over this shard: halo exchange -> typed SpMM -> MFMA linear
         (+ fused ReLU).  Output rows = this rank's nodes.  After backward,
         call allreduce_gradients(layer.parameters()) to complete dW / db.
-        chunks: see aggregate."""
+        chunks: see aggregate.  Unpipelined (chunks=None), the layer after the
+        exchange is grl.ops.graph_conv on [own | halo] rows: on large shards
+        its forward is one kernel and its data gradient the one-kernel form
+        over the shard's typed transpose, whose halo rows then travel home
+        in the exchange's backward."""
+        if chunks is None:
+            return graph_conv(self.exchange(X_loc), self.graph.with_dropedge(dropedge), layer.h_weights, layer.bias,
+                              relu=relu)
         Z = self.aggregate(X_loc, dropedge, chunks)
         return graph_linear(Z, layer.h_weights, layer.bias, relu=relu)

@@ -220,19 +220,21 @@ class TypedGraph:
         return c
 
     def typed_transpose(self):
-        """(gt, eid): the typed transpose of a square graph, built once and
-        cached -- gt's row m, segment t lists the forward rows n with a type-t
-        edge n <- m, in forward-CSR order; eid[e] = entry e's forward CSR
-        position (its DropEdge id minus edge_id_base); values follow.  It is
-        the CSC builder (grl_csr_to_csc: a stable radix sort by column) run
-        with the column of edge (n, t, m) keyed as m * L + t.  The one-kernel
-        data gradient (grl_graphconv_bwd_data) runs the GraphConv forward
-        kernel over it."""
+        """(gt, eid): the typed transpose, built once and cached -- gt's row m
+        (one per column of this graph: a shard's own and halo rows), segment
+        t lists the forward rows n with a type-t edge n <- m, in forward-CSR
+        order; eid[e] = entry e's forward CSR position (its DropEdge id minus
+        edge_id_base); values follow.  It is the CSC builder (grl_csr_to_csc:
+        a stable radix sort by column) run with the column of edge (n, t, m)
+        keyed as m * L + t.  The one-kernel data gradient
+        (grl_graphconv_bwd_data) runs the GraphConv forward kernel over it;
+        rows m < num_rows carry the self term there."""
         tt = self._shared.get("typed_transpose")
         if tt is not None:
             return tt
-        if self.num_rows != self.num_cols or self.self_rows < self.num_rows:
-            raise _lib.GrlError("typed_transpose needs a square graph whose every row has its self loop")
+        if self.self_rows != self.num_rows or self.num_cols < self.num_rows:
+            raise _lib.GrlError("typed_transpose needs every row to own its self loop (self_rows == num_rows) and "
+                                "the rows among the columns")
         L, S = self.num_types, self.segments
         if self.num_cols * L >= 2 ** 31:
             raise _lib.GrlError("typed_transpose: num_cols * num_types exceeds int32")
@@ -246,7 +248,7 @@ class TypedGraph:
         n = max(self.nnz, 1)
         gt = TypedGraph(c["colptr"], (c["zrow"][:n] // S).contiguous(), L, vals=c["cvals"], has_self=self.has_self,
                         num_cols=self.num_rows, edge_id_base=self.edge_id_base, self_id_base=self.self_id_base,
-                        self_rows=self.num_rows) if self.nnz else None
+                        self_rows=self.num_rows) if self.nnz else None  # rows: self.num_cols
         if gt is None:  # no edges: every segment empty
             gt = TypedGraph(torch.zeros(self.num_cols * L + 1, dtype=torch.int32, device=self.device),
                             torch.zeros(0, dtype=torch.int32, device=self.device), L, has_self=self.has_self,

@@ -276,8 +276,9 @@ def graph_conv_bwd_data(g: torch.Tensor, graph: TypedGraph, W: torch.Tensor, F: 
     wblk = (-(-F // nblk) + 3) // 4 * 4 if nblk > 1 else F  # block width, a multiple of 4
     bounds = [(f0, min(F, f0 + wblk)) for f0 in range(0, F, wblk)]
     # cheap pre-checks before the (cached, once per graph) transpose build; the library decides
-    if (C not in (64, 128, 256) or F % 4 or F > 1024 or L > 7 or graph.num_rows != graph.num_cols
-            or graph.self_rows < graph.num_rows or 2.0 * M * S * C * min(b - a for a, b in bounds) < 1.6e10
+    if (C not in (64, 128, 256) or F % 4 or F > 1024 or L > 7 or graph.num_cols < graph.num_rows
+            or graph.self_rows != graph.num_rows or M != graph.num_rows
+            or 2.0 * graph.num_cols * S * C * min(b - a for a, b in bounds) < 1.6e10
             or g.dtype != torch.float32 or not g.is_contiguous() or W.dtype != torch.float32
             or tuple(W.shape) != (S * F, C)):
         return None
@@ -293,12 +294,13 @@ def graph_conv_bwd_data(g: torch.Tensor, graph: TypedGraph, W: torch.Tensor, F: 
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=g.device)
     de = graph.dropedge.to_c() if graph.dropedge is not None else None
     stream = current_stream_handle(g.device)
-    dX = torch.empty(M, F, dtype=torch.float32, device=g.device)
+    rows = graph.num_cols  # dX rows: every column of the graph (a shard's halo rows get partials)
+    dX = torch.empty(rows, F, dtype=torch.float32, device=g.device)
     for f0, f1 in bounds:
         w = f1 - f0
         Wb = W.contiguous() if len(bounds) == 1 else W.view(S, F, C)[:, f0:f1, :].reshape(S * w, C).contiguous()
-        out = dX if len(bounds) == 1 else torch.empty(M, w, dtype=torch.float32, device=g.device)
-        call("grl_graphconv_bwd_data", ctypes.byref(csr), eid.data_ptr(), g.data_ptr(), g.stride(0), C,
+        out = dX if len(bounds) == 1 else torch.empty(rows, w, dtype=torch.float32, device=g.device)
+        call("grl_graphconv_bwd_data", ctypes.byref(csr), eid.data_ptr(), g.data_ptr(), g.stride(0), M, C,
              Wb.data_ptr(), w, out.data_ptr(), ctypes.byref(de) if de is not None else None, ws.data_ptr(), ws_bytes,
              stream)
         if len(bounds) > 1:

@@ -312,8 +312,10 @@ int grl_graphconv_fwd_train(const GrlTypedCsr* g, const float* X, int64_t ldx,
  * (ldg); W the forward h_weights [(has_self+num_types)*F, C]; dX
  * [num_rows, F] contiguous, overwritten.  Floating point: the same products
  * summed in another order than the two-kernel chain (fp32-level difference,
- * tests/test_gpu_graphconv.py).  Square graphs only (gt->num_rows rows of G
- * hold the self terms).  Eligible shapes: a nonzero
+ * tests/test_gpu_graphconv.py).  G has g_rows rows (the forward rows); gt
+ * rows m < g_rows carry the self term w_self(m) G[m] W_0^T, rows beyond
+ * (a node-range shard's halo columns) none -- dX of those rows is the
+ * partial gradient the halo exchange sends home.  Eligible shapes: a nonzero
  * grl_graphconv_bwd_data_workspace_query(), which is also the workspace
  * size; otherwise GRL_E_UNSUPPORTED and the caller runs the chain.       */
 size_t grl_graphconv_bwd_data_workspace_query(const GrlTypedCsr* gt,
@@ -321,8 +323,8 @@ size_t grl_graphconv_bwd_data_workspace_query(const GrlTypedCsr* gt,
                                               int32_t C, const float* W,
                                               int32_t F);
 int grl_graphconv_bwd_data(const GrlTypedCsr* gt, const int32_t* eid,
-                           const float* G, int64_t ldg, int32_t C,
-                           const float* W, int32_t F, float* dX,
+                           const float* G, int64_t ldg, int64_t g_rows,
+                           int32_t C, const float* W, int32_t F, float* dX,
                            const GrlDropEdge* de, void* workspace,
                            size_t workspace_bytes, grl_stream_t stream);
 

@@ -278,3 +278,55 @@ def test_two_ranks_fused_graphconv_on_shards(mode):
     import torch.multiprocessing as mp
 
     mp.spawn(_fused_shard_worker, args=(2, _free_port(), mode), nprocs=2, join=True)
+
+
+def _fused_train_shard_worker(rank, world, port, mode):
+    """One rank of a 2-rank gloo world, a training GraphConv on shards big
+    enough for the one-kernel paths: forward one kernel on [own | halo] rows
+    (out bitwise the one-GPU rows), data gradient one kernel over the shard's
+    typed transpose whose halo rows go home in the exchange's backward (dX
+    and the all-reduced dW / db within fp32 tolerance of one GPU)."""
+    import os
+
+    import torch.distributed as dist
+
+    from gnn.models import GraphConv
+    from grl.dist import allreduce_gradients
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        N, deg, L, F, C = 40_000, 16.0, 6, 256, 256
+        sg = ShardedGraph.synthetic(N, deg, L, kind="er", seed=6, device=DEV, halo=mode)
+        g = TypedGraph.synthetic(N, deg, L, kind="er", seed=6, device=DEV)
+        rb, re = sg.plan.row_begin, sg.plan.row_end
+        gen = torch.Generator().manual_seed(41)
+        X = torch.randn(N, F, generator=gen).to(DEV)
+        R = torch.randn(N, C, generator=gen).to(DEV)
+        de = DropEdge(0.3, 8, 1, True)
+        torch.manual_seed(21)
+        layer = GraphConv(F, C, L).to(DEV)
+        torch.manual_seed(21)
+        layer1 = GraphConv(F, C, L).to(DEV)
+        Xg = X.clone().requires_grad_(True)
+        out1 = layer1.propagate(Xg[None], g.with_dropedge(de), relu=True)[0]
+        (out1 * R).sum().backward()
+        X_loc = X[rb:re].clone().requires_grad_(True)
+        out = sg.graphconv(X_loc, layer, de, relu=True)
+        assert torch.equal(out, out1[rb:re].detach())
+        (out * R[rb:re]).sum().backward()
+        assert "typed_transpose" in sg.graph._shared  # the shard's dX took the one-kernel path
+        allreduce_gradients(layer.parameters())
+        torch.testing.assert_close(X_loc.grad, Xg.grad[rb:re], rtol=1e-4, atol=1e-4)
+        torch.testing.assert_close(layer.h_weights.grad, layer1.h_weights.grad, rtol=1e-4, atol=1e-3)
+        torch.testing.assert_close(layer.bias.grad, layer1.bias.grad, rtol=1e-4, atol=1e-3)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["sparse", "dense"])
+def test_two_ranks_one_kernel_training_layer_on_shards(mode):
+    import torch.multiprocessing as mp
+
+    mp.spawn(_fused_train_shard_worker, args=(2, _free_port(), mode), nprocs=2, join=True)

@@ -305,7 +305,7 @@ def test_bwd_data_falls_back_outside_its_shapes():
     gt, eid = g.typed_transpose()
     csr = gt.csr_c(96)
     G = torch.randn(30_000, 96, device=DEV)
-    rc = _lib.lib().grl_graphconv_bwd_data(ctypes.byref(csr), eid.data_ptr(), G.data_ptr(), 96, 96,
+    rc = _lib.lib().grl_graphconv_bwd_data(ctypes.byref(csr), eid.data_ptr(), G.data_ptr(), 96, 30_000, 96,
                                            torch.empty(7 * 256, 96, device=DEV).data_ptr(), 256,
                                            torch.empty(30_000, 256, device=DEV).data_ptr(), None, None, 0, None)
     assert rc == _lib.GRL_E_UNSUPPORTED
