@@ -298,7 +298,7 @@ def graph_conv_bwd_data(g: torch.Tensor, graph: TypedGraph, W: torch.Tensor, F: 
     dX = torch.empty(rows, F, dtype=torch.float32, device=g.device)
     for f0, f1 in bounds:
         w = f1 - f0
-        Wb = W.contiguous() if len(bounds) == 1 else W.view(S, F, C)[:, f0:f1, :].reshape(S * w, C).contiguous()
+        Wb = W.contiguous() if len(bounds) == 1 else W.reshape(S, F, C)[:, f0:f1, :].reshape(S * w, C).contiguous()
         out = dX if len(bounds) == 1 else torch.empty(rows, w, dtype=torch.float32, device=g.device)
         call("grl_graphconv_bwd_data", ctypes.byref(csr), eid.data_ptr(), g.data_ptr(), g.stride(0), M, C,
              Wb.data_ptr(), w, out.data_ptr(), ctypes.byref(de) if de is not None else None, ws.data_ptr(), ws_bytes,
