@@ -103,14 +103,18 @@ bool pair_rows_enabled() {
   return !(e && e[0] == '0');
 }
 
-// Persistent-grid size: 16 four-wave blocks per CU (tuned on C3).  The
+// Persistent-grid size: 24 four-wave blocks per CU.  Measured
+// (tools/ab_spmm_blocks*.sh, interleaved, two boxes): against 16, C3 forward
+// 6.24 vs 6.41-6.67 ms, p=0.3 forward and CSC backward 2-3 % faster, C4
+// 28.3-28.9 vs 29.1-29.6 ms, C5 125.9 vs 130.3 ms; 20 and 26 are slower
+// than either (6.45-6.55 ms at C3), 22 and 28 close to 24.  The
 // GRL_SPMM_BLOCKS_PER_CU environment variable overrides it (tuning aid, e.g.
 // to leave room for a concurrent GEMM on another stream).
 int spmm_blocks_per_cu() {
   static const int v = [] {
     const char* e = getenv("GRL_SPMM_BLOCKS_PER_CU");
     const int x = e ? atoi(e) : 0;
-    return x > 0 && x <= 64 ? x : 16;
+    return x > 0 && x <= 64 ? x : 24;
   }();
   return v;
 }
