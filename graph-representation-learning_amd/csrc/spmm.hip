@@ -103,6 +103,11 @@ bool pair_rows_enabled() {
   return !(e && e[0] == '0');
 }
 
+// Whole-row (F <= 256) gathers in flight per wave (A/B builds: -DGRL_SPMM_U=n).
+#ifndef GRL_SPMM_U
+#define GRL_SPMM_U 8
+#endif
+
 // Persistent-grid size: 24 four-wave blocks per CU.  Measured
 // (tools/ab_spmm_blocks*.sh, interleaved, two boxes): against 16, C3 forward
 // 6.24 vs 6.41-6.67 ms, p=0.3 forward and CSC backward 2-3 % faster, C4
@@ -654,7 +659,7 @@ int launch_spmm(int64_t num_rows, int64_t self_rows, int S, int hs, const int32_
                            vals, edge_base, self_base, self_row0, src, lds, F, out, ldo, zseg, de, sp, eid,
                            self_rows);
     } else if (sh.nv == 1) {
-      if (v) GRL_SPMM_LAUNCH(4, 1, 8, true); else GRL_SPMM_LAUNCH(4, 1, 8, false);
+      if (v) GRL_SPMM_LAUNCH(4, 1, GRL_SPMM_U, true); else GRL_SPMM_LAUNCH(4, 1, GRL_SPMM_U, false);
     } else if (!BWD && wide_rows_in_flight() == 8) {  // A/B aid: twice the whole rows in flight per wave
       if (v) GRL_SPMM_LAUNCH(4, 2, 8, true); else GRL_SPMM_LAUNCH(4, 2, 8, false);
     } else {
