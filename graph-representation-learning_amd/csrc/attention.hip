@@ -1234,13 +1234,36 @@ int launch_attn(AttnPass pass, const AttnArgs& a0, int64_t B, int S, hipStream_t
   return GRL_OK;
 }
 
-// Key (forward, dQ) / query (dH, dK) split for small N: one workgroup per 128
-// rows leaves the chip idle below ~2 x CUs workgroups; split the loop range
-// into S pieces of >= 256 rows (multiples of 32) whose partials are combined
-// in split order (deterministic).  Returns S, sets *kr (rows per split).
+// Key (forward, dQ) / query (dH, dK) split: the loop range is cut into S
+// pieces of >= 256 rows (multiples of 32) whose partials are combined in
+// split order (deterministic).  The kernels run 2 four-wave workgroups per
+// CU and every workgroup (128 rows x N / S) does the same work, so the grid
+// runs in rounds of 2 x CUs and a partial last round idles the rest of the
+// chip: S is the one (<= 16) that maximises the filled fraction of the
+// rounds, B ceil(N / 128) S / (rounds x 2 CUs), less 0.5 % per extra split
+// (partials and their combine).  N = 100k, 782 workgroups: 1.53 rounds
+// (76 %) unsplit; S = 7 fills 97 % -- forward 17.6 -> 13.9 ms, forward +
+// backward 80.2 -> 61.7 ms (tools/ab_attn_splits.sh).  N = 131072 (1024
+// workgroups, two full rounds) stays unsplit.  Returns S, sets *kr (rows
+// per split).
 int attn_splits(int64_t B, int64_t N, int64_t* kr) {
-  const int64_t blocks = ceil_div(N, 128) * B, want = 2 * (int64_t)device_cu_count();
-  int64_t S = blocks >= want ? 1 : std::min<int64_t>(ceil_div(want, blocks), std::max<int64_t>(1, N / 256));
+  const int64_t blocks = ceil_div(N, 128) * B, slots = 2 * (int64_t)device_cu_count();
+  const int64_t smax = std::max<int64_t>(1, std::min<int64_t>(16, N / 256));
+  auto filled = [&](int64_t s) {
+    const int64_t w = blocks * s;
+    return (double)w / (double)(ceil_div(w, slots) * slots);
+  };
+  int64_t S = 1;
+  double best = filled(1);
+  for (int64_t s = 2; s <= smax; ++s) {
+    const double score = filled(s) - 0.005 * (double)(s - 1);
+    if (score > best + 1e-9) {
+      best = score;
+      S = s;
+    }
+  }
+  const char* e = getenv("GRL_ATTN_SPLITS");  // A/B aid: force the split count
+  if (e && atoi(e) > 0) S = std::min<int64_t>(atoi(e), std::max<int64_t>(1, N / 256));
   S = std::max<int64_t>(1, std::min<int64_t>(S, 64));
   *kr = ceil_div(ceil_div(N, S), 32) * 32;
   return (int)ceil_div(N, *kr);
