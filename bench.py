@@ -577,6 +577,11 @@ def extras(args, graph, X_full, L, F, dev, E_loc, n_loc):
     res["graphconv_layer_fwd_bwd_p0.3"] = {"ms": _time(layer, max(3, iters // 2), warm=3),
                                            "path": "fwd: one kernel writing Z; bwd: dX one kernel over the typed "
                                                    "transpose (grl_graphconv_bwd_data) + dW/db GEMM"}
+    res["graphconv_layer_fwd_bwd_p0.3_recompute"] = {
+        "ms": _time(lambda: graph_conv(Xl, gl, Wp, bp, relu=True, recompute=True).sum().backward(),
+                    max(3, iters // 2), warm=2),
+        "path": "keeps X, not Z (7.2 GB less held): fwd one kernel without Z; bwd dX one kernel that also writes "
+                "G_s = A_s^T g, dW_s = X^T G_s (no re-aggregation)"}
     os.environ["GRL_GRAPHCONV_FUSED_BWD"] = "0"
     try:
         res["graphconv_layer_fwd_bwd_p0.3_chain_bwd"] = {

@@ -959,7 +959,7 @@ int graphconv_fused_fwd(const GrlTypedCsr* g, const float* X, int64_t ldx, int F
 // and W's planes taken block-transposed.  Cin = G's width (the forward's C),
 // Cout = dX's width (the forward's F).
 int graphconv_fused_bwd_data(const GrlTypedCsr* gt, const int32_t* eid, const float* G, int64_t ldg, int64_t self_rows,
-                             int Cin, const float* W, int Cout, float* dX, const GrlDropEdge* de, void* ws,
+                             int Cin, const float* W, int Cout, float* dX, float* Gagg, const GrlDropEdge* de, void* ws,
                              hipStream_t st) {
   const int hs = gt->has_self ? 1 : 0;
   const int64_t K = (int64_t)(gt->num_types + hs) * Cin;
@@ -979,12 +979,12 @@ int graphconv_fused_bwd_data(const GrlTypedCsr* gt, const int32_t* eid, const fl
     if (v)                                                                                                           \
       hipLaunchKernelGGL((graphconv_ws_kernel<KS_, true, true>), dim3((unsigned)grid), dim3(64 * (WS_PROD + WS_CONS)), \
                          0, st, M, gt->num_types, hs, gt->rowptr, gt->colidx, gt->vals, gt->edge_id_base,             \
-                         gt->self_id_base, G, ldg, Wf, nullptr, 0, dX, Cout, d, ws_tiles, nullptr, 0, eid, self_rows); \
+                         gt->self_id_base, G, ldg, Wf, nullptr, 0, dX, Cout, d, ws_tiles, Gagg, K, eid, self_rows); \
     else                                                                                                             \
       hipLaunchKernelGGL((graphconv_ws_kernel<KS_, false, true>), dim3((unsigned)grid),                              \
                          dim3(64 * (WS_PROD + WS_CONS)), 0, st, M, gt->num_types, hs, gt->rowptr, gt->colidx,         \
                          gt->vals, gt->edge_id_base, gt->self_id_base, G, ldg, Wf, nullptr, 0, dX, Cout, d, ws_tiles,  \
-                         nullptr, 0, eid, self_rows);                                                               \
+                         Gagg, K, eid, self_rows);                                                                  \
   } while (0)
   if (Cin == 256)
     GRL_WSB_LAUNCH(16);

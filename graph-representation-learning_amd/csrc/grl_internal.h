@@ -77,7 +77,7 @@ int graphconv_fused_fwd(const GrlTypedCsr* g, const float* X, int64_t ldx, int F
                         int C, int relu, float* out, const GrlDropEdge* de, void* ws, hipStream_t st,
                         float* Z = nullptr);
 int graphconv_fused_bwd_data(const GrlTypedCsr* gt, const int32_t* eid, const float* G, int64_t ldg, int64_t self_rows,
-                             int Cin, const float* W, int Cout, float* dX, const GrlDropEdge* de, void* ws,
+                             int Cin, const float* W, int Cout, float* dX, float* Gagg, const GrlDropEdge* de, void* ws,
                              hipStream_t st);
 
 // Plain-data copy of GrlDropEdge passed by value to kernels.

@@ -1363,7 +1363,7 @@ extern "C" size_t grl_graphconv_bwd_data_workspace_query(const GrlTypedCsr* gt, 
 }
 
 extern "C" int grl_graphconv_bwd_data(const GrlTypedCsr* gt, const int32_t* eid, const float* G, int64_t ldg,
-                                      int64_t g_rows, int32_t C, const float* W, int32_t F, float* dX,
+                                      int64_t g_rows, int32_t C, const float* W, int32_t F, float* dX, float* G_agg,
                                       const GrlDropEdge* de, void* workspace, size_t workspace_bytes,
                                       grl_stream_t stream) {
   TraceRange trace_("grl_graphconv_bwd_data");
@@ -1381,7 +1381,7 @@ extern "C" int grl_graphconv_bwd_data(const GrlTypedCsr* gt, const int32_t* eid,
   const size_t need = graphconv_fused_ws_bytes((int64_t)(gt->num_types + (gt->has_self ? 1 : 0)) * C);
   if (!workspace || !al16(workspace) || workspace_bytes < need)
     GRL_FAIL(GRL_E_WORKSPACE, "grl_graphconv_bwd_data: workspace %zu < %zu (16-B aligned)", workspace_bytes, need);
-  return graphconv_fused_bwd_data(gt, eid, G, ldg, g_rows, C, W, F, dX, de, workspace, as_stream(stream));
+  return graphconv_fused_bwd_data(gt, eid, G, ldg, g_rows, C, W, F, dX, G_agg, de, workspace, as_stream(stream));
 }
 
 extern "C" int grl_graphconv_fwd_train(const GrlTypedCsr* g, const float* X, int64_t ldx, int32_t F, const float* W,

@@ -142,7 +142,7 @@ SIGNATURES = {
                                          _c_vp, _P(GrlDropEdge), _c_vp, _c_size, _c_vp]),
     "grl_graphconv_bwd_data_workspace_query": (_c_size, [_P(GrlTypedCsr), _c_vp, _c_i64, _c_i32, _c_vp, _c_i32]),
     "grl_graphconv_bwd_data": (_c_i32, [_P(GrlTypedCsr), _c_vp, _c_vp, _c_i64, _c_i64, _c_i32, _c_vp, _c_i32,
-                                        _c_vp, _P(GrlDropEdge), _c_vp, _c_size, _c_vp]),
+                                        _c_vp, _c_vp, _P(GrlDropEdge), _c_vp, _c_size, _c_vp]),
     "grl_graphconv_fwd": (_c_i32, [_P(GrlTypedCsr), _c_vp, _c_i64, _c_i32, _c_vp, _c_vp, _c_i32, _c_i32, _c_vp,
                                    _P(GrlDropEdge), _c_vp, _c_size, _c_vp]),
     "grl_linear_fwd_workspace_size": (_c_size, [_c_i64, _c_i32, _c_i32]),

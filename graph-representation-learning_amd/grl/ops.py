@@ -259,7 +259,8 @@ def _bwd_data_enabled() -> bool:
     return os.environ.get("GRL_GRAPHCONV_FUSED_BWD", "1") != "0"
 
 
-def graph_conv_bwd_data(g: torch.Tensor, graph: TypedGraph, W: torch.Tensor, F: int, relu_out=None):
+def graph_conv_bwd_data(g: torch.Tensor, graph: TypedGraph, W: torch.Tensor, F: int, relu_out=None,
+                        want_aggregate: bool = False):
     """dX of one GraphConv layer in one kernel (grl_graphconv_bwd_data):
     dX = sum_s (A_drop,s^T g) W_s^T over the graph's typed transpose, for g
     the output gradient ([num_rows, C]; through the ReLU's [relu_out > 0]
@@ -267,7 +268,9 @@ def graph_conv_bwd_data(g: torch.Tensor, graph: TypedGraph, W: torch.Tensor, F: 
     <= 256-column block of dX (the gather repeats per block; dZ still never
     exists).  None when the shape is outside the one-kernel path (the caller
     then runs dZ = g W^T and the CSC gather).  GRL_GRAPHCONV_FUSED_BWD=0
-    disables it."""
+    disables it.  want_aggregate: return (dX, G_agg, g_eff) with G_agg =
+    [A_drop,s^T g_eff]_s ([num_cols, segments * C], written by the same
+    kernel) and g_eff the gradient through the ReLU, for dW_s = X^T G_agg_s."""
     if not _bwd_data_enabled() or isinstance(graph, EdgeBlockedGraph):
         return None
     M, C = g.shape
@@ -296,16 +299,17 @@ def graph_conv_bwd_data(g: torch.Tensor, graph: TypedGraph, W: torch.Tensor, F: 
     stream = current_stream_handle(g.device)
     rows = graph.num_cols  # dX rows: every column of the graph (a shard's halo rows get partials)
     dX = torch.empty(rows, F, dtype=torch.float32, device=g.device)
-    for f0, f1 in bounds:
+    G_agg = torch.empty(rows, S * C, dtype=torch.float32, device=g.device) if want_aggregate else None
+    for i, (f0, f1) in enumerate(bounds):
         w = f1 - f0
         Wb = W.contiguous() if len(bounds) == 1 else W.reshape(S, F, C)[:, f0:f1, :].reshape(S * w, C).contiguous()
         out = dX if len(bounds) == 1 else torch.empty(rows, w, dtype=torch.float32, device=g.device)
         call("grl_graphconv_bwd_data", ctypes.byref(csr), eid.data_ptr(), g.data_ptr(), g.stride(0), M, C,
-             Wb.data_ptr(), w, out.data_ptr(), ctypes.byref(de) if de is not None else None, ws.data_ptr(), ws_bytes,
-             stream)
+             Wb.data_ptr(), w, out.data_ptr(), G_agg.data_ptr() if G_agg is not None and i == 0 else None,
+             ctypes.byref(de) if de is not None else None, ws.data_ptr(), ws_bytes, stream)
         if len(bounds) > 1:
             dX[:, f0:f1] = out
-    return dX
+    return (dX, G_agg, g) if want_aggregate else dX
 
 
 class _GraphConv(torch.autograd.Function):
@@ -337,11 +341,24 @@ class _GraphConv(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g: torch.Tensor):
         Z, W, out = ctx.saved_tensors
-        if ctx.recompute and (ctx.needs_input_grad[2] or (ctx.has_b and ctx.needs_input_grad[3])):
-            Z = spmm_forward(Z, ctx.graph)
         g, mask = relu_grad(g.contiguous().float(), out if ctx.relu else None)
         want_w = ctx.needs_input_grad[2]
         want_b = ctx.has_b and ctx.needs_input_grad[3]
+        if ctx.recompute and ctx.needs_input_grad[0] and want_w:
+            # X was kept, not Z: the one-kernel data gradient also writes G_s = A_drop,s^T g and
+            # dW_s = Z_s^T g = X^T G_s -- no re-aggregation of Z (same products, another order)
+            res = graph_conv_bwd_data(g, ctx.graph, W, ctx.xshape[-1], mask, want_aggregate=True)
+            if res is not None:
+                dX, G_agg, g_eff = res
+                X2 = _rows_view(Z)
+                S, F, C = ctx.graph.segments, X2.shape[1], g.shape[1]
+                dWt, _ = linear_bwd_weight(X2, G_agg, None, False)  # [F, S*C]
+                del G_agg
+                dW = dWt.view(F, S, C).transpose(0, 1).reshape(S * F, C)
+                db = g_eff.sum(0) if want_b else None
+                return dX.view(ctx.xshape), None, dW, db, None, None
+        if ctx.recompute and (want_w or want_b):
+            Z = spmm_forward(Z, ctx.graph)
         dW = db = dX = None
         if ctx.needs_input_grad[0]:
             F = ctx.xshape[-1]

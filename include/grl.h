@@ -315,7 +315,11 @@ int grl_graphconv_fwd_train(const GrlTypedCsr* g, const float* X, int64_t ldx,
  * tests/test_gpu_graphconv.py).  G has g_rows rows (the forward rows); gt
  * rows m < g_rows carry the self term w_self(m) G[m] W_0^T, rows beyond
  * (a node-range shard's halo columns) none -- dX of those rows is the
- * partial gradient the halo exchange sends home.  Eligible shapes: a nonzero
+ * partial gradient the halo exchange sends home.  G_agg (NULL, or
+ * [gt->num_rows, (has_self+num_types)*C] contiguous) also receives the
+ * gathered sums A_drop,s^T G per segment -- with them the weight gradient
+ * is dW_s = X^T (A_drop,s^T G), so a layer that kept X instead of Z needs
+ * no re-aggregation (grl.ops.graph_conv, recompute mode).  Eligible shapes: a nonzero
  * grl_graphconv_bwd_data_workspace_query(), which is also the workspace
  * size; otherwise GRL_E_UNSUPPORTED and the caller runs the chain.       */
 size_t grl_graphconv_bwd_data_workspace_query(const GrlTypedCsr* gt,
@@ -325,8 +329,9 @@ size_t grl_graphconv_bwd_data_workspace_query(const GrlTypedCsr* gt,
 int grl_graphconv_bwd_data(const GrlTypedCsr* gt, const int32_t* eid,
                            const float* G, int64_t ldg, int64_t g_rows,
                            int32_t C, const float* W, int32_t F, float* dX,
-                           const GrlDropEdge* de, void* workspace,
-                           size_t workspace_bytes, grl_stream_t stream);
+                           float* G_agg, const GrlDropEdge* de,
+                           void* workspace, size_t workspace_bytes,
+                           grl_stream_t stream);
 
 /* Backward of grl_linear_fwd (autograd MmBackward0 of robust_gcn.py:50, with
  * the ReLU of drop_robust_gcn.py:76 folded in when relu_out != NULL):

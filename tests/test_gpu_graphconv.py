@@ -307,5 +307,42 @@ def test_bwd_data_falls_back_outside_its_shapes():
     G = torch.randn(30_000, 96, device=DEV)
     rc = _lib.lib().grl_graphconv_bwd_data(ctypes.byref(csr), eid.data_ptr(), G.data_ptr(), 96, 30_000, 96,
                                            torch.empty(7 * 256, 96, device=DEV).data_ptr(), 256,
-                                           torch.empty(30_000, 256, device=DEV).data_ptr(), None, None, 0, None)
+                                           torch.empty(30_000, 256, device=DEV).data_ptr(), None, None, None, 0, None)
     assert rc == _lib.GRL_E_UNSUPPORTED
+
+
+@pytest.mark.parametrize("de", [None, DropEdge(0.3, 4, 2, True)])
+def test_recompute_takes_weight_gradient_from_the_aggregate(de):
+    """recompute=True on a one-kernel-eligible layer: X is kept, not Z, and
+    the backward re-aggregates nothing -- the data-gradient kernel also
+    writes G_s = A_drop,s^T g and dW_s = X^T G_s.  out and dX bitwise the
+    saved-Z path's; dW and db the same products in another order (within
+    1e-5 of the sums of |terms|); the held memory drops by Z."""
+    from grl.ops import linear_bwd_weight, spmm_forward
+
+    N, L, F, C = 20_011, 6, 256, 256
+    g = TypedGraph.synthetic(N, 16.0, L, seed=3, device=DEV).with_dropedge(de)
+    gen = torch.Generator(device=DEV).manual_seed(5)
+    X0 = torch.randn(N, F, device=DEV, generator=gen)
+    W0 = torch.randn(7 * F, C, device=DEV, generator=gen) / 40
+    b0 = torch.randn(C, device=DEV, generator=gen)
+    R = torch.randn(N, C, device=DEV, generator=gen)
+    res, held = {}, {}
+    for rc in (False, True):
+        X, W, b = (t.clone().requires_grad_(True) for t in (X0, W0, b0))
+        torch.cuda.synchronize()
+        base = torch.cuda.memory_allocated(DEV)
+        out = graph_conv(X, g, W, b, relu=True, recompute=rc)
+        torch.cuda.synchronize()
+        held[rc] = torch.cuda.memory_allocated(DEV) - base
+        (out * R).sum().backward()
+        res[rc] = (out.detach(), X.grad, W.grad, b.grad)
+        del out
+    assert torch.equal(res[True][0], res[False][0]) and torch.equal(res[True][1], res[False][1])
+    assert held[False] - held[True] >= 0.9 * N * 7 * F * 4, held
+    ge = torch.where(res[False][0] > 0, R, torch.zeros((), device=DEV))
+    Z = spmm_forward(X0, g)
+    bound_w, _ = linear_bwd_weight(Z.abs(), ge.abs(), None, False)
+    assert bool(((res[True][2] - res[False][2]).abs() <= 1e-5 * bound_w + 1e-6).all())
+    bound_b = ge.abs().sum(0)
+    assert bool(((res[True][3] - res[False][3]).abs() <= 1e-5 * bound_b + 1e-6).all())
