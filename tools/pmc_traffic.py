@@ -31,7 +31,7 @@ def per_dispatch(path, counter, substr):
 
 def main():
     key, fdir, wdir = sys.argv[1:4]
-    substr = sys.argv[4] if len(sys.argv) > 4 else "spmm_kernel<4, 1, 8, false, false>"
+    substr = sys.argv[4] if len(sys.argv) > 4 else "spmm_kernel<4, 1, 8, false, false, false>"
     f = per_dispatch(fdir, "FETCH_SIZE", substr)
     w = per_dispatch(wdir, "WRITE_SIZE", substr)
     # FETCH_SIZE correction measured on this kernel's own access pattern (tools/pmc_calib.py:
