@@ -187,15 +187,15 @@ def test_two_ranks_on_one_gpu_match_single_gpu(mode, kind):
     mp.spawn(_shard_worker, args=(2, _free_port(), mode, kind), nprocs=2, join=True)
 
 
-def _bench_two_ranks(extra):
+def _bench_two_ranks(extra, nproc=2):
     import json
     import os
     import subprocess
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", str(nproc),
            "--dist-backend", "gloo", "--steps", "2", "--warmup", "1", "--cpu-seconds", "0"] + extra
     r = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=280)
     assert r.returncode == 0, r.stderr[-2000:]
@@ -205,7 +205,7 @@ def _bench_two_ranks(extra):
     for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
               "vs_baseline", "dtype", "data", "config", "roofline", "halo"):
         assert k in out, k
-    assert out["n_gpus"] == 2 and out["value"] > 0
+    assert out["n_gpus"] == nproc and out["value"] > 0
     return out
 
 
@@ -230,6 +230,17 @@ def test_bench_two_ranks_weak_and_c5_shape():
     out = _bench_two_ranks(["--workload", "C5", "--nodes-per-gpu", "65536", "--chunks", "4"])
     assert out["config"]["graph"] == "rmat" and out["config"]["d"] == 512 and out["config"]["dropedge_p"] == 0.2
     assert out["config"]["nodes_total"] == 131072 and out["halo"]["chunks"] == 4
+
+
+def test_bench_four_ranks_c4_shape():
+    """World 4 (the driver's N=4 launch shape): a C4-style ER graph at 20k
+    nodes cut into 4 node-range shards, dense halo pipelined over 2 slices;
+    one JSON line, the halo breakdown in both directions.  (The full 4M-node
+    C4 at P=4 ran the same way: tools/rehearse_p4.sh,
+    profiles/r02_rehearse_p4_c4_line.json.)"""
+    out = _bench_two_ranks(["--workload", "weak", "--nodes-per-gpu", "20000"], nproc=4)
+    assert out["config"]["nodes_total"] == 80000 and out["halo"]["chunks"] == 2
+    assert "error" not in out["halo"]["backward"]
 
 
 def _fused_shard_worker(rank, world, port, mode):
