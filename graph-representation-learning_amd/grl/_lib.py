@@ -163,6 +163,9 @@ SIGNATURES = {
     "grl_split_plan_count": (_c_i32, [_c_vp, _c_i64, _c_i32, _c_i32, _c_i32, _c_vp, _c_vp, _c_size, _c_vp]),
     "grl_split_plan_build": (_c_i32, [_c_vp, _c_i64, _c_i32, _P(GrlSplitPlan), _c_vp, _c_size, _c_vp]),
     "grl_bag_linear_fwd": (_c_i32, [_c_vp, _c_i64, _c_i64, _c_i32, _c_vp, _c_i32, _c_vp, _c_i32, _c_vp, _c_vp]),
+    "grl_bag_linear_bwd_weight_workspace_size": (_c_size, [_c_i64, _c_i32, _c_i32]),
+    "grl_bag_linear_bwd_weight": (_c_i32, [_c_vp, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_i32, _c_i32, _c_vp,
+                                           _c_size, _c_vp]),
     "grl_node_attention_workspace_size": (_c_size, [_c_i64, _c_i64, _c_i32, _c_i32]),
     "grl_node_attention_fwd": (_c_i32, [_c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_i64,
                                         _c_i32, _c_i32, _c_vp, _c_size, _c_vp]),

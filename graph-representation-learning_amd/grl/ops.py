@@ -581,6 +581,28 @@ def bag_linear_forward(V2: torch.Tensor, Wt: torch.Tensor, b, relu: bool) -> tor
     return out
 
 
+# emb1's weight gradient on the sparse kernel from this many rows on (A/B at
+# K = 4369, C = 256, ~7 + 4 nonzeros per row, profiles/r02_probe_bag_dw.json:
+# M = 4096 dense GEMM 0.16 vs sparse 0.26 ms; 20k 0.59 vs 0.49; 100k 2.72 vs 1.63)
+BAG_DW_SPARSE_ROWS = 16384
+
+
+def bag_linear_bwd_weight(V2: torch.Tensor, g: torch.Tensor, relu_out, want_db: bool):
+    """(dWt [K, C], db [C] or None) = V2^T g', 1^T g' with g' = g [out > 0],
+    reading a row of g' only for V2's nonzeros (grl_bag_linear_bwd_weight)."""
+    M, K = V2.shape
+    C = g.shape[1]
+    dWt = torch.empty(K, C, dtype=torch.float32, device=g.device)
+    db = torch.empty(C, dtype=torch.float32, device=g.device) if want_db else None
+    ws_bytes = _lib.lib().grl_bag_linear_bwd_weight_workspace_size(M, K, C)
+    ws = torch.empty(max(ws_bytes, 1), dtype=torch.uint8, device=g.device)
+    call("grl_bag_linear_bwd_weight", V2.data_ptr(), V2.stride(0), g.data_ptr(),
+         relu_out.data_ptr() if relu_out is not None else None, dWt.data_ptr(),
+         db.data_ptr() if db is not None else None, M, K, C, ws.data_ptr(), ws_bytes,
+         current_stream_handle(g.device))
+    return dWt, db
+
+
 class _BagLinear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, V2, W, b, relu: bool):
@@ -596,7 +618,10 @@ class _BagLinear(torch.autograd.Function):
         V2, Wt, out = ctx.saved_tensors
         g, relu_out = relu_grad(g.contiguous().float(), out if ctx.relu else None)
         dV = linear_bwd_data(g, relu_out, Wt) if ctx.needs_input_grad[0] else None
-        dWt, db = linear_bwd_weight(V2, g, relu_out, ctx.has_b)
+        if V2.shape[0] >= BAG_DW_SPARSE_ROWS:  # large M: only V's nonzeros read a row of g
+            dWt, db = bag_linear_bwd_weight(V2, g, relu_out, ctx.has_b)
+        else:  # few rows: the split-K MFMA GEMM is faster (tools/probe_bag_dw.py)
+            dWt, db = linear_bwd_weight(V2, g, relu_out, ctx.has_b)
         return dV, dWt.t(), db, None
 
 

@@ -360,11 +360,24 @@ int grl_linear_bwd_weight(const float* Z, int64_t ldz, const float* g,
  *   out[m, :] = relu?(bias + sum_{k: V[m,k] != 0, ascending} V[m,k] Wt[k, :])
  * V [M, K] row stride ldv (dense storage, mostly zeros), Wt [K, C]
  * contiguous (= nn.Linear.weight^T), bias [C] or NULL, out [M, C].  Only the
- * nonzeros cost gathers; C in [1, 512].  Backward: grl_linear_bwd_weight
- * with Z = V gives dWt and db.                                             */
+ * nonzeros cost gathers; C in [1, 512].  Backward: grl_bag_linear_bwd_weight
+ * (dWt, db) and grl_linear_bwd_data (dV).                                 */
 int grl_bag_linear_fwd(const float* V, int64_t ldv, int64_t M, int32_t K,
                        const float* Wt, int32_t C, const float* bias,
                        int32_t relu, float* out, grl_stream_t stream);
+
+/* emb1's weight gradient (autograd MmBackward0 / AddmmBackward0 of
+ * drop_robust_gcn.py:64 through nn.Linear) on the same sparse rows:
+ *   dWt[k, :] = sum_{m: V[m,k] != 0, ascending m} V[m,k] g'[m, :],
+ *   db = sum_m g'[m, :],   g' = g * [relu_out > 0] (relu_out NULL: g' = g).
+ * V [M, K] stride ldv, g / relu_out [M, C] contiguous, dWt [K, C], db [C] or
+ * NULL; C in [1, 512].  Only V's nonzeros read a row of g'.  Row ranges are
+ * summed in range order (deterministic).  Workspace from the query.       */
+size_t grl_bag_linear_bwd_weight_workspace_size(int64_t M, int32_t K, int32_t C);
+int grl_bag_linear_bwd_weight(const float* V, int64_t ldv, const float* g,
+                              const float* relu_out, float* dWt, float* db,
+                              int64_t M, int32_t K, int32_t C, void* workspace,
+                              size_t workspace_bytes, grl_stream_t stream);
 
 /* ---------------------------------------------------------------------- */
 /* Node self-attention                                                     */

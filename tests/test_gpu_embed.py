@@ -76,3 +76,68 @@ def test_errors():
         bag_linear(V, torch.zeros(600, 8, device=DEV), None)
     with pytest.raises(_lib.GrlError):
         bag_linear(V.cpu(), torch.zeros(4, 8), None)
+
+
+def _dw_ref(V, g, relu_out):
+    """float64 dWt, db and the Sigma|terms| bound per element."""
+    gd = g.double()
+    if relu_out is not None:
+        gd = torch.where(relu_out > 0, gd, torch.zeros((), dtype=gd.dtype, device=gd.device))
+    Vd = V.double()
+    return Vd.T @ gd, gd.sum(0), Vd.abs().T @ gd.abs(), gd.abs().sum(0)
+
+
+@pytest.mark.parametrize("M,K,C,relu", [(20_000, 4369, 256, False), (5_000, 4369, 53, True), (3_100, 300, 512, True),
+                                        (1, 17, 8, False)])
+def test_bag_weight_gradient_sparse_kernel(M, K, C, relu):
+    """grl_bag_linear_bwd_weight (emb1's dW / db, one row of g' per nonzero of V)
+    against float64 within 1e-5 of sum|terms|, on bag rows (the 4 dense box
+    columns make the heaviest column block), several row ranges (M > 1536),
+    the fused ReLU mask, C > 256; run to run bitwise."""
+    from grl.ops import bag_linear_bwd_weight
+
+    V = _bag_rows(M, K, seed=M) if K > 8 else torch.randn(M, K, device=DEV)
+    gen = torch.Generator(device=DEV).manual_seed(5)
+    g = torch.randn(M, C, generator=gen, device=DEV)
+    relu_out = torch.relu(torch.randn(M, C, generator=gen, device=DEV)) if relu else None
+    dWt, db = bag_linear_bwd_weight(V, g, relu_out, True)
+    rW, rb, aW, ab = _dw_ref(V, g, relu_out)
+    assert float(((dWt.double() - rW).abs() - 1e-5 * aW).max()) <= 1e-30
+    assert float(((db.double() - rb).abs() - 1e-5 * ab).max()) <= 1e-30
+    dWt2, db2 = bag_linear_bwd_weight(V, g, relu_out, True)
+    assert torch.equal(dWt, dWt2) and torch.equal(db, db2)
+    dWt3, none = bag_linear_bwd_weight(V, g, relu_out, False)
+    assert none is None and torch.equal(dWt, dWt3)
+
+
+def test_bag_weight_gradient_dense_rows_and_strided_V():
+    """Every entry nonzero (the list holds whole chunks) and V a column slice
+    of a wider tensor (ldv > K)."""
+    from grl.ops import bag_linear_bwd_weight
+
+    big = torch.randn(700, 130, device=DEV)
+    V = big[:, :100]
+    g = torch.randn(700, 40, device=DEV)
+    dWt, db = bag_linear_bwd_weight(V, g, None, True)
+    rW, rb, aW, ab = _dw_ref(V, g, None)
+    assert float(((dWt.double() - rW).abs() - 1e-5 * aW).max()) <= 1e-30
+    assert float(((db.double() - rb).abs() - 1e-5 * ab).max()) <= 1e-30
+
+
+def test_model_path_routes_large_bags_to_the_sparse_gradient():
+    """bag_linear's backward at M >= BAG_DW_SPARSE_ROWS takes the sparse dW
+    kernel and still matches float64 (1e-5 of sum|terms|)."""
+    from grl.ops import BAG_DW_SPARSE_ROWS
+
+    M, K, C = BAG_DW_SPARSE_ROWS + 100, 4369, 64
+    V = _bag_rows(M, K, seed=11)
+    W = (torch.randn(C, K, generator=torch.Generator().manual_seed(2)) / 8).to(DEV).requires_grad_(True)
+    b = torch.zeros(C, device=DEV, requires_grad=True)
+    out = bag_linear(V, W, b, relu=True)
+    dout = torch.randn(out.shape, generator=torch.Generator(device=DEV).manual_seed(3), device=DEV)
+    out.backward(dout)
+    gref = torch.where(out.detach() > 0, dout, torch.zeros((), device=DEV)).double()
+    rW = (V.double().T @ gref).T
+    aW = (V.double().abs().T @ gref.abs()).T
+    assert float(((W.grad.double() - rW).abs() - 1e-5 * aW).max()) <= 1e-30
+    torch.testing.assert_close(b.grad.double(), gref.sum(0), rtol=1e-5, atol=1e-4)
