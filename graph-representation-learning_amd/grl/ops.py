@@ -583,7 +583,7 @@ def bag_linear_forward(V2: torch.Tensor, Wt: torch.Tensor, b, relu: bool) -> tor
 
 # emb1's weight gradient on the sparse kernel from this many rows on (A/B at
 # K = 4369, C = 256, ~7 + 4 nonzeros per row, profiles/r02_probe_bag_dw.json:
-# M = 4096 dense GEMM 0.16 vs sparse 0.26 ms; 20k 0.59 vs 0.49; 100k 2.72 vs 1.63)
+# M = 4096 dense GEMM 0.16 vs sparse 0.25 ms; 20k 0.59 vs 0.47; 100k 2.71 vs 1.51)
 BAG_DW_SPARSE_ROWS = 16384
 
 
