@@ -141,3 +141,18 @@ def test_model_path_routes_large_bags_to_the_sparse_gradient():
     aW = (V.double().abs().T @ gref.abs()).T
     assert float(((W.grad.double() - rW).abs() - 1e-5 * aW).max()) <= 1e-30
     torch.testing.assert_close(b.grad.double(), gref.sum(0), rtol=1e-5, atol=1e-4)
+
+
+def test_bag_weight_gradient_edges():
+    """No rows: zero gradients; one output column; all-zero V (no entries)."""
+    from grl.ops import bag_linear_bwd_weight
+
+    dWt, db = bag_linear_bwd_weight(torch.zeros(0, 30, device=DEV), torch.zeros(0, 7, device=DEV), None, True)
+    assert dWt.shape == (30, 7) and not dWt.any() and not db.any()
+    V = _bag_rows(3000, 100, seed=4)
+    g = torch.randn(3000, 1, device=DEV)
+    dWt, db = bag_linear_bwd_weight(V, g, None, True)
+    torch.testing.assert_close(dWt.double(), V.double().T @ g.double(), rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(db.double(), g.double().sum(0), rtol=1e-5, atol=1e-4)
+    dWt, db = bag_linear_bwd_weight(torch.zeros(2000, 50, device=DEV), torch.randn(2000, 9, device=DEV), None, False)
+    assert db is None and not dWt.any()
