@@ -5,6 +5,8 @@ roofline, d=256, 1/2/4/8 GPU".
 
     python bench.py [--gpus N --steps K --warmup W] [--workload C3|C4|C5|C2|weak]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one rank per GPU)
+With --gpus N > 1 and no launcher (WORLD_SIZE unset) bench.py starts the N
+rank processes itself (spawn_ranks); under a launcher WORLD_SIZE must equal N.
 
 Workloads (BASELINE.json configs):
   C3 (default at N=1)  seeded Erdos-Renyi typed graph, N=1M, avg total
@@ -121,12 +123,80 @@ def _events(n):
     return [torch.cuda.Event(enable_timing=True) for _ in range(n)]
 
 
+def _free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_ranks(nproc):
+    """`python bench.py --gpus N` (N > 1) without a launcher: start N rank
+    processes of this same command (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*
+    as torch.distributed.run sets them, rendezvous on 127.0.0.1) and relay
+    rank 0's output.  This parent never touches a GPU and never execs: it
+    waits for the children, stops the rest when one fails, and exits with
+    the first failing status."""
+    import signal
+    import subprocess
+    import threading
+
+    port = str(_free_port())
+    procs = []
+    for r in range(nproc):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nproc), LOCAL_WORLD_SIZE=str(nproc),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, "-u", os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=subprocess.PIPE if r == 0 else None, text=True, start_new_session=True))
+
+    def relay():  # rank 0's stdout (the JSON line), as it comes
+        for line in procs[0].stdout:
+            sys.stdout.write(line)
+            sys.stdout.flush()
+
+    t = threading.Thread(target=relay, daemon=True)
+    t.start()
+    status = 0
+    live = set(range(nproc))
+    while live:
+        for r in sorted(live):
+            rc = procs[r].poll()
+            if rc is None:
+                continue
+            live.discard(r)
+            if rc != 0 and status == 0:
+                status = rc if rc > 0 else 128 - rc
+                print(f"bench.py: rank {r} exited with status {rc}; stopping the other ranks", file=sys.stderr,
+                      flush=True)
+                for q in live:
+                    try:
+                        os.killpg(procs[q].pid, signal.SIGTERM)  # the exact process group this parent started
+                    except ProcessLookupError:
+                        pass
+        time.sleep(0.2)
+    t.join(timeout=10)
+    return status
+
+
 def main():
     args = parse()
+    if args.gpus < 1:
+        raise SystemExit(f"--gpus must be >= 1 (got {args.gpus})")
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            raise SystemExit(spawn_ranks(args.gpus))
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        raise SystemExit(f"bench.py: WORLD_SIZE={os.environ['WORLD_SIZE']} from the launcher but --gpus {args.gpus}: "
+                         "launch one rank per GPU with --gpus equal to the number of ranks")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     ndev = torch.cuda.device_count()
+    if ndev == 0:
+        raise SystemExit(f"bench.py rank {rank}: no ROCm GPU visible (the path runs on MI355X only)")
     if args.dist_backend == "nccl" and world > 1 and local_rank >= ndev:
         raise SystemExit(f"rank {rank}: LOCAL_RANK {local_rank} but only {ndev} GPU(s) visible")
     dev = torch.device("cuda", local_rank % ndev)

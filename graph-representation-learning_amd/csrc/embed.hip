@@ -132,6 +132,11 @@ void launch_bag(const float* V, int64_t ldv, int64_t M, int K, const float* Wt, 
 constexpr int DW_KB = 16;
 constexpr int DW_ROWS = 256;  // chunk height (A/B 64 / 128 / 256 at M = 100k: 1.83 / 1.62 / 1.52 ms)
 constexpr int DW_U = 16;
+// ent_key packs (column in block << 8) | row in chunk
+static_assert(DW_ROWS <= 256 && DW_KB <= 16, "bag_dw_kernel's ent_key holds the row in 8 bits");
+// LDS per workgroup: ent_key + ent_v (2 x 4 x DW_KB x DW_ROWS B) + acc_s (4 x DW_KB x 256 x CPT B) + 16 B.
+// CPT = 2 (C in (256, 512]) needs 65,552 B: more than 64 KiB, within gfx950's 160 KB per workgroup.
+static_assert(2 * 4 * DW_KB * DW_ROWS + 4 * DW_KB * 256 * 2 + 16 <= 160 * 1024, "bag_dw_kernel<2> exceeds gfx950 LDS");
 
 template <int CPT>  // output columns per thread: C <= 256 * CPT
 __global__ __launch_bounds__(256) void bag_dw_kernel(const float* __restrict__ V, int64_t ldv, int64_t M, int K,
@@ -282,7 +287,14 @@ __global__ void bag_dw_reduce_kernel(const float* __restrict__ part, int S, int 
   }
 }
 
-int bag_dw_splits(int64_t M) { return (int)std::max<int64_t>(1, std::min<int64_t>(128, ceil_div(M, 512))); }
+// Row splits of the sparse dW: up to 128 ranges of >= 512 rows, and at most
+// DW_PART_BUDGET bytes of fp32 partials (every split writes its whole
+// Keff x C slab, which the ordered reduce reads back).
+constexpr int64_t DW_PART_BUDGET = 128ll << 20;
+int bag_dw_splits(int64_t M, int64_t Keff, int64_t C) {
+  const int64_t by_mem = std::max<int64_t>(1, DW_PART_BUDGET / std::max<int64_t>(1, Keff * C * 4));
+  return (int)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(128, by_mem), ceil_div(M, 512)));
+}
 
 }  // namespace
 }  // namespace grl
@@ -312,7 +324,7 @@ extern "C" int grl_bag_linear_fwd(const float* V, int64_t ldv, int64_t M, int32_
 
 extern "C" size_t grl_bag_linear_bwd_weight_workspace_size(int64_t M, int32_t K, int32_t C) {
   if (M <= 0 || K < 0 || C <= 0) return 0;
-  return (size_t)bag_dw_splits(M) * (size_t)(K + 1) * (size_t)C * 4;
+  return (size_t)bag_dw_splits(M, (int64_t)K + 1, C) * (size_t)(K + 1) * (size_t)C * 4;
 }
 
 extern "C" int grl_bag_linear_bwd_weight(const float* V, int64_t ldv, const float* g, const float* relu_out,
@@ -332,7 +344,7 @@ extern "C" int grl_bag_linear_bwd_weight(const float* V, int64_t ldv, const floa
   GRL_CHECK_ARG((V || K == 0) && g, "grl_bag_linear_bwd_weight: NULL pointer");
   const int Keff = K + (db ? 1 : 0);
   if (Keff == 0) return GRL_OK;
-  const int S = bag_dw_splits(M);
+  const int S = bag_dw_splits(M, (int64_t)K + 1, C);  // the size query's split count (db or not)
   const size_t need = (size_t)S * (size_t)Keff * (size_t)C * 4;
   if (!workspace || workspace_bytes < need)
     GRL_FAIL(GRL_E_WORKSPACE, "grl_bag_linear_bwd_weight: workspace %zu < %zu", workspace_bytes, need);

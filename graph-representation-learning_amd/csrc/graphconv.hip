@@ -23,6 +23,8 @@
 // order, the same DropEdge weights), split and multiplied in the same K16
 // order and product order as gemm_x6_kernel, so the result is bitwise that
 // of the two-kernel path (tests/test_gpu_graphconv.py).
+#include <cstring>
+
 #include "grl_internal.h"
 
 #include <cstdlib>
@@ -405,7 +407,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GRL_FG_WPE,
 //    tile's last unit it stores the tile.
 // Every wave walks the same unit sequence and units complete in order, so
 // the waits cannot form a cycle; each spin is bounded anyway (a kernel that
-// could hang the GPU is not an option), and a wave that gives up stops.
+// could hang the GPU is not an option): a wave whose bound runs out sets the
+// call's status word (vector atomic OR into the caller's workspace) and
+// stops, and the host entry point reports GRL_E_TIMEOUT (graphconv_status).
 // Arithmetic per element is the same as graphconv_fused_kernel's (same
 // chains, split, K order, product order): bitwise the two-kernel result.
 // GRL_WS_PLANES=1: the gather waves store x6 bf16 planes (the MFMA waves only
@@ -436,7 +440,8 @@ constexpr int WS_NB = GRL_WS_PLANES ? 3 : 4;  // ring slots
 #define GRL_WS_U 12
 #endif
 constexpr int WS_U = GRL_WS_U;             // neighbour rows in flight per gather wave
-constexpr int WS_SPIN = 1 << 24;           // bounded waits (~ seconds)
+constexpr int WS_SPIN = 1 << 24;           // bounded waits (~0.5 s of s_sleep 1); GRL_WS_SPIN overrides
+constexpr int WS_STATUS_TIMEOUT = 1;       // status bit: a bounded wait ran out (results invalid)
 
 // GRL_WS_STAMP=1 (diagnostic builds only): every wave adds up the cycles it
 // spent waiting on the ring and its total, read back with grl_debug_ws_stats
@@ -469,12 +474,14 @@ __device__ __forceinline__ int lds_load_acq(int* p) {
 __device__ __forceinline__ void lds_add_rel(int* p, int v) {
   __hip_atomic_fetch_add(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
-// wait until *p >= target (wave-uniform); false if the bound ran out
-__device__ __forceinline__ bool wait_ge(int* p, int target, unsigned long long* waited) {
+// wait until *p >= target (wave-uniform); false if the bound ran out, after
+// recording it in *status (one lane, vector atomic to global memory)
+__device__ __forceinline__ bool wait_ge(int* p, int target, unsigned long long* waited, int spin_limit,
+                                        int* status) {
 #if GRL_WS_STAMP
   const unsigned long long t0 = __builtin_amdgcn_s_memtime();
 #endif
-  for (int spin = 0; spin < WS_SPIN; ++spin) {
+  for (int spin = 0; spin < spin_limit; ++spin) {
     if (lds_load_acq(p) >= target) {
 #if GRL_WS_STAMP
       *waited += __builtin_amdgcn_s_memtime() - t0;
@@ -483,6 +490,7 @@ __device__ __forceinline__ bool wait_ge(int* p, int target, unsigned long long* 
     }
     __builtin_amdgcn_s_sleep(1);
   }
+  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_or(status, WS_STATUS_TIMEOUT, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   return false;
 }
 
@@ -496,7 +504,7 @@ __global__ __launch_bounds__(64 * (WS_PROD + WS_CONS)) void graphconv_ws_kernel(
     const float* __restrict__ vals, uint64_t edge_base, uint64_t self_base, const float* __restrict__ X,
     int64_t ldx, const uint16_t* __restrict__ Wf, const float* __restrict__ bias, int relu,
     float* __restrict__ out, int C, DropDev de, int64_t num_tiles, float* __restrict__ Zout, int64_t ldz,
-    const int32_t* __restrict__ eid, int64_t self_rows) {
+    const int32_t* __restrict__ eid, int64_t self_rows, int spin_limit, int* __restrict__ status) {
   constexpr int F = KS * 16;
   constexpr int KC = F < WS_KC ? F : WS_KC;  // Z columns per unit
   constexpr int NH = F / KC;                  // units per segment
@@ -595,7 +603,8 @@ __global__ __launch_bounds__(64 * (WS_PROD + WS_CONS)) void graphconv_ws_kernel(
           if (have) return true;
 #pragma unroll
           for (int q = 0; q < NH; ++q)
-            if (!wait_ge(&consumed[(u + q) % WS_NB], WS_CONS * ((u + q) / WS_NB), &waited)) return false;
+            if (!wait_ge(&consumed[(u + q) % WS_NB], WS_CONS * ((u + q) / WS_NB), &waited, spin_limit, status))
+              return false;
           have = true;
           return true;
         };
@@ -783,7 +792,7 @@ __global__ __launch_bounds__(64 * (WS_PROD + WS_CONS)) void graphconv_ws_kernel(
       for (int su = 0; su < S * NH; ++su, ++u) {
         const int slot = u % WS_NB, g = u / WS_NB;
         const float* zs = ring + slot * WS_SLOT;
-        if (!wait_ge(&produced[slot], WS_PROD * (g + 1), &waited)) return;
+        if (!wait_ge(&produced[slot], WS_PROD * (g + 1), &waited, spin_limit, status)) return;
 #if GRL_WS_WHATIF == 4
         if (lane == 0) lds_add_rel(&consumed[slot], 1);
         continue;
@@ -890,7 +899,50 @@ bool graphconv_fused_shape_ok(int F, int C, int L) {
   return (F == 256 || F == 128 || F == 64) && C >= 1 && C <= 256 && L >= 1 && FG_RW * L < 64;
 }
 
+// W's planes, then 256 B whose first word is the call's status
 size_t graphconv_fused_ws_bytes(int64_t K) { return (size_t)K * FG_CB * 32 * 3 * 2 + 256; }
+
+static int* ws_status(void* ws, int64_t K) {
+  return reinterpret_cast<int*>(static_cast<char*>(ws) + (size_t)K * FG_CB * 32 * 3 * 2);
+}
+
+static int ws_spin_limit() {
+  const char* e = getenv("GRL_WS_SPIN");  // test / diagnostic aid: a tiny bound forces the timeout path
+  const long v = e ? strtol(e, nullptr, 10) : 0;
+  return v > 0 && v < (1L << 30) ? (int)v : WS_SPIN;
+}
+
+// A persistent kernel whose bounded wait ran out left its outputs partly
+// unwritten.  Outside stream capture the call waits for its kernel and reads
+// the status word (GRL_E_TIMEOUT); inside a capture (no host sync possible),
+// or with GRL_WS_STATUS=poison, a follow-up kernel fills the outputs with NaN
+// when the word is set, so a replay that timed out cannot pass for a result.
+__global__ void ws_poison_kernel(const int* __restrict__ status, float* __restrict__ a, int64_t na,
+                                 float* __restrict__ b, int64_t nb) {
+  if (*status == 0) return;
+  const float nan = __builtin_nanf("");
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < na + nb; i += (int64_t)gridDim.x * blockDim.x)
+    (i < na ? a[i] : b[i - na]) = nan;
+}
+
+static int graphconv_status(const int* status, float* a, int64_t na, float* b, int64_t nb, hipStream_t st,
+                            const char* who) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  GRL_HIP(hipStreamIsCapturing(st, &cs));
+  const char* mode = getenv("GRL_WS_STATUS");  // "poison": never sync, NaN outputs on a timeout (as in a capture)
+  if (cs != hipStreamCaptureStatusNone || (mode && strcmp(mode, "poison") == 0)) {
+    hipLaunchKernelGGL(ws_poison_kernel, dim3(1024), dim3(256), 0, st, status, a, na, b, b ? nb : 0);
+    GRL_LAUNCH_CHECK();
+    return GRL_OK;
+  }
+  int h = 0;
+  GRL_HIP(hipMemcpyAsync(&h, status, sizeof(int), hipMemcpyDeviceToHost, st));
+  GRL_HIP(hipStreamSynchronize(st));
+  if (h & WS_STATUS_TIMEOUT)
+    GRL_FAIL(GRL_E_TIMEOUT, "%s: a wave of the persistent GraphConv kernel gave up waiting on its LDS ring "
+             "(bound %d sleeps); the outputs are invalid", who, ws_spin_limit());
+  return GRL_OK;
+}
 
 int graphconv_fused_fwd(const GrlTypedCsr* g, const float* X, int64_t ldx, int F, const float* W, const float* bias,
                         int C, int relu, float* out, const GrlDropEdge* de, void* ws, hipStream_t st, float* Z) {
@@ -911,16 +963,19 @@ int graphconv_fused_fwd(const GrlTypedCsr* g, const float* X, int64_t ldx, int F
     const int64_t ldz = K;
     const int64_t ws_tiles = ceil_div(M, WS_R);
     const int64_t grid = std::min<int64_t>(ws_tiles, (int64_t)device_cu_count());
+    int* status = ws_status(ws, K);
+    const int spin = ws_spin_limit();
+    GRL_HIP(hipMemsetAsync(status, 0, sizeof(int), st));
 #define GRL_WS_LAUNCH(KS_)                                                                                           \
   do {                                                                                                               \
     if (v)                                                                                                           \
       hipLaunchKernelGGL((graphconv_ws_kernel<KS_, true>), dim3((unsigned)grid), dim3(64 * (WS_PROD + WS_CONS)), 0,  \
                          st, M, g->num_types, hs, g->rowptr, g->colidx, g->vals, g->edge_id_base, g->self_id_base, X, \
-                         ldx, Wf, bias, relu, out, C, d, ws_tiles, Z, ldz, nullptr, M);                              \
+                         ldx, Wf, bias, relu, out, C, d, ws_tiles, Z, ldz, nullptr, M, spin, status);                \
     else                                                                                                             \
       hipLaunchKernelGGL((graphconv_ws_kernel<KS_, false>), dim3((unsigned)grid), dim3(64 * (WS_PROD + WS_CONS)), 0, \
                          st, M, g->num_types, hs, g->rowptr, g->colidx, g->vals, g->edge_id_base, g->self_id_base, X, \
-                         ldx, Wf, bias, relu, out, C, d, ws_tiles, Z, ldz, nullptr, M);                              \
+                         ldx, Wf, bias, relu, out, C, d, ws_tiles, Z, ldz, nullptr, M, spin, status);                \
   } while (0)
     if (F == 256)
       GRL_WS_LAUNCH(16);
@@ -930,7 +985,7 @@ int graphconv_fused_fwd(const GrlTypedCsr* g, const float* X, int64_t ldx, int F
       GRL_WS_LAUNCH(4);
 #undef GRL_WS_LAUNCH
     GRL_LAUNCH_CHECK();
-    return GRL_OK;
+    return graphconv_status(status, out, M * C, Z, M * ldz, st, Z ? "grl_graphconv_fwd_train" : "grl_graphconv_fwd");
   }
 #define GRL_FUSED_LAUNCH(KS_)                                                                                        \
   do {                                                                                                               \
@@ -974,17 +1029,21 @@ int graphconv_fused_bwd_data(const GrlTypedCsr* gt, const int32_t* eid, const fl
   const int64_t grid = std::min<int64_t>(ws_tiles, (int64_t)device_cu_count());
   const DropDev d = to_dev(de);
   const bool v = gt->vals != nullptr;
+  int* status = ws_status(ws, K);
+  const int spin = ws_spin_limit();
+  GRL_HIP(hipMemsetAsync(status, 0, sizeof(int), st));
 #define GRL_WSB_LAUNCH(KS_)                                                                                          \
   do {                                                                                                               \
     if (v)                                                                                                           \
       hipLaunchKernelGGL((graphconv_ws_kernel<KS_, true, true>), dim3((unsigned)grid), dim3(64 * (WS_PROD + WS_CONS)), \
                          0, st, M, gt->num_types, hs, gt->rowptr, gt->colidx, gt->vals, gt->edge_id_base,             \
-                         gt->self_id_base, G, ldg, Wf, nullptr, 0, dX, Cout, d, ws_tiles, Gagg, K, eid, self_rows); \
+                         gt->self_id_base, G, ldg, Wf, nullptr, 0, dX, Cout, d, ws_tiles, Gagg, K, eid, self_rows,   \
+                         spin, status);                                                                             \
     else                                                                                                             \
       hipLaunchKernelGGL((graphconv_ws_kernel<KS_, false, true>), dim3((unsigned)grid),                              \
                          dim3(64 * (WS_PROD + WS_CONS)), 0, st, M, gt->num_types, hs, gt->rowptr, gt->colidx,         \
                          gt->vals, gt->edge_id_base, gt->self_id_base, G, ldg, Wf, nullptr, 0, dX, Cout, d, ws_tiles,  \
-                         Gagg, K, eid, self_rows);                                                                  \
+                         Gagg, K, eid, self_rows, spin, status);                                                    \
   } while (0)
   if (Cin == 256)
     GRL_WSB_LAUNCH(16);
@@ -994,7 +1053,7 @@ int graphconv_fused_bwd_data(const GrlTypedCsr* gt, const int32_t* eid, const fl
     GRL_WSB_LAUNCH(4);
 #undef GRL_WSB_LAUNCH
   GRL_LAUNCH_CHECK();
-  return GRL_OK;
+  return graphconv_status(status, dX, M * Cout, Gagg, M * K, st, "grl_graphconv_bwd_data");
 }
 
 }  // namespace grl

@@ -29,6 +29,7 @@ GRL_E_UNSUPPORTED = -2
 GRL_E_HIP = -3
 GRL_E_WORKSPACE = -4
 GRL_E_OVERFLOW = -5
+GRL_E_TIMEOUT = -6
 
 _c_i32 = ctypes.c_int32
 _c_i64 = ctypes.c_int64

@@ -53,7 +53,7 @@ def _rank(group) -> int:
 def _host_staged(group) -> bool:
     """gloo moves device tensors only through host copies (used to smoke-test
     the N>1 path with several ranks on one GPU; production uses RCCL)."""
-    return dist.get_backend(group) == "gloo"
+    return dist.is_available() and dist.is_initialized() and dist.get_backend(group) == "gloo"
 
 
 def all_to_all_v(out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits, group=None) -> None:
@@ -115,29 +115,103 @@ def build_halo_plan(colidx: torch.Tensor, row_begin: int, row_end: int, group=No
         raise ValueError(f"halo mode must be auto|sparse|dense, got {mode!r}")
     dev = colidx.device
     world, rank = _world(group), _rank(group)
-    n_loc = row_end - row_begin
     c = colidx.long()
     if world > 1:
         rr = torch.tensor([row_begin, row_end, colidx.numel()], dtype=torch.int64, device=dev)
         allr = torch.stack([x.cpu() for x in all_gather_list(rr, group)])
         begins, ends, nnzs = allr[:, 0].tolist(), allr[:, 1].tolist(), allr[:, 2].tolist()
-        if begins != sorted(begins) or any(ends[i] != begins[i + 1] for i in range(world - 1)):
-            raise ValueError(f"node ranges must be contiguous in rank order: {list(zip(begins, ends))}")
-        bounds = begins + [ends[-1]]
-        edge_id_base = sum(nnzs[:rank])
-        num_edges_total = sum(nnzs)
+        bounds = _check_bounds(begins, ends)
     else:
-        bounds = [row_begin, row_end]
-        edge_id_base, num_edges_total = 0, colidx.numel()
-    if world > 1 and c.numel() and (int(c.min()) < bounds[0] or int(c.max()) >= bounds[-1]):
-        raise ValueError(f"column ids outside the global node range [{bounds[0]}, {bounds[-1]})")
-    own = (c >= row_begin) & (c < row_end)
-    halo_ids = torch.unique(c[~own])  # sorted ascending => grouped by owner
+        bounds, nnzs = [row_begin, row_end], [colidx.numel()]
+    _check_columns(c, bounds, world)
+    halo_ids = _halo_ids(c, row_begin, row_end)
     if world > 1 and mode == "auto":
         referenced = sum(int(x) for x in all_gather_list(
             torch.tensor([halo_ids.numel()], dtype=torch.int64, device=dev), group))
-        remote = (world - 1) * (bounds[-1] - bounds[0])
-        mode = "dense" if remote and referenced >= DENSE_HALO_FRACTION * remote else "sparse"
+        mode = _auto_mode(referenced, bounds)
+    asked = None
+    if world > 1 and mode != "dense":
+        ends_t = torch.tensor(bounds[1:], dtype=torch.int64, device=dev)
+        owner = torch.searchsorted(ends_t, halo_ids, right=True)
+        need = torch.bincount(owner, minlength=world).to(torch.int64)
+        asked_counts = torch.empty_like(need)
+        all_to_all_v(asked_counts, need, None, None, group)
+        recv_counts = need.cpu().tolist()
+        send_counts = asked_counts.cpu().tolist()
+        asked_ids = torch.empty(sum(send_counts), dtype=torch.int64, device=dev)
+        all_to_all_v(asked_ids, halo_ids.contiguous(), send_counts, recv_counts, group)
+        asked = (asked_ids, send_counts, recv_counts)
+    return _make_plan(c, row_begin, row_end, bounds, nnzs, rank, "dense" if mode == "dense" else "sparse",
+                      halo_ids, asked)
+
+
+def build_halo_plans_local(colidx_per_rank: List[torch.Tensor], bounds: List[int],
+                           mode: str = "auto") -> List[HaloPlan]:
+    """Every rank's HaloPlan at once, in one process, without a process group:
+    the plans build_halo_plan returns on rank r of a P-rank group when rank r
+    holds colidx_per_rank[r] and the rows [bounds[r], bounds[r+1]).  (Used to
+    drive several shards from one process, e.g. the one-GPU tests of the
+    pipelined exchange.)"""
+    if mode not in ("auto", "sparse", "dense"):
+        raise ValueError(f"halo mode must be auto|sparse|dense, got {mode!r}")
+    world = len(bounds) - 1
+    if len(colidx_per_rank) != world:
+        raise ValueError(f"{len(colidx_per_rank)} shards for {world} node ranges")
+    bounds = _check_bounds(bounds[:-1], bounds[1:])
+    nnzs = [int(c.numel()) for c in colidx_per_rank]
+    cs = [c.long() for c in colidx_per_rank]
+    for c in cs:
+        _check_columns(c, bounds, world)
+    halo = [_halo_ids(c, bounds[r], bounds[r + 1]) for r, c in enumerate(cs)]
+    if mode == "auto":
+        mode = _auto_mode(sum(int(h.numel()) for h in halo), bounds) if world > 1 else "sparse"
+    plans = []
+    for r, c in enumerate(cs):
+        asked = None
+        if world > 1 and mode != "dense":
+            ends_t = torch.tensor(bounds[1:], dtype=torch.int64, device=c.device)
+            owners = [torch.searchsorted(ends_t, h, right=True) for h in halo]
+            recv_counts = torch.bincount(owners[r], minlength=world).tolist()
+            mine = [halo[q][owners[q] == r].to(c.device) for q in range(world)]  # what peer q asks of me
+            asked = (torch.cat(mine), [int(m.numel()) for m in mine], recv_counts)
+        plans.append(_make_plan(c, bounds[r], bounds[r + 1], bounds, nnzs, r,
+                                "dense" if mode == "dense" else "sparse", halo[r], asked))
+    return plans
+
+
+def _check_bounds(begins, ends) -> List[int]:
+    begins, ends = [int(b) for b in begins], [int(e) for e in ends]
+    if begins != sorted(begins) or any(ends[i] != begins[i + 1] for i in range(len(begins) - 1)):
+        raise ValueError(f"node ranges must be contiguous in rank order: {list(zip(begins, ends))}")
+    return begins + [ends[-1]]
+
+
+def _check_columns(c: torch.Tensor, bounds: List[int], world: int) -> None:
+    if world > 1 and c.numel() and (int(c.min()) < bounds[0] or int(c.max()) >= bounds[-1]):
+        raise ValueError(f"column ids outside the global node range [{bounds[0]}, {bounds[-1]})")
+
+
+def _halo_ids(c: torch.Tensor, row_begin: int, row_end: int) -> torch.Tensor:
+    own = (c >= row_begin) & (c < row_end)
+    return torch.unique(c[~own])  # sorted ascending => grouped by owner
+
+
+def _auto_mode(referenced: int, bounds: List[int]) -> str:
+    remote = (len(bounds) - 2) * (bounds[-1] - bounds[0])
+    return "dense" if remote and referenced >= DENSE_HALO_FRACTION * remote else "sparse"
+
+
+def _make_plan(c: torch.Tensor, row_begin: int, row_end: int, bounds: List[int], nnzs: List[int], rank: int,
+               mode: str, halo_ids: torch.Tensor, asked) -> HaloPlan:
+    """The plan of one shard from what the collective (or the in-process
+    builder) learned: the node ranges, every shard's edge count and, for the
+    sparse layout, (ids the peers ask of this rank in peer order, send counts,
+    receive counts)."""
+    dev = c.device
+    world = len(bounds) - 1
+    n_loc = row_end - row_begin
+    edge_id_base, num_edges_total = sum(nnzs[:rank]), sum(nnzs)
+    own = (c >= row_begin) & (c < row_end)
     if world > 1 and mode == "dense":
         stride = max(bounds[i + 1] - bounds[i] for i in range(world))
         ends_t = torch.tensor(bounds[1:], dtype=torch.int64, device=dev)
@@ -149,16 +223,8 @@ def build_halo_plan(colidx: torch.Tensor, row_begin: int, row_end: int, group=No
         return HaloPlan(row_begin, row_end, n_loc, stride * (world + 1) - n_loc, bounds, empty, [0] * world,
                         [0] * world, halo_ids, colidx_local, edge_id_base, num_edges_total, "dense", stride, rank)
     if world > 1:
-        ends_t = torch.tensor(bounds[1:], dtype=torch.int64, device=dev)
-        owner = torch.searchsorted(ends_t, halo_ids, right=True)
-        need = torch.bincount(owner, minlength=world).to(torch.int64)
-        asked_counts = torch.empty_like(need)
-        all_to_all_v(asked_counts, need, None, None, group)
-        recv_counts = need.cpu().tolist()
-        send_counts = asked_counts.cpu().tolist()
-        asked = torch.empty(sum(send_counts), dtype=torch.int64, device=dev)
-        all_to_all_v(asked, halo_ids.contiguous(), send_counts, recv_counts, group)
-        send_index = asked - row_begin
+        asked_ids, send_counts, recv_counts = asked
+        send_index = asked_ids.to(dev) - row_begin
         if send_index.numel() and (int(send_index.min()) < 0 or int(send_index.max()) >= n_loc):
             raise RuntimeError("halo plan: a peer asked for rows this rank does not own")
     else:
@@ -168,8 +234,8 @@ def build_halo_plan(colidx: torch.Tensor, row_begin: int, row_end: int, group=No
         send_index = torch.zeros(0, dtype=torch.int64, device=dev)
     slot = n_loc + torch.searchsorted(halo_ids, c)
     colidx_local = torch.where(own, c - row_begin, slot).to(torch.int32)
-    return HaloPlan(row_begin, row_end, n_loc, int(halo_ids.numel()), bounds, send_index, send_counts, recv_counts,
-                    halo_ids, colidx_local, edge_id_base, num_edges_total, "sparse", n_loc, rank)
+    return HaloPlan(row_begin, row_end, n_loc, int(halo_ids.numel()), bounds, send_index, list(send_counts),
+                    list(recv_counts), halo_ids, colidx_local, edge_id_base, num_edges_total, "sparse", n_loc, rank)
 
 
 class _HaloExchange(torch.autograd.Function):
@@ -255,14 +321,25 @@ class HaloPipeline:
       sparse: [own rows | referenced halo rows in owner order]
     """
 
-    def __init__(self, sg: "ShardedGraph", F: int, chunks: int = 2, device=None):
+    def __init__(self, sg: "ShardedGraph", F: int, chunks: int = 2, device=None, exchange=None):
+        """exchange: None = torch.distributed collectives on sg.group.
+        Otherwise an object standing in for them (several shards driven from
+        one process, e.g. the one-GPU tests of the overlapped branch) with
+          .world, .async_op                     (the side-stream branch runs iff async_op)
+          .forward(pipe, c, async_op)           fill pipe.tables[c]'s halo rows
+          .backward(pipe, c, async_op)          fill pipe.gback[c] from the peers' pipe.gtables[c]
+        each returning None (done, in stream order) or, when async_op, a
+        handle whose .wait() orders the current stream after the transfer --
+        torch.distributed's async work semantics: the transfer starts after
+        the work queued on the current stream when it was issued."""
         plan = sg.plan
         if chunks < 1 or F % chunks:
             raise ValueError(f"chunks must divide F={F} (got {chunks}); slices of a multiple of 4 columns take "
                              "the vector path")
         self.sg, self.plan, self.F, self.K, self.Fc = sg, plan, F, chunks, F // chunks
         self.group = sg.group
-        self.world = _world(self.group)
+        self.xchg = exchange
+        self.world = exchange.world if exchange is not None else _world(self.group)
         dev = torch.device(device) if device is not None else sg.graph.device
         rows = plan.n_loc + plan.n_halo
         self.tables = torch.empty(chunks, rows, self.Fc, device=dev)
@@ -271,7 +348,10 @@ class HaloPipeline:
         self.send = None
         if plan.mode == "sparse" and self.world > 1:
             self.send = torch.empty(chunks, plan.send_index.numel(), self.Fc, device=dev)
-        self.side = torch.cuda.Stream(dev) if dev.type == "cuda" and not _host_staged(self.group) else None
+        if exchange is not None:
+            self.side = torch.cuda.Stream(dev) if dev.type == "cuda" and exchange.async_op else None
+        else:
+            self.side = torch.cuda.Stream(dev) if dev.type == "cuda" and not _host_staged(self.group) else None
 
     def _slices(self, X: torch.Tensor) -> torch.Tensor:
         """[rows, F] -> [chunks, rows, Fc] view (no copy)."""
@@ -291,6 +371,8 @@ class HaloPipeline:
             return self._exchange_slice(c)
 
     def _exchange_slice(self, c: int):
+        if self.xchg is not None:
+            return self.xchg.forward(self, c, self.side is not None)
         p, t = self.plan, self.tables[c]
         if p.mode == "dense":
             if self.side is None:
@@ -352,6 +434,8 @@ class HaloPipeline:
             return None
         p, g, back = self.plan, self.gtables[c], self.gback[c]
         with trace(f"grl.halo_back_slice{c}"):
+            if self.xchg is not None:
+                return self.xchg.backward(self, c, async_op)
             if p.mode == "dense":
                 splits = [p.stride] * self.world
                 if not async_op:
@@ -513,12 +597,37 @@ class ShardedGraph:
 
     def __init__(self, rowptr: torch.Tensor, colidx_global: torch.Tensor, num_types: int, row_begin: int,
                  row_end: int, *, vals: Optional[torch.Tensor] = None, group=None, halo: str = "auto"):
-        self.group = group
-        self.plan = build_halo_plan(colidx_global, row_begin, row_end, group, mode=halo)
-        p = self.plan
+        self._init(rowptr, build_halo_plan(colidx_global, row_begin, row_end, group, mode=halo), num_types, vals,
+                   group)
+
+    def _init(self, rowptr, plan: HaloPlan, num_types: int, vals, group):
+        self.group, self.plan = group, plan
+        p = plan
         self.graph = TypedGraph(rowptr, p.colidx_local, num_types, vals=vals, has_self=True,
                                 num_cols=p.n_loc + p.n_halo, edge_id_base=p.edge_id_base,
-                                self_id_base=p.num_edges_total + row_begin, self_rows=p.n_loc)
+                                self_id_base=p.num_edges_total + p.row_begin, self_rows=p.n_loc)
+
+    @classmethod
+    def in_process(cls, graph: TypedGraph, bounds: List[int], halo: str = "auto") -> List["ShardedGraph"]:
+        """All P node-range shards of `graph` in this process (no process
+        group): shard r is what ShardedGraph.from_graph builds on rank r of a
+        P-rank group with these bounds.  For driving several shards from one
+        process (their exchanges then go through a HaloPipeline `exchange`
+        object instead of collectives)."""
+        L = graph.num_types
+        parts = []
+        for r in range(len(bounds) - 1):
+            e0, e1 = int(graph.rowptr[bounds[r] * L]), int(graph.rowptr[bounds[r + 1] * L])
+            parts.append(((graph.rowptr[bounds[r] * L: bounds[r + 1] * L + 1] - e0).contiguous(),
+                          graph.colidx[e0:e1], None if graph.vals is None else graph.vals[e0:e1]))
+        plans = build_halo_plans_local([c for _, c, _ in parts], bounds, mode=halo)
+        out = []
+        for (rowptr, _, vals), plan in zip(parts, plans):
+            sg = cls.__new__(cls)
+            sg._init(rowptr, plan, L, vals, None)
+            sg.graph.split_threshold, sg.graph.split_chunk = graph.split_threshold, graph.split_chunk
+            out.append(sg)
+        return out
 
     @classmethod
     def synthetic(cls, num_nodes: int, avg_deg: float, num_types: int = 6, *, kind: str = "er", seed: int = 0,

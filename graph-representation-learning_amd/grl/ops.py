@@ -439,7 +439,9 @@ def graph_conv_infer(X: torch.Tensor, graph: TypedGraph, W: torch.Tensor, b=None
 
 # Z bytes above which a training GraphConv keeps X and recomputes Z in the
 # backward instead of holding Z between the passes (recompute=None): at C5
-# scale (2^23 nodes, d=512) Z is 120 GB per layer, X 17 GB.
+# scale (2^23 nodes, d=512) Z is 120 GB per layer, X 17 GB.  (The one-kernel
+# backward's transient G_agg is Z-sized when C == F: recompute bounds the
+# memory held between the passes, not the backward's peak -- graph_conv.)
 RECOMPUTE_Z_BYTES = 8 << 30
 
 
@@ -449,9 +451,16 @@ def graph_conv(X: torch.Tensor, graph: TypedGraph, W: torch.Tensor, b=None, relu
     X: [num_cols, F] (or [B, N, F] for a batch graph).  When no gradient is
     wanted (eval, torch.no_grad) it is one grl_graphconv_fwd call instead:
     the same kernels, so the same bits.
-    recompute: True keeps X and re-aggregates Z in the backward (one more
-    SpMM pass for (L+1)x less saved memory); None decides by Z's size
-    (RECOMPUTE_Z_BYTES); both give the same gradients bit for bit."""
+    recompute: True keeps X instead of Z between the passes ((L+1)x less
+    saved memory); None decides by Z's size (RECOMPUTE_Z_BYTES).  Where the
+    one-kernel data gradient applies (grl_graphconv_bwd_data), the backward
+    takes dW_s = X^T G_s from the aggregate G_s = A_drop,s^T g it writes:
+    out and dX are bitwise the saved-Z path's, dW / db the same products
+    summed in another order (fp32 rounding level).  Elsewhere Z is
+    re-aggregated (one more SpMM pass) and every gradient is bitwise the
+    saved-Z path's.  Peak memory in the G_s form: the transient G_agg
+    [num_cols, (L+1) C] of the backward is Z-sized when C == F, so recompute
+    lowers the memory held BETWEEN the passes, not the backward's peak."""
     if not (torch.is_grad_enabled() and any(t is not None and t.requires_grad for t in (X, W, b))):
         if isinstance(graph, EdgeBlockedGraph):  # one int32 CSR per call: aggregate by blocks, then the linear
             return linear_fwd(spmm_forward(X, graph), W.contiguous(), b.contiguous() if b is not None else None,

@@ -15,7 +15,12 @@
  *    memory; scratch comes from a caller workspace sized by *_workspace_size.
  *  - Every call is stream-ordered on `stream` (a hipStream_t passed as void*,
  *    NULL = default stream) and never synchronises the device, so calls can
- *    be captured into a hipGraph.
+ *    be captured into a hipGraph.  One exception: where grl_graphconv_fwd,
+ *    grl_graphconv_fwd_train and grl_graphconv_bwd_data run their
+ *    persistent one-kernel form outside a stream capture, they wait for that
+ *    kernel and read its status word (GRL_E_TIMEOUT if a bounded wait ran
+ *    out); inside a capture they instead enqueue a kernel that fills their
+ *    outputs with NaN when the word is set.
  *  - Return value 0 = success, negative GRL_E_* = failure; grl_last_error()
  *    returns a thread-local message for the last failure on this thread.
  *  - fp32 features, int32 indices.  Sums over a row's edges run in CSR order
@@ -40,7 +45,9 @@ enum {
   GRL_E_UNSUPPORTED = -2, /* well-formed request this build does not handle  */
   GRL_E_HIP = -3,         /* a HIP runtime call failed                       */
   GRL_E_WORKSPACE = -4,   /* workspace smaller than *_workspace_size()       */
-  GRL_E_OVERFLOW = -5     /* a count does not fit the int32 index type       */
+  GRL_E_OVERFLOW = -5,    /* a count does not fit the int32 index type       */
+  GRL_E_TIMEOUT = -6      /* a persistent kernel's bounded wait ran out; its  */
+                          /* outputs are invalid (see grl_graphconv_fwd)      */
 };
 
 /*

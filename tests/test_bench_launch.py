@@ -1,0 +1,40 @@
+"""CPU: bench.py's launch handling for the driver's N > 1 runs.
+
+  * under a launcher (WORLD_SIZE set) --gpus must equal WORLD_SIZE, else it
+    exits non-zero before touching a GPU;
+  * `--gpus N` without a launcher starts N rank processes itself; when a rank
+    fails (here: no GPU in this container) the parent stops and exits
+    non-zero instead of hanging or printing a one-GPU line.
+The GPU half (two gloo ranks print one line with n_gpus 2) is
+tests/test_gpu_dist.py::test_bench_spawns_its_ranks_without_a_launcher."""
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(args, **env_over):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_over)
+    return subprocess.run([sys.executable, "bench.py"] + args, cwd=ROOT, env=env, capture_output=True, text=True,
+                          timeout=240)
+
+
+def test_world_size_mismatch_is_an_error():
+    r = _bench(["--gpus", "8", "--cpu-seconds", "0"], WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    assert r.returncode != 0
+    assert "WORLD_SIZE=2" in r.stderr and "--gpus 8" in r.stderr
+    assert not any(ln.startswith("{") for ln in r.stdout.splitlines())
+
+
+def test_spawned_ranks_fail_loudly_without_a_gpu():
+    r = _bench(["--gpus", "2", "--dist-backend", "gloo", "--cpu-seconds", "0"])
+    assert r.returncode != 0
+    assert "no ROCm GPU visible" in r.stderr
+    assert not any(ln.startswith("{") for ln in r.stdout.splitlines())
+
+
+def test_gpus_must_be_positive():
+    r = _bench(["--gpus", "0"])
+    assert r.returncode != 0 and "--gpus must be >= 1" in r.stderr

@@ -74,6 +74,17 @@ def _worker(rank, world, port, bounds, mode):
         assert plan.edge_id_base == int(rowptr[rb * L]) and plan.num_edges_total == colidx.size
         # every halo id is remote and referenced; slots are in owner order
         assert not ((plan.halo_ids >= rb) & (plan.halo_ids < re)).any()
+        # the in-process builder (every shard's plan in one process, no collective) gives this rank's plan
+        from grl.dist import build_halo_plans_local
+
+        cols = [torch.from_numpy(colidx[rowptr[bounds[q] * L]:rowptr[bounds[q + 1] * L]].copy())
+                for q in range(world)]
+        local = build_halo_plans_local(cols, bounds, mode=mode)[rank]
+        for f in ("row_begin", "row_end", "n_loc", "n_halo", "bounds", "send_counts", "recv_counts",
+                  "edge_id_base", "num_edges_total", "mode", "stride", "rank"):
+            assert getattr(local, f) == getattr(plan, f), f
+        for f in ("send_index", "halo_ids", "colidx_local"):
+            assert torch.equal(getattr(local, f), getattr(plan, f)), f
         X_loc = torch.from_numpy(X[rb:re].copy()).requires_grad_(True)
         X_ext = halo_exchange(X_loc, plan)
         # every column resolves to the right global feature row, whatever the layout

@@ -209,6 +209,27 @@ def _bench_two_ranks(extra, nproc=2):
     return out
 
 
+def test_bench_spawns_its_ranks_without_a_launcher():
+    """`python bench.py --gpus 2` with no torchrun: bench.py starts the two
+    rank processes itself (the parent never touches the GPU) and prints
+    rank 0's one line with n_gpus 2."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    cmd = [sys.executable, "bench.py", "--gpus", "2", "--dist-backend", "gloo", "--workload", "weak",
+           "--nodes-per-gpu", "20000", "--steps", "2", "--warmup", "1", "--cpu-seconds", "0"]
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["config"]["nodes_total"] == 40000 and out["value"] > 0
+
+
 def test_bench_two_ranks_contract():
     """The driver's N>1 launch (torch.distributed.run, one rank per GPU) of
     bench.py, rehearsed with two gloo ranks sharing the box's GPU: exactly

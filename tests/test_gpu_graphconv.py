@@ -346,3 +346,46 @@ def test_recompute_takes_weight_gradient_from_the_aggregate(de):
     assert bool(((res[True][2] - res[False][2]).abs() <= 1e-5 * bound_w + 1e-6).all())
     bound_b = ge.abs().sum(0)
     assert bool(((res[True][3] - res[False][3]).abs() <= 1e-5 * bound_b + 1e-6).all())
+
+
+def test_persistent_kernel_timeout_is_an_error(monkeypatch):
+    """graphconv_ws_kernel's bounded waits: with a one-sleep bound
+    (GRL_WS_SPIN=1) the MFMA waves give up before the gather waves fill the
+    ring.  Eager calls (forward, training forward, data gradient) raise
+    GrlError(GRL_E_TIMEOUT) instead of returning a partly written result; a
+    captured call cannot sync, so its replay fills the outputs with NaN.
+    With the normal bound the next call is correct again (no sticky state)."""
+    from grl.ops import graph_conv_bwd_data
+
+    N, L, F, C = 20_011, 6, 256, 256
+    g = TypedGraph.synthetic(N, 16.0, L, seed=3, device=DEV)
+    gen = torch.Generator(device=DEV).manual_seed(9)
+    X = torch.randn(N, F, device=DEV, generator=gen)
+    W = torch.randn(7 * F, C, device=DEV, generator=gen) / 40
+    b = torch.randn(C, device=DEV, generator=gen)
+    ref = graph_conv_infer(X, g, W, b, True)
+    assert torch.equal(ref, _two_op(X, g, W, b, True))  # the one-kernel shape
+    G = torch.randn(N, C, device=DEV, generator=gen)
+    dX_ref = graph_conv_bwd_data(G, g, W, F)
+    assert dX_ref is not None
+    monkeypatch.setenv("GRL_WS_SPIN", "1")
+    with pytest.raises(_lib.GrlError, match="gave up waiting"):
+        graph_conv_infer(X, g, W, b, True)
+    with pytest.raises(_lib.GrlError, match="grl_graphconv_fwd_train"):
+        Xg = X.clone().requires_grad_(True)
+        graph_conv(Xg, g, W, b, relu=True)
+    with pytest.raises(_lib.GrlError, match="grl_graphconv_bwd_data"):
+        graph_conv_bwd_data(G, g, W, F)
+    # inside a capture: no sync, the replay's outputs are NaN
+    hg = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(hg):
+        out_c = graph_conv_infer(X, g, W, b, True)
+    hg.replay()
+    torch.cuda.synchronize()
+    assert bool(torch.isnan(out_c).all())
+    monkeypatch.delenv("GRL_WS_SPIN")
+    assert torch.equal(graph_conv_infer(X, g, W, b, True), ref)
+    assert torch.equal(graph_conv_bwd_data(G, g, W, F), dX_ref)
+    hg.replay()  # the captured call reads the bound at capture: it still times out
+    torch.cuda.synchronize()
+    assert bool(torch.isnan(out_c).all())

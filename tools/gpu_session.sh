@@ -114,6 +114,10 @@ for step in "$@"; do
                   GRBM_GUI_ACTIVE SQ_BUSY_CU_CYCLES --kernel-trace -d "$OUT/pmc_x6_stagger" -o run --output-format csv \
                   -- python bench.py --only linear --steps 5 --warmup 1; unset GRL_X6_STAGGER ;;
     probe_contig) run probe_contig 300 python tools/probe_contig.py ;;
+    ab_ws_status) run ab_ws_status 900 tools/ab_ws_status.sh r2gc ;;
+    tests_r3) run pytest_gpu_r3 600 python -u -m pytest tests/test_gpu_halo_async.py tests/test_gpu_graphconv.py \
+                  tests/test_gpu_embed.py tests/test_gpu_dist.py::test_bench_spawns_its_ranks_without_a_launcher \
+                  -m gpu -v -rf --timeout 240 --timeout-method thread ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -1,0 +1,47 @@
+"""A/B probe: the persistent one-kernel GraphConv (graphconv_ws_kernel) at C3
+(N=1M, avg_deg 32, L=6, F=C=256): inference p=0 / p=0.3 and the data
+gradient p=0.3, HIP events over back-to-back calls; the library under test is
+GRL_LIB_PATH (default the in-tree libgrl.so), GRL_WS_STATUS as set."""
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "graph-representation-learning_amd"))
+import torch  # noqa: E402
+
+from grl import DropEdge, TypedGraph  # noqa: E402
+from grl.ops import graph_conv_bwd_data, graph_conv_infer  # noqa: E402
+
+
+def timeit(fn, n=10, warm=2):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(n):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / n
+
+
+def main():
+    dev = torch.device("cuda:0")
+    N, F, C = 1_000_000, 256, 256
+    g0 = TypedGraph.synthetic(N, 32.0, 6, seed=0, device=dev)
+    gen = torch.Generator(device=dev).manual_seed(1)
+    X = torch.randn(N, F, device=dev, generator=gen)
+    W = torch.randn(7 * F, C, device=dev, generator=gen) / 40
+    b = torch.randn(C, device=dev, generator=gen)
+    G = torch.randn(N, C, device=dev, generator=gen)
+    gd = g0.with_dropedge(DropEdge(0.3, 2, 1, True))
+    gd.typed_transpose()
+    lib = os.path.basename(os.environ.get("GRL_LIB_PATH", "libgrl.so"))
+    tag = f"{lib} status={os.environ.get('GRL_WS_STATUS', 'sync')}"
+    r = [timeit(lambda: graph_conv_infer(X, g0, W, b, True)), timeit(lambda: graph_conv_infer(X, gd, W, b, True)),
+         timeit(lambda: graph_conv_bwd_data(G, gd, W, F))]
+    print(f"{tag}: infer p0 {r[0]:.3f} ms, infer p0.3 {r[1]:.3f} ms, bwd_data p0.3 {r[2]:.3f} ms", flush=True)
+
+
+if __name__ == "__main__":
+    main()
