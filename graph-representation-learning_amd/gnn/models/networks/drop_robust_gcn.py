@@ -53,11 +53,19 @@ class EdgeDropout(nn.Dropout):
     in a HIP graph redraws every mask on each replay.  A fixed `seed` numbers
     calls 0, 1, 2, ... (reset_calls()) for parity tests.  Dense tensors get
     plain nn.Dropout.
+    `stream` (data-parallel rank, set by the training procedure) keeps the
+    ranks' masks independent when every rank is seeded alike
+    (cl_warper.py:36-40): it is the DropEdge call id under a device-drawn
+    seed, and the upper 32 bits of the call id under a fixed seed (rank r's
+    call c is c + r * 2^32).
     """
+
+    STREAM_SHIFT = 32
 
     def __init__(self, p: float = 0.5, seed: Optional[int] = None):
         super().__init__(p=p)
         self.seed = seed
+        self.stream = 0
         self._calls = 0
 
     def reset_calls(self) -> None:
@@ -70,9 +78,10 @@ class EdgeDropout(nn.Dropout):
             return A.with_dropedge(None)
         if self.seed is None:
             seed_t = torch.randint(0, 2**62, (1,), dtype=torch.int64, device=A.device)
-            return A.with_dropedge(DropEdge(p=float(self.p), seed=0, call=0, drop_self=drop_self, seed_tensor=seed_t))
+            return A.with_dropedge(DropEdge(p=float(self.p), seed=0, call=self.stream, drop_self=drop_self,
+                                            seed_tensor=seed_t))
         else:
-            seed, call = self.seed, self._calls
+            seed, call = self.seed, self._calls + (self.stream << self.STREAM_SHIFT)
             self._calls += 1
         return A.with_dropedge(DropEdge(p=float(self.p), seed=seed, call=call, drop_self=drop_self))
 

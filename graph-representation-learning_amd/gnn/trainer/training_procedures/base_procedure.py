@@ -8,7 +8,11 @@ declared-but-broken DDP, base_procedure.py:79-93 / cl_warper.py:73-75):
 each rank trains on its DistributedSampler shard; parameters and buffers
 are broadcast from rank 0 once, and after every backward the gradients are
 averaged over the ranks with one bucketed all-reduce (RCCL), so the
-replicas stay identical.  Only rank 0 writes checkpoints."""
+replicas stay identical.  Only rank 0 writes checkpoints.  Every rank is
+seeded alike (cl_warper.py:36-40), so after the broadcast each rank's CUDA
+generator is re-seeded with seed + rank and its EdgeDropout modules get
+stream = rank: ranks draw independent feature-dropout and DropEdge masks
+instead of the same ones on different documents."""
 from __future__ import annotations
 
 import logging
@@ -51,6 +55,7 @@ class BaseProcedure:
             from grl.dist import broadcast_module
 
             broadcast_module(self.model, src=0)
+            self._independent_dropout_streams()
         self.criterion = self._init_criterion()
         self.optimizer = self._init_optimizer()
         self.lr_scheduler = self._init_lr_scheduler()
@@ -69,6 +74,15 @@ class BaseProcedure:
         if self.distributed and n_gpu > 0:
             return torch.device("cuda", torch.cuda.current_device()), [torch.cuda.current_device()]
         return torch.device("cuda:0" if n_gpu_use > 0 else "cpu"), list(range(n_gpu_use))
+
+    def _independent_dropout_streams(self) -> None:
+        from gnn.models.networks.drop_robust_gcn import EdgeDropout
+
+        for m in self.model.modules():
+            if isinstance(m, EdgeDropout):
+                m.stream = self.rank
+        if self.device.type == "cuda":
+            torch.cuda.manual_seed(torch.initial_seed() + self.rank)
 
     def _sync_gradients(self) -> None:
         """DDP's gradient averaging, as one bucketed all-reduce per step."""

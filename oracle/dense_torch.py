@@ -36,13 +36,21 @@ def graph_conv(V, A_pre, W, b):
 
 
 def forward(P: dict, V: torch.Tensor, A_bnln: torch.Tensor, train: bool = False, p_edge: float = 0.3,
-            p_feat: float = 0.5) -> torch.Tensor:
+            p_feat: float = 0.5, edge_mults=None) -> torch.Tensor:
+    """edge_mults: optional three (B, (L+1)N, N) multipliers over A_pre
+    injected in place of the three edge_dropout draws (parity tests; feature
+    dropout is then whatever `train` / p_feat say)."""
     drop = (lambda x, p: F.dropout(x, p, True)) if train else (lambda x, p: x)
     A_pre = preprocess_adj(A_bnln.permute(0, 1, 3, 2))
+    it = iter(edge_mults) if edge_mults is not None else None
+
+    def edrop(A):
+        return A * next(it) if it is not None else drop(A, p_edge)
+
     emb = drop(F.relu(F.linear(V, P["emb1.0.weight"], P["emb1.0.bias"])), p_feat)
-    g1 = drop(F.relu(graph_conv(emb, drop(A_pre, p_edge), P["gcn1.h_weights"], P["gcn1.bias"])), p_feat)
-    g2 = drop(F.relu(graph_conv(g1, drop(A_pre, p_edge), P["gcn2.h_weights"], P["gcn2.bias"])), p_feat)
-    g3 = drop(F.relu(graph_conv(torch.cat([g1, g2], -1), drop(A_pre, p_edge), P["gcn3.h_weights"], P["gcn3.bias"])),
+    g1 = drop(F.relu(graph_conv(emb, edrop(A_pre), P["gcn1.h_weights"], P["gcn1.bias"])), p_feat)
+    g2 = drop(F.relu(graph_conv(g1, edrop(A_pre), P["gcn2.h_weights"], P["gcn2.bias"])), p_feat)
+    g3 = drop(F.relu(graph_conv(torch.cat([g1, g2], -1), edrop(A_pre), P["gcn3.h_weights"], P["gcn3.bias"])),
               p_feat)
     x = F.relu(F.linear(torch.cat([g1, g3], -1), P["emb2.0.weight"], P["emb2.0.bias"]))
     if "self_atten.gamma" in P:

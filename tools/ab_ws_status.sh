@@ -11,4 +11,3 @@ for rep in 1 2 3; do
     GRL_LIB_PATH=$L/diag/libgrl_$n.so timeout -k 10 200 python tools/probe_ws_status.py >> gpurun_out/ab_ws_status.log 2>&1 || exit 1
   done
 done
-cat gpurun_out/ab_ws_status.log
