@@ -831,11 +831,103 @@ def c1_extras(dev, iters=20):
     except Exception as err:  # report, never fall back silently
         res["train_step_ms_B4_hip_graph"] = None
         res["train_hip_graph_error"] = repr(err)[:200]
+    try:  # the product's own training loop on debug.json pages: KVProcedure._run_train_step per batch
+        res["warper_train_step_B4"] = c1_procedure_steps(dev, iters)
+    except Exception as err:  # report, never fall back silently
+        res["warper_train_step_B4"] = {"error": repr(err)[:300]}
     res["cpu_kind"] = ("port: oracle/dense_torch.py, the reference's dense fp32 torch math on CPU (A_pre "
                        "materialised, Bernoulli masks over it in training, Adam)")
     res["logits_max_abs_diff_vs_oracle"] = float(np.abs(logits - ref).max())
     res["tolerance"] = 1e-4
     return res
+
+
+def _debug_datapile(root, copies=8, seed=0):
+    """`copies` debug.json pages (N=74) as VIA datapile documents with seeded
+    random sumi labels: the reference's training input format
+    (datapile_dataset.py), one page size, so every B=4 batch has one shape."""
+    assets = os.path.join(HERE, "tests", "golden", "assets")
+    with open(os.path.join(assets, "debug.json"), encoding="utf-8-sig") as f:
+        regions = json.load(f)
+    with open(os.path.join(assets, "sumi_classes.json"), encoding="utf-8-sig") as f:
+        classes = json.load(f)["classes"]
+    rng = np.random.default_rng(seed)
+    os.makedirs(root, exist_ok=True)
+    for d in range(copies):
+        regs = []
+        for r in regions:
+            fk, kt = ((classes[int(rng.integers(len(classes)))], ["key", "value"][int(rng.integers(2))])
+                      if rng.random() < 0.5 else (None, None))
+            regs.append({"shape_attributes": {"name": "polygon", "all_points_x": [p[0] for p in r["location"]],
+                                              "all_points_y": [p[1] for p in r["location"]]},
+                         "region_attributes": {"label": r["text"], "formal_key": fk, "key_type": kt}})
+        with open(os.path.join(root, f"page{d}.json"), "w", encoding="utf-8") as f:
+            json.dump({"attributes": {"_via_img_metadata": {"regions": regs}}}, f)
+    return root
+
+
+def c1_procedure_steps(dev, iters):
+    """SURVEY.md §8(b)'s caller, timed: the drop-in KVProcedure (what
+    GNNLearningWarper.train() runs per batch, kv_procedure.py:143-164) on B=4
+    batches of debug.json pages -- graph build from the collated dense A,
+    forward, CE, backward, clip, Adam, metrics -- eager, and with
+    capture_train_step (the step as one HIP graph per batch shape)."""
+    import tempfile
+
+    from gnn.models import GraphCNNDropEdge
+    from gnn.trainer.training_procedures import KVProcedure
+    from gnn.utils.config import AttrDict
+
+    assets = os.path.join(HERE, "tests", "golden", "assets")
+    out = {}
+    with tempfile.TemporaryDirectory() as tmp:
+        root = _debug_datapile(os.path.join(tmp, "pages"))
+        split = {"data_path": [root], "class_path": os.path.join(assets, "sumi_classes.json"),
+                 "charset_path": os.path.join(assets, "master_charset.json"), "key_types": ["key", "value"],
+                 "batch_size": 4, "num_workers": 0, "shuffle": False, "drop_last": True, "pin_memory": False,
+                 "augmentations": [],
+                 "data_collate": {"NumpyPadding": {"name_value_pairs": {"textline_encoding": 0.0,
+                                                                        "adjacency_matrix": 0.0, "node_label": -100.0},
+                                                   "only_selected_items": True}},
+                 "data_process": {"TextlineEncoding": {"is_normalized_text": True},
+                                  "HeuristicGraphBuilder": {"num_edges": 6, "edge_type": "normal_binary"},
+                                  "NodeLabeling": {}}}
+        for mode in (None, True):
+            cfg = AttrDict({
+                "experiment_name": "bench", "seed": 1111, "is_train": True, "output_dir": os.path.join(tmp, "out"),
+                "checkpoint_path": None, "num_gpus": 1, "distributed": False, "local_rank": 0, "num_epochs": 1,
+                "max_grad_norm": 5.0, "model_dir_name": "models", "capture_train_step": mode,
+                "data_config": {"dataset": {"type": "DatapileDataset",
+                                            "args": {"node_label_padding_value": -100, "other_class_index": None}},
+                                "training": split, "validation": dict(split, batch_size=1)},
+                "loss": {"type": "CrossEntropyLoss", "args": {}},
+                "lr_scheduler": {"type": "DecayLearningRate", "args": {"lr": 0.001, "factor": 0.9, "num_epochs": 100}},
+                "optimizer": {"type": "BuitlinOptimizer", "args": {"type_optimizer": "Adam", "lr": 0.001}}})
+            torch.manual_seed(0)
+            proc = KVProcedure(GraphCNNDropEdge(4369, 53, 6, 256), cfg)
+            batches = list(proc.train_loader)
+
+            def one(i):
+                proc._run_train_step(batches[i % len(batches)])
+                if proc.step_graph is None:
+                    proc.model.zero_grad()
+
+            for i in range(4):  # warm: lazy workspaces; the second sighting of a shape captures it
+                one(i)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for i in range(iters):
+                one(i)
+            torch.cuda.synchronize()
+            key = "captured" if mode else "eager"
+            out[f"{key}_ms"] = (time.perf_counter() - t0) / iters * 1e3
+            if mode:
+                out["capture_stats"] = proc.step_graph.stats()
+            del proc
+    out["note"] = ("KVProcedure._run_train_step on B=4 batches of debug.json pages (74 nodes), the drop-in's own "
+                   "training loop: dense A -> typed graph, forward, CE, backward, clip, Adam, and the per-batch "
+                   "metrics (argmax + sklearn report, host); captured = capture_train_step: true")
+    return out
 
 
 def model_extras(dev, N=100_000, avg_deg=16.0, iters=3):

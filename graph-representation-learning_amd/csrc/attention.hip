@@ -70,6 +70,17 @@ __device__ __forceinline__ int kappa(int s, int h) { return (s & 3) + 8 * (s >> 
 // unchanged running max) and 0 at x = -inf
 __device__ __forceinline__ float aexp(float x) { return __builtin_amdgcn_exp2f(x * 1.44269504088896341f); }
 
+// The x6 kernels score in base 2: the lane's register operand of S (Q in the
+// forward and dQ, K in dH / dK) is scaled by log2(e) before its split, so S
+// arrives as log2(e) q.k and p = 2^(s - shift) is one v_sub + one v_exp
+// (no per-score v_mul).  Saved row stats stay natural-log (rmax = max q.k,
+// rsum): the backward forms lse2 = rmax log2(e) + log2(rsum) once per query
+// and p = 2^(s - lse2), the normalisation folded into the exponent.
+constexpr float ALOG2E = 1.44269504088896341f;
+constexpr float ALN2 = 0.69314718055994531f;
+__device__ __forceinline__ float aexp2(float x) { return __builtin_amdgcn_exp2f(x); }
+__device__ __forceinline__ float alog2(float x) { return __builtin_amdgcn_logf(x); }
+
 __device__ __forceinline__ f32x16 zero16() {
   f32x16 z;
 #pragma unroll
@@ -637,7 +648,7 @@ __global__ __launch_bounds__(256) void attn_fwd_x6_kernel(AttnArgs a) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int d = kc * 16 + 8 * h + j;
-      v[j] = (q < N && d < a.dk) ? Qb[q * a.dk + d] : 0.0f;
+      v[j] = (q < N && d < a.dk) ? Qb[q * a.dk + d] * ALOG2E : 0.0f;  // base-2 scores
     }
     asplit8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]), qp[kc][0], qp[kc][1],
             qp[kc][2]);
@@ -704,16 +715,16 @@ __global__ __launch_bounds__(256) void attn_fwd_x6_kernel(AttnArgs a) {
       for (int r = 0; r < 16; ++r)
         if (k0 + kappa(r, h) >= k_hi) s[r] = -INFINITY;
     }
-    float mx = -INFINITY;
+    float mx = fmaxf(s[0], s[1]);
 #pragma unroll
-    for (int r = 0; r < 16; ++r) mx = fmaxf(mx, s[r]);
+    for (int r = 2; r < 16; r += 2) mx = fmaxf(fmaxf(mx, s[r]), s[r + 1]);  // v_max3
     mx = fmaxf(mx, __shfl_xor(mx, 32));
     const float mn = fmaxf(m, mx);
-    const float alpha = aexp(m - mn);
+    const float alpha = aexp2(m - mn);
     float ps = 0.0f;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      s[r] = aexp(s[r] - mn);
+      s[r] = aexp2(s[r] - mn);
       ps += s[r];
     }
     ps += __shfl_xor(ps, 32);
@@ -784,7 +795,7 @@ __global__ __launch_bounds__(256) void attn_fwd_x6_kernel(AttnArgs a) {
         }
       }
     if (h == 0 && a.rmax) {
-      a.rmax[b * N + q] = m;
+      a.rmax[b * N + q] = m * ALN2;  // natural-log row max (the saved-stat contract)
       a.rsum[b * N + q] = l;
     }
   }
@@ -812,14 +823,15 @@ __device__ __forceinline__ abf16x8_t tr8(const uint16_t* p0, const uint16_t* p1)
 
 // lane's own 8-value slices v[c*16 + 8h + j] of a row, split into planes
 template <int NC>
-__device__ __forceinline__ void row_planes(const float* row, bool valid, int width, int h, abf16x8_t (&pl)[NC][3]) {
+__device__ __forceinline__ void row_planes(const float* row, bool valid, int width, int h, abf16x8_t (&pl)[NC][3],
+                                           float scale = 1.0f) {
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
     float v[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int d = c * 16 + 8 * h + j;
-      v[j] = (valid && d < width) ? row[d] : 0.0f;
+      v[j] = (valid && d < width) ? row[d] * scale : 0.0f;
     }
     asplit8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]), pl[c][0], pl[c][1], pl[c][2]);
   }
@@ -847,10 +859,10 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_x6_kernel(AttnArgs a) {
   const bool qv = q < N;
   const int64_t k_lo = SPLIT ? (int64_t)blockIdx.z * a.kr : 0, k_hi = SPLIT ? min<int64_t>(N, k_lo + a.kr) : N;
   abf16x8_t qp[KC][3], dop[FC][3];
-  row_planes<KC>(a.Q + (b * N + q) * a.dk, qv, a.dk, h, qp);
+  row_planes<KC>(a.Q + (b * N + q) * a.dk, qv, a.dk, h, qp, ALOG2E);  // base-2 scores
   row_planes<FC>(a.dO + (b * N + q) * a.dv, qv, a.dv, h, dop);
-  const float mq = qv ? a.smax[b * N + q] : 0.0f;
-  const float il = qv ? 1.0f / a.ssum[b * N + q] : 0.0f;
+  // p = 2^(s - lse2); a padded query gets lse2 = +inf, so p = 0
+  const float lse2 = qv ? fmaf(a.smax[b * N + q], ALOG2E, alog2(a.ssum[b * N + q])) : INFINITY;
   const float Dq = qv ? a.Drow[b * N + q] : 0.0f;
   f32x16 dq = zero16();
   if (!PRE && DKP < 32)  // zero pad columns of the K planes, never written by the staging
@@ -914,7 +926,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_x6_kernel(AttnArgs a) {
       MFMA6(dp, h0, h1, h2, dop[fc][0], dop[fc][1], dop[fc][2]);
     }
 #pragma unroll
-    for (int r = 0; r < 16; ++r) s[r] = aexp(s[r] - mq) * il * (dp[r] - Dq);  // dS^T = P (dP - D)
+    for (int r = 0; r < 16; ++r) s[r] = aexp2(s[r] - lse2) * (dp[r] - Dq);  // dS^T = P (dP - D)
     if (k0 + 32 > k_hi) {  // the last, partial key block only (wave-uniform)
 #pragma unroll
       for (int r = 0; r < 16; ++r)
@@ -948,7 +960,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_x6_kernel(AttnArgs a) {
   constexpr int KC = DKP / 16, FC = 8;
   __shared__ __attribute__((aligned(16))) uint16_t Qp_s[(PRE ? 2 : 1) * 3 * 32 * 32];  // PRE: 2 stages
   __shared__ __attribute__((aligned(16))) uint16_t Op_s[(PRE ? 2 : 1) * 3 * 32 * 128];
-  __shared__ float Ms_s[(PRE ? 2 : 1) * 32], Ls_s[(PRE ? 2 : 1) * 32], Ds_s[(PRE ? 2 : 1) * 32];
+  __shared__ float Ms_s[(PRE ? 2 : 1) * 32], Ds_s[(PRE ? 2 : 1) * 32];  // lse2, D per query
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, h = lane >> 5;
   const int64_t N = a.N, b = blockIdx.y;
   const float* Qb = a.Q + b * N * a.dk;
@@ -957,7 +969,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_x6_kernel(AttnArgs a) {
   const bool kv = key < N;
   const int64_t q_lo = SPLIT ? (int64_t)blockIdx.z * a.kr : 0, q_hi = SPLIT ? min<int64_t>(N, q_lo + a.kr) : N;
   abf16x8_t kp[KC][3];
-  row_planes<KC>(a.K + (b * N + key) * a.dk, kv, a.dk, h, kp);
+  row_planes<KC>(a.K + (b * N + key) * a.dk, kv, a.dk, h, kp, ALOG2E);  // base-2 scores
   abf16x8_t hp[WANT_H ? 1 : FC][3];
   if (!WANT_H) row_planes<WANT_H ? 1 : FC>(a.H + (b * N + key) * a.dv, kv, a.dv, h, hp);
   f32x16 acc[WANT_H ? 4 : 1];
@@ -974,13 +986,13 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_x6_kernel(AttnArgs a) {
   const uint16_t* Qpb = a.Qpl + b * N * 32;
   const uint16_t* Opb = a.Opl + b * N * 128;
   const bool vq = vec_ok(Qb, a.dk), vo = vec_ok(dOb, a.dv);
-  float pm = 0.0f, pl_ = 0.0f, pd = 0.0f;
+  float pm = 0.0f, pd = 0.0f;
   auto fetch_stats = [&](int64_t q0) {
     if (tid < 32) {
       const int64_t qq = q0 + tid;
       const bool v = qq < q_hi;
-      pm = v ? a.smax[b * N + qq] : 0.0f;
-      pl_ = v ? 1.0f / a.ssum[b * N + qq] : 0.0f;  // 0 => P = 0 for padded queries
+      // lse2 = +inf => P = 0 for padded queries
+      pm = v ? fmaf(a.smax[b * N + qq], ALOG2E, alog2(a.ssum[b * N + qq])) : INFINITY;
       pd = v ? a.Drow[b * N + qq] : 0.0f;
     }
   };
@@ -1007,7 +1019,6 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_x6_kernel(AttnArgs a) {
     uint16_t* Qp = Qp_s + stg * 3 * 1024;
     uint16_t* Op = Op_s + stg * 3 * 4096;
     float* Ms = Ms_s + stg * 32;
-    float* Ls = Ls_s + stg * 32;
     float* Ds = Ds_s + stg * 32;
     if (!PRE) {
       sq.store(Qp, tid);
@@ -1015,7 +1026,6 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_x6_kernel(AttnArgs a) {
     }
     if (tid < 32) {
       Ms[tid] = pm;
-      Ls[tid] = pl_;
       Ds[tid] = pd;
     }
     if constexpr (PRE) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1047,7 +1057,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_x6_kernel(AttnArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int qi = kappa(r, h);
-        s[r] = kv ? aexp(s[r] - Ms[qi]) * Ls[qi] : 0.0f;  // P
+        s[r] = aexp2(s[r] - Ms[qi]);  // P (a padded key's column is never stored)
       }
       abf16x8_t pp[2][3];
       reg_planes(s, pp);
@@ -1075,8 +1085,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_x6_kernel(AttnArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int qi = kappa(r, h);
-        const float p = kv ? aexp(s[r] - Ms[qi]) * Ls[qi] : 0.0f;
-        s[r] = p * (dp[r] - Ds[qi]);  // dS
+        s[r] = aexp2(s[r] - Ms[qi]) * (dp[r] - Ds[qi]);  // dS (a padded key's column is never stored)
       }
       abf16x8_t dsp[2][3];
       reg_planes(s, dsp);
@@ -1117,8 +1126,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_x6_kernel(AttnArgs a) {
 
 
 // Key split of the forward: out / o_norm / row_max / row_sum from the S
-// partial (o, m, l) in split order (deterministic):
-//   M = max_s m_s,  L = sum_s l_s e^(m_s - M),  O = sum_s o_s e^(m_s - M) / L
+// partial (o, m, l) in split order (deterministic), m_s in base 2:
+//   M = max_s m_s,  L = sum_s l_s 2^(m_s - M),  O = sum_s o_s 2^(m_s - M) / L
 __global__ void attn_fwd_combine_kernel(AttnArgs a, int64_t rows, int S) {
   const int64_t n_all = rows * a.dv;
   const float* pm = a.part + (int64_t)S * rows * a.dv;
@@ -1130,7 +1139,7 @@ __global__ void attn_fwd_combine_kernel(AttnArgs a, int64_t rows, int S) {
     for (int s = 0; s < S; ++s) M = fmaxf(M, pm[s * rows + row]);
     float L = 0.0f, O = 0.0f;
     for (int s = 0; s < S; ++s) {
-      const float w = aexp(pm[s * rows + row] - M);
+      const float w = aexp2(pm[s * rows + row] - M);  // partial maxima are base-2 (x6 forward)
       L += pl[s * rows + row] * w;
       O += a.part[(int64_t)s * n_all + i] * w;
     }
@@ -1138,7 +1147,7 @@ __global__ void attn_fwd_combine_kernel(AttnArgs a, int64_t rows, int S) {
     a.out[i] = a.gamma[f] * O + a.V[i];
     if (a.onorm) a.onorm[i] = O;
     if (f == 0 && a.rmax) {
-      a.rmax[row] = M;
+      a.rmax[row] = M * ALN2;
       a.rsum[row] = L;
     }
   }

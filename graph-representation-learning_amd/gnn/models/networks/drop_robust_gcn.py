@@ -58,6 +58,11 @@ class EdgeDropout(nn.Dropout):
     (cl_warper.py:36-40): it is the DropEdge call id under a device-drawn
     seed, and the upper 32 bits of the call id under a fixed seed (rank r's
     call c is c + r * 2^32).
+    `seed_source` (a 1-element int64 device tensor, set by a training
+    procedure that captures its step, KVProcedure) takes precedence: every
+    call reads the seed from it at launch, with call ids numbered from
+    reset_calls() -- the procedure writes a new seed before each step, so a
+    replayed HIP graph draws new masks, identical to the eager step's.
     """
 
     STREAM_SHIFT = 32
@@ -66,6 +71,7 @@ class EdgeDropout(nn.Dropout):
         super().__init__(p=p)
         self.seed = seed
         self.stream = 0
+        self.seed_source: Optional[torch.Tensor] = None
         self._calls = 0
 
     def reset_calls(self) -> None:
@@ -76,6 +82,11 @@ class EdgeDropout(nn.Dropout):
             return super().forward(A)
         if not self.training or self.p == 0.0:
             return A.with_dropedge(None)
+        if self.seed_source is not None:
+            call = self._calls + (self.stream << self.STREAM_SHIFT)
+            self._calls += 1
+            return A.with_dropedge(DropEdge(p=float(self.p), seed=0, call=call, drop_self=drop_self,
+                                            seed_tensor=self.seed_source))
         if self.seed is None:
             seed_t = torch.randint(0, 2**62, (1,), dtype=torch.int64, device=A.device)
             return A.with_dropedge(DropEdge(p=float(self.p), seed=0, call=self.stream, drop_self=drop_self,

@@ -127,7 +127,10 @@ class BaseProcedure:
     def _update_learning_rate(self, epoch: int, step: int) -> float:
         lr = self.lr_scheduler._step_lr(epoch, step)
         for group in self.optimizer.param_groups:
-            group["lr"] = lr
+            if isinstance(group["lr"], torch.Tensor):  # a captured step reads it from device memory
+                group["lr"].fill_(float(lr))
+            else:
+                group["lr"] = lr
         return lr
 
     def __call__(self):

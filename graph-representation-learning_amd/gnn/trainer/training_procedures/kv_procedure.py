@@ -42,6 +42,13 @@ class KVProcedure(BaseProcedure):
         self.global_step = 0
         self.activator = torch.nn.Softmax(dim=2)
         self.train_loader, self.val_loader, self.class_names = self._init_dataloaders()
+        # additive config key: capture_train_step = true ("capture") replays each
+        # batch shape's training step as one HIP graph (step_graph.py); "static"
+        # runs the same static-buffer step eagerly (its parity reference)
+        from gnn.trainer.training_procedures.step_graph import StepGraph, as_mode
+
+        mode = as_mode(config.get("capture_train_step"))
+        self.step_graph = StepGraph(self, mode) if mode else None
 
     def _init_dataloaders(self):
         loader = BaseDataLoader(self.config)
@@ -81,6 +88,14 @@ class KVProcedure(BaseProcedure):
         return loss, scores, items
 
     def _run_train_step(self, batch: Dict[str, Any], **kwargs):
+        if self.step_graph is not None:
+            out = self.step_graph.run(batch)
+            if out is not None:  # forward .. optimizer step done (replayed or static); metrics outside the graph
+                loss, logits, targets = out
+                predicts = self.activator(logits).argmax(dim=-1)
+                scores, items = self._get_metric_scores(predicts, targets, item_name="Node classification")
+                scores["loss"] = loss.item()
+                return scores, items
         self.model.train()
         self.optimizer.zero_grad()
         with torch.set_grad_enabled(True):
@@ -119,7 +134,8 @@ class KVProcedure(BaseProcedure):
             scores, _ = self._run_train_step(batch)
             train._update(scores)
             self.tb_writer.add_scalar("Train_step_loss", scores["loss"], self.global_step)
-            self.model.zero_grad()
+            if self.step_graph is None:  # a captured step's .grad buffers belong to its graph
+                self.model.zero_grad()
             self.global_step += 1
             n = len(self.train_loader)
             self.model.lambda_value = self.cosine_schedule_lambda(self.global_step, epoch, self.config.num_epochs * n,

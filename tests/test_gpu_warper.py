@@ -116,3 +116,61 @@ def test_data_parallel_training_keeps_replicas_identical(tmp_path):
     s.close()
     cfg = make_config(str(tmp_path), epochs=1)  # writes the dataset once, before the ranks start
     mp.spawn(_dp_worker, args=(2, port, cfg), nprocs=2, join=True)
+
+
+def _fixed_size_datapile(root, n_docs, n_regions, seed=3):
+    """Datapile pages of one size (so every batch of 2 has the same shape and
+    the captured training step replays)."""
+    import inputs as gi
+    from test_data_pipeline import _via
+
+    rng = np.random.default_rng(seed)
+    with open(os.path.join(ASSETS, "sumi_classes.json"), encoding="utf-8-sig") as f:
+        classes = json.load(f)["classes"]
+    os.makedirs(root, exist_ok=True)
+    for d in range(n_docs):
+        regs = gi.synthetic_document(200 + d, n_regions)
+        labels = [(classes[int(rng.integers(len(classes)))], ["key", "value"][int(rng.integers(2))])
+                  if rng.random() < 0.5 else (None, None) for _ in regs]
+        with open(os.path.join(root, f"doc{d}.json"), "w", encoding="utf-8") as f:
+            json.dump(_via(regs, labels), f)
+    return root
+
+
+def test_captured_train_step_equals_eager(tmp_path, monkeypatch):
+    """capture_train_step: warper.train() replays each batch shape's whole
+    training step (forward, CE, backward, clip, Adam) as one HIP graph
+    (gnn/trainer/training_procedures/step_graph.py).  Against the same static
+    pipeline run eagerly ("static": same static graphs, same per-step DropEdge
+    seeds from a fixed dropedge_seed): the same per-step losses and the same
+    trained weights, bit for bit, with most steps replayed."""
+    from gnn.trainer.training_procedures import base_procedure
+
+    losses = {}
+    recorded = []
+    monkeypatch.setattr(base_procedure.NullWriter, "add_scalar",
+                        lambda self, tag, value, step=None: recorded.append(float(value)))
+    models = {}
+    for mode in ("static", True):
+        recorded.clear()
+        cfg = make_config(str(tmp_path / str(mode)), epochs=3)
+        root = _fixed_size_datapile(str(tmp_path / str(mode) / "fixed"), n_docs=6, n_regions=40)
+        cfg.data_config.training.data_path = [root]
+        cfg.data_config.validation.data_path = [root]
+        cfg.capture_train_step = mode
+        torch.manual_seed(0)
+        model = GraphCNNDropEdge(4369, 15, 6, net_size=64, dropedge_seed=5)
+        model.dropout.p = 0.0  # feature dropout's CUDA RNG is not part of the comparison
+        warper = GNNLearningWarper(model, config=cfg)
+        warper.train()
+        sg = warper.trainer.step_graph
+        assert sg is not None and sg.step == 9, sg.stats()
+        if mode is True:
+            assert sg.captures >= 1 and sg.replays >= 6, sg.stats()
+        else:
+            assert sg.replays == 0
+        losses[mode] = list(recorded)
+        models[mode] = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    assert len(losses["static"]) == 9 and losses["static"] == losses[True], losses
+    for k in models["static"]:
+        assert torch.equal(models["static"][k], models[True][k]), k

@@ -115,6 +115,13 @@ for step in "$@"; do
                   -- python bench.py --only linear --steps 5 --warmup 1; unset GRL_X6_STAGGER ;;
     probe_contig) run probe_contig 300 python tools/probe_contig.py ;;
     ab_ws_status) run ab_ws_status 900 tools/ab_ws_status.sh r2gc ;;
+    tests_warper) run pytest_gpu_warper 600 python -u -m pytest tests/test_gpu_warper.py tests/test_gpu_graph_capture.py \
+                  -m gpu -v -rf --timeout 300 --timeout-method thread ;;
+    ab_noslp) export ATTN_N="100000 131072"; run ab_attn_noslp 900 tools/ab_attn_lib.sh attn_noslp && \
+              run ab_gc_noslp 900 tools/ab_ws_status.sh gc_noslp && run ab_lin_noslp 900 tools/ab_gemm_lib.sh lin_noslp ;;
+    tests_attn) run pytest_gpu_attn 600 python -u -m pytest tests/test_gpu_attention.py tests/test_gpu_model.py -m gpu -q -rf \
+                  --timeout 300 --timeout-method thread ;;
+    ab_attn) export ATTN_N="100000 131072"; run ab_attn 900 tools/ab_attn_lib.sh ${AB_LIBS:-attn_prev} ;;
     tests_r3) run pytest_gpu_r3 600 python -u -m pytest tests/test_gpu_halo_async.py tests/test_gpu_graphconv.py \
                   tests/test_gpu_embed.py tests/test_gpu_dist.py::test_bench_spawns_its_ranks_without_a_launcher \
                   -m gpu -v -rf --timeout 240 --timeout-method thread ;;
