@@ -27,6 +27,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <type_traits>
 
 namespace grl {
 namespace {
@@ -802,6 +803,277 @@ __global__ __launch_bounds__(256) void attn_fwd_x6_kernel(AttnArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// The x6 forward software-pipelined within the wave (PRE staging only):
+// iteration k runs block k's O^T += H^T P^T MFMAs with the softmax of block
+// k+1 -- max, 2^(s - m), row sum, the split of P into planes -- in the same
+// basic block, so the VALU issues in the MFMA gaps instead of between the
+// blocks' MFMA phases (attn_fwd_x6_kernel: 61 % MFMA busy at N = 100k, the
+// softmax on the critical path of every block).  Block k+1's scores come
+// from its K planes, so K is staged three blocks deep (block k+2 in flight)
+// and H two.  Same products, same order of every sum as attn_fwd_x6_kernel,
+// hence the same bits.  The last block's partial-key mask is applied in its
+// own instantiation of the iteration (MASK), outside the interleaved body.
+template <int DKP, int NT, bool SPLIT>
+__global__ __launch_bounds__(256) void attn_fwd_x6p_kernel(AttnArgs a) {
+  constexpr int DV = NT * 32, KC = DKP / 16;
+  constexpr int KPL = 32 * DKP, HPL = 32 * DV;  // bf16 per plane
+  constexpr int KST = 3 * KPL, HST = 3 * HPL;   // one stage: the three planes
+  __shared__ __attribute__((aligned(16))) uint16_t Kp_s[3 * KST];
+  __shared__ __attribute__((aligned(16))) uint16_t Hp_s[2 * HST];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, h = lane >> 5;
+  const int64_t N = a.N, b = blockIdx.y;
+  const float* Qb = a.Q + b * N * a.dk;
+  const int64_t q = (int64_t)blockIdx.x * 128 + wave * 32 + l32;
+  const int64_t k_lo = SPLIT ? (int64_t)blockIdx.z * a.kr : 0, k_hi = SPLIT ? min<int64_t>(N, k_lo + a.kr) : N;
+  const int nblk = (int)((k_hi - k_lo + 31) >> 5);
+  const bool partial = ((k_hi - k_lo) & 31) != 0;
+
+  abf16x8_t qp[KC][3];
+#pragma unroll
+  for (int kc = 0; kc < KC; ++kc) {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int d = kc * 16 + 8 * h + j;
+      v[j] = (q < N && d < a.dk) ? Qb[q * a.dk + d] * ALOG2E : 0.0f;  // base-2 scores
+    }
+    asplit8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]), qp[kc][0], qp[kc][1],
+            qp[kc][2]);
+  }
+  f32x16 o[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) o[t] = zero16();
+  float m = -INFINITY, l = 0.0f;
+  const int64_t kps = (int64_t)gridDim.y * N * DKP, hps = (int64_t)gridDim.y * N * DV;
+  DmaRows<DKP, PL_PLAIN> kd;
+  DmaRows<DV, PL_HSWZ> hd;
+  kd.init(a.Kpl + b * N * DKP, kps, wave, lane);
+  hd.init(a.Hpl + b * N * DV, hps, wave, lane);
+  kd.issue(k_lo, N, Kp_s, wave, lane);
+  hd.issue(k_lo, N, Hp_s, wave, lane);
+  if (nblk > 1) kd.issue(k_lo + 32, N, Kp_s + KST, wave, lane);
+  const int trq = (lane & 15) >> 2;
+  const int trc = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+
+  // S^T = K Q^T of the block staged at Kp (base 2)
+  auto scores = [&](const uint16_t* Kp) {
+    f32x16 sc = zero16();
+#pragma unroll
+    for (int kc = 0; kc < KC; ++kc) {
+      const int off = l32 * DKP + kc * 16 + 8 * h;
+      const abf16x8_t k0p = *reinterpret_cast<const abf16x8_t*>(&Kp[off]);
+      const abf16x8_t k1p = *reinterpret_cast<const abf16x8_t*>(&Kp[KPL + off]);
+      const abf16x8_t k2p = *reinterpret_cast<const abf16x8_t*>(&Kp[2 * KPL + off]);
+      MFMA6(sc, k0p, k1p, k2p, qp[kc][0], qp[kc][1], qp[kc][2]);
+    }
+    return sc;
+  };
+  // online softmax of one block: updates m, l; P -> planes; returns alpha
+  auto softmax = [&](f32x16& sc, abf16x8_t (&pp)[2][3]) {
+    float mx = fmaxf(sc[0], sc[1]);
+#pragma unroll
+    for (int r = 2; r < 16; r += 2) mx = fmaxf(fmaxf(mx, sc[r]), sc[r + 1]);
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    const float mn = fmaxf(m, mx);
+    const float alpha = aexp2(m - mn);
+    float ps = 0.0f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      sc[r] = aexp2(sc[r] - mn);
+      ps += sc[r];
+    }
+    ps += __shfl_xor(ps, 32);
+    l = l * alpha + ps;
+    m = mn;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+      asplit8(make_float4(sc[8 * u], sc[8 * u + 1], sc[8 * u + 2], sc[8 * u + 3]),
+              make_float4(sc[8 * u + 4], sc[8 * u + 5], sc[8 * u + 6], sc[8 * u + 7]), pp[u][0], pp[u][1],
+              pp[u][2]);
+    return alpha;
+  };
+  auto mask = [&](f32x16& sc, int64_t k0) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      if (k0 + kappa(r, h) >= k_hi) sc[r] = -INFINITY;
+  };
+  // O^T += H^T P^T of the block staged at Hp
+  auto pv = [&](const uint16_t* Hp, const abf16x8_t (&pp)[2][3]) {
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        abf16x8_t hp[3];
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) {
+          typedef __attribute__((address_space(3))) ai16x4_t lds_v4;
+          const int key0 = kappa(8 * u + trq, h), key1 = kappa(8 * u + 4 + trq, h);
+          const uint16_t* p0 = &Hp[pl * HPL + hswz<DV>(key0, t * 32 + trc)];
+          const uint16_t* p1 = &Hp[pl * HPL + hswz<DV>(key1, t * 32 + trc)];
+          const ai16x4_t x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(uintptr_t)(uint32_t)(uintptr_t)p0);
+          const ai16x4_t x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(uintptr_t)(uint32_t)(uintptr_t)p1);
+          const ai16x8_t v = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+          hp[pl] = __builtin_bit_cast(abf16x8_t, v);
+        }
+        MFMA6(o[t], hp[0], hp[1], hp[2], pp[u][0], pp[u][1], pp[u][2]);
+      }
+  };
+  auto rescale = [&](float alpha) {
+    if (__any(alpha != 1.0f)) {  // wave-uniform; x * 1 == x, so skipping is exact
+#pragma unroll
+      for (int t = 0; t < NT; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[t][r] *= alpha;
+    }
+  };
+
+  // prologue: block 0's scores and softmax (o is zero: no rescale)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  abf16x8_t pp[2][3];
+  {
+    f32x16 sc = scores(Kp_s);
+    if (nblk == 1 && partial) mask(sc, k_lo);
+    softmax(sc, pp);
+  }
+  float alpha = 1.0f;
+  // iteration it: block it's P.H with block it+1's softmax in the same body
+  auto iteration = [&](int it, auto masked) {
+    constexpr bool MASK = decltype(masked)::value;
+    const int64_t k0 = k_lo + 32 * (int64_t)it;
+    // block it's H and block it+1's K landed; every wave is done with the
+    // stages the next DMAs overwrite (H of block it-1, K of block it-1)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (it + 1 < nblk) hd.issue(k0 + 32, N, Hp_s + ((it + 1) & 1) * HST, wave, lane);
+    if (it + 2 < nblk) kd.issue(k0 + 64, N, Kp_s + ((it + 2) % 3) * KST, wave, lane);
+    rescale(alpha);
+    f32x16 sc = scores(Kp_s + ((it + 1) % 3) * KST);
+    if constexpr (MASK) mask(sc, k0 + 32);
+    abf16x8_t pn[2][3];
+    // block it's P.H in 2 NT groups of 6 MFMAs; block it+1's softmax cut into
+    // 7 pieces placed after groups 1 .. 2 NT - 1 (group 0 covers the score
+    // MFMAs' latency), each group fenced so its VALU fills that group's gaps
+    const uint16_t* Hp = Hp_s + (it & 1) * HST;
+    float mn = 0.0f, an = 1.0f, ps = 0.0f;
+    auto piece = [&](int pc) {
+      if (pc == 0) {
+        float mx = fmaxf(sc[0], sc[1]);
+#pragma unroll
+        for (int r = 2; r < 16; r += 2) mx = fmaxf(fmaxf(mx, sc[r]), sc[r + 1]);
+        mx = fmaxf(mx, __shfl_xor(mx, 32));
+        mn = fmaxf(m, mx);
+        an = aexp2(m - mn);
+      } else if (pc <= 2) {
+#pragma unroll
+        for (int r = 8 * (pc - 1); r < 8 * pc; ++r) {
+          sc[r] = aexp2(sc[r] - mn);
+          ps += sc[r];
+        }
+        if (pc == 2) {
+          ps += __shfl_xor(ps, 32);
+          l = l * an + ps;
+          m = mn;
+        }
+      } else {
+        const int u = (pc - 3) >> 1, half = (pc - 3) & 1;
+        if (half == 0) {
+          uint2 l0, l1, l2;
+          asplit3(make_float4(sc[8 * u], sc[8 * u + 1], sc[8 * u + 2], sc[8 * u + 3]), l0, l1, l2);
+          pn[u][0] = __builtin_bit_cast(abf16x8_t, make_uint4(l0.x, l0.y, 0u, 0u));
+          pn[u][1] = __builtin_bit_cast(abf16x8_t, make_uint4(l1.x, l1.y, 0u, 0u));
+          pn[u][2] = __builtin_bit_cast(abf16x8_t, make_uint4(l2.x, l2.y, 0u, 0u));
+        } else {
+          uint2 h0, h1, h2;
+          asplit3(make_float4(sc[8 * u + 4], sc[8 * u + 5], sc[8 * u + 6], sc[8 * u + 7]), h0, h1, h2);
+          uint4 w0 = __builtin_bit_cast(uint4, pn[u][0]), w1 = __builtin_bit_cast(uint4, pn[u][1]),
+                w2 = __builtin_bit_cast(uint4, pn[u][2]);
+          pn[u][0] = __builtin_bit_cast(abf16x8_t, make_uint4(w0.x, w0.y, h0.x, h0.y));
+          pn[u][1] = __builtin_bit_cast(abf16x8_t, make_uint4(w1.x, w1.y, h1.x, h1.y));
+          pn[u][2] = __builtin_bit_cast(abf16x8_t, make_uint4(w2.x, w2.y, h2.x, h2.y));
+        }
+      }
+    };
+#pragma unroll
+    for (int g = 0; g < 2 * NT; ++g) {
+      const int t = g >> 1, u = g & 1;
+      abf16x8_t hp[3];
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) {
+        typedef __attribute__((address_space(3))) ai16x4_t lds_v4;
+        const int key0 = kappa(8 * u + trq, h), key1 = kappa(8 * u + 4 + trq, h);
+        const uint16_t* p0 = &Hp[pl * HPL + hswz<DV>(key0, t * 32 + trc)];
+        const uint16_t* p1 = &Hp[pl * HPL + hswz<DV>(key1, t * 32 + trc)];
+        const ai16x4_t x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(uintptr_t)(uint32_t)(uintptr_t)p0);
+        const ai16x4_t x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(uintptr_t)(uint32_t)(uintptr_t)p1);
+        const ai16x8_t v = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+        hp[pl] = __builtin_bit_cast(abf16x8_t, v);
+      }
+      MFMA6(o[t], hp[0], hp[1], hp[2], pp[u][0], pp[u][1], pp[u][2]);
+      // pieces assigned to this group: piece pc runs after group 1 + pc * (2 NT - 1) / 7
+#pragma unroll
+      for (int pc = 0; pc < 7; ++pc)
+        if (g >= 1 && 1 + pc * (2 * NT - 1) / 7 == g) piece(pc);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    alpha = an;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) pp[u][pl] = pn[u][pl];
+  };
+  int it = 0;
+  for (; it + 2 < nblk; ++it) iteration(it, std::false_type{});
+  if (it + 1 < nblk) {
+    if (partial)
+      iteration(it, std::true_type{});
+    else
+      iteration(it, std::false_type{});
+    ++it;
+  }
+  // the last block: its P.H only
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  rescale(alpha);
+  pv(Hp_s + (it & 1) * HST, pp);
+
+  if (SPLIT && q < N) {  // key split: unnormalised partials, combined by attn_fwd_combine_kernel
+    const int64_t rows = (int64_t)gridDim.y * N, row = b * N + q, zs = blockIdx.z;
+    float* po = a.part + zs * rows * a.dv + row * a.dv;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int f = t * 32 + kappa(r, h);
+        if (f < a.dv) po[f] = o[t][r];
+      }
+    if (h == 0) {
+      float* pm = a.part + (int64_t)gridDim.z * rows * a.dv;
+      pm[zs * rows + row] = m;
+      pm[((int64_t)gridDim.z + zs) * rows + row] = l;
+    }
+  } else if (q < N) {
+    const float inv = 1.0f / l;
+    const int64_t base = (b * N + q) * a.dv;
+#pragma unroll
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int f = t * 32 + kappa(r, h);
+        if (f < a.dv) {
+          const float on = o[t][r] * inv;
+          a.out[base + f] = a.gamma[f] * on + a.V[base + f];
+          if (a.onorm) a.onorm[base + f] = on;
+        }
+      }
+    if (h == 0 && a.rmax) {
+      a.rmax[b * N + q] = m * ALN2;  // natural-log row max (the saved-stat contract)
+      a.rsum[b * N + q] = l;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Backward on the bf16 matrix cores (x6), for dv in (96, 128] (NT = 4: the
 // model's 128-wide values).  Three kernels instead of two: the key-stationary
 // work is split into dH (needs P only) and dK (needs dP, so the lane's H row
@@ -1172,6 +1444,12 @@ bool attn_x6_enabled() {
   return !(e && e[0] == '0');
 }
 
+// GRL_ATTN_PIPE=0 (read per call) keeps the unpipelined x6 forward (A/B aid)
+bool attn_pipe_enabled() {
+  const char* e = getenv("GRL_ATTN_PIPE");
+  return !(e && e[0] == '0');
+}
+
 template <int DKP, int NT>
 int launch_attn(AttnPass pass, const AttnArgs& a0, int64_t B, int S, hipStream_t st) {
   AttnArgs a = a0;
@@ -1205,7 +1483,14 @@ int launch_attn(AttnPass pass, const AttnArgs& a0, int64_t B, int S, hipStream_t
     else
       hipLaunchKernelGGL((attn_bwd_kv_kernel<DKP, NT>), grid, dim3(256), 0, st, a);
   } else if (pass == PASS_FWD && x6) {
-    GRL_X6L(attn_fwd_x6_kernel, DKP, NT);
+    if (pre && attn_pipe_enabled()) {
+      if (S > 1)
+        hipLaunchKernelGGL((attn_fwd_x6p_kernel<DKP, NT, true>), grid, dim3(256), 0, st, a);
+      else
+        hipLaunchKernelGGL((attn_fwd_x6p_kernel<DKP, NT, false>), grid, dim3(256), 0, st, a);
+    } else {
+      GRL_X6L(attn_fwd_x6_kernel, DKP, NT);
+    }
     if (S > 1) {
       GRL_LAUNCH_CHECK();
       hipLaunchKernelGGL(attn_fwd_combine_kernel, dim3(red), dim3(256), 0, st, a, rows, S);

@@ -116,3 +116,25 @@ def test_bad_widths_raise():
         node_attention_forward(Q, K, H, V, gamma)
     with pytest.raises(_lib.GrlError, match="attention shapes"):
         node_attention_forward(Q[..., :8], K[..., :8], H, V[..., :8], gamma)
+
+
+@pytest.mark.parametrize("B,N,dk,dv", [(1, 74, 16, 128), (4, 1100, 16, 128), (64, 1024, 16, 128), (2, 300, 32, 256),
+                                       (1, 2048, 16, 128), (2, 1000, 5, 100), (3, 4099, 16, 64), (2, 4127, 32, 32)])
+def test_pipelined_forward_same_bits(B, N, dk, dv, monkeypatch):
+    """attn_fwd_x6p_kernel (block k+1's softmax inside block k's P.H MFMAs)
+    against the unpipelined x6 forward (GRL_ATTN_PIPE=0): same products, same
+    order of every sum -- out and the saved row stats bitwise, with key
+    splits, partial last blocks and every value width."""
+    from grl.ops import node_self_attention
+
+    Q, K, H, V, gamma = _inputs(B, N, dk, dv, seed=7 * N + dk)
+    res = {}
+    for pipe in ("1", "0"):
+        monkeypatch.setenv("GRL_ATTN_PIPE", pipe)
+        out = node_attention_forward(Q, K, H, V, gamma)
+        leaves = [t.clone().requires_grad_(True) for t in (Q, K, H, V, gamma)]
+        node_self_attention(*leaves).square().sum().backward()
+        res[pipe] = (out, [t.grad for t in leaves])
+    assert torch.equal(res["1"][0], res["0"][0])
+    for a, b in zip(res["1"][1], res["0"][1]):
+        assert torch.equal(a, b)

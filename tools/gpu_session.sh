@@ -122,6 +122,11 @@ for step in "$@"; do
     tests_attn) run pytest_gpu_attn 600 python -u -m pytest tests/test_gpu_attention.py tests/test_gpu_model.py -m gpu -q -rf \
                   --timeout 300 --timeout-method thread ;;
     ab_attn) export ATTN_N="100000 131072"; run ab_attn 900 tools/ab_attn_lib.sh ${AB_LIBS:-attn_prev} ;;
+    prof_attn100k) run prof_attn100k 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_attn100k" -o run \
+                  --output-format csv -- python tools/probe_attn.py 100000 ;;
+    pmc_attn100k) run pmc_attn100k 300 timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA \
+                  SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE \
+                  --kernel-trace -d "$OUT/pmc_attn100k" -o run --output-format csv -- python tools/probe_attn.py 100000 ;;
     tests_r3) run pytest_gpu_r3 600 python -u -m pytest tests/test_gpu_halo_async.py tests/test_gpu_graphconv.py \
                   tests/test_gpu_embed.py tests/test_gpu_dist.py::test_bench_spawns_its_ranks_without_a_launcher \
                   -m gpu -v -rf --timeout 240 --timeout-method thread ;;

@@ -62,3 +62,14 @@ def main():
 
 if __name__ == "__main__":
     main()
+
+
+def pattern(path, sym, lo, hi):
+    """Compact class string of instructions [lo, hi] of a kernel: M mfma, v valu,
+    e transcendental, d lds, g vmem, s salu, w wait."""
+    lines = kernel_lines(path, sym)
+    insts = [t.strip().split(";")[0].strip() for t in lines
+             if t.strip() and not t.strip().startswith((";", ".")) and not t.strip().endswith(":")]
+    code = {"mfma": "M", "valu": "v", "trans": "e", "lds": "d", "vmem": "g", "salu": "s", "wait": "w",
+            "accvgpr": "a", "other": "o"}
+    return "".join(code[classify(x.split()[0])] for x in insts[lo:hi + 1])
