@@ -849,10 +849,12 @@ def _debug_datapile(root, copies=8, seed=0):
     assets = os.path.join(HERE, "tests", "golden", "assets")
     with open(os.path.join(assets, "debug.json"), encoding="utf-8-sig") as f:
         regions = json.load(f)
-    with open(os.path.join(assets, "sumi_classes.json"), encoding="utf-8-sig") as f:
-        classes = json.load(f)["classes"]
-    rng = np.random.default_rng(seed)
+    # 26 classes x {key, value} + other = the config-1 model's 53 outputs
+    classes = [f"c{i}" for i in range(26)]
     os.makedirs(root, exist_ok=True)
+    with open(os.path.join(root, "..", "classes26.json"), "w") as f:
+        json.dump({"classes": classes}, f)
+    rng = np.random.default_rng(seed)
     for d in range(copies):
         regs = []
         for r in regions:
@@ -882,7 +884,7 @@ def c1_procedure_steps(dev, iters):
     out = {}
     with tempfile.TemporaryDirectory() as tmp:
         root = _debug_datapile(os.path.join(tmp, "pages"))
-        split = {"data_path": [root], "class_path": os.path.join(assets, "sumi_classes.json"),
+        split = {"data_path": [root], "class_path": os.path.join(tmp, "classes26.json"),
                  "charset_path": os.path.join(assets, "master_charset.json"), "key_types": ["key", "value"],
                  "batch_size": 4, "num_workers": 0, "shuffle": False, "drop_last": True, "pin_memory": False,
                  "augmentations": [],

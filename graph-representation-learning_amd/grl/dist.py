@@ -521,6 +521,100 @@ class _PipelinedAggregate(torch.autograd.Function):
             return ctx.pipe.backward(dZ, ctx.dropedge), None, None
 
 
+def _p2p_exchange(sends, recvs, group):
+    """Post point-to-point transfers: sends [(tensor, dst)], recvs [(tensor,
+    src)] (group ranks).  RCCL: one batch_isend_irecv, asynchronous (the
+    transfer waits for the work queued on the current stream); returns the
+    works and a finish() that copies host-staged receives back (gloo moves
+    device tensors through host copies)."""
+    if not sends and not recvs:
+        return [], lambda: None
+    staged = _host_staged(group)
+    ops, back = [], []
+    for t, dst in sends:
+        ops.append(dist.P2POp(dist.isend, t.cpu() if staged and t.is_cuda else t, dst, group))
+    for t, src in recvs:
+        buf = torch.empty(t.shape, dtype=t.dtype) if staged and t.is_cuda else t
+        if buf is not t:
+            back.append((t, buf))
+        ops.append(dist.P2POp(dist.irecv, buf, src, group))
+    works = dist.batch_isend_irecv(ops)
+
+    def finish():
+        for t, buf in back:
+            t.copy_(buf)
+
+    return works, finish
+
+
+class _RowPipelinedGraphConv(torch.autograd.Function):
+    """One GraphConv layer (robust_gcn.py:45-51) on a node-range shard with
+    the one-kernel forms in both directions and the reverse halo exchange
+    pipelined over ROW blocks (ShardedGraph.graphconv(pipeline="rows")).
+
+    forward:  the halo exchange (every slot), then the one-kernel training
+              forward over [own | halo] rows (grl_graphconv_fwd_train: out,
+              and Z for dW) -- out bitwise the one-GPU rows.
+    backward: dW, db from Z (partials: allreduce_gradients completes them);
+              dX_ext = the one-kernel data gradient over the shard's typed
+              transpose computed in row blocks -- peer q's halo rows for
+              q = rank+1, rank+2, ... first, each block's partials posted to
+              q (RCCL point-to-point, asynchronous) while the next block
+              computes, the own rows last -- and the owner adds the peers'
+              partials in peer order, as the unpipelined exchange does: dX
+              bitwise the unpipelined one-kernel sharded layer's.
+    ER shards reference nearly every remote row, so no forward overlap exists
+    that keeps out's per-element summation order (a row's sum needs all its
+    sources); the column-slice pipeline (chunks=k) overlaps the forward
+    exchange but runs the two-kernel layer."""
+
+    @staticmethod
+    def forward(ctx, X_loc: torch.Tensor, sg: "ShardedGraph", W: torch.Tensor, b, relu: bool, dropedge):
+        from .ops import graph_conv_fwd_train
+
+        with trace("grl.rows_pipeline_fwd"):
+            with torch.no_grad():
+                X_ext = halo_exchange(X_loc.detach().contiguous(), sg.plan, sg.group)
+            graph = sg.graph.with_dropedge(dropedge)
+            out, Z = graph_conv_fwd_train(X_ext, graph, W.contiguous(), b.contiguous() if b is not None else None,
+                                          relu)
+        ctx.sg, ctx.graph, ctx.relu, ctx.has_b, ctx.F = sg, graph, relu, b is not None, X_loc.shape[1]
+        ctx.save_for_backward(Z, W.contiguous(), out if relu else None)
+        return out
+
+    @staticmethod
+    def backward(ctx, g: torch.Tensor):
+        from .ops import graph_conv_bwd_data, linear_bwd_weight, relu_grad
+
+        Z, W, out = ctx.saved_tensors
+        sg, graph, F = ctx.sg, ctx.graph, ctx.F
+        # the ReLU handling of ops._GraphConv.backward (same kernels, same bits)
+        g, mask = relu_grad(g.contiguous().float(), out if ctx.relu else None)
+        want_w, want_b = ctx.needs_input_grad[2], ctx.has_b and ctx.needs_input_grad[3]
+        dW = db = None
+        if want_w or want_b:
+            dW, db = linear_bwd_weight(Z, g, mask, want_b)
+        dX_loc = None
+        if ctx.needs_input_grad[0]:
+            g_data = g if mask is None else torch.where(mask > 0, g, torch.zeros((), dtype=g.dtype, device=g.device))
+            with trace("grl.rows_pipeline_bwd"):
+                dX_loc = sg.rows_backward(g_data, W, F, graph)
+            if dX_loc is None:  # a block outside the one-kernel path: whole range, then the exchange
+                dX_ext = graph_conv_bwd_data(g_data, graph, W, F)
+                if dX_ext is None:
+                    from .ops import linear_bwd_data, spmm_backward
+
+                    dX_ext = spmm_backward(linear_bwd_data(g_data, None, W), graph, F)
+                dX_loc = _HaloExchange.backward(types_ns(plan=sg.plan, group=sg.group), dX_ext)[0]
+        return dX_loc, None, dW if want_w else None, db, None, None
+
+
+def types_ns(**kw):
+    import types
+
+    return types.SimpleNamespace(**kw)
+
+
 def broadcast_module(module: torch.nn.Module, src: int = 0, group=None) -> None:
     """Copy `src`'s parameters and buffers to every rank (replica start)."""
     if _world(group) == 1:
@@ -695,8 +789,77 @@ class ShardedGraph:
             return typed_aggregate(self.exchange(X_loc), self.graph.with_dropedge(dropedge))
         return _PipelinedAggregate.apply(X_loc, self.pipeline(X_loc.shape[1], chunks), dropedge)
 
+    def halo_blocks(self):
+        """[(peer q, r0, r1)]: the X_ext rows holding peer q's rows, for
+        q = rank+1, rank+2, ... (mod P) -- the order rows_backward sends in."""
+        p, world = self.plan, len(self.plan.bounds) - 1
+        out = []
+        for j in range(1, world):
+            q = (p.rank + j) % world
+            if p.mode == "dense":
+                r0 = p.stride * (1 + q)
+                out.append((q, r0, r0 + p.bounds[q + 1] - p.bounds[q]))
+            else:
+                r0 = p.n_loc + sum(p.recv_counts[:q])
+                out.append((q, r0, r0 + p.recv_counts[q]))
+        return out
+
+    def rows_backward(self, g: torch.Tensor, W: torch.Tensor, F: int, graph: TypedGraph):
+        """dX_loc of a GraphConv layer on this shard (g: the output gradient
+        through the ReLU): the one-kernel data gradient in row blocks, each
+        peer's halo block posted to that peer as soon as it is computed, the
+        own rows last, then the peers' partials for my rows added in peer
+        order.  None when a block is outside the one-kernel path."""
+        from .ops import graph_conv_bwd_data_rows
+
+        p, world = self.plan, len(self.plan.bounds) - 1
+        dev = g.device
+        blocks = self.halo_blocks()
+        dX_ext = torch.empty(graph.num_cols, F, dtype=torch.float32, device=dev)
+        # receive buffers: what peer q computed for my rows (dense: all of them; sparse: the ones q referenced)
+        recv = {}
+        for q in range(world):
+            if q != p.rank:
+                n = p.n_loc if p.mode == "dense" else p.send_counts[q]
+                recv[q] = torch.empty(n, F, dtype=torch.float32, device=dev)
+        pending = []
+        step = {"j": 0}
+
+        def post(r0, r1):
+            step["j"] += 1
+            j = step["j"]
+            if j > len(blocks):
+                return  # the own rows: nothing to send
+            dst = blocks[j - 1][0]
+            src = (p.rank - j) % world
+            sends = [(dX_ext[r0:r1], dst)] if r1 > r0 else []
+            recvs = [(recv[src], src)] if recv[src].shape[0] else []
+            pending.append(_p2p_exchange(sends, recvs, self.group))
+
+        order = [(r0, r1) for _, r0, r1 in blocks] + [(0, p.n_loc)]
+        if world > 1 and not graph_conv_bwd_data_rows(g, graph, W, F, order, dX_ext, on_block=post):
+            return None
+        if world == 1 and not graph_conv_bwd_data_rows(g, graph, W, F, [(0, p.n_loc)], dX_ext):
+            return None
+        for works, finish in pending:
+            for w in works:
+                w.wait()
+            finish()
+        dX_loc = dX_ext[:p.n_loc].clone()
+        off = 0
+        for q in range(world):  # peer order: the unpipelined exchange's (_HaloExchange.backward)
+            if q == p.rank:
+                continue
+            if p.mode == "dense":
+                dX_loc += recv[q]
+            elif p.send_counts[q]:
+                cnt = p.send_counts[q]
+                dX_loc.index_add_(0, p.send_index[off:off + cnt], recv[q])
+            off += p.send_counts[q] if p.mode != "dense" else 0
+        return dX_loc
+
     def graphconv(self, X_loc: torch.Tensor, layer, dropedge: Optional[DropEdge] = None,
-                  relu: bool = False, chunks: Optional[int] = None) -> torch.Tensor:
+                  relu: bool = False, chunks: Optional[int] = None, pipeline: Optional[str] = None) -> torch.Tensor:
         """One GraphConv (gnn.models.GraphConv or anything with h_weights /
         bias) over this shard: halo exchange -> typed SpMM -> MFMA linear
         (+ fused ReLU).  Output rows = this rank's nodes.  After backward,
@@ -705,7 +868,13 @@ class ShardedGraph:
         exchange is grl.ops.graph_conv on [own | halo] rows: on large shards
         its forward is one kernel and its data gradient the one-kernel form
         over the shard's typed transpose, whose halo rows then travel home
-        in the exchange's backward."""
+        in the exchange's backward.  pipeline="rows": the one-kernel forms in
+        both directions with the reverse exchange pipelined over row blocks
+        (_RowPipelinedGraphConv); out and dX bitwise the unpipelined layer's."""
+        if pipeline == "rows":
+            return _RowPipelinedGraphConv.apply(X_loc, self, layer.h_weights, layer.bias, relu, dropedge)
+        if pipeline is not None:
+            raise ValueError(f"pipeline must be None or 'rows', got {pipeline!r}")
         if chunks is None:
             return graph_conv(self.exchange(X_loc), self.graph.with_dropedge(dropedge), layer.h_weights, layer.bias,
                               relu=relu)

@@ -312,6 +312,67 @@ def graph_conv_bwd_data(g: torch.Tensor, graph: TypedGraph, W: torch.Tensor, F: 
     return (dX, G_agg, g) if want_aggregate else dX
 
 
+def graph_conv_bwd_data_rows(g: torch.Tensor, graph: TypedGraph, W: torch.Tensor, F: int, blocks, dX: torch.Tensor,
+                             on_block=None) -> bool:
+    """The one-kernel data gradient (graph_conv_bwd_data) computed in row
+    blocks of dX, one grl_graphconv_bwd_data call per block [r0, r1) over a
+    row-range view of the cached typed transpose, so a caller can act on a
+    block (e.g. send a node-range shard's halo rows home) while the next one
+    computes.  Every row is the same arithmetic as in the whole-range call
+    (rows do not mix in the kernel), so dX is bitwise that call's.  A block
+    starting at row 0 carries the self term of rows < graph.num_rows; other
+    blocks must lie at or beyond num_rows (a shard's halo rows: no self term).
+    g: the output gradient already through the ReLU.  dX: [graph.num_cols, F]
+    (written).  on_block(r0, r1) runs after each block's launch.  False (and
+    nothing written) when some block is outside the one-kernel path or F > 256;
+    the caller then takes the whole-range path."""
+    if not _bwd_data_enabled() or isinstance(graph, EdgeBlockedGraph) or F > 256:
+        return False
+    M, C = g.shape
+    L, S = graph.num_types, graph.segments
+    if (C not in (64, 128, 256) or F % 4 or L > 7 or graph.num_cols < graph.num_rows
+            or graph.self_rows != graph.num_rows or M != graph.num_rows or g.dtype != torch.float32
+            or not g.is_contiguous() or W.dtype != torch.float32 or tuple(W.shape) != (S * F, C)
+            or tuple(dX.shape) != (graph.num_cols, F) or not dX.is_contiguous()):
+        return False
+    for r0, r1 in blocks:
+        if not (r0 == 0 or r0 >= graph.num_rows) or r1 < r0 or r1 > graph.num_cols:
+            raise _lib.GrlError(f"row block [{r0}, {r1}) must start at 0 or at/after row {graph.num_rows}")
+    gt, eid = graph.typed_transpose()
+    Wc = W.contiguous()
+    views = []
+    for r0, r1 in blocks:
+        if r1 == r0:
+            views.append(None)
+            continue
+        v = TypedGraph(gt.rowptr[r0 * L: r1 * L + 1], gt.colidx, L, vals=gt.vals, has_self=gt.has_self,
+                       num_cols=gt.num_cols, edge_id_base=gt.edge_id_base, self_id_base=gt.self_id_base,
+                       self_rows=r1 - r0, _shared={"csc": None})
+        v.split_threshold, v.split_chunk = gt.split_threshold, gt.split_chunk
+        v = v.with_dropedge(graph.dropedge)
+        csr = v.csr_c(C)
+        ws_bytes = _lib.lib().grl_graphconv_bwd_data_workspace_query(ctypes.byref(csr), g.data_ptr(), g.stride(0),
+                                                                     C, Wc.data_ptr(), F)
+        if ws_bytes == 0:
+            return False
+        views.append((v, csr, ws_bytes))
+    de = graph.dropedge.to_c() if graph.dropedge is not None else None
+    stream = current_stream_handle(g.device)
+    ws = None
+    for (r0, r1), view in zip(blocks, views):
+        if view is not None:
+            v, csr, ws_bytes = view
+            if ws is None or ws.numel() < ws_bytes:
+                ws = torch.empty(ws_bytes, dtype=torch.uint8, device=g.device)
+            g_rows = M if r0 == 0 else 0  # the self term: forward rows only
+            call("grl_graphconv_bwd_data", ctypes.byref(csr), eid.data_ptr(), g.data_ptr(), g.stride(0),
+                 min(g_rows, r1 - r0), C, Wc.data_ptr(), F, dX[r0:r1].data_ptr(), None,
+                 ctypes.byref(de) if de is not None else None, ws.data_ptr(), ws_bytes, stream)
+        if on_block is not None:
+            on_block(r0, r1)
+    return True
+
+
 class _GraphConv(torch.autograd.Function):
     """One GraphConv layer, X -> Z = A_drop X -> out = Z W + b [ReLU]
     (robust_gcn.py:45-51), as one autograd node: the same kernels and

@@ -362,3 +362,58 @@ def test_two_ranks_one_kernel_training_layer_on_shards(mode):
     import torch.multiprocessing as mp
 
     mp.spawn(_fused_train_shard_worker, args=(2, _free_port(), mode), nprocs=2, join=True)
+
+
+def _rows_pipeline_worker(rank, world, port, mode):
+    """One rank of a gloo world on the GPU: ShardedGraph.graphconv(pipeline=
+    "rows") -- one-kernel forward on [own | halo] rows, one-kernel data
+    gradient in row blocks with each peer's halo block sent as soon as it is
+    computed -- against the unpipelined one-kernel sharded layer: out, dX,
+    dW and db bitwise; out bitwise the one-GPU rows."""
+    import os
+
+    import torch.distributed as dist
+
+    from gnn.models import GraphConv
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        N, deg, L, F, C = 30_000 * world, 16.0, 6, 256, 256  # shards large enough for the one-kernel paths
+        sg = ShardedGraph.synthetic(N, deg, L, kind="er", seed=6, device=DEV, halo=mode)
+        assert sg.plan.mode == mode
+        g = TypedGraph.synthetic(N, deg, L, kind="er", seed=6, device=DEV)
+        rb, re = sg.plan.row_begin, sg.plan.row_end
+        gen = torch.Generator().manual_seed(43)
+        X = torch.randn(N, F, generator=gen).to(DEV)
+        R = torch.randn(N, C, generator=gen).to(DEV)
+        de = DropEdge(0.3, 8, 1, True)
+        torch.manual_seed(21)
+        layer = GraphConv(F, C, L).to(DEV)
+        res = {}
+        for pipe in ("rows", None):
+            layer.zero_grad()
+            X_loc = X[rb:re].clone().requires_grad_(True)
+            out = sg.graphconv(X_loc, layer, de, relu=True, pipeline=pipe)
+            (out * R[rb:re]).sum().backward()
+            res[pipe] = (out.detach(), X_loc.grad, layer.h_weights.grad.clone(), layer.bias.grad.clone())
+        bad = [(name, float((a - b).abs().max()), float(b.abs().max()))
+               for name, a, b in zip(("out", "dX", "dW", "db"), res["rows"], res[None]) if not torch.equal(a, b)]
+        if bad:
+            raise AssertionError(f"rank {rank}: not bitwise {bad}")
+        # the forward is the one-GPU rows
+        from grl.ops import graph_conv_infer
+
+        full = graph_conv_infer(X, g.with_dropedge(de), layer.h_weights.detach(), layer.bias.detach(), True)
+        assert torch.equal(res["rows"][0], full[rb:re])
+        assert "typed_transpose" in sg.graph._shared
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,mode", [(2, "dense"), (2, "sparse"), (3, "dense"), (3, "sparse")])
+def test_rows_pipelined_graphconv_on_shards(world, mode):
+    import torch.multiprocessing as mp
+
+    mp.spawn(_rows_pipeline_worker, args=(world, _free_port(), mode), nprocs=world, join=True)

@@ -127,6 +127,8 @@ for step in "$@"; do
     pmc_attn100k) run pmc_attn100k 300 timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_MFMA \
                   SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE \
                   --kernel-trace -d "$OUT/pmc_attn100k" -o run --output-format csv -- python tools/probe_attn.py 100000 ;;
+    tests_rows) run pytest_gpu_rows 600 python -u -m pytest tests/test_gpu_dist.py -k rows_pipelined -m gpu -v -rf \
+                  --timeout 300 --timeout-method thread ;;
     tests_r3) run pytest_gpu_r3 600 python -u -m pytest tests/test_gpu_halo_async.py tests/test_gpu_graphconv.py \
                   tests/test_gpu_embed.py tests/test_gpu_dist.py::test_bench_spawns_its_ranks_without_a_launcher \
                   -m gpu -v -rf --timeout 240 --timeout-method thread ;;
