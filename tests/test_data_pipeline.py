@@ -190,3 +190,28 @@ def test_warper_refuses_cpu(tmp_path):
     warper = GNNLearningWarper(GraphCNNDropEdge(4369, 15, 6, net_size=16), config=cfg)
     with pytest.raises(GrlError, match="ROCm device"):
         warper.train()
+
+
+def test_macro_report_equals_sklearn():
+    """The procedure's per-step metric (kv_procedure.macro_report, class ids +
+    bincounts) gives exactly sklearn's classification_report macro avg on the
+    class names, including absent classes, zero divisions and repeated names."""
+    from sklearn.metrics import classification_report
+
+    from gnn.trainer.training_procedures.kv_procedure import macro_report
+
+    rng = np.random.default_rng(0)
+    names = tuple(["other"] + [f"k{i}_{t}" for i in range(12) for t in ("key", "value")])
+    for trial in range(60):
+        n = int(rng.integers(0, 300))
+        k = int(rng.integers(1, len(names)))
+        yt = rng.integers(0, k, n)
+        yp = np.where(rng.random(n) < 0.6, yt, rng.integers(0, len(names), n))
+        nm = names if trial % 3 else tuple(names[:5]) + tuple(names[1:])  # repeated names
+        got = macro_report(yt, yp, nm)
+        tn, pn = [nm[i] for i in yt.tolist()], [nm[i] for i in yp.tolist()]
+        if n == 0:
+            assert got == {"precision": 0.0, "recall": 0.0, "f1-score": 0.0, "support": 0.0}
+            continue
+        ref = classification_report(tn, pn, output_dict=True, zero_division=0)["macro avg"]
+        assert got == {k2: ref[k2] for k2 in ("precision", "recall", "f1-score", "support")}, (trial, got, ref)
