@@ -884,6 +884,10 @@ __global__ __launch_bounds__(512) void gemm_x6_kernel(GemmArgs p, const uint16_t
 // aligned operands, lda, ldb, M, N multiples of 4.
 typedef short i16x4_t __attribute__((ext_vector_type(4)));
 
+#ifndef GRL_X6T_INTERLEAVE
+#define GRL_X6T_INTERLEAVE 0
+#endif
+
 __device__ __forceinline__ bf16x8_t tr_pair(const uint16_t* plane, int k, int col) {
   // k = 8h + qq for this lane's first block row (qq = (lane & 15) >> 2); the
   // second read is the same block 4 k further
@@ -983,6 +987,31 @@ __global__ __launch_bounds__(512) void gemm_x6t_kernel(GemmArgs p) {
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int q = 0; q < 3; ++q) b_[j][q] = tr_pair(cur + (3 + q) * X6_PLANE, tk, wn * 64 + j * 32 + tc);
+#if GRL_X6T_INTERLEAVE
+    // the next step's split + LDS stores issued between this step's MFMA
+    // groups (one operand row set after each odd group) instead of after all
+    // of them, so the VALU fills the MFMA gaps (A/B: GRL_X6T_INTERLEAVE)
+    uint16_t* nxt_stage = smem + ((t + 1) & 1) * X6_STAGE;
+    const bool more = t + 1 < nk;
+#pragma unroll
+    for (int g = 0; g < 8; ++g) {
+      const int i = g >> 1, j = g & 1;
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_[i][2], b_[j][0], acc[i][j], 0, 0, 0);
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_[i][1], b_[j][1], acc[i][j], 0, 0, 0);
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_[i][0], b_[j][2], acc[i][j], 0, 0, 0);
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_[i][1], b_[j][0], acc[i][j], 0, 0, 0);
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_[i][0], b_[j][1], acc[i][j], 0, 0, 0);
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_[i][0], b_[j][0], acc[i][j], 0, 0, 0);
+      if (more) {
+        if (g == 1) X6T_SPLIT(in0 ? ra0 : zero4, nxt_stage, st_off0);
+        if (g == 3) X6T_SPLIT(in1 ? ra1 : zero4, nxt_stage, st_off1);
+        if (g == 5) X6T_SPLIT(in0 ? rb0 : zero4, nxt_stage + 3 * X6_PLANE, st_off0);
+        if (g == 7) X6T_SPLIT(in1 ? rb1 : zero4, nxt_stage + 3 * X6_PLANE, st_off1);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (t + 2 < nk) X6T_LOAD(t + 2);
+#else
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -998,6 +1027,7 @@ __global__ __launch_bounds__(512) void gemm_x6t_kernel(GemmArgs p) {
       X6T_STASH(smem + ((t + 1) & 1) * X6_STAGE);  // the other stage: last read in step t-1
       if (t + 2 < nk) X6T_LOAD(t + 2);
     }
+#endif
     __syncthreads();
   }
 #undef X6T_LOAD

@@ -130,6 +130,7 @@ for step in "$@"; do
     tests_rows) run pytest_gpu_rows 600 python -u -m pytest tests/test_gpu_dist.py -k rows_pipelined -m gpu -v -rf \
                   --timeout 300 --timeout-method thread ;;
     probe_c1p) run probe_c1p 300 python tools/probe_c1_procedure.py ;;
+    ab_dw) rm -f gpurun_out/ab_dw.log; run ab_dw 900 tools/ab_dw.sh ${AB_LIBS:-x6t_il} ;;
     tests_r3) run pytest_gpu_r3 600 python -u -m pytest tests/test_gpu_halo_async.py tests/test_gpu_graphconv.py \
                   tests/test_gpu_embed.py tests/test_gpu_dist.py::test_bench_spawns_its_ranks_without_a_launcher \
                   -m gpu -v -rf --timeout 240 --timeout-method thread ;;
