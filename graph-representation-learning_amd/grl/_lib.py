@@ -152,6 +152,8 @@ SIGNATURES = {
     "grl_linear_bwd_data_workspace_size": (_c_size, [_c_i64, _c_i32, _c_i32]),
     "grl_linear_bwd_data": (_c_i32, [_c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_i64, _c_i32, _c_i32, _c_vp, _c_size,
                                      _c_vp]),
+    "grl_relu_grad_workspace_size": (_c_size, [_c_i64, _c_i32]),
+    "grl_relu_grad": (_c_i32, [_c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_i32, _c_vp, _c_size, _c_vp]),
     "grl_linear_bwd_weight_workspace_size": (_c_size, [_c_i64, _c_i32, _c_i32]),
     "grl_linear_bwd_weight": (_c_i32, [_c_vp, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_i32, _c_i32, _c_vp,
                                        _c_size, _c_vp]),

@@ -589,11 +589,13 @@ class _RowPipelinedGraphConv(torch.autograd.Function):
         Z, W, out = ctx.saved_tensors
         sg, graph, F = ctx.sg, ctx.graph, ctx.F
         # the ReLU handling of ops._GraphConv.backward (same kernels, same bits)
-        g, mask = relu_grad(g.contiguous().float(), out if ctx.relu else None)
         want_w, want_b = ctx.needs_input_grad[2], ctx.has_b and ctx.needs_input_grad[3]
+        g, mask, db_pre = relu_grad(g.contiguous().float(), out if ctx.relu else None, want_b)
         dW = db = None
-        if want_w or want_b:
-            dW, db = linear_bwd_weight(Z, g, mask, want_b)
+        if want_w or (want_b and db_pre is None):
+            dW, db = linear_bwd_weight(Z, g, mask, want_b and db_pre is None)
+        if db_pre is not None:
+            db = db_pre
         dX_loc = None
         if ctx.needs_input_grad[0]:
             g_data = g if mask is None else torch.where(mask > 0, g, torch.zeros((), dtype=g.dtype, device=g.device))

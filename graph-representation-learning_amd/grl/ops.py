@@ -180,13 +180,28 @@ def typed_aggregate(X: torch.Tensor, graph: TypedGraph) -> torch.Tensor:
 PREMASK_ROWS = 65536
 
 
-def relu_grad(g: torch.Tensor, out):
-    """(g_eff, mask_for_the_gemm): g through ReLU's derivative [out > 0]."""
+def relu_grad(g: torch.Tensor, out, want_db: bool = False):
+    """(g_eff, mask_for_the_gemm, db): g through ReLU's derivative [out > 0].
+    From PREMASK_ROWS rows the mask is applied here, in one pass
+    (grl_relu_grad) that also sums db when asked -- bitwise the db
+    linear_bwd_weight would give on g_eff; otherwise db is None and the GEMM
+    (which then masks on its loads) gives it."""
     if out is None:
-        return g, None
-    if g.shape[0] >= PREMASK_ROWS:
-        return torch.where(out > 0, g, torch.zeros((), dtype=g.dtype, device=g.device)), None
-    return g, out
+        return g, None, None
+    if g.shape[0] < PREMASK_ROWS:
+        return g, out, None
+    _require_device(g, "relu_grad g")
+    M, C = g.shape
+    if out.shape != g.shape or not out.is_contiguous() or not g.is_contiguous():
+        raise _lib.GrlError(f"relu_grad: g {tuple(g.shape)} and the ReLU output {tuple(out.shape)} "
+                            "must be contiguous and of one shape")
+    g_eff = torch.empty_like(g)
+    db = torch.empty(C, dtype=torch.float32, device=g.device) if want_db else None
+    ws_bytes = _lib.lib().grl_relu_grad_workspace_size(M, C) if want_db else 0
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=g.device) if ws_bytes else None
+    call("grl_relu_grad", g.data_ptr(), out.data_ptr(), g_eff.data_ptr(), db.data_ptr() if db is not None else None,
+         M, C, ws.data_ptr() if ws is not None else None, ws_bytes, current_stream_handle(g.device))
+    return g_eff, None, db
 
 
 def linear_fwd(Z2: torch.Tensor, W: torch.Tensor, b, relu: bool) -> torch.Tensor:
@@ -244,15 +259,16 @@ class _GraphLinear(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g: torch.Tensor):
         Z2, W, out = ctx.saved_tensors
-        g, mask = relu_grad(g.contiguous().float(), out if ctx.relu else None)
+        want_b = ctx.has_b and ctx.needs_input_grad[2]
+        g, mask, db_pre = relu_grad(g.contiguous().float(), out if ctx.relu else None, want_b)
         dZ = dW = db = None
         if ctx.needs_input_grad[0]:
             dZ = linear_bwd_data(g, mask, W)
-        if ctx.needs_input_grad[1] or (ctx.has_b and ctx.needs_input_grad[2]):
-            dW, db = linear_bwd_weight(Z2, g, mask, ctx.has_b and ctx.needs_input_grad[2])
+        if ctx.needs_input_grad[1] or (want_b and db_pre is None):
+            dW, db = linear_bwd_weight(Z2, g, mask, want_b and db_pre is None)
             if not ctx.needs_input_grad[1]:
                 dW = None
-        return dZ, dW, db, None
+        return dZ, dW, db_pre if db_pre is not None else db, None
 
 
 def _bwd_data_enabled() -> bool:
@@ -402,9 +418,9 @@ class _GraphConv(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g: torch.Tensor):
         Z, W, out = ctx.saved_tensors
-        g, mask = relu_grad(g.contiguous().float(), out if ctx.relu else None)
         want_w = ctx.needs_input_grad[2]
         want_b = ctx.has_b and ctx.needs_input_grad[3]
+        g, mask, db_pre = relu_grad(g.contiguous().float(), out if ctx.relu else None, want_b)
         if ctx.recompute and ctx.needs_input_grad[0] and want_w:
             # X was kept, not Z: the one-kernel data gradient also writes G_s = A_drop,s^T g and
             # dW_s = Z_s^T g = X^T G_s -- no re-aggregation of Z (same products, another order)
@@ -416,9 +432,9 @@ class _GraphConv(torch.autograd.Function):
                 dWt, _ = linear_bwd_weight(X2, G_agg, None, False)  # [F, S*C]
                 del G_agg
                 dW = dWt.view(F, S, C).transpose(0, 1).reshape(S * F, C)
-                db = g_eff.sum(0) if want_b else None
+                db = (db_pre if db_pre is not None else g_eff.sum(0)) if want_b else None
                 return dX.view(ctx.xshape), None, dW, db, None, None
-        if ctx.recompute and (want_w or want_b):
+        if ctx.recompute and (want_w or (want_b and db_pre is None)):
             Z = spmm_forward(Z, ctx.graph)
         dW = db = dX = None
         if ctx.needs_input_grad[0]:
@@ -429,8 +445,10 @@ class _GraphConv(torch.autograd.Function):
                 dX = spmm_backward(dZ, ctx.graph, F)
                 del dZ
             dX = dX.view(ctx.xshape)
-        if want_w or want_b:
-            dW, db = linear_bwd_weight(Z, g, mask, want_b)
+        if want_w or (want_b and db_pre is None):
+            dW, db = linear_bwd_weight(Z, g, mask, want_b and db_pre is None)
+        if db_pre is not None:
+            db = db_pre
         return dX, None, dW if want_w else None, db, None, None
 
 
@@ -686,7 +704,7 @@ class _BagLinear(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         V2, Wt, out = ctx.saved_tensors
-        g, relu_out = relu_grad(g.contiguous().float(), out if ctx.relu else None)
+        g, relu_out, _ = relu_grad(g.contiguous().float(), out if ctx.relu else None)
         dV = linear_bwd_data(g, relu_out, Wt) if ctx.needs_input_grad[0] else None
         if V2.shape[0] >= BAG_DW_SPARSE_ROWS:  # large M: only V's nonzeros read a row of g
             dWt, db = bag_linear_bwd_weight(V2, g, relu_out, ctx.has_b)

@@ -361,6 +361,19 @@ int grl_linear_bwd_weight(const float* Z, int64_t ldz, const float* g,
                           int32_t K, int32_t C, void* workspace,
                           size_t workspace_bytes, grl_stream_t stream);
 
+/* ReLU's derivative applied once (autograd ThresholdBackward of the ReLU at
+ * drop_robust_gcn.py:76, the bias gradient of robust_gcn.py:51 with it):
+ *   g_eff = g * [relu_out > 0]  (masked entries +0.0; g_eff may alias g)
+ *   db    = sum over rows of g_eff                     (db may be NULL)
+ * in one pass.  db is summed in the row blocks and order grl_linear_bwd_weight
+ * uses for its db, so the two are bitwise equal on the same g_eff.  Used
+ * before the large-M backward GEMMs, whose LDS-DMA operand path cannot mask
+ * on the way.  g, relu_out, g_eff: [M, C] contiguous.                       */
+size_t grl_relu_grad_workspace_size(int64_t M, int32_t C);
+int grl_relu_grad(const float* g, const float* relu_out, float* g_eff, float* db,
+                  int64_t M, int32_t C, void* workspace, size_t workspace_bytes,
+                  grl_stream_t stream);
+
 /* emb1: Linear(K -> C) (+ReLU) over sparse bag-of-characters rows
  * (drop_robust_gcn.py:36,64; rows from TextlineEncoding,
  * textline_encoding.py:23-42):

@@ -289,6 +289,34 @@ def test_linear_backward_matches_fp64(M, K, C, relu):
     np.testing.assert_allclose(db.cpu().numpy(), gm.sum(0), rtol=1e-5, atol=1e-4 * np.sqrt(M))
 
 
+@pytest.mark.parametrize("M,C", [(65536, 256), (100003, 200), (70000, 7)])
+def test_relu_grad_one_pass(M, C):
+    """grl_relu_grad (the layer backward's ReLU mask + db, M >= PREMASK_ROWS):
+    g_eff bitwise torch.where(out > 0, g, 0) (NaN outputs masked, -0.0 / NaN
+    gradients passed), db bitwise linear_bwd_weight's db on g_eff."""
+    from grl.ops import PREMASK_ROWS, linear_bwd_weight, relu_grad
+
+    assert M >= PREMASK_ROWS
+    rng = np.random.default_rng(M + C)
+    g = rng.standard_normal((M, C)).astype(np.float32)
+    out = rng.standard_normal((M, C)).astype(np.float32)
+    out[::97, 0] = np.nan
+    out[1::89, -1] = 0.0
+    g[2::101, 0] = -0.0
+    g[3::103, -1] = np.nan
+    gd, od = to_dev(g), to_dev(out)
+    g_eff, mask, db = relu_grad(gd, od, True)
+    assert mask is None
+    ref = torch.where(od > 0, gd, torch.zeros((), device=gd.device))
+    assert torch.equal(g_eff.view(torch.int32), ref.view(torch.int32))
+    Z = to_dev(rng.standard_normal((M, 8)).astype(np.float32))
+    _, db_gemm = linear_bwd_weight(Z, ref, None, True)
+    assert torch.equal(db.view(torch.int32), db_gemm.view(torch.int32))
+    g2, _, none = relu_grad(gd, od, False)
+    assert none is None and torch.equal(g2.view(torch.int32), ref.view(torch.int32))
+    assert torch.equal(gd.cpu().view(torch.int32), torch.from_numpy(g).view(torch.int32))  # g untouched
+
+
 def test_linear_backward_deterministic():
     from grl.ops import linear_bwd_weight
 
