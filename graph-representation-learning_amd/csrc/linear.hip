@@ -19,7 +19,6 @@
 // second pass adds in split order: deterministic, no atomics.
 #include "grl_internal.h"
 
-#include <type_traits>
 
 #include <cstdlib>
 
@@ -918,10 +917,6 @@ __global__ __launch_bounds__(512) void gemm_x6_kernel(GemmArgs p, const uint16_t
 // aligned operands, lda, ldb, M, N multiples of 4.
 typedef short i16x4_t __attribute__((ext_vector_type(4)));
 
-#ifndef GRL_X6T_INTERLEAVE
-#define GRL_X6T_INTERLEAVE 0
-#endif
-
 __device__ __forceinline__ bf16x8_t tr_pair(const uint16_t* plane, int k, int col) {
   // k = 8h + qq for this lane's first block row (qq = (lane & 15) >> 2); the
   // second read is the same block 4 k further
@@ -1021,31 +1016,6 @@ __global__ __launch_bounds__(512) void gemm_x6t_kernel(GemmArgs p) {
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int q = 0; q < 3; ++q) b_[j][q] = tr_pair(cur + (3 + q) * X6_PLANE, tk, wn * 64 + j * 32 + tc);
-#if GRL_X6T_INTERLEAVE
-    // the next step's split + LDS stores issued between this step's MFMA
-    // groups (one operand row set after each odd group) instead of after all
-    // of them, so the VALU fills the MFMA gaps (A/B: GRL_X6T_INTERLEAVE)
-    uint16_t* nxt_stage = smem + ((t + 1) & 1) * X6_STAGE;
-    const bool more = t + 1 < nk;
-#pragma unroll
-    for (int g = 0; g < 8; ++g) {
-      const int i = g >> 1, j = g & 1;
-      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_[i][2], b_[j][0], acc[i][j], 0, 0, 0);
-      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_[i][1], b_[j][1], acc[i][j], 0, 0, 0);
-      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_[i][0], b_[j][2], acc[i][j], 0, 0, 0);
-      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_[i][1], b_[j][0], acc[i][j], 0, 0, 0);
-      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_[i][0], b_[j][1], acc[i][j], 0, 0, 0);
-      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_[i][0], b_[j][0], acc[i][j], 0, 0, 0);
-      if (more) {
-        if (g == 1) X6T_SPLIT(in0 ? ra0 : zero4, nxt_stage, st_off0);
-        if (g == 3) X6T_SPLIT(in1 ? ra1 : zero4, nxt_stage, st_off1);
-        if (g == 5) X6T_SPLIT(in0 ? rb0 : zero4, nxt_stage + 3 * X6_PLANE, st_off0);
-        if (g == 7) X6T_SPLIT(in1 ? rb1 : zero4, nxt_stage + 3 * X6_PLANE, st_off1);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (t + 2 < nk) X6T_LOAD(t + 2);
-#else
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -1061,7 +1031,6 @@ __global__ __launch_bounds__(512) void gemm_x6t_kernel(GemmArgs p) {
       X6T_STASH(smem + ((t + 1) & 1) * X6_STAGE);  // the other stage: last read in step t-1
       if (t + 2 < nk) X6T_LOAD(t + 2);
     }
-#endif
     __syncthreads();
   }
 #undef X6T_LOAD
@@ -1071,145 +1040,6 @@ __global__ __launch_bounds__(512) void gemm_x6t_kernel(GemmArgs p) {
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int64_t gn = n0 + wn * 64 + j * 32 + l32;
-    if (gn >= p.N) continue;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int64_t gm = m0 + wm * 128 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        if (gm < p.M) Cz[gm * p.ldc + gn] = acc[i][j][r];
-      }
-  }
-}
-
-// gemm_x6t_kernel re-tiled for ONE wave per SIMD (GRL_X6T_W1): a 256-thread
-// workgroup owns the 256 x 256 output tile, each wave 128 x 128 (16 MFMA
-// blocks: 256 accumulator registers), so a K16 step reads 24 fragment pairs
-// per 96 MFMAs (the 8-wave form: 18 per 48).  Three LDS stages (144 KB):
-// during step t the wave's MFMAs run on step t's fragments (registers) while
-// step t+1's fragments are read from LDS, step t+2's rows are split and
-// stored, and step t+3's rows are loaded -- all in the gaps of the 16 MFMA
-// groups.  Per output element the same K16 order and product order as
-// gemm_x6t_kernel: the same bits.
-#ifndef GRL_X6T_W1
-#define GRL_X6T_W1 0
-#endif
-template <int EPI>
-__global__ __launch_bounds__(256, 1) void gemm_x6t_w1_kernel(GemmArgs p) {
-  __shared__ __attribute__((aligned(16))) uint16_t smem[3 * X6_STAGE];  // 3 stages x (A, B) x 3 planes x 8 KB
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
-  int64_t mi, ni, zi;
-  tile_of(p, mi, ni, zi);
-  const int64_t m0 = mi * LB_M, n0 = ni * LB_N;
-  const int64_t kbeg = zi * p.k_per_split;
-  const int64_t kend = min(p.K, kbeg + p.k_per_split);
-  const int64_t nk = kend > kbeg ? (kend - kbeg + X6_K - 1) / X6_K : 0;
-  // staging: float4 f = tid + 256 i (i < 4) of each operand: k row (tid >> 6) + 4 i, 4 columns at (tid & 63) * 4
-  const int kr = tid >> 6;
-  const int col = (tid & 63) * 4;
-  const int64_t am = min<int64_t>(m0 + col, p.M - 4), bn = min<int64_t>(n0 + col, p.N - 4);
-  const float* __restrict__ a_base = p.A + am;
-  const float* __restrict__ b_base = p.B + bn;
-  int st_off[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int k = kr + 4 * i;
-    st_off[i] = k * 256 + (col ^ ((k & 3) << 5));
-  }
-  float4 ra[4], rb[4];
-  bool in[4];
-  const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  auto load = [&](int64_t t) {
-    const int64_t k_ = kbeg + t * X6_K;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      in[i] = k_ + kr + 4 * i < kend;
-      const int64_t r = in[i] ? k_ + kr + 4 * i : kbeg;
-      ra[i] = *reinterpret_cast<const float4*>(a_base + r * p.lda);
-      rb[i] = *reinterpret_cast<const float4*>(b_base + r * p.ldb);
-    }
-  };
-  auto split_store = [&](uint16_t* base, const float4& v, int off) {
-    uint2 q0, q1, q2;
-    split3(v, q0, q1, q2);
-    *reinterpret_cast<uint2*>(base + off) = q0;
-    *reinterpret_cast<uint2*>(base + X6_PLANE + off) = q1;
-    *reinterpret_cast<uint2*>(base + 2 * X6_PLANE + off) = q2;
-  };
-  // piece q of the stash (q < 8): operand q >> 2, row set q & 3
-  auto stash_piece = [&](uint16_t* st, int q) {
-    const int i = q & 3;
-    if (q < 4)
-      split_store(st, in[i] ? ra[i] : zero4, st_off[i]);
-    else
-      split_store(st + 3 * X6_PLANE, in[i] ? rb[i] : zero4, st_off[i]);
-  };
-  const int tk = 8 * (lane >> 5) + ((lane & 15) >> 2);
-  const int tc = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
-  f32x16 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
-  // fragments, one set: A block i is dead after its 4 MFMA groups (4i..4i+3)
-  // and B block j after group 12 + j, so step t+1's block is read into the
-  // same registers right after (>= 4 groups before its first use)
-  bf16x8_t fa[4][3], fb[4][3];
-  auto read_a = [&](const uint16_t* stg, int blk) {
-#pragma unroll
-    for (int q = 0; q < 3; ++q) fa[blk][q] = tr_pair(stg + q * X6_PLANE, tk, wm * 128 + blk * 32 + tc);
-  };
-  auto read_b = [&](const uint16_t* stg, int blk) {
-#pragma unroll
-    for (int q = 0; q < 3; ++q) fb[blk][q] = tr_pair(stg + (3 + q) * X6_PLANE, tk, wn * 128 + blk * 32 + tc);
-  };
-  if (nk > 0) {
-    load(0);
-#pragma unroll
-    for (int q = 0; q < 8; ++q) stash_piece(smem, q);
-    if (nk > 1) {
-      load(1);
-#pragma unroll
-      for (int q = 0; q < 8; ++q) stash_piece(smem + X6_STAGE, q);
-      if (nk > 2) load(2);
-    }
-  }
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < 4; ++i) read_a(smem, i);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) read_b(smem, j);
-  // one K16 step; step t+1's fragments arrive in the gaps
-  auto step = [&](int64_t t) {
-    const uint16_t* nstage = smem + (int)((t + 1) % 3) * X6_STAGE;
-    uint16_t* sstage = smem + (int)((t + 2) % 3) * X6_STAGE;
-    const bool has_next = t + 1 < nk, has_stash = t + 2 < nk, has_load = t + 3 < nk;
-#pragma unroll
-    for (int g = 0; g < 16; ++g) {
-      const int i = g >> 2, j = g & 3;
-      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][2], fb[j][0], acc[i][j], 0, 0, 0);
-      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][1], acc[i][j], 0, 0, 0);
-      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][2], acc[i][j], 0, 0, 0);
-      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][1], fb[j][0], acc[i][j], 0, 0, 0);
-      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][1], acc[i][j], 0, 0, 0);
-      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i][0], fb[j][0], acc[i][j], 0, 0, 0);
-      if (has_next && j == 3) read_a(nstage, i);   // A block i's last group done
-      if (has_next && i == 3) read_b(nstage, j);   // B block j's last group done
-      if (has_stash && g >= 4 && g < 12) stash_piece(sstage, g - 4);
-      if (has_load && g == 12) load(t + 3);
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    __syncthreads();  // stage (t+2) % 3 written; stage t % 3 free for step t+3's stash
-  };
-  for (int64_t t = 0; t < nk; ++t) step(t);
-  float* Cz = p.C + (EPI == EPI_SLAB ? zi * p.M * p.ldc : 0);
-  const int l32 = lane & 31, h = lane >> 5;
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int64_t gn = n0 + wn * 128 + j * 32 + l32;
     if (gn >= p.N) continue;
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -1739,11 +1569,7 @@ extern "C" int grl_linear_bwd_weight(const float* Z, int64_t ldz, const float* g
     a.inner_n = 0;
     GRL_CHECK_ARG(a.mt * a.nt * a.zt < 2147483647LL, "gemm: grid too large");
     const dim3 grid((unsigned)(a.mt * a.nt * a.zt));
-    if (GRL_X6T_W1 && used > 1)
-      hipLaunchKernelGGL(gemm_x6t_w1_kernel<EPI_SLAB>, grid, dim3(256), 0, st, a);
-    else if (GRL_X6T_W1)
-      hipLaunchKernelGGL(gemm_x6t_w1_kernel<EPI_STORE>, grid, dim3(256), 0, st, a);
-    else if (used > 1)
+    if (used > 1)
       hipLaunchKernelGGL(gemm_x6t_kernel<EPI_SLAB>, grid, dim3(512), 0, st, a);
     else
       hipLaunchKernelGGL(gemm_x6t_kernel<EPI_STORE>, grid, dim3(512), 0, st, a);
