@@ -21,6 +21,8 @@
 //            dQ^T += K^T dS^T
 //   kernel B (key-stationary):   recompute S with keys on lanes, dP likewise,
 //            dH^T += dO^T P,  dK^T += Q^T dS
+//   dk <= 16 with a workspace: kernel A's dQ is folded into kernel B's dK
+//   pass instead (attn_bwd_kq_x6_kernel: per-workgroup slabs, ordered sum)
 #include "grl_internal.h"
 
 #include <math.h>
@@ -56,10 +58,12 @@ struct AttnArgs {
   const uint16_t* Hpl;  // W = DV
   const uint16_t* Qpl;  // W = DKP
   const uint16_t* Opl;  // W = DV (dO)
+  const uint16_t* Qpl16;  // bwd_kq: Q planes 16 wide
   // key / query split (small N): keys per split, and partial slabs (or NULL)
   int64_t kr;
   float* part;   // fwd: o [S][B*N][dv] + m, l [S][B*N]; bwd_q: dQ [S][B*N][dk]; bwd_kv: dH [S][B*N][dv]
   float* part2;  // bwd_kv: dK [S][B*N][dk]
+  float* qslab;  // bwd_kq: dQ partials [B][ceil(N / 128)][N][16], one row block per key workgroup
   int64_t N;
   int dk, dv;
 };
@@ -1397,6 +1401,224 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_x6_kernel(AttnArgs a) {
 }
 
 
+// Key-stationary dK with dQ folded in (dk <= 16, PRE staging): what the
+// query-stationary attn_bwd_q_x6_kernel computes, without recomputing S and
+// dP = dO H^T for it -- 66 MFMAs per 32 x 32 block pair there, 18 more here.
+// Per query block, after the dK kernel's work:
+//  - dS (keys on lanes, queries in registers) is transposed EXACTLY by MFMAs
+//    against a 0/1 permutation operand: D[key][q] = sum over the 3 planes of
+//    dS's split, one nonzero product per element and plane, and hi + mid + lo
+//    is exact in fp32; so D's registers hold keys and its lanes queries;
+//  - dQ_blk[q][d] = D^T K over the wave's 32 keys: A = D's planes, B = the
+//    wave's K rows (natural scale, planes in LDS, read transposed like Q^T
+//    for dK; lanes 16..31 read columns 0..15 again, their outputs dropped);
+//  - every wave parks its partial in LDS; after a barrier wave w adds
+//    queries [8w, 8w + 8) of the four in wave order and writes them to this
+//    workgroup's slab, qslab[b][blockIdx.x][d][npad].
+// attn_qslab_sum_kernel then adds the slabs in workgroup order: dQ is
+// deterministic.  The scores are natural-scale here (K is shared with dQ)
+// and p = 2^(fma(s, log2 e, -lse2)): the same instruction count as the
+// base-2 kernels' v_sub.  Q comes as 16-wide planes (LDS for the partials).
+// N = 100k fwd+bwd: 61.7 -> 54.5 ms on one box (tools/ab_kq.sh); the extra
+// barrier and the partials cost ~3.5 ms of that (GRL_KQ_WHATIF=2).
+template <bool SPLIT>
+__global__ __launch_bounds__(256, 2) void attn_bwd_kq_x6_kernel(AttnArgs a) {
+  constexpr int FC = 8;
+  __shared__ __attribute__((aligned(16))) uint16_t Qp_s[2 * 3 * 32 * 16];  // 2 stages, 16-wide planes
+  __shared__ __attribute__((aligned(16))) uint16_t Op_s[2 * 3 * 32 * 128];
+  __shared__ __attribute__((aligned(16))) uint16_t Kt_s[3 * 128 * 16];  // this workgroup's K rows, planes [key][16]
+  __shared__ __attribute__((aligned(16))) float Red_s[4 * 16 * 32];     // the waves' dQ partials [w][d][q]
+  __shared__ float Ms_s[2 * 32], Ds_s[2 * 32];                          // lse2, D per query
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, h = lane >> 5;
+  const int64_t N = a.N, b = blockIdx.y;
+  const int64_t key = (int64_t)blockIdx.x * 128 + wave * 32 + l32;
+  const bool kv = key < N;
+  const int64_t q_lo = SPLIT ? (int64_t)blockIdx.z * a.kr : 0, q_hi = SPLIT ? min<int64_t>(N, q_lo + a.kr) : N;
+  abf16x8_t hp[FC][3];
+  row_planes<FC>(a.H + (b * N + key) * a.dv, kv, a.dv, h, hp);
+  {  // K rows, natural scale (the scores' B operand, and dQ's; zero for padded keys)
+    abf16x8_t kt[1][3];
+    row_planes<1>(a.K + (b * N + key) * a.dk, kv, a.dk, h, kt);
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+      *reinterpret_cast<abf16x8_t*>(&Kt_s[pl * 2048 + (wave * 32 + l32) * 16 + 8 * h]) = kt[0][pl];
+  }
+  // permutation operand of MFMA u: B[k = 8h + j][n] = 1 iff query kappa(8u + j, h) == n (n = l32),
+  // i.e. u == n >> 4 and, in half h == (n >> 2) & 1, slot j == 4 ((n >> 3) & 1) + (n & 3)
+  const int perm_u = l32 >> 4;
+  ai16x8_t onehot;
+  {
+    const int jj = 4 * ((l32 >> 3) & 1) + (l32 & 3);
+    const bool mine = h == ((l32 >> 2) & 1);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) onehot[j] = (mine && j == jj) ? (short)0x3F80 : (short)0;
+  }
+  f32x16 acc = zero16();
+  const int64_t qps = (int64_t)gridDim.y * N * 16, ops = (int64_t)gridDim.y * N * 128;
+  const uint16_t* Qpb = a.Qpl16 + b * N * 16;
+  const uint16_t* Opb = a.Opl + b * N * 128;
+  const int64_t npad = (N + 31) & ~(int64_t)31;  // slab rows padded to whole query blocks
+  float* slab = a.qslab + ((int64_t)b * gridDim.x + blockIdx.x) * 16 * npad;  // [d][npad]
+  float pm = 0.0f, pd = 0.0f;
+  auto fetch_stats = [&](int64_t q0) {
+    if (tid < 32) {
+      const int64_t qq = q0 + tid;
+      const bool v = qq < q_hi;
+      pm = v ? fmaf(a.smax[b * N + qq], ALOG2E, alog2(a.ssum[b * N + qq])) : INFINITY;  // P = 0 when padded
+      pd = v ? a.Drow[b * N + qq] : 0.0f;
+    }
+  };
+  dma_block<16, PL_PLAIN>(Qpb, qps, q_lo, N, Qp_s, wave, lane);
+  dma_block<128, PL_SWZ128>(Opb, ops, q_lo, N, Op_s, wave, lane);
+  fetch_stats(q_lo);
+  const int trq = (lane & 15) >> 2, trc = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
+
+  for (int64_t q0 = q_lo; q0 < q_hi; q0 += 32) {
+    const int stg = (int)(((q0 - q_lo) >> 5) & 1);
+    uint16_t* Qp = Qp_s + stg * 3 * 512;
+    uint16_t* Op = Op_s + stg * 3 * 4096;
+    float* Ms = Ms_s + stg * 32;
+    float* Ds = Ds_s + stg * 32;
+    if (tid < 32) {
+      Ms[tid] = pm;
+      Ds[tid] = pd;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (q0 + 32 < q_hi) {
+      dma_block<16, PL_PLAIN>(Qpb, qps, q0 + 32, N, Qp_s + (stg ^ 1) * 3 * 512, wave, lane);
+      dma_block<128, PL_SWZ128>(Opb, ops, q0 + 32, N, Op_s + (stg ^ 1) * 3 * 4096, wave, lane);
+      fetch_stats(q0 + 32);
+    }
+    // S[query][key]: lanes = keys, registers = queries kappa(r, h)
+    f32x16 s = zero16();  // natural-scale scores q.k (base 2 applied in the exponent's fma)
+    {
+      const int off = l32 * 16 + 8 * h, koff = (wave * 32 + l32) * 16 + 8 * h;
+      const abf16x8_t q0p = *reinterpret_cast<const abf16x8_t*>(&Qp[off]);
+      const abf16x8_t q1p = *reinterpret_cast<const abf16x8_t*>(&Qp[512 + off]);
+      const abf16x8_t q2p = *reinterpret_cast<const abf16x8_t*>(&Qp[1024 + off]);
+      const abf16x8_t k0p = *reinterpret_cast<const abf16x8_t*>(&Kt_s[koff]);
+      const abf16x8_t k1p = *reinterpret_cast<const abf16x8_t*>(&Kt_s[2048 + koff]);
+      const abf16x8_t k2p = *reinterpret_cast<const abf16x8_t*>(&Kt_s[4096 + koff]);
+      MFMA6(s, q0p, q1p, q2p, k0p, k1p, k2p);
+    }
+    f32x16 dp = zero16();  // dP[query][key] = sum_f dO[query][f] H[key][f]
+#pragma unroll
+    for (int fc = 0; fc < FC; ++fc) {
+      const int off = swz128(l32, fc * 16 + 8 * h);
+      const abf16x8_t o0 = *reinterpret_cast<const abf16x8_t*>(&Op[off]);
+      const abf16x8_t o1 = *reinterpret_cast<const abf16x8_t*>(&Op[4096 + off]);
+      const abf16x8_t o2 = *reinterpret_cast<const abf16x8_t*>(&Op[8192 + off]);
+      MFMA6(dp, o0, o1, o2, hp[fc][0], hp[fc][1], hp[fc][2]);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int qi = kappa(r, h);
+      s[r] = aexp2(fmaf(s[r], ALOG2E, -Ms[qi])) * (dp[r] - Ds[qi]);  // dS
+    }
+    abf16x8_t dsp[2][3];
+    reg_planes(s, dsp);
+    f32x16 dt = zero16();  // dS transposed: lanes = queries, registers = keys kappa(r, h)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int r0 = kappa(8 * u + trq, h), r1 = kappa(8 * u + 4 + trq, h);
+      abf16x8_t qt[3];
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        qt[pl] = tr8(&Qp[pl * 512 + r0 * 16 + (trc & 15)], &Qp[pl * 512 + r1 * 16 + (trc & 15)]);
+      MFMA6(acc, qt[0], qt[1], qt[2], dsp[u][0], dsp[u][1], dsp[u][2]);  // dK^T += Q^T dS
+      ai16x8_t pv;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pv[j] = u == perm_u ? onehot[j] : (short)0;
+      const abf16x8_t perm = __builtin_bit_cast(abf16x8_t, pv);
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl) dt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(dsp[u][pl], perm, dt, 0, 0, 0);
+    }
+#if GRL_KQ_WHATIF == 3
+    if (dt[0] == 12345.0f) acc[0] += 1.0f;  // timing diagnostic: no dQ work (WRONG dQ)
+    continue;
+#endif
+    abf16x8_t dtp[2][3];
+    reg_planes(dt, dtp);
+    f32x16 dq = zero16();  // dQ_blk[query][d] over this wave's 32 keys (columns d >= 16 discarded)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int r0 = wave * 32 + kappa(8 * u + trq, h), r1 = wave * 32 + kappa(8 * u + 4 + trq, h);
+      abf16x8_t kt[3];
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        kt[pl] = tr8(&Kt_s[pl * 2048 + r0 * 16 + (trc & 15)], &Kt_s[pl * 2048 + r1 * 16 + (trc & 15)]);
+      MFMA6(dq, dtp[u][0], dtp[u][1], dtp[u][2], kt[0], kt[1], kt[2]);
+    }
+    // dq: lanes = d (valid l32 < 16), registers r = query kappa(r, h); registers 4g..4g+3 are
+    // the 4 consecutive queries 8g + 4h + 0..3.  Every wave parks its partial in LDS, then
+    // wave w adds queries [8w, 8w + 8) of all four in wave order and writes them to the slab.
+#if GRL_KQ_WHATIF == 2
+    if (dq[0] == 12345.0f) acc[0] += 1.0f;  // timing diagnostic: no reduction, no stores (WRONG dQ)
+    continue;
+#endif
+    if (l32 < 16) {
+      float* dst = Red_s + wave * 512 + l32 * 32 + 4 * h;
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+        *reinterpret_cast<float4*>(dst + 8 * g) = make_float4(dq[4 * g], dq[4 * g + 1], dq[4 * g + 2], dq[4 * g + 3]);
+    }
+    __syncthreads();
+    {
+      const int d = lane >> 2, qq = 8 * wave + 2 * (lane & 3);
+      const float* src = Red_s + d * 32 + qq;
+      float2 x = *reinterpret_cast<const float2*>(src);
+#pragma unroll
+      for (int w = 1; w < 4; ++w) {
+        const float2 y = *reinterpret_cast<const float2*>(src + w * 512);
+        x.x += y.x;
+        x.y += y.y;
+      }
+      // split ranges are whole query blocks, so a block never reaches into
+      // another split's rows; past N it writes the padding (zeros: P = 0)
+#if GRL_KQ_WHATIF == 1
+      if (x.x == 12345.0f) acc[0] += 1.0f;  // timing diagnostic: no slab stores (WRONG dQ)
+#else
+      *reinterpret_cast<float2*>(slab + d * npad + q0 + qq) = x;
+#endif
+    }
+  }
+  if (kv) {  // query split: partial dK into slab blockIdx.z (summed in split order afterwards)
+    const int64_t rows = (int64_t)gridDim.y * N;
+    float* dst = SPLIT ? a.part2 + (int64_t)blockIdx.z * rows * a.dk : a.dK;
+    const int64_t rowk = (b * N + key) * a.dk;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int d = kappa(r, h);
+      if (d < a.dk) dst[rowk + d] = acc[r];
+    }
+  }
+}
+
+// dQ[b][q][d] = sum over key workgroups x of qslab[b][x][q][d], in x order
+__global__ void attn_qslab_sum_kernel(const float* __restrict__ qslab, int64_t B, int64_t X, int64_t N, int dk,
+                                      float* __restrict__ dQ) {
+  const int64_t n_all = B * N * dk;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_all; i += (int64_t)gridDim.x * blockDim.x) {
+    // i = (b * dk + d) * N + q: consecutive threads read consecutive q of one slab row
+    const int64_t bd = i / N, q = i - bd * N, b = bd / dk;
+    const int d = (int)(bd - b * dk);
+    const int64_t npad = (N + 31) & ~(int64_t)31, xs = 16 * npad;  // slab [b][x][d][npad]
+    const float* p = qslab + b * X * xs + (int64_t)d * npad + q;
+    float acc = 0.0f;
+    int64_t x = 0;
+    for (; x + 4 <= X; x += 4) {
+      const float v0 = p[(x + 0) * xs], v1 = p[(x + 1) * xs], v2 = p[(x + 2) * xs], v3 = p[(x + 3) * xs];
+      acc += v0;
+      acc += v1;
+      acc += v2;
+      acc += v3;
+    }
+    for (; x < X; ++x) acc += p[x * xs];
+    dQ[(b * N + q) * dk + d] = acc;
+  }
+}
+
 // Key split of the forward: out / o_norm / row_max / row_sum from the S
 // partial (o, m, l) in split order (deterministic), m_s in base 2:
 //   M = max_s m_s,  L = sum_s l_s 2^(m_s - M),  O = sum_s o_s 2^(m_s - M) / L
@@ -1441,6 +1663,18 @@ enum AttnPass { PASS_FWD, PASS_BWD_Q, PASS_BWD_KV };
 // GRL_ATTN_X6=0 (read per call) keeps the fp32-MFMA kernels
 bool attn_x6_enabled() {
   const char* e = getenv("GRL_ATTN_X6");
+  return !(e && e[0] == '0');
+}
+
+// GRL_KQ_WHATIF (timing diagnostics only, WRONG dQ): 1 = no slab stores,
+// 2 = no cross-wave reduction either, 3 = no dQ work after the transpose
+#ifndef GRL_KQ_WHATIF
+#define GRL_KQ_WHATIF 0
+#endif
+
+// GRL_ATTN_FUSED_DQ=0 (read per call) keeps the separate dQ kernel (A/B aid)
+bool attn_fused_dq_enabled() {
+  const char* e = getenv("GRL_ATTN_FUSED_DQ");
   return !(e && e[0] == '0');
 }
 
@@ -1508,7 +1742,21 @@ int launch_attn(AttnPass pass, const AttnArgs& a0, int64_t B, int S, hipStream_t
       if (S > 1) a.part2 = a.part + (int64_t)S * rows * a.dv;
       GRL_X6L(attn_bwd_kv_x6_kernel, DKP, true);
       GRL_LAUNCH_CHECK();
-      GRL_X6L(attn_bwd_kv_x6_kernel, DKP, false);
+      bool kq = false;
+      if constexpr (DKP == 16) {
+        if (a.qslab && pre) {  // dK with dQ folded in (grl_node_attention_bwd skipped the dQ pass)
+          kq = true;
+          if (S > 1)
+            hipLaunchKernelGGL((attn_bwd_kq_x6_kernel<true>), grid, dim3(256), 0, st, a);
+          else
+            hipLaunchKernelGGL((attn_bwd_kq_x6_kernel<false>), grid, dim3(256), 0, st, a);
+          GRL_LAUNCH_CHECK();
+          if (a.dk > 0)
+            hipLaunchKernelGGL(attn_qslab_sum_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(rows * a.dk, 256), 8192)),
+                               dim3(256), 0, st, a.qslab, B, (int64_t)grid.x, a.N, a.dk, a.dQ);
+        }
+      }
+      if (!kq) GRL_X6L(attn_bwd_kv_x6_kernel, DKP, false);
       if (S > 1) {
         GRL_LAUNCH_CHECK();
         hipLaunchKernelGGL(attn_slab_sum_kernel, dim3(red), dim3(256), 0, st, a.part, rows * a.dv, S, a.dH);
@@ -1632,6 +1880,21 @@ extern "C" size_t grl_node_attention_workspace_size(int64_t B, int64_t N, int32_
   return planes + part ? planes + part + 512 : 0;
 }
 
+// the backward's dQ slabs (attn_bwd_kq_x6_kernel): dk <= 16, x6 planes, and
+// at most kAttnQslabMax bytes (N^2 / 2 at B = 1: 5 GB at N = 100k)
+constexpr size_t kAttnQslabMax = (size_t)24 << 30;
+static size_t attn_qslab_bytes(int64_t B, int64_t N, int dk, int dv) {
+  if (!attn_fused_dq_enabled() || dk > 16 || attn_dvp(dv) != 128 || B * N < kAttnPlaneMinRows) return 0;
+  const size_t n = (size_t)B * (size_t)ceil_div(N, 128) * (size_t)(ceil_div(N, 32) * 32) * 16 * 4;
+  return n <= kAttnQslabMax ? (n + 255) / 256 * 256 : 0;
+}
+
+extern "C" size_t grl_node_attention_bwd_workspace_size(int64_t B, int64_t N, int32_t dk, int32_t dv) {
+  const size_t base = grl_node_attention_workspace_size(B, N, dk, dv);
+  const size_t q = base ? attn_qslab_bytes(B, N, dk, dv) : 0;
+  return base + (q ? q + attn_plane_bytes(B * N, 16) : 0);
+}
+
 extern "C" int grl_node_attention_fwd(const float* Q, const float* K, const float* H, const float* V,
                                       const float* gamma, float* out, float* o_norm, float* row_max, float* row_sum,
                                       int64_t B, int64_t N, int32_t dk, int32_t dv, void* workspace,
@@ -1725,11 +1988,26 @@ extern "C" int grl_node_attention_bwd(const float* Q, const float* K, const floa
     if (S > 1 && cur + (size_t)S * B * N * (dv + dk) * 4 <= end) {
       a.part = reinterpret_cast<float*>(cur);
       a.kr = kr;
+      cur += ((size_t)S * B * N * (dv + dk) * 4 + 255) / 256 * 256;
     } else {
       S = 1;
     }
+    const size_t qs = attn_qslab_bytes(B, N, dk, dv);
+    const uint16_t* q16 = nullptr;
+    if (qs && a.Qpl && dk > 0 && cur + qs <= end) {
+      a.qslab = reinterpret_cast<float*>(cur);
+      cur += qs;
+      if (attn_split(Q, B * N, dk, 16, cur, end, &q16, st)) {
+        a.Qpl16 = q16;
+      } else {
+        a.qslab = nullptr;
+      }
+      GRL_LAUNCH_CHECK();
+    }
   }
-  rc = dispatch(PASS_BWD_Q, a, B, S, st);
-  if (rc) return rc;
+  if (!a.qslab) {
+    rc = dispatch(PASS_BWD_Q, a, B, S, st);
+    if (rc) return rc;
+  }
   return dispatch(PASS_BWD_KV, a, B, S, st);
 }

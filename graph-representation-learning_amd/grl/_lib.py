@@ -170,6 +170,7 @@ SIGNATURES = {
     "grl_bag_linear_bwd_weight": (_c_i32, [_c_vp, _c_i64, _c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_i32, _c_i32, _c_vp,
                                            _c_size, _c_vp]),
     "grl_node_attention_workspace_size": (_c_size, [_c_i64, _c_i64, _c_i32, _c_i32]),
+    "grl_node_attention_bwd_workspace_size": (_c_size, [_c_i64, _c_i64, _c_i32, _c_i32]),
     "grl_node_attention_fwd": (_c_i32, [_c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_i64,
                                         _c_i32, _c_i32, _c_vp, _c_size, _c_vp]),
     "grl_node_attention_bwd": (_c_i32, [_c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_i64,

@@ -568,9 +568,11 @@ def _attn_check(Q, K, H, V, gamma):
                             f"V {tuple(V.shape)}, gamma {tuple(gamma.shape)}")
 
 
-def _attn_workspace(B, N, dk, dv, device):
-    """bf16 planes of the attention operands, split once per call (grl.h)."""
-    n = _lib.lib().grl_node_attention_workspace_size(B, N, dk, dv)
+def _attn_workspace(B, N, dk, dv, device, backward: bool = False):
+    """bf16 planes of the attention operands, split once per call, and the
+    backward's partials (grl.h)."""
+    lib = _lib.lib()
+    n = (lib.grl_node_attention_bwd_workspace_size if backward else lib.grl_node_attention_workspace_size)(B, N, dk, dv)
     return (torch.empty(n, dtype=torch.uint8, device=device), n) if n else (None, 0)
 
 
@@ -638,7 +640,7 @@ class _NodeAttention(torch.autograd.Function):
             dQ_b, dK_b = torch.empty_like(Q), torch.empty_like(K)
             dH_b = torch.empty(B, N, b - a, dtype=H.dtype, device=H.device)
             H_b = H[..., a:b].contiguous()
-            ws, ws_bytes = _attn_workspace(B, N, dk, b - a, Q.device)
+            ws, ws_bytes = _attn_workspace(B, N, dk, b - a, Q.device, backward=True)
             call("grl_node_attention_bwd", Q.data_ptr(), K.data_ptr(), H_b.data_ptr(), dO_b.data_ptr(),
                  rmax.data_ptr(), rsum.data_ptr(), D.data_ptr(), dQ_b.data_ptr(), dK_b.data_ptr(), dH_b.data_ptr(),
                  B, N, dk, b - a, ws.data_ptr() if ws is not None else None, ws_bytes,

@@ -428,9 +428,15 @@ int grl_node_attention_fwd(const float* Q, const float* K, const float* H,
 /* Backward of the attention core.  dO = gamma * d_out [B, N, dv] and
  * D = rowsum(dO * o_norm) [B, N] come from the caller (elementwise); the
  * kernels recompute P from row_max/row_sum and write dQ, dK [B, N, dk] and
- * dH [B, N, dv] (fully overwritten).  Deterministic: dQ is query-stationary,
- * dK/dH key-stationary, no atomics.  d gamma = sum(d_out * o_norm) and the
- * residual's d_out are the caller's.                                        */
+ * dH [B, N, dv] (fully overwritten).  Deterministic, no atomics: dK / dH are
+ * key-stationary; dQ is query-stationary, or -- with a workspace of
+ * grl_node_attention_bwd_workspace_size bytes, dk <= 16 -- folded into the
+ * dK kernel as one partial slab per 128-key workgroup (B ceil(N/128) N 64
+ * bytes, at most 24 GiB; larger N keeps the dQ kernel) added in workgroup
+ * order.  d gamma = sum(d_out * o_norm) and the residual's d_out are the
+ * caller's.                                                                  */
+size_t grl_node_attention_bwd_workspace_size(int64_t B, int64_t N, int32_t dk,
+                                             int32_t dv);
 int grl_node_attention_bwd(const float* Q, const float* K, const float* H,
                            const float* dO, const float* row_max,
                            const float* row_sum, const float* D, float* dQ,

@@ -47,7 +47,7 @@ def _set_mode(mode, monkeypatch):
 
     monkeypatch.setenv("GRL_ATTN_X6", "0" if mode == "f32" else "1")
     if mode == "x6-no-workspace":
-        monkeypatch.setattr(grl.ops, "_attn_workspace", lambda *a: (None, 0))
+        monkeypatch.setattr(grl.ops, "_attn_workspace", lambda *a, **k: (None, 0))
 
 
 @pytest.mark.parametrize("mode", MODES)
@@ -138,3 +138,31 @@ def test_pipelined_forward_same_bits(B, N, dk, dv, monkeypatch):
     assert torch.equal(res["1"][0], res["0"][0])
     for a, b in zip(res["1"][1], res["0"][1]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("B,N,dk,dv", [(1, 8192, 16, 128), (2, 5000, 16, 100), (3, 4099, 9, 128), (1, 6000, 1, 97)])
+def test_fused_dq_backward(B, N, dk, dv, monkeypatch):
+    """dQ folded into the key-stationary dK kernel (attn_bwd_kq_x6_kernel:
+    exact MFMA transpose of dS, per-workgroup slabs added in order) against
+    fp64 and against the separate dQ kernel (GRL_ATTN_FUSED_DQ=0); dK / dH
+    within the same tolerance, deterministic run to run."""
+    lib = _lib.lib()
+    assert lib.grl_node_attention_bwd_workspace_size(B, N, dk, dv) > lib.grl_node_attention_workspace_size(B, N, dk, dv)
+    Q, K, H, V, gamma = _inputs(B, N, dk, dv, seed=N + 3 * dk)
+    dout = torch.randn(B, N, dv, generator=torch.Generator().manual_seed(4)).to(DEV)
+    grads = {}
+    for fused in ("1", "0", "1"):
+        monkeypatch.setenv("GRL_ATTN_FUSED_DQ", fused)
+        leaves = [t.clone().requires_grad_(True) for t in (Q, K, H, V, gamma)]
+        node_self_attention(*leaves).backward(dout)
+        g = [t.grad for t in leaves]
+        if fused in grads:
+            for a, b in zip(grads[fused], g):
+                assert torch.equal(a, b)
+        grads[fused] = g
+    ref_leaves = [t.double().clone().requires_grad_(True) for t in (Q, K, H, V, gamma)]
+    _ref(*ref_leaves).backward(dout.double())
+    for name, a, c, r in zip("QKHVg", grads["1"], grads["0"], ref_leaves):
+        scale = r.grad.abs().max().item() + 1.0
+        torch.testing.assert_close(a.double(), r.grad, rtol=1e-4, atol=2e-5 * scale, msg=f"fused d{name}")
+        torch.testing.assert_close(a.double(), c.double(), rtol=1e-4, atol=2e-5 * scale, msg=f"fused vs dQ kernel d{name}")

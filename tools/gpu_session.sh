@@ -134,6 +134,9 @@ for step in "$@"; do
     tests_r3) run pytest_gpu_r3 600 python -u -m pytest tests/test_gpu_halo_async.py tests/test_gpu_graphconv.py \
                   tests/test_gpu_embed.py tests/test_gpu_dist.py::test_bench_spawns_its_ranks_without_a_launcher \
                   -m gpu -v -rf --timeout 240 --timeout-method thread ;;
+    ab_fused_dq) rm -f gpurun_out/ab_fused_dq.log; run ab_fused_dq 900 tools/ab_fused_dq.sh ;;
+    prof_attn_fused) run prof_attn_fused 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_attn_fused" -o run \
+                  --output-format csv -- python tools/probe_attn.py 100000 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
