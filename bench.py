@@ -197,7 +197,8 @@ def main():
     ndev = torch.cuda.device_count()
     if ndev == 0:
         raise SystemExit(f"bench.py rank {rank}: no ROCm GPU visible (the path runs on MI355X only)")
-    if args.dist_backend == "nccl" and world > 1 and local_rank >= ndev:
+    # one visible GPU per rank (a launcher that isolates devices) -> cuda:0; otherwise LOCAL_RANK picks it
+    if args.dist_backend == "nccl" and world > 1 and ndev > 1 and local_rank >= ndev:
         raise SystemExit(f"rank {rank}: LOCAL_RANK {local_rank} but only {ndev} GPU(s) visible")
     dev = torch.device("cuda", local_rank % ndev)
     torch.cuda.set_device(dev)
