@@ -574,14 +574,14 @@ __device__ __forceinline__ void adma16(const void* src, const void* lds_base) {
 // is its destination.  Rows past N re-read row N-1 (finite values whose
 // scores / probabilities the kernels mask to zero).  Completion: the
 // caller's vmcnt(0) + barrier at the top of the block that reads it.
-template <int W, int LAYOUT>
+template <int W, int LAYOUT, int NW = 4>
 __device__ __forceinline__ void dma_block(const uint16_t* planes, int64_t ps, int64_t r0, int64_t N, uint16_t* lds,
                                           int wave, int lane) {
-  constexpr int PL = 32 * W, NI = 3 * PL / 512;
+  constexpr int PL = 32 * W, NI = 3 * PL / 512;  // 1 KB chunks, dealt to the NW waves of the workgroup
   const int ln = lane;
 #pragma unroll
-  for (int j = 0; j < (NI + 3) / 4; ++j) {
-    const int i = wave + 4 * j;
+  for (int j = 0; j < (NI + NW - 1) / NW; ++j) {
+    const int i = wave + NW * j;
     if (i < NI) {
       const int e = i * 512 + ln * 8;
       const int pl = e / PL, rem = e % PL, r = rem / W, pos = rem % W;
@@ -1404,7 +1404,9 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_x6_kernel(AttnArgs a) {
 // Key-stationary dK with dQ folded in (dk <= 16, PRE staging): what the
 // query-stationary attn_bwd_q_x6_kernel computes, without recomputing S and
 // dP = dO H^T for it -- 66 MFMAs per 32 x 32 block pair there, 18 more here.
-// Per query block, after the dK kernel's work:
+// 8 waves (256 keys) per workgroup, one workgroup per CU: the query block's
+// Q / dO stage is shared by twice the keys, and the LDS holds the partials
+// of two blocks.  Per query block, after the dK kernel's work:
 //  - dS (keys on lanes, queries in registers) is transposed EXACTLY by MFMAs
 //    against a 0/1 permutation operand: D[key][q] = sum over the 3 planes of
 //    dS's split, one nonzero product per element and plane, and hi + mid + lo
@@ -1412,26 +1414,29 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_x6_kernel(AttnArgs a) {
 //  - dQ_blk[q][d] = D^T K over the wave's 32 keys: A = D's planes, B = the
 //    wave's K rows (natural scale, planes in LDS, read transposed like Q^T
 //    for dK; lanes 16..31 read columns 0..15 again, their outputs dropped);
-//  - every wave parks its partial in LDS; after a barrier wave w adds
-//    queries [8w, 8w + 8) of the four in wave order and writes them to this
-//    workgroup's slab, qslab[b][blockIdx.x][d][npad].
+//  - every wave parks its partial in the block's LDS slot (block parity);
+//    after the NEXT block's barrier wave w adds queries [4w, 4w + 4) of the
+//    eight in wave order and writes them to this workgroup's slab,
+//    qslab[b][blockIdx.x][d][npad] -- no barrier of its own (the slot is
+//    rewritten two blocks later, behind another barrier).
 // attn_qslab_sum_kernel then adds the slabs in workgroup order: dQ is
 // deterministic.  The scores are natural-scale here (K is shared with dQ)
 // and p = 2^(fma(s, log2 e, -lse2)): the same instruction count as the
-// base-2 kernels' v_sub.  Q comes as 16-wide planes (LDS for the partials).
-// N = 100k fwd+bwd: 61.7 -> 54.5 ms on one box (tools/ab_kq.sh); the extra
-// barrier and the partials cost ~3.5 ms of that (GRL_KQ_WHATIF=2).
+// base-2 kernels' v_sub.  Q comes as 16-wide planes.
+constexpr int KQ_WAVES = 8, KQ_KEYS = 32 * KQ_WAVES;
 template <bool SPLIT>
-__global__ __launch_bounds__(256, 2) void attn_bwd_kq_x6_kernel(AttnArgs a) {
-  constexpr int FC = 8;
+__global__ __launch_bounds__(64 * KQ_WAVES, 1) void attn_bwd_kq_x6_kernel(AttnArgs a) {
+  constexpr int FC = 8, NW = KQ_WAVES, KW = KQ_KEYS;
+  constexpr int RP = 36;  // partial row pitch in floats: d-major rows, conflict-free reads of 4 queries x 16 d
+  constexpr int RSLOT = NW * 16 * RP;
   __shared__ __attribute__((aligned(16))) uint16_t Qp_s[2 * 3 * 32 * 16];  // 2 stages, 16-wide planes
   __shared__ __attribute__((aligned(16))) uint16_t Op_s[2 * 3 * 32 * 128];
-  __shared__ __attribute__((aligned(16))) uint16_t Kt_s[3 * 128 * 16];  // this workgroup's K rows, planes [key][16]
-  __shared__ __attribute__((aligned(16))) float Red_s[4 * 16 * 32];     // the waves' dQ partials [w][d][q]
-  __shared__ float Ms_s[2 * 32], Ds_s[2 * 32];                          // lse2, D per query
+  __shared__ __attribute__((aligned(16))) uint16_t Kt_s[3 * KW * 16];  // this workgroup's K rows, planes [key][16]
+  __shared__ __attribute__((aligned(16))) float Red_s[2 * RSLOT];      // 2 slots x the waves' partials [w][d][RP]
+  __shared__ float Ms_s[2 * 32], Ds_s[2 * 32];                         // lse2, D per query
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, h = lane >> 5;
   const int64_t N = a.N, b = blockIdx.y;
-  const int64_t key = (int64_t)blockIdx.x * 128 + wave * 32 + l32;
+  const int64_t key = (int64_t)blockIdx.x * KW + wave * 32 + l32;
   const bool kv = key < N;
   const int64_t q_lo = SPLIT ? (int64_t)blockIdx.z * a.kr : 0, q_hi = SPLIT ? min<int64_t>(N, q_lo + a.kr) : N;
   abf16x8_t hp[FC][3];
@@ -1441,7 +1446,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kq_x6_kernel(AttnArgs a) {
     row_planes<1>(a.K + (b * N + key) * a.dk, kv, a.dk, h, kt);
 #pragma unroll
     for (int pl = 0; pl < 3; ++pl)
-      *reinterpret_cast<abf16x8_t*>(&Kt_s[pl * 2048 + (wave * 32 + l32) * 16 + 8 * h]) = kt[0][pl];
+      *reinterpret_cast<abf16x8_t*>(&Kt_s[pl * KW * 16 + (wave * 32 + l32) * 16 + 8 * h]) = kt[0][pl];
   }
   // permutation operand of MFMA u: B[k = 8h + j][n] = 1 iff query kappa(8u + j, h) == n (n = l32),
   // i.e. u == n >> 4 and, in half h == (n >> 2) & 1, slot j == 4 ((n >> 3) & 1) + (n & 3)
@@ -1468,8 +1473,19 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kq_x6_kernel(AttnArgs a) {
       pd = v ? a.Drow[b * N + qq] : 0.0f;
     }
   };
-  dma_block<16, PL_PLAIN>(Qpb, qps, q_lo, N, Qp_s, wave, lane);
-  dma_block<128, PL_SWZ128>(Opb, ops, q_lo, N, Op_s, wave, lane);
+  // block qb's eight partials (its slot, visible behind a barrier): wave w adds queries
+  // [4w, 4w + 4) x 16 d in wave order.  Split ranges are whole query blocks, so a block
+  // never reaches into another split's rows; past N it writes the padding (zeros: P = 0).
+  auto reduce = [&](int64_t qb) {
+    const float* src = Red_s + (int)(((qb - q_lo) >> 5) & 1) * RSLOT;
+    const int q = 4 * wave + (lane >> 4), d = lane & 15;
+    float x = src[d * RP + q];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) x += src[w * 16 * RP + d * RP + q];
+    slab[d * npad + qb + q] = x;
+  };
+  dma_block<16, PL_PLAIN, NW>(Qpb, qps, q_lo, N, Qp_s, wave, lane);
+  dma_block<128, PL_SWZ128, NW>(Opb, ops, q_lo, N, Op_s, wave, lane);
   fetch_stats(q_lo);
   const int trq = (lane & 15) >> 2, trc = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
 
@@ -1486,10 +1502,11 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kq_x6_kernel(AttnArgs a) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (q0 + 32 < q_hi) {
-      dma_block<16, PL_PLAIN>(Qpb, qps, q0 + 32, N, Qp_s + (stg ^ 1) * 3 * 512, wave, lane);
-      dma_block<128, PL_SWZ128>(Opb, ops, q0 + 32, N, Op_s + (stg ^ 1) * 3 * 4096, wave, lane);
+      dma_block<16, PL_PLAIN, NW>(Qpb, qps, q0 + 32, N, Qp_s + (stg ^ 1) * 3 * 512, wave, lane);
+      dma_block<128, PL_SWZ128, NW>(Opb, ops, q0 + 32, N, Op_s + (stg ^ 1) * 3 * 4096, wave, lane);
       fetch_stats(q0 + 32);
     }
+    if (q0 > q_lo) reduce(q0 - 32);
     // S[query][key]: lanes = keys, registers = queries kappa(r, h)
     f32x16 s = zero16();  // natural-scale scores q.k (base 2 applied in the exponent's fma)
     {
@@ -1498,8 +1515,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kq_x6_kernel(AttnArgs a) {
       const abf16x8_t q1p = *reinterpret_cast<const abf16x8_t*>(&Qp[512 + off]);
       const abf16x8_t q2p = *reinterpret_cast<const abf16x8_t*>(&Qp[1024 + off]);
       const abf16x8_t k0p = *reinterpret_cast<const abf16x8_t*>(&Kt_s[koff]);
-      const abf16x8_t k1p = *reinterpret_cast<const abf16x8_t*>(&Kt_s[2048 + koff]);
-      const abf16x8_t k2p = *reinterpret_cast<const abf16x8_t*>(&Kt_s[4096 + koff]);
+      const abf16x8_t k1p = *reinterpret_cast<const abf16x8_t*>(&Kt_s[KW * 16 + koff]);
+      const abf16x8_t k2p = *reinterpret_cast<const abf16x8_t*>(&Kt_s[2 * KW * 16 + koff]);
       MFMA6(s, q0p, q1p, q2p, k0p, k1p, k2p);
     }
     f32x16 dp = zero16();  // dP[query][key] = sum_f dO[query][f] H[key][f]
@@ -1534,10 +1551,6 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kq_x6_kernel(AttnArgs a) {
 #pragma unroll
       for (int pl = 0; pl < 3; ++pl) dt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(dsp[u][pl], perm, dt, 0, 0, 0);
     }
-#if GRL_KQ_WHATIF == 3
-    if (dt[0] == 12345.0f) acc[0] += 1.0f;  // timing diagnostic: no dQ work (WRONG dQ)
-    continue;
-#endif
     abf16x8_t dtp[2][3];
     reg_planes(dt, dtp);
     f32x16 dq = zero16();  // dQ_blk[query][d] over this wave's 32 keys (columns d >= 16 discarded)
@@ -1547,42 +1560,20 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kq_x6_kernel(AttnArgs a) {
       abf16x8_t kt[3];
 #pragma unroll
       for (int pl = 0; pl < 3; ++pl)
-        kt[pl] = tr8(&Kt_s[pl * 2048 + r0 * 16 + (trc & 15)], &Kt_s[pl * 2048 + r1 * 16 + (trc & 15)]);
+        kt[pl] = tr8(&Kt_s[pl * KW * 16 + r0 * 16 + (trc & 15)], &Kt_s[pl * KW * 16 + r1 * 16 + (trc & 15)]);
       MFMA6(dq, dtp[u][0], dtp[u][1], dtp[u][2], kt[0], kt[1], kt[2]);
     }
     // dq: lanes = d (valid l32 < 16), registers r = query kappa(r, h); registers 4g..4g+3 are
-    // the 4 consecutive queries 8g + 4h + 0..3.  Every wave parks its partial in LDS, then
-    // wave w adds queries [8w, 8w + 8) of all four in wave order and writes them to the slab.
-#if GRL_KQ_WHATIF == 2
-    if (dq[0] == 12345.0f) acc[0] += 1.0f;  // timing diagnostic: no reduction, no stores (WRONG dQ)
-    continue;
-#endif
+    // the 4 consecutive queries 8g + 4h + 0..3 -> this block's slot, row d of wave's partial
     if (l32 < 16) {
-      float* dst = Red_s + wave * 512 + l32 * 32 + 4 * h;
+      float* dst = Red_s + stg * RSLOT + wave * 16 * RP + l32 * RP + 4 * h;
 #pragma unroll
       for (int g = 0; g < 4; ++g)
         *reinterpret_cast<float4*>(dst + 8 * g) = make_float4(dq[4 * g], dq[4 * g + 1], dq[4 * g + 2], dq[4 * g + 3]);
     }
-    __syncthreads();
-    {
-      const int d = lane >> 2, qq = 8 * wave + 2 * (lane & 3);
-      const float* src = Red_s + d * 32 + qq;
-      float2 x = *reinterpret_cast<const float2*>(src);
-#pragma unroll
-      for (int w = 1; w < 4; ++w) {
-        const float2 y = *reinterpret_cast<const float2*>(src + w * 512);
-        x.x += y.x;
-        x.y += y.y;
-      }
-      // split ranges are whole query blocks, so a block never reaches into
-      // another split's rows; past N it writes the padding (zeros: P = 0)
-#if GRL_KQ_WHATIF == 1
-      if (x.x == 12345.0f) acc[0] += 1.0f;  // timing diagnostic: no slab stores (WRONG dQ)
-#else
-      *reinterpret_cast<float2*>(slab + d * npad + q0 + qq) = x;
-#endif
-    }
   }
+  __syncthreads();
+  if (q_hi > q_lo) reduce(q_lo + ((q_hi - q_lo - 1) >> 5 << 5));  // the last block's partials
   if (kv) {  // query split: partial dK into slab blockIdx.z (summed in split order afterwards)
     const int64_t rows = (int64_t)gridDim.y * N;
     float* dst = SPLIT ? a.part2 + (int64_t)blockIdx.z * rows * a.dk : a.dK;
@@ -1666,12 +1657,6 @@ bool attn_x6_enabled() {
   return !(e && e[0] == '0');
 }
 
-// GRL_KQ_WHATIF (timing diagnostics only, WRONG dQ): 1 = no slab stores,
-// 2 = no cross-wave reduction either, 3 = no dQ work after the transpose
-#ifndef GRL_KQ_WHATIF
-#define GRL_KQ_WHATIF 0
-#endif
-
 // GRL_ATTN_FUSED_DQ=0 (read per call) keeps the separate dQ kernel (A/B aid)
 bool attn_fused_dq_enabled() {
   const char* e = getenv("GRL_ATTN_FUSED_DQ");
@@ -1746,14 +1731,15 @@ int launch_attn(AttnPass pass, const AttnArgs& a0, int64_t B, int S, hipStream_t
       if constexpr (DKP == 16) {
         if (a.qslab && pre) {  // dK with dQ folded in (grl_node_attention_bwd skipped the dQ pass)
           kq = true;
+          const dim3 gkq((unsigned)ceil_div(a.N, KQ_KEYS), (unsigned)B, (unsigned)S);
           if (S > 1)
-            hipLaunchKernelGGL((attn_bwd_kq_x6_kernel<true>), grid, dim3(256), 0, st, a);
+            hipLaunchKernelGGL((attn_bwd_kq_x6_kernel<true>), gkq, dim3(64 * KQ_WAVES), 0, st, a);
           else
-            hipLaunchKernelGGL((attn_bwd_kq_x6_kernel<false>), grid, dim3(256), 0, st, a);
+            hipLaunchKernelGGL((attn_bwd_kq_x6_kernel<false>), gkq, dim3(64 * KQ_WAVES), 0, st, a);
           GRL_LAUNCH_CHECK();
           if (a.dk > 0)
             hipLaunchKernelGGL(attn_qslab_sum_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(rows * a.dk, 256), 8192)),
-                               dim3(256), 0, st, a.qslab, B, (int64_t)grid.x, a.N, a.dk, a.dQ);
+                               dim3(256), 0, st, a.qslab, B, (int64_t)gkq.x, a.N, a.dk, a.dQ);
         }
       }
       if (!kq) GRL_X6L(attn_bwd_kv_x6_kernel, DKP, false);
@@ -1881,11 +1867,11 @@ extern "C" size_t grl_node_attention_workspace_size(int64_t B, int64_t N, int32_
 }
 
 // the backward's dQ slabs (attn_bwd_kq_x6_kernel): dk <= 16, x6 planes, and
-// at most kAttnQslabMax bytes (N^2 / 2 at B = 1: 5 GB at N = 100k)
+// at most kAttnQslabMax bytes (N^2 / 4 at B = 1: 2.5 GB at N = 100k)
 constexpr size_t kAttnQslabMax = (size_t)24 << 30;
 static size_t attn_qslab_bytes(int64_t B, int64_t N, int dk, int dv) {
   if (!attn_fused_dq_enabled() || dk > 16 || attn_dvp(dv) != 128 || B * N < kAttnPlaneMinRows) return 0;
-  const size_t n = (size_t)B * (size_t)ceil_div(N, 128) * (size_t)(ceil_div(N, 32) * 32) * 16 * 4;
+  const size_t n = (size_t)B * (size_t)ceil_div(N, KQ_KEYS) * (size_t)(ceil_div(N, 32) * 32) * 16 * 4;
   return n <= kAttnQslabMax ? (n + 255) / 256 * 256 : 0;
 }
 

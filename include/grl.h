@@ -431,7 +431,7 @@ int grl_node_attention_fwd(const float* Q, const float* K, const float* H,
  * dH [B, N, dv] (fully overwritten).  Deterministic, no atomics: dK / dH are
  * key-stationary; dQ is query-stationary, or -- with a workspace of
  * grl_node_attention_bwd_workspace_size bytes, dk <= 16 -- folded into the
- * dK kernel as one partial slab per 128-key workgroup (B ceil(N/128) N 64
+ * dK kernel as one partial slab per 256-key workgroup (B ceil(N/256) N 64
  * bytes, at most 24 GiB; larger N keeps the dQ kernel) added in workgroup
  * order.  d gamma = sum(d_out * o_norm) and the residual's d_out are the
  * caller's.                                                                  */
