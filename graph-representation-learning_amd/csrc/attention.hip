@@ -597,9 +597,9 @@ __device__ __forceinline__ void dma_block(const uint16_t* planes, int64_t ps, in
 // dma_block with this lane's chunk addresses computed once: per block only a
 // uniform row offset is added (the last, partial block takes dma_block's
 // clamped path).  Costs 2 VGPRs per chunk slot (the forward has the room).
-template <int W, int LAYOUT>
+template <int W, int LAYOUT, int NW = 4>
 struct DmaRows {
-  static constexpr int PL = 32 * W, NI = 3 * PL / 512, NJ = (NI + 3) / 4;
+  static constexpr int PL = 32 * W, NI = 3 * PL / 512, NJ = (NI + NW - 1) / NW;
   const uint16_t* planes;
   const uint16_t* src[NJ];
   int64_t ps;
@@ -608,7 +608,7 @@ struct DmaRows {
     ps = ps_;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-      const int i = wave + 4 * j;
+      const int i = wave + NW * j;
       const int e = (i < NI ? i : 0) * 512 + lane * 8;
       const int pl = e / PL, rem = e % PL, r = rem / W, pos = rem % W;
       int c = pos;
@@ -621,11 +621,11 @@ struct DmaRows {
     if (r0 + 32 <= N) {
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
-        const int i = wave + 4 * j;
+        const int i = wave + NW * j;
         if (i < NI) adma16(src[j] + r0 * W, lds + i * 512);
       }
     } else {
-      dma_block<W, LAYOUT>(planes, ps, r0, N, lds, wave, lane);
+      dma_block<W, LAYOUT, NW>(planes, ps, r0, N, lds, wave, lane);
     }
   }
 };
@@ -1231,8 +1231,11 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_x6_kernel(AttnArgs a) {
 }
 
 // key-stationary.  WANT_H: dH^T += dO^T P;  else dK^T += Q^T dS (needs dP)
-template <int DKP, bool WANT_H, bool PRE, bool SPLIT>
-__global__ __launch_bounds__(256, 2) void attn_bwd_kv_x6_kernel(AttnArgs a) {
+// NW = 8 (PRE only): 256 keys per workgroup, one per CU -- the query block's
+// Q / dO stage serves twice the keys (half the LDS-DMA per key)
+template <int DKP, bool WANT_H, bool PRE, bool SPLIT, int NW = 4>
+__global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_kv_x6_kernel(AttnArgs a) {
+  static_assert(NW == 4 || (NW == 8 && PRE), "8-wave workgroups stage by LDS-DMA only");
   constexpr int KC = DKP / 16, FC = 8;
   __shared__ __attribute__((aligned(16))) uint16_t Qp_s[(PRE ? 2 : 1) * 3 * 32 * 32];  // PRE: 2 stages
   __shared__ __attribute__((aligned(16))) uint16_t Op_s[(PRE ? 2 : 1) * 3 * 32 * 128];
@@ -1241,7 +1244,7 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_x6_kernel(AttnArgs a) {
   const int64_t N = a.N, b = blockIdx.y;
   const float* Qb = a.Q + b * N * a.dk;
   const float* dOb = a.dO + b * N * a.dv;
-  const int64_t key = (int64_t)blockIdx.x * 128 + wave * 32 + l32;
+  const int64_t key = (int64_t)blockIdx.x * (32 * NW) + wave * 32 + l32;
   const bool kv = key < N;
   const int64_t q_lo = SPLIT ? (int64_t)blockIdx.z * a.kr : 0, q_hi = SPLIT ? min<int64_t>(N, q_lo + a.kr) : N;
   abf16x8_t kp[KC][3];
@@ -1273,16 +1276,16 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_x6_kernel(AttnArgs a) {
     }
   };
   // dH (WANT_H) has the VGPR room for precomputed DMA addresses; dK does not
-  DmaRows<32, PL_PLAIN> qd;
-  DmaRows<128, PL_SWZ128> od;
+  DmaRows<32, PL_PLAIN, NW> qd;
+  DmaRows<128, PL_SWZ128, NW> od;
   if constexpr (PRE && WANT_H) {
     qd.init(Qpb, qps, wave, lane);
     od.init(Opb, ops, wave, lane);
     qd.issue(q_lo, N, Qp_s, wave, lane);
     od.issue(q_lo, N, Op_s, wave, lane);
   } else if constexpr (PRE) {
-    dma_block<32, PL_PLAIN>(Qpb, qps, q_lo, N, Qp_s, wave, lane);
-    dma_block<128, PL_SWZ128>(Opb, ops, q_lo, N, Op_s, wave, lane);
+    dma_block<32, PL_PLAIN, NW>(Qpb, qps, q_lo, N, Qp_s, wave, lane);
+    dma_block<128, PL_SWZ128, NW>(Opb, ops, q_lo, N, Op_s, wave, lane);
   } else {
     sq.fetch(Qb, q_lo, N, a.dk, vq, tid);
     so.fetch(dOb, q_lo, N, a.dv, vo, tid);
@@ -1311,8 +1314,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_kv_x6_kernel(AttnArgs a) {
         qd.issue(q0 + 32, N, Qp_s + (stg ^ 1) * 3 * 1024, wave, lane);
         od.issue(q0 + 32, N, Op_s + (stg ^ 1) * 3 * 4096, wave, lane);
       } else if constexpr (PRE) {
-        dma_block<32, PL_PLAIN>(Qpb, qps, q0 + 32, N, Qp_s + (stg ^ 1) * 3 * 1024, wave, lane);
-        dma_block<128, PL_SWZ128>(Opb, ops, q0 + 32, N, Op_s + (stg ^ 1) * 3 * 4096, wave, lane);
+        dma_block<32, PL_PLAIN, NW>(Qpb, qps, q0 + 32, N, Qp_s + (stg ^ 1) * 3 * 1024, wave, lane);
+        dma_block<128, PL_SWZ128, NW>(Opb, ops, q0 + 32, N, Op_s + (stg ^ 1) * 3 * 4096, wave, lane);
       } else {
         sq.fetch(Qb, q0 + 32, N, a.dk, vq, tid);
         so.fetch(dOb, q0 + 32, N, a.dv, vo, tid);
@@ -1657,6 +1660,12 @@ bool attn_x6_enabled() {
   return !(e && e[0] == '0');
 }
 
+// GRL_ATTN_DH8=0 (read per call) keeps dH on 4-wave workgroups (A/B aid)
+bool attn_dh8_enabled() {
+  const char* e = getenv("GRL_ATTN_DH8");
+  return !(e && e[0] == '0');
+}
+
 // GRL_ATTN_FUSED_DQ=0 (read per call) keeps the separate dQ kernel (A/B aid)
 bool attn_fused_dq_enabled() {
   const char* e = getenv("GRL_ATTN_FUSED_DQ");
@@ -1725,7 +1734,15 @@ int launch_attn(AttnPass pass, const AttnArgs& a0, int64_t B, int S, hipStream_t
       }
     } else {
       if (S > 1) a.part2 = a.part + (int64_t)S * rows * a.dv;
-      GRL_X6L(attn_bwd_kv_x6_kernel, DKP, true);
+      if (pre && attn_dh8_enabled()) {  // dH on 256-key workgroups
+        const dim3 g8((unsigned)ceil_div(a.N, 256), (unsigned)B, (unsigned)S);
+        if (S > 1)
+          hipLaunchKernelGGL((attn_bwd_kv_x6_kernel<DKP, true, true, true, 8>), g8, dim3(512), 0, st, a);
+        else
+          hipLaunchKernelGGL((attn_bwd_kv_x6_kernel<DKP, true, true, false, 8>), g8, dim3(512), 0, st, a);
+      } else {
+        GRL_X6L(attn_bwd_kv_x6_kernel, DKP, true);
+      }
       GRL_LAUNCH_CHECK();
       bool kq = false;
       if constexpr (DKP == 16) {
