@@ -817,8 +817,8 @@ __global__ __launch_bounds__(256) void attn_fwd_x6_kernel(AttnArgs a) {
 // and H two.  Same products, same order of every sum as attn_fwd_x6_kernel,
 // hence the same bits.  The last block's partial-key mask is applied in its
 // own instantiation of the iteration (MASK), outside the interleaved body.
-template <int DKP, int NT, bool SPLIT>
-__global__ __launch_bounds__(256) void attn_fwd_x6p_kernel(AttnArgs a) {
+template <int DKP, int NT, bool SPLIT, int NW = 4>
+__global__ __launch_bounds__(64 * NW) void attn_fwd_x6p_kernel(AttnArgs a) {
   constexpr int DV = NT * 32, KC = DKP / 16;
   constexpr int KPL = 32 * DKP, HPL = 32 * DV;  // bf16 per plane
   constexpr int KST = 3 * KPL, HST = 3 * HPL;   // one stage: the three planes
@@ -827,7 +827,7 @@ __global__ __launch_bounds__(256) void attn_fwd_x6p_kernel(AttnArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, h = lane >> 5;
   const int64_t N = a.N, b = blockIdx.y;
   const float* Qb = a.Q + b * N * a.dk;
-  const int64_t q = (int64_t)blockIdx.x * 128 + wave * 32 + l32;
+  const int64_t q = (int64_t)blockIdx.x * (32 * NW) + wave * 32 + l32;
   const int64_t k_lo = SPLIT ? (int64_t)blockIdx.z * a.kr : 0, k_hi = SPLIT ? min<int64_t>(N, k_lo + a.kr) : N;
   const int nblk = (int)((k_hi - k_lo + 31) >> 5);
   const bool partial = ((k_hi - k_lo) & 31) != 0;
@@ -849,8 +849,8 @@ __global__ __launch_bounds__(256) void attn_fwd_x6p_kernel(AttnArgs a) {
   for (int t = 0; t < NT; ++t) o[t] = zero16();
   float m = -INFINITY, l = 0.0f;
   const int64_t kps = (int64_t)gridDim.y * N * DKP, hps = (int64_t)gridDim.y * N * DV;
-  DmaRows<DKP, PL_PLAIN> kd;
-  DmaRows<DV, PL_HSWZ> hd;
+  DmaRows<DKP, PL_PLAIN, NW> kd;
+  DmaRows<DV, PL_HSWZ, NW> hd;
   kd.init(a.Kpl + b * N * DKP, kps, wave, lane);
   hd.init(a.Hpl + b * N * DV, hps, wave, lane);
   kd.issue(k_lo, N, Kp_s, wave, lane);
@@ -1660,6 +1660,12 @@ bool attn_x6_enabled() {
   return !(e && e[0] == '0');
 }
 
+// GRL_ATTN_FWD8=0 (read per call) keeps the pipelined forward on 4-wave workgroups (A/B aid)
+bool attn_fwd8_enabled() {
+  const char* e = getenv("GRL_ATTN_FWD8");
+  return !(e && e[0] == '0');
+}
+
 // GRL_ATTN_DH8=0 (read per call) keeps dH on 4-wave workgroups (A/B aid)
 bool attn_dh8_enabled() {
   const char* e = getenv("GRL_ATTN_DH8");
@@ -1711,7 +1717,13 @@ int launch_attn(AttnPass pass, const AttnArgs& a0, int64_t B, int S, hipStream_t
     else
       hipLaunchKernelGGL((attn_bwd_kv_kernel<DKP, NT>), grid, dim3(256), 0, st, a);
   } else if (pass == PASS_FWD && x6) {
-    if (pre && attn_pipe_enabled()) {
+    if (pre && attn_pipe_enabled() && attn_fwd8_enabled()) {  // 256 queries per workgroup
+      const dim3 g8((unsigned)ceil_div(a.N, 256), (unsigned)B, (unsigned)S);
+      if (S > 1)
+        hipLaunchKernelGGL((attn_fwd_x6p_kernel<DKP, NT, true, 8>), g8, dim3(512), 0, st, a);
+      else
+        hipLaunchKernelGGL((attn_fwd_x6p_kernel<DKP, NT, false, 8>), g8, dim3(512), 0, st, a);
+    } else if (pre && attn_pipe_enabled()) {
       if (S > 1)
         hipLaunchKernelGGL((attn_fwd_x6p_kernel<DKP, NT, true>), grid, dim3(256), 0, st, a);
       else
