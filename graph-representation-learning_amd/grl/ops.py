@@ -573,7 +573,17 @@ def _attn_workspace(B, N, dk, dv, device, backward: bool = False):
     backward's partials (grl.h)."""
     lib = _lib.lib()
     n = (lib.grl_node_attention_bwd_workspace_size if backward else lib.grl_node_attention_workspace_size)(B, N, dk, dv)
-    return (torch.empty(n, dtype=torch.uint8, device=device), n) if n else (None, 0)
+    if not n:
+        return None, 0
+    try:
+        return torch.empty(n, dtype=torch.uint8, device=device), n
+    except torch.cuda.OutOfMemoryError:
+        if not backward:
+            raise
+        # the backward's dQ slabs (N^2 / 4 bytes at dk <= 16) do not fit: the smaller
+        # workspace runs the separate dQ kernel instead (grl.h)
+        n = lib.grl_node_attention_workspace_size(B, N, dk, dv)
+        return (torch.empty(n, dtype=torch.uint8, device=device), n) if n else (None, 0)
 
 
 # Value columns per kernel call: the kernels hold one query's output row in
