@@ -134,6 +134,12 @@ for step in "$@"; do
     tests_r3) run pytest_gpu_r3 600 python -u -m pytest tests/test_gpu_halo_async.py tests/test_gpu_graphconv.py \
                   tests/test_gpu_embed.py tests/test_gpu_dist.py::test_bench_spawns_its_ranks_without_a_launcher \
                   -m gpu -v -rf --timeout 240 --timeout-method thread ;;
+    pmc_infer_mfma) run pmc_infer_mfma 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CU_CYCLES \
+                  SQ_INSTS_VALU SQ_INSTS_MFMA --kernel-trace -d "$OUT/pmc_infer_mfma" -o run --output-format csv \
+                  -- python bench.py --only infer --steps 5 --warmup 1 ;;
+    pmc_layer_mfma) run pmc_layer_mfma 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CU_CYCLES \
+                  SQ_INSTS_VALU SQ_INSTS_MFMA --kernel-trace -d "$OUT/pmc_layer_mfma" -o run --output-format csv \
+                  -- python bench.py --only layer --steps 3 --warmup 1 ;;
     ab_fused_dq) rm -f gpurun_out/ab_fused_dq.log; run ab_fused_dq 900 tools/ab_fused_dq.sh ;;
     prof_attn_fused) run prof_attn_fused 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_attn_fused" -o run \
                   --output-format csv -- python tools/probe_attn.py 100000 ;;
