@@ -1100,6 +1100,8 @@ int pick_splits_small(int64_t M, int64_t N, int64_t K) {
   if (tiles >= cus) return 1;
   int64_t s = (2 * cus) / std::max<int64_t>(tiles, 1);
   s = std::min<int64_t>(s, ceil_div(K, GEMM_BK));  // >= one K tile per split
+  const char* e = getenv("GRL_GEMM_SMALL_SPLITS");  // A/B aid: force the split count
+  if (e && atoi(e) > 0) s = std::min<int64_t>(atoi(e), ceil_div(K, GEMM_BK));
   return (int)std::max<int64_t>(1, std::min<int64_t>(s, 64));
 }
 
