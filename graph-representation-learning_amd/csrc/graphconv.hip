@@ -418,8 +418,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GRL_FG_WPE,
 #ifndef GRL_WS_PLANES
 #define GRL_WS_PLANES 0
 #endif
+#ifndef GRL_WS_KC
+#define GRL_WS_KC 128
+#endif
 constexpr int WS_R = 64;                   // rows per tile
-constexpr int WS_KC = 128;                 // Z columns per ring unit (F > 128: F / 128 units per segment)
+constexpr int WS_KC = GRL_WS_KC;           // Z columns per ring unit (F > WS_KC: F / WS_KC units per segment)
 #if GRL_WS_PLANES
 constexpr int WS_LDF = WS_KC + 8;          // bf16 per plane row (+ one 16-B pad chunk: conflict-free)
 constexpr int WS_PLANE = WS_R * WS_LDF;    // bf16 per plane
@@ -435,7 +438,8 @@ constexpr int WS_PROD = 8;                 // gather waves
 constexpr int WS_CONS = GRL_WS_CONS;       // MFMA waves (4: 64 output columns each; 8: 32, two per SIMD)
 constexpr int WS_CB = FG_CB / WS_CONS;     // 32-column blocks per MFMA wave
 constexpr int WS_RW = WS_R / WS_PROD;      // rows per gather wave
-constexpr int WS_NB = GRL_WS_PLANES ? 3 : 4;  // ring slots
+// ring slots: as many as ~140 KB hold (fp32 128-col units: 4; bf16 planes of 64-col units: 5)
+constexpr int WS_NB = (GRL_WS_PLANES && WS_KC == 128) ? 3 : (140 * 1024) / (WS_SLOT * 4);
 #ifndef GRL_WS_U
 #define GRL_WS_U 12
 #endif
@@ -509,7 +513,7 @@ __global__ __launch_bounds__(64 * (WS_PROD + WS_CONS)) void graphconv_ws_kernel(
   constexpr int KC = F < WS_KC ? F : WS_KC;  // Z columns per unit
   constexpr int NH = F / KC;                  // units per segment
   constexpr int KSU = KC / 16;                // K16 steps per unit
-  static_assert(NH <= 2 && NH < WS_NB, "a segment's units are distinct ring slots");
+  static_assert(NH < WS_NB, "a segment's units are distinct ring slots, and one more is free");
   __shared__ __attribute__((aligned(16))) float ring[WS_NB * WS_SLOT];
   __shared__ int produced[WS_NB], consumed[WS_NB];
   if (threadIdx.x < WS_NB) {
@@ -610,6 +614,7 @@ __global__ __launch_bounds__(64 * (WS_PROD + WS_CONS)) void graphconv_ws_kernel(
         };
 #if GRL_WS_PLANES
         uint16_t* const dst = reinterpret_cast<uint16_t*>(ring + ((u + part) % WS_NB) * WS_SLOT) + ucol;
+        float* const zrow = Zout ? Zout + rw0 * ldz + (int64_t)s * F + col : nullptr;
         auto flush = [&](int r, const float4& v) {
           if (col_ok) {
             uint2 q0, q1, q2;
@@ -618,6 +623,10 @@ __global__ __launch_bounds__(64 * (WS_PROD + WS_CONS)) void graphconv_ws_kernel(
             *reinterpret_cast<uint2*>(d) = q0;
             *reinterpret_cast<uint2*>(d + WS_PLANE) = q1;
             *reinterpret_cast<uint2*>(d + 2 * WS_PLANE) = q2;
+            if (zrow && r < nvalid) {
+              f32x4_t t = {v.x, v.y, v.z, v.w};
+              __builtin_nontemporal_store(t, reinterpret_cast<f32x4_t*>(zrow + (int64_t)r * ldz));
+            }
           }
         };
 #else

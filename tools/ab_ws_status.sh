@@ -4,6 +4,8 @@
 # named on the command line (tools/build_diag.sh), interleaved, three rounds.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 L=graph-representation-learning_amd/grl
+export AB_SAVE=/tmp/ab_ws_ref.pt
+rm -f $AB_SAVE
 for rep in 1 2 3; do
   timeout -k 10 200 python tools/probe_ws_status.py >> gpurun_out/ab_ws_status.log 2>&1 || exit 1
   GRL_WS_STATUS=poison timeout -k 10 200 python tools/probe_ws_status.py >> gpurun_out/ab_ws_status.log 2>&1 || exit 1

@@ -40,7 +40,17 @@ def main():
     tag = f"{lib} status={os.environ.get('GRL_WS_STATUS', 'sync')}"
     r = [timeit(lambda: graph_conv_infer(X, g0, W, b, True)), timeit(lambda: graph_conv_infer(X, gd, W, b, True)),
          timeit(lambda: graph_conv_bwd_data(G, gd, W, F))]
-    print(f"{tag}: infer p0 {r[0]:.3f} ms, infer p0.3 {r[1]:.3f} ms, bwd_data p0.3 {r[2]:.3f} ms", flush=True)
+    same = None
+    path = os.environ.get("AB_SAVE")  # first run saves the outputs, later runs compare bit for bit
+    if path:
+        outs = (graph_conv_infer(X, gd, W, b, True).cpu(), graph_conv_bwd_data(G, gd, W, F).cpu())
+        if os.path.exists(path):
+            ref = torch.load(path, weights_only=True)
+            same = all(torch.equal(x, y) for x, y in zip(outs, ref))
+        else:
+            torch.save(outs, path)
+    print(f"{tag}: infer p0 {r[0]:.3f} ms, infer p0.3 {r[1]:.3f} ms, bwd_data p0.3 {r[2]:.3f} ms"
+          f" bitwise_vs_first={same}", flush=True)
 
 
 if __name__ == "__main__":
