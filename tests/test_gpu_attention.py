@@ -166,3 +166,21 @@ def test_fused_dq_backward(B, N, dk, dv, monkeypatch):
         scale = r.grad.abs().max().item() + 1.0
         torch.testing.assert_close(a.double(), r.grad, rtol=1e-4, atol=2e-5 * scale, msg=f"fused d{name}")
         torch.testing.assert_close(a.double(), c.double(), rtol=1e-4, atol=2e-5 * scale, msg=f"fused vs dQ kernel d{name}")
+
+
+@pytest.mark.parametrize("B,N,dk,dv", [(1, 8192, 16, 128), (3, 4099, 9, 100), (2, 5000, 32, 128)])
+def test_eight_wave_workgroups_same_bits(B, N, dk, dv, monkeypatch):
+    """The forward and dH kernels on 8-wave (256-row) workgroups compute every
+    row exactly as on 4-wave ones (GRL_ATTN_FWD8 / GRL_ATTN_DH8 = 0): out and
+    every gradient bitwise, partial last blocks and splits included."""
+    Q, K, H, V, gamma = _inputs(B, N, dk, dv, seed=N + dv)
+    res = {}
+    for v in ("1", "0"):
+        monkeypatch.setenv("GRL_ATTN_FWD8", v)
+        monkeypatch.setenv("GRL_ATTN_DH8", v)
+        leaves = [t.clone().requires_grad_(True) for t in (Q, K, H, V, gamma)]
+        out = node_self_attention(*leaves)
+        out.square().sum().backward()
+        res[v] = [out.detach()] + [t.grad for t in leaves]
+    for a, b in zip(res["1"], res["0"]):
+        assert torch.equal(a, b)
