@@ -38,6 +38,7 @@ def _graphs(kind, block, threshold=None):
 @pytest.mark.parametrize("kind,block", [("er", 60_000), ("rmat", 90_000), ("er", 10**9)])
 def test_blocks_equal_one_csr(kind, block, threshold):
     F = 40
+    torch.manual_seed(kind == "er")
     g, gb, g64 = _graphs(kind, block, threshold)
     N = g.num_rows
     assert gb.nnz == g.nnz == g64.nnz and (len(gb.blocks) > 1) == (block < g.nnz)
@@ -52,13 +53,15 @@ def test_blocks_equal_one_csr(kind, block, threshold):
         assert torch.equal(spmm_forward(X, graph.with_dropedge(de)), Z)
     dZ = torch.randn_like(Z)
     dX = spmm_backward(dZ, g.with_dropedge(de), F)
+    absum = spmm_backward(dZ.abs(), g.with_dropedge(de), F)  # sum of |terms| per element
     for graph in (gb, g64):
         dXb = spmm_backward(dZ, graph.with_dropedge(de), F)
         if kind == "er":
             assert torch.equal(dXb, dX)  # no heavy columns: the one-CSC chain exactly
         else:  # R-MAT hub columns are chunked per block: the same terms, chunk sums grouped
-            # differently (hubs sum thousands of terms: the north-star fp32 tolerance)
-            torch.testing.assert_close(dXb, dX, rtol=1e-4, atol=1e-4)
+            # differently -- hubs sum thousands of terms with cancellation, so the bound is
+            # relative to the sum of |terms| (fp32 reassociation), not to the result
+            assert torch.all((dXb - dX).abs() <= 1e-5 * absum + 1e-6), float(((dXb - dX).abs() / absum).max())
     if threshold is not None:
         return
     # a whole GraphConv (autograd) on the blocked graph
