@@ -944,7 +944,8 @@ __global__ __launch_bounds__(512) void gemm_x6t_kernel(GemmArgs p) {
   const int64_t nk = kend > kbeg ? (kend - kbeg + X6_K - 1) / X6_K : 0;
 
   // staging: float4 f = tid + 512 i of each operand: k row f >> 6, 4 columns at (f & 63) * 4
-  const int kr0 = tid >> 6, kr1 = (tid + 512) >> 6;
+  // the staged k rows are wave-uniform: row offsets and the range checks stay scalar
+  const int kr0 = __builtin_amdgcn_readfirstlane(tid >> 6), kr1 = kr0 + 8;
   const int col = (tid & 63) * 4;
   const int64_t am = min<int64_t>(m0 + col, p.M - 4), bn = min<int64_t>(n0 + col, p.N - 4);
   const float* __restrict__ a_base = p.A + am;
@@ -980,10 +981,12 @@ __global__ __launch_bounds__(512) void gemm_x6t_kernel(GemmArgs p) {
   } while (0)
 #define X6T_STASH(st)                                                                                     \
   do {                                                                                                    \
-    X6T_SPLIT(in0 ? ra0 : zero4, (st), st_off0);                                                          \
-    X6T_SPLIT(in1 ? ra1 : zero4, (st), st_off1);                                                          \
-    X6T_SPLIT(in0 ? rb0 : zero4, (st) + 3 * X6_PLANE, st_off0);                                           \
-    X6T_SPLIT(in1 ? rb1 : zero4, (st) + 3 * X6_PLANE, st_off1);                                           \
+    if (!in0) ra0 = rb0 = zero4; /* wave-uniform: only a split's last K16 step branches */                \
+    if (!in1) ra1 = rb1 = zero4;                                                                          \
+    X6T_SPLIT(ra0, (st), st_off0);                                                                        \
+    X6T_SPLIT(ra1, (st), st_off1);                                                                        \
+    X6T_SPLIT(rb0, (st) + 3 * X6_PLANE, st_off0);                                                         \
+    X6T_SPLIT(rb1, (st) + 3 * X6_PLANE, st_off1);                                                         \
   } while (0)
 
   // this lane's transposed-read coordinates: k = 8h + ((lane & 15) >> 2),
