@@ -140,7 +140,8 @@ def test_pipelined_forward_same_bits(B, N, dk, dv, monkeypatch):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("B,N,dk,dv", [(1, 8192, 16, 128), (2, 5000, 16, 100), (3, 4099, 9, 128), (1, 6000, 1, 97)])
+@pytest.mark.parametrize("B,N,dk,dv", [(1, 8192, 16, 128), (2, 5000, 16, 100), (3, 4099, 9, 128), (1, 6000, 1, 97),
+                                       (200, 24, 16, 128)])  # many pages shorter than one query block
 def test_fused_dq_backward(B, N, dk, dv, monkeypatch):
     """dQ folded into the key-stationary dK kernel (attn_bwd_kq_x6_kernel:
     exact MFMA transpose of dS, per-workgroup slabs added in order) against
