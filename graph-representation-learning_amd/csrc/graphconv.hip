@@ -861,6 +861,27 @@ __global__ __launch_bounds__(64 * (WS_PROD + WS_CONS)) void graphconv_ws_kernel(
       // tile done: bias + ReLU, as gemm_x6_kernel
       const int64_t m0 = tile * WS_R;
       const bool epi = bias != nullptr || relu;
+      if (m0 + WS_R <= M) {  // whole tile (wave-uniform): row offsets are uniform multiples of C
+#pragma unroll
+        for (int j = 0; j < WS_CB; ++j) {
+          const int n = (c * WS_CB + j) * 32 + l32;
+          const float bv = (bias && n < C) ? bias[n] : 0.0f;
+          float* const o = out + (m0 + 4 * h) * C + n;
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              float v = acc[i][j][r];
+              if (epi) {
+                v = v + bv;
+                if (relu) v = v > 0.0f ? v : 0.0f;
+              }
+              if (n < C) o[(int64_t)(i * 32 + (r & 3) + 8 * (r >> 2)) * C] = v;
+              acc[i][j][r] = 0.0f;
+            }
+        }
+        continue;
+      }
 #pragma unroll
       for (int j = 0; j < WS_CB; ++j) {
         const int n = (c * WS_CB + j) * 32 + l32;
