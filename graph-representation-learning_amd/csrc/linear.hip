@@ -883,6 +883,23 @@ __global__ __launch_bounds__(512) void gemm_x6_kernel(GemmArgs p, const uint16_t
     }
   }
   float* Cz = p.C;
+  if (m0 + LB_M <= p.M) {  // whole row tile (uniform): row offsets are uniform multiples of ldc
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int64_t gn = n0 + wn * 64 + j * 32 + l32;
+      const float bv = (EPI == EPI_BIAS && p.bias && gn < p.N) ? p.bias[gn] : 0.0f;
+      float* const o = Cz + (m0 + wm * 128 + 4 * h) * p.ldc + gn;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float v = acc[i][j][r] + bv;
+          if (EPI == EPI_BIAS && p.relu) v = v > 0.0f ? v : 0.0f;
+          if (gn < p.N) o[(int64_t)(i * 32 + (r & 3) + 8 * (r >> 2)) * p.ldc] = v;
+        }
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int64_t gn = n0 + wn * 64 + j * 32 + l32;
