@@ -468,6 +468,10 @@ constexpr int WS_STATUS_TIMEOUT = 1;       // status bit: a bounded wait ran out
 #ifndef GRL_WS_PRIO
 #define GRL_WS_PRIO 0
 #endif
+// GRL_WS_NTX (A/B aid): 1 = the gather waves load source rows non-temporally
+#ifndef GRL_WS_NTX
+#define GRL_WS_NTX 0
+#endif
 #if GRL_WS_STAMP
 __device__ unsigned long long g_ws_dbg[1024 * 12 * 2];
 #endif
@@ -690,7 +694,17 @@ __global__ __launch_bounds__(64 * (WS_PROD + WS_CONS)) void graphconv_ws_kernel(
               for (int q = 0; q < WS_U; ++q) {
                 if (jj[q] >= 0) {
                   const int src = readlane_i(sidx, jj[q]);
+#if GRL_WS_NTX
+                  // A/B aid: streamed source rows, so the W planes stay L2-resident
+                  if (col_ok) {
+                    const f32x4_t t = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(X + (int64_t)src * ldx + col));
+                    xv[q] = make_float4(t[0], t[1], t[2], t[3]);
+                  } else {
+                    xv[q] = zero4();
+                  }
+#else
                   xv[q] = col_ok ? *reinterpret_cast<const float4*>(X + (int64_t)src * ldx + col) : zero4();
+#endif
                 }
               }
 #pragma unroll

@@ -252,7 +252,7 @@ class _HaloExchange(torch.autograd.Function):
         if plan.mode == "dense":
             X_ext[plan.n_loc: plan.stride].zero_()
             all_gather_into(X_ext[plan.stride:], X_ext[: plan.stride], group)
-        elif _world(group) > 1:
+        elif _world(group) > 1 or plan.n_halo:
             send = X_loc.index_select(0, plan.send_index)
             all_to_all_v(X_ext[plan.n_loc:], send, plan.recv_counts, plan.send_counts, group)
         ctx.plan, ctx.group = plan, group
@@ -271,7 +271,7 @@ class _HaloExchange(torch.autograd.Function):
             for q in range(world):  # peer order, like the sparse path
                 if q != me:
                     dX_loc += back[q * st: q * st + plan.n_loc]
-        elif _world(group) > 1:
+        elif _world(group) > 1 or plan.n_halo:
             back = dX_ext.new_empty(sum(plan.send_counts), dX_ext.shape[1])
             all_to_all_v(back, dX_ext[plan.n_loc:], plan.send_counts, plan.recv_counts, group)
             off = 0
@@ -345,8 +345,11 @@ class HaloPipeline:
         self.tables = torch.empty(chunks, rows, self.Fc, device=dev)
         if plan.mode == "dense":
             self.tables[:, plan.n_loc:plan.stride].zero_()  # shard padding rows: travel, never read
+        # a shard exchanges when its group has peers or its plan has halo rows
+        # (a one-rank group with a loopback plan: tests/rccl_loopback.py)
+        self.moves = self.world > 1 or plan.n_halo > 0
         self.send = None
-        if plan.mode == "sparse" and self.world > 1:
+        if plan.mode == "sparse" and self.moves:
             self.send = torch.empty(chunks, plan.send_index.numel(), self.Fc, device=dev)
         if exchange is not None:
             self.side = torch.cuda.Stream(dev) if dev.type == "cuda" and exchange.async_op else None
@@ -365,7 +368,7 @@ class HaloPipeline:
 
     def _exchange(self, c: int):
         """Start slice c's exchange; returns a work handle (or None if done)."""
-        if self.world == 1:
+        if not self.moves:
             return None
         with trace(f"grl.halo_slice{c}"):
             return self._exchange_slice(c)
@@ -430,7 +433,7 @@ class HaloPipeline:
     def _exchange_back(self, c: int, async_op: bool):
         """Send slice c's halo-row gradients to their owners (the reverse of
         the forward exchange); returns a work handle when async_op."""
-        if self.world == 1:
+        if not self.moves:
             return None
         p, g, back = self.plan, self.gtables[c], self.gback[c]
         with trace(f"grl.halo_back_slice{c}"):
@@ -455,7 +458,7 @@ class HaloPipeline:
         p, g, back = self.plan, self.gtables[c], self.gback[c]
         out = dX_loc[:, c * self.Fc:(c + 1) * self.Fc]
         out.copy_(g[:p.n_loc])
-        if self.world == 1:
+        if not self.moves:
             return
         if p.mode == "dense":
             st = p.stride

@@ -1,0 +1,139 @@
+"""Child process of tests/test_gpu_rccl.py: the product's halo exchange on REAL
+RCCL (torch.distributed "nccl") on a one-GPU box.
+
+RCCL refuses two ranks on one device, so the group here has one rank, and
+the shard's plan is a *loopback*: every edge's source column points into the
+halo region of X_ext instead of the own rows, so every source feature the
+aggregation reads has travelled through an RCCL collective -- the dense
+layout's all_gather_into_tensor (the shard's rows "gathered" back into the
+slot of a peer) or the sparse layout's all_to_all_single (the referenced rows
+packed, sent and received).  The backward sends the halo-row gradients back
+the same way and the combine adds them, as a peer's partials.  What runs:
+  * HaloPipeline.run / .backward -- the side-stream / async_op branch RCCL
+    takes on a multi-GPU node: real work handles, .wait() on the compute
+    stream, buffers reused by back-to-back calls; inputs made final late on
+    the compute stream (a spin kernel first), so a missing stream wait reads
+    stale rows;
+  * _HaloExchange (ShardedGraph.aggregate, autograd) -- the synchronous
+    collectives, forward and backward;
+  * the bench's max-over-ranks all_reduce (float64 on the device) and barrier.
+Checked: Z bitwise the one-GPU aggregation; the pipelined dX bitwise the
+unpipelined sharded dX (the loopback combine adds the edge sums to the self
+term as a peer's partial, so dX is within fp32 rounding of the one-GPU
+spmm_backward, also checked).  Prints one JSON line; exit 0 iff every check
+passed.  Test infrastructure only."""
+import json
+import os
+import socket
+import sys
+
+import torch
+import torch.distributed as dist
+
+REPO = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+sys.path.insert(0, os.path.join(REPO, "graph-representation-learning_amd"))
+
+from grl import DropEdge, TypedGraph  # noqa: E402
+from grl.dist import HaloPlan, HaloPipeline, ShardedGraph  # noqa: E402
+from grl.ops import spmm_backward, spmm_forward  # noqa: E402
+
+DEV = torch.device("cuda", 0)
+SPIN = 20_000_000  # spin-kernel cycles (~10 ms): far longer than a slice's collective or gather here
+
+
+def loopback_plan(g: TypedGraph, mode: str) -> HaloPlan:
+    """A one-rank plan whose sources all come through the exchange.
+    dense:  X_ext = [own rows | own rows as rank 0's gathered slot]; the
+            shard's rank is set to -1 so the gathered slot counts as a peer's
+            (its gradient partials are added, as a peer's would be);
+    sparse: X_ext = [own rows | referenced rows, ascending]; send_index the
+            same rows, sent to and received from the one rank."""
+    n, c = g.num_rows, g.colidx.long()
+    E = int(c.numel())
+    ids = torch.unique(c)
+    empty = torch.zeros(0, dtype=torch.int64, device=c.device)
+    if mode == "dense":
+        return HaloPlan(0, n, n, n, [0, n], empty, [0], [0], ids, (n + c).to(torch.int32), 0, E, "dense", n, -1)
+    k = int(ids.numel())
+    slot = n + torch.searchsorted(ids, c)
+    return HaloPlan(0, n, n, k, [0, n], ids, [k], [k], ids, slot.to(torch.int32), 0, E, "sparse", 0, 0)
+
+
+def loopback_shard(g: TypedGraph, mode: str) -> ShardedGraph:
+    sg = ShardedGraph.__new__(ShardedGraph)
+    sg._init(g.rowptr, loopback_plan(g, mode), g.num_types, g.vals, dist.group.WORLD)
+    return sg
+
+
+def main():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    torch.cuda.set_device(DEV)
+    dist.init_process_group("nccl", device_id=DEV)
+    assert dist.get_backend() == "nccl"
+    results = {"backend": dist.get_backend(), "checks": {}}
+    ok = True
+
+    def check(name, cond, detail=None):
+        nonlocal ok
+        results["checks"][name] = bool(cond) if detail is None else {"ok": bool(cond), **detail}
+        ok = ok and bool(cond)
+
+    N, deg, L, F, K = 20000, 16.0, 6, 256, 2
+    g = TypedGraph.synthetic(N, deg, L, kind="er", seed=11, device=DEV)
+    de = DropEdge(0.3, 4, 1)
+    gen = torch.Generator(device=DEV).manual_seed(3)
+    Xs = [torch.randn(N, F, generator=gen, device=DEV) for _ in range(2)]
+    dZs = [torch.randn(N, (L + 1) * F, generator=gen, device=DEV) for _ in range(2)]
+    ref_Z = [spmm_forward(X, g.with_dropedge(de)) for X in Xs]
+    ref_dX = [spmm_backward(dZ, g.with_dropedge(de), F) for dZ in dZs]
+
+    for mode in ("dense", "sparse"):
+        sg = loopback_shard(g, mode)
+        # the synchronous collectives under autograd (_HaloExchange), the unpipelined sharded reference
+        sync_Z, sync_dX = [], []
+        for i in range(2):
+            X = Xs[i].clone().requires_grad_(True)
+            Z = sg.aggregate(X, de)
+            Z.backward(dZs[i])
+            sync_Z.append(Z.detach())
+            sync_dX.append(X.grad)
+        pipe = HaloPipeline(sg, F, chunks=K, device=DEV)
+        check(f"{mode}_side_stream", pipe.side is not None)
+        X_in = torch.empty(N, F, device=DEV)
+        dZ_in = torch.empty(N, (L + 1) * F, device=DEV)
+        Zb = [torch.full((N, (L + 1) * F), float("nan"), device=DEV) for _ in range(2)]
+        dXb = []
+        for i in range(2):  # back to back on the same pipeline buffers, no host sync in between
+            torch.cuda._sleep(SPIN)  # X_in becomes final late on the compute stream
+            X_in.copy_(Xs[i])
+            pipe.run(X_in, Zb[i], de)
+            torch.cuda._sleep(SPIN)
+            dZ_in.copy_(dZs[i])
+            dXb.append(pipe.backward(dZ_in, de))
+        torch.cuda.synchronize(DEV)
+        for i in range(2):
+            check(f"{mode}_sync_Z_bitwise_one_gpu[{i}]", torch.equal(sync_Z[i], ref_Z[i]))
+            check(f"{mode}_pipelined_Z_bitwise_one_gpu[{i}]", torch.equal(Zb[i], ref_Z[i]))
+            check(f"{mode}_pipelined_dX_bitwise_sync[{i}]", torch.equal(dXb[i], sync_dX[i]))
+            scale = float(ref_dX[i].abs().max())
+            err = float((dXb[i] - ref_dX[i]).abs().max())
+            check(f"{mode}_dX_vs_one_gpu[{i}]", err <= 1e-5 * scale, {"max_abs": err, "scale": scale})
+        results[f"{mode}_halo_rows"] = sg.plan.n_halo
+
+    # the bench's max-over-ranks reduction and barriers
+    tt = torch.tensor([1.5, 2.5, 3.5], dtype=torch.float64, device=DEV)
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    dist.barrier()
+    check("all_reduce_max_f64", tt.tolist() == [1.5, 2.5, 3.5])
+    dist.destroy_process_group()
+    results["ok"] = ok
+    print(json.dumps(results), flush=True)
+    return 0 if ok else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())
