@@ -15,6 +15,8 @@
 // the nonzeros of V cost a row of g'.
 #include "grl_internal.h"
 
+#include <cstdlib>
+
 namespace grl {
 namespace {
 
@@ -289,9 +291,17 @@ __global__ void bag_dw_reduce_kernel(const float* __restrict__ part, int S, int 
 
 // Row splits of the sparse dW: up to 128 ranges of >= 512 rows, and at most
 // DW_PART_BUDGET bytes of fp32 partials (every split writes its whole
-// Keff x C slab, which the ordered reduce reads back).
-constexpr int64_t DW_PART_BUDGET = 128ll << 20;
+// Keff x C slab, which the ordered reduce reads back).  A workgroup walks its
+// range's chunks one after another, so the split count is the kernel's
+// parallelism: at M = 100k, K = 4369, C = 256 (kernel + reduce,
+// tools/probe_bag_dw_splits.py, profiles/r03_probe_bag_dw_splits.json)
+// S = 16 / 29 / 64 / 128 / 196 take 3.41 / 2.33 / 1.70 / 1.52 / 1.57 ms; a
+// 128 MB budget (S = 29 there) cost the 100k-node train step 0.9 ms, so the
+// budget is 1 GiB (S = 128: 573 MB at C = 256; C = 512: S = 120, 1.07 GB).
+constexpr int64_t DW_PART_BUDGET = 1ll << 30;
 int bag_dw_splits(int64_t M, int64_t Keff, int64_t C) {
+  const char* e = getenv("GRL_BAG_DW_SPLITS");  // A/B aid (read by the size query and the call alike)
+  if (e && atoi(e) > 0) return (int)std::max<int64_t>(1, std::min<int64_t>(atoi(e), M));
   const int64_t by_mem = std::max<int64_t>(1, DW_PART_BUDGET / std::max<int64_t>(1, Keff * C * 4));
   return (int)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(128, by_mem), ceil_div(M, 512)));
 }

@@ -27,7 +27,7 @@ dev = torch.device("cuda:0")
 N = int(os.environ.get("PROBE_N", "1000000"))
 F = int(os.environ.get("PROBE_F", "256"))
 g = TypedGraph.synthetic(N, 32.0, 6, seed=0, device=dev)
-X = torch.randn(N, F, device=dev)
+X = torch.randn(N, F, device=dev, generator=torch.Generator(device=dev).manual_seed(1))  # fixed: zbits compare builds
 gd = g.with_dropedge(DropEdge(0.3, 2, 0, True))
 Xg = X.clone().requires_grad_(True)
 Z = typed_aggregate(Xg, g)
@@ -37,4 +37,5 @@ tag = os.path.basename(os.environ.get("GRL_LIB_PATH", "libgrl.so"))
 r = {"fwd_p0": timeit(lambda: typed_aggregate(X, g)),
      "fwd_p0.3": timeit(lambda: typed_aggregate(X, gd)),
      "bwd_p0": timeit(lambda: torch.autograd.grad(Z, Xg, dZ, retain_graph=True))}
-print(tag, F, " ".join(f"{k}={v:.3f}ms" for k, v in r.items()), flush=True)
+zc = int(typed_aggregate(X, g).view(torch.int32).to(torch.int64).sum())  # bit checksum: equal across builds iff same bits
+print(tag, F, " ".join(f"{k}={v:.3f}ms" for k, v in r.items()), f"zbits={zc}", flush=True)
