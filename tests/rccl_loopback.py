@@ -41,14 +41,15 @@ DEV = torch.device("cuda", 0)
 SPIN = 20_000_000  # spin-kernel cycles (~10 ms): far longer than a slice's collective or gather here
 
 
-def loopback_plan(g: TypedGraph, mode: str) -> HaloPlan:
+def loopback_plan(colidx: torch.Tensor, n: int, mode: str) -> HaloPlan:
     """A one-rank plan whose sources all come through the exchange.
     dense:  X_ext = [own rows | own rows as rank 0's gathered slot]; the
             shard's rank is set to -1 so the gathered slot counts as a peer's
             (its gradient partials are added, as a peer's would be);
     sparse: X_ext = [own rows | referenced rows, ascending]; send_index the
-            same rows, sent to and received from the one rank."""
-    n, c = g.num_rows, g.colidx.long()
+            same rows, sent to and received from the one rank.
+    (Also used by tests/test_dist_gloo.py on CPU.)"""
+    c = colidx.long()
     E = int(c.numel())
     ids = torch.unique(c)
     empty = torch.zeros(0, dtype=torch.int64, device=c.device)
@@ -61,7 +62,7 @@ def loopback_plan(g: TypedGraph, mode: str) -> HaloPlan:
 
 def loopback_shard(g: TypedGraph, mode: str) -> ShardedGraph:
     sg = ShardedGraph.__new__(ShardedGraph)
-    sg._init(g.rowptr, loopback_plan(g, mode), g.num_types, g.vals, dist.group.WORLD)
+    sg._init(g.rowptr, loopback_plan(g.colidx, g.num_rows, mode), g.num_types, g.vals, dist.group.WORLD)
     return sg
 
 

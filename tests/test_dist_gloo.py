@@ -159,6 +159,40 @@ def test_sharded_equals_single_process(bounds, mode):
     mp.spawn(_worker, args=(world, _free_port(), bounds, mode), nprocs=world, join=True)
 
 
+def _loopback_worker(rank, world, port, mode):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from rccl_loopback import loopback_plan
+
+        rowptr, colidx, X, dZ, Zref, dXref = _reference()
+        plan = loopback_plan(torch.from_numpy(colidx.copy()), N, mode)
+        X_loc = torch.from_numpy(X.copy()).requires_grad_(True)
+        X_ext = halo_exchange(X_loc, plan)  # a one-rank group with halo rows still exchanges them
+        assert X_ext.shape[0] == N + plan.n_halo
+        np.testing.assert_array_equal(X_ext[plan.colidx_local.long()].detach().numpy(), X[colidx])
+        assert (plan.colidx_local >= N).all()  # every source row came through the collective
+        d = c_oracle.drop(*DROP, True)
+        Z = _OracleAggregate.apply(X_ext, rowptr, plan.colidx_local.numpy(), N + plan.n_halo, N, 0,
+                                   int(colidx.size), d)
+        np.testing.assert_array_equal(Z.detach().numpy(), Zref)
+        Z.backward(torch.from_numpy(dZ.copy()))
+        np.testing.assert_allclose(X_loc.grad.numpy(), dXref, rtol=0, atol=1e-5)
+        _check_pipeline(plan, rowptr, X, Zref, 0, d, dZ, X_loc.grad)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["dense", "sparse"])
+def test_one_rank_loopback_plan_exchanges(mode):
+    """The loopback plans of tests/rccl_loopback.py (what the one-GPU box runs
+    on real RCCL) through the product's exchange on a one-rank gloo group:
+    Z bitwise one process, dX within fp32 rounding (the edge sums come back
+    as a peer's partial), the sliced pipeline bitwise the unsliced exchange."""
+    mp.spawn(_loopback_worker, args=(1, _free_port(), mode), nprocs=1, join=True)
+
+
 def test_single_shard_plan_is_identity():
     rowptr, colidx = ohash.synth_csr(0, L, 50, 300, 1)
     plan = build_halo_plan(torch.from_numpy(colidx), 0, 50)
