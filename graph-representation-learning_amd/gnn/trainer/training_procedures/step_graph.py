@@ -6,12 +6,21 @@ debug.json): an eager step launches ~130 small kernels and is host-bound
 (DESIGN.md §4.8).  Captured, the whole step replays with one launch.
 
 What stays outside the graph, every step (host work, or shapes that change):
-  * the batch's TypedGraph (dense -> typed CSR, its CSC) -- then copied into
-    the bucket's STATIC buffers: rowptr [B*N*L+1], colidx / CSC arrays at a
-    capacity `cap` (a power of two >= nnz).  Kernels walk rowptr / colptr, so
-    entries past nnz are never read; the static graph's self-loop DropEdge ids
-    start at `cap` (any fixed id scheme gives i.i.d. masks; eager steps of
-    this procedure use the same static graph, so they draw the same masks);
+  * a dense adjacency batch (the collate's (B, N, L, N), B*N*L*N <=
+    DENSE_IN_GRAPH_MAX entries): only its copy into the bucket's static A --
+    the typed CSR and its CSC are built INSIDE the graph into static buffers
+    at the capacity cap = B*N*L*N (grl_dense_to_csr_rowptr / _fill, entries
+    past nnz given a sentinel column = B*N that the CSC sort puts last,
+    grl_csr_to_csc over cap entries and B*N + 1 columns), so no host sync
+    on nnz and no host graph objects per step;
+  * otherwise the batch's TypedGraph (dense -> typed CSR, its CSC, or the
+    typed edge list) -- then copied into the bucket's STATIC buffers: rowptr
+    [B*N*L+1], colidx / CSC arrays at a capacity `cap` (a power of two >=
+    nnz).
+  Kernels walk rowptr / colptr, so entries past nnz are never read; the
+  static graph's self-loop DropEdge ids start at `cap` (any fixed id scheme
+  gives i.i.d. masks; eager steps of this procedure use the same static
+  graph, so they draw the same masks);
   * V and the labels, copied into static tensors;
   * the DropEdge seed of the step, written into a device word every
     EdgeDropout reads at launch (`seed_source`), call ids 0, 1, 2 per step;
@@ -29,6 +38,7 @@ mode "capture" replays; mode "static" runs the same static pipeline eagerly
 """
 from __future__ import annotations
 
+import ctypes
 from collections import OrderedDict
 from typing import Any, Dict, Optional, Tuple
 
@@ -36,9 +46,13 @@ import torch
 import torch.nn as nn
 
 from grl import TypedGraph
+from grl._lib import call
+from grl._lib import lib as _grl
+from grl.graph import current_stream_handle
 
 MAX_BUCKETS = 32
 MAX_ROWS = 1 << 14  # larger batches are not launch-bound: they run the normal eager step
+DENSE_IN_GRAPH_MAX = 1 << 22  # B*N*L*N entries: dense batches up to this build their graph inside the replay
 
 
 def _mix64(x: int) -> int:
@@ -51,7 +65,7 @@ def _mix64(x: int) -> int:
 class _Bucket:
     """Static device buffers of one (B, N, F, cap, vals) bucket and its graph."""
 
-    def __init__(self, B: int, N: int, F: int, L: int, cap: int, vals: bool, device):
+    def __init__(self, B: int, N: int, F: int, L: int, cap: int, vals: bool, device, dense: bool = False):
         rows = B * N
         self.cap = cap
         self.V = torch.zeros(B, N, F, device=device)
@@ -59,7 +73,8 @@ class _Bucket:
         self.rowptr = torch.zeros(rows * L + 1, dtype=torch.int32, device=device)
         self.colidx = torch.zeros(cap, dtype=torch.int32, device=device)
         self.vals = torch.zeros(cap, device=device) if vals else None
-        self.csc = {"colptr": torch.zeros(rows + 1, dtype=torch.int32, device=device),
+        # dense: one more column, the sentinel B*N of the padding entries (sorted last)
+        self.csc = {"colptr": torch.zeros(rows + (2 if dense else 1), dtype=torch.int32, device=device),
                     "zrow": torch.zeros(cap, dtype=torch.int32, device=device),
                     "eid": torch.zeros(cap, dtype=torch.int32, device=device),
                     "cvals": torch.zeros(cap, device=device) if vals else None}
@@ -70,6 +85,39 @@ class _Bucket:
         self.hip_graph: Optional[torch.cuda.CUDAGraph] = None
         self.out: Optional[Tuple[torch.Tensor, torch.Tensor]] = None  # static (loss, logits)
         self.failed = False
+        self.A = None
+        if dense:  # the graph is built from A inside the step (build_graph)
+            self.A = torch.zeros(B, N, L, N, device=device)
+            self.ws_rowptr = torch.empty(max(1, int(_grl().grl_dense_to_csr_workspace_size(rows * L))),
+                                         dtype=torch.uint8, device=device)
+            self.ws_csc = torch.empty(int(_grl().grl_csr_to_csc_workspace_size(cap, rows + 1)), dtype=torch.uint8,
+                                      device=device)
+            self.slot = torch.arange(cap, dtype=torch.int32, device=device)
+
+    def load_dense(self, V: torch.Tensor, A: torch.Tensor, y: torch.Tensor) -> None:
+        self.V.copy_(V)
+        self.y.copy_(y)
+        self.A.copy_(A)
+
+    def build_graph(self) -> None:
+        """Dense A -> the static typed CSR and CSC, on the stream (capturable:
+        no host sync).  rowptr and the first nnz entries are what
+        TypedGraph.from_dense builds; entries past nnz get column B*N, so the
+        CSC builder's stable sort (over cap entries, B*N + 1 columns) puts them
+        after every real entry and colptr[B*N] = nnz."""
+        B, N, L, _ = self.A.shape
+        rows = B * N
+        st = current_stream_handle(self.A.device)
+        strides = (ctypes.c_int64 * 4)(*self.A.stride())
+        call("grl_dense_to_csr_rowptr", self.A.data_ptr(), B, N, L, strides, self.rowptr.data_ptr(),
+             self.ws_rowptr.data_ptr(), self.ws_rowptr.numel(), st)
+        call("grl_dense_to_csr_fill", self.A.data_ptr(), B, N, L, strides, self.rowptr.data_ptr(),
+             self.colidx.data_ptr(), self.vals.data_ptr() if self.vals is not None else None, st)
+        self.colidx.masked_fill_(self.slot >= self.rowptr[-1], rows)  # device compare: no sync
+        c = self.csc
+        call("grl_csr_to_csc", ctypes.byref(self.graph.csr_c()), rows + 1, c["colptr"].data_ptr(),
+             c["zrow"].data_ptr(), c["eid"].data_ptr(), c["cvals"].data_ptr() if c["cvals"] is not None else None,
+             self.ws_csc.data_ptr(), self.ws_csc.numel(), st)
 
     def load(self, V: torch.Tensor, g: TypedGraph, y: torch.Tensor) -> None:
         n = g.nnz
@@ -129,6 +177,28 @@ class StepGraph:
         cap = max(1024, 1 << max(0, int(g.nnz - 1).bit_length()))
         return tuple(V.shape) + (cap, g.vals is not None)
 
+    def _dense_in_graph(self, V: torch.Tensor, A: torch.Tensor) -> bool:
+        """A dense batch whose graph can be built inside the replay: the
+        collate layout, a small capacity, and no row that could be heavy
+        (a row segment holds at most N entries)."""
+        if V.dim() != 3 or A.dim() != 4 or A.shape[0] != V.shape[0] or A.shape[1] != V.shape[1] \
+                or A.shape[3] != A.shape[1] or V.shape[0] * V.shape[1] > MAX_ROWS:
+            return False
+        from grl.graph import SPLIT_THRESHOLD
+
+        B, N, L, _ = A.shape
+        return B * N * L * N <= DENSE_IN_GRAPH_MAX and L * N <= SPLIT_THRESHOLD
+
+    def _bucket(self, key, make) -> _Bucket:
+        b = self.buckets.get(key)
+        if b is None:
+            b = make()
+            self.buckets[key] = b
+            while len(self.buckets) > MAX_BUCKETS:
+                self.buckets.popitem(last=False)
+        self.buckets.move_to_end(key)
+        return b
+
     def eligible(self, V: torch.Tensor, g: TypedGraph) -> bool:
         if V.dim() != 3 or V.shape[0] * V.shape[1] > MAX_ROWS or g.nnz >= 2 ** 31:
             return False
@@ -136,6 +206,8 @@ class StepGraph:
 
     def _compute(self, b: _Bucket):
         p = self.proc
+        if b.A is not None:
+            b.build_graph()
         logits = p.model.forward([b.V, b.graph])
         loss = p.criterion(logits, b.y)
         loss.backward()
@@ -151,20 +223,24 @@ class StepGraph:
 
         p = self.proc
         V = batch["textline_encoding"].float().to(self.device)
-        A = batch_graph(batch, self.device)
-        g = A if isinstance(A, TypedGraph) else p.model.to_graph(A)
         y = batch["node_label"].to(self.device)
-        if not self.eligible(V, g):
-            return None
-        key = self._key(V, g)
-        b = self.buckets.get(key)
-        if b is None:
-            b = _Bucket(V.shape[0], V.shape[1], V.shape[2], g.num_types, key[-2], g.vals is not None, self.device)
-            self.buckets[key] = b
-            while len(self.buckets) > MAX_BUCKETS:
-                self.buckets.popitem(last=False)
-        self.buckets.move_to_end(key)
-        b.load(V, g, y)
+        A_src = batch.get("adjacency_matrix") if "typed_edges" not in batch else None
+        if A_src is not None and self._dense_in_graph(V, A_src):
+            B, N, L, _ = A_src.shape
+            # values other than 0 / 1 (fc_similarity graphs) keep a vals array; checked on the host copy
+            vals = bool(((A_src != 0) & (A_src != 1)).any()) if not A_src.is_cuda else True
+            key = tuple(V.shape) + ("dense", L, vals)
+            b = self._bucket(key, lambda: _Bucket(B, N, V.shape[2], L, B * N * L * N, vals, self.device, dense=True))
+            b.load_dense(V, A_src, y)
+        else:
+            A = batch_graph(batch, self.device)
+            g = A if isinstance(A, TypedGraph) else p.model.to_graph(A)
+            if not self.eligible(V, g):
+                return None
+            key = self._key(V, g)
+            b = self._bucket(key, lambda: _Bucket(V.shape[0], V.shape[1], V.shape[2], g.num_types, key[-2],
+                                                  g.vals is not None, self.device))
+            b.load(V, g, y)
         self.seed_t.fill_(self._step_seed())
         self.step += 1
         p.model.train()

@@ -174,3 +174,54 @@ def test_captured_train_step_equals_eager(tmp_path, monkeypatch):
     assert len(losses["static"]) == 9 and losses["static"] == losses[True], losses
     for k in models["static"]:
         assert torch.equal(models["static"][k], models[True][k]), k
+
+
+def test_dense_bucket_builds_the_graph_of_from_dense():
+    """A dense batch's captured step builds its typed CSR and CSC inside the
+    replay (step_graph._Bucket.build_graph: no host sync on nnz): rowptr and
+    the first nnz entries of colidx / vals / colptr / zrow / eid / cvals are
+    TypedGraph.from_dense's bit for bit, the padding entries carry the
+    sentinel column B*N that the CSC puts last; eager and from a HIP graph
+    replayed on new data in the same static buffers."""
+    from gnn.trainer.training_procedures.step_graph import _Bucket
+    from grl import TypedGraph
+
+    dev = torch.device("cuda:0")
+    gen = torch.Generator().manual_seed(3)
+
+    def batch(B, N, p, vals):
+        A = (torch.rand(B, N, 6, N, generator=gen) < p).float()
+        if vals:
+            A = A * (0.5 + torch.rand(B, N, 6, N, generator=gen))
+        A[0, 0, 0, :] = 0  # an empty row segment
+        return A
+
+    def check(b, A, vals):
+        B, N = A.shape[0], A.shape[1]
+        ref = TypedGraph.from_dense(A.to(dev), layout="bnln", keep_values=vals)
+        n = ref.nnz  # 0 too: a page without edges
+        assert torch.equal(b.rowptr, ref.rowptr)
+        assert torch.equal(b.colidx[:n], ref.colidx) and bool((b.colidx[n:] == B * N).all())
+        c, rc = b.csc, ref.csc()
+        assert torch.equal(c["colptr"][:B * N + 1], rc["colptr"]) and int(c["colptr"][B * N + 1]) == b.cap
+        for k in ("zrow", "eid"):
+            assert torch.equal(c[k][:n], rc[k][:n]), k
+        if vals:
+            assert torch.equal(b.vals[:n], ref.vals) and torch.equal(c["cvals"][:n], rc["cvals"][:n])
+
+    for B, N, vals in ((4, 74, False), (2, 33, True), (1, 5, False)):
+        b = _Bucket(B, N, 8, 6, B * N * 6 * N, vals, dev, dense=True)
+        V, y = torch.zeros(B, N, 8), torch.zeros(B, N, dtype=torch.int64)
+        A = batch(B, N, 0.03, vals)
+        b.load_dense(V, A, y)
+        b.build_graph()
+        check(b, A, vals)
+        torch.cuda.synchronize()
+        hg = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(hg):
+            b.build_graph()
+        for p in (0.08, 0.01):  # new batches into the same static buffers, replayed
+            A = batch(B, N, p, vals)
+            b.load_dense(V, A, y)
+            hg.replay()
+            check(b, A, vals)
