@@ -69,19 +69,22 @@ def main():
             t0 = time.perf_counter()
             proc._run_train_step(b)
             t["total"] += time.perf_counter() - t0
+        key, bk = next(reversed(sg.buckets.items()))  # every batch here has one shape: one bucket
         for i in range(n):
             b = batches[i % len(batches)]
             t0 = time.perf_counter()
             V = b["textline_encoding"].float().to(dev)
-            A = batch_graph(b, dev)
-            g = proc.model.to_graph(A)
             y = b["node_label"].to(dev)
-            g.csc()
+            if bk.A is None:  # the graph is built on the host path, then copied in
+                A = batch_graph(b, dev)
+                g = proc.model.to_graph(A)
+                g.csc()
             torch.cuda.synchronize()
             t1 = time.perf_counter()
-            key = sg._key(V, g)
-            bk = sg.buckets[key]
-            bk.load(V, g, y)
+            if bk.A is None:
+                bk.load(V, g, y)
+            else:  # dense: the graph is built inside the replay from the static A
+                bk.load_dense(V, b["adjacency_matrix"], y)
             torch.cuda.synchronize()
             t2 = time.perf_counter()
             bk.hip_graph.replay()
@@ -94,7 +97,8 @@ def main():
             t["load"] += t2 - t1
             t["replay_to_loss"] += t3 - t2
             t["metrics"] += t4 - t3
-        print({k: round(v / n * 1e3, 3) for k, v in t.items()}, sg.stats(), flush=True)
+        t["bucket"] = str(key)
+        print({k: (round(v / n * 1e3, 3) if isinstance(v, float) else v) for k, v in t.items()}, sg.stats(), flush=True)
 
 
 if __name__ == "__main__":
