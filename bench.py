@@ -146,6 +146,7 @@ def spawn_ranks(nproc):
 
     port = str(_free_port())
     procs = []
+    signal.signal(signal.SIGTERM, lambda *_: (_ for _ in ()).throw(KeyboardInterrupt()))
     for r in range(nproc):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nproc), LOCAL_WORLD_SIZE=str(nproc),
                    GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
@@ -161,22 +162,29 @@ def spawn_ranks(nproc):
     t.start()
     status = 0
     live = set(range(nproc))
-    while live:
-        for r in sorted(live):
-            rc = procs[r].poll()
-            if rc is None:
-                continue
-            live.discard(r)
-            if rc != 0 and status == 0:
-                status = rc if rc > 0 else 128 - rc
-                print(f"bench.py: rank {r} exited with status {rc}; stopping the other ranks", file=sys.stderr,
-                      flush=True)
-                for q in live:
-                    try:
-                        os.killpg(procs[q].pid, signal.SIGTERM)  # the exact process group this parent started
-                    except ProcessLookupError:
-                        pass
-        time.sleep(0.2)
+
+    def stop(ranks):
+        for q in ranks:
+            try:
+                os.killpg(procs[q].pid, signal.SIGTERM)  # the exact process group this parent started
+            except ProcessLookupError:
+                pass
+
+    try:
+        while live:
+            for r in sorted(live):
+                rc = procs[r].poll()
+                if rc is None:
+                    continue
+                live.discard(r)
+                if rc != 0 and status == 0:
+                    status = rc if rc > 0 else 128 - rc
+                    print(f"bench.py: rank {r} exited with status {rc}; stopping the other ranks", file=sys.stderr,
+                          flush=True)
+                    stop(live)
+            time.sleep(0.2)
+    finally:  # Ctrl-C / SIGTERM of this parent: no rank keeps its GPU
+        stop([q for q in live if procs[q].poll() is None])
     t.join(timeout=10)
     return status
 

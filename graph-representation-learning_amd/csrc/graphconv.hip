@@ -957,25 +957,36 @@ static int ws_spin_limit() {
 }
 
 // A persistent kernel whose bounded wait ran out left its outputs partly
-// unwritten.  Outside stream capture the call waits for its kernel and reads
-// the status word (GRL_E_TIMEOUT); inside a capture (no host sync possible),
-// or with GRL_WS_STATUS=poison, a follow-up kernel fills the outputs with NaN
-// when the word is set, so a replay that timed out cannot pass for a result.
+// unwritten.  Stream-ordered handling (no host sync on the call): a
+// follow-up kernel fills the call's outputs with NaN when the call's status
+// word is set, and ORs the entry point's bit into the per-device sticky
+// word, which grl_check() reads and clears at the caller's next sync point.
+// GRL_WS_STATUS=sync (debug aid) makes an eager call wait for its kernel and
+// return GRL_E_TIMEOUT itself, as round 3's entry points did.
+__device__ int g_grl_sticky;  // WS_WHO_* bits of the calls whose outputs were poisoned
+
+constexpr int WS_WHO_FWD = 1, WS_WHO_FWD_TRAIN = 2, WS_WHO_BWD_DATA = 4;
+
 __global__ void ws_poison_kernel(const int* __restrict__ status, float* __restrict__ a, int64_t na,
-                                 float* __restrict__ b, int64_t nb) {
+                                 float* __restrict__ b, int64_t nb, int who) {
   if (*status == 0) return;
+  if (blockIdx.x == 0 && threadIdx.x == 0) __hip_atomic_fetch_or(&g_grl_sticky, who, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const float nan = __builtin_nanf("");
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < na + nb; i += (int64_t)gridDim.x * blockDim.x)
     (i < na ? a[i] : b[i - na]) = nan;
 }
 
-static int graphconv_status(const int* status, float* a, int64_t na, float* b, int64_t nb, hipStream_t st,
-                            const char* who) {
+static const char* who_name(int who) {
+  return who == WS_WHO_FWD ? "grl_graphconv_fwd" : who == WS_WHO_FWD_TRAIN ? "grl_graphconv_fwd_train"
+                                                                          : "grl_graphconv_bwd_data";
+}
+
+static int graphconv_status(const int* status, float* a, int64_t na, float* b, int64_t nb, hipStream_t st, int who) {
+  const char* mode = getenv("GRL_WS_STATUS");
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  GRL_HIP(hipStreamIsCapturing(st, &cs));
-  const char* mode = getenv("GRL_WS_STATUS");  // "poison": never sync, NaN outputs on a timeout (as in a capture)
-  if (cs != hipStreamCaptureStatusNone || (mode && strcmp(mode, "poison") == 0)) {
-    hipLaunchKernelGGL(ws_poison_kernel, dim3(1024), dim3(256), 0, st, status, a, na, b, b ? nb : 0);
+  if (mode && strcmp(mode, "sync") == 0) GRL_HIP(hipStreamIsCapturing(st, &cs));
+  if (!(mode && strcmp(mode, "sync") == 0) || cs != hipStreamCaptureStatusNone) {
+    hipLaunchKernelGGL(ws_poison_kernel, dim3(1024), dim3(256), 0, st, status, a, na, b, b ? nb : 0, who);
     GRL_LAUNCH_CHECK();
     return GRL_OK;
   }
@@ -984,7 +995,7 @@ static int graphconv_status(const int* status, float* a, int64_t na, float* b, i
   GRL_HIP(hipStreamSynchronize(st));
   if (h & WS_STATUS_TIMEOUT)
     GRL_FAIL(GRL_E_TIMEOUT, "%s: a wave of the persistent GraphConv kernel gave up waiting on its LDS ring "
-             "(bound %d sleeps); the outputs are invalid", who, ws_spin_limit());
+             "(bound %d sleeps); the outputs are invalid", who_name(who), ws_spin_limit());
   return GRL_OK;
 }
 
@@ -1029,7 +1040,7 @@ int graphconv_fused_fwd(const GrlTypedCsr* g, const float* X, int64_t ldx, int F
       GRL_WS_LAUNCH(4);
 #undef GRL_WS_LAUNCH
     GRL_LAUNCH_CHECK();
-    return graphconv_status(status, out, M * C, Z, M * ldz, st, Z ? "grl_graphconv_fwd_train" : "grl_graphconv_fwd");
+    return graphconv_status(status, out, M * C, Z, M * ldz, st, Z ? WS_WHO_FWD_TRAIN : WS_WHO_FWD);
   }
 #define GRL_FUSED_LAUNCH(KS_)                                                                                        \
   do {                                                                                                               \
@@ -1097,7 +1108,25 @@ int graphconv_fused_bwd_data(const GrlTypedCsr* gt, const int32_t* eid, const fl
     GRL_WSB_LAUNCH(4);
 #undef GRL_WSB_LAUNCH
   GRL_LAUNCH_CHECK();
-  return graphconv_status(status, dX, M * Cout, Gagg, M * K, st, "grl_graphconv_bwd_data");
+  return graphconv_status(status, dX, M * Cout, Gagg, M * K, st, WS_WHO_BWD_DATA);
 }
 
 }  // namespace grl
+
+extern "C" int grl_check(grl_stream_t stream) {
+  using namespace grl;
+  hipStream_t st = as_stream(stream);
+  int h = 0;
+  GRL_HIP(hipMemcpyFromSymbolAsync(&h, HIP_SYMBOL(g_grl_sticky), sizeof(int), 0, hipMemcpyDeviceToHost, st));
+  GRL_HIP(hipStreamSynchronize(st));
+  if (h == 0) return GRL_OK;
+  const int zero = 0;
+  GRL_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_grl_sticky), &zero, sizeof(int), 0, hipMemcpyHostToDevice, st));
+  GRL_HIP(hipStreamSynchronize(st));
+  GRL_FAIL(GRL_E_TIMEOUT, "%s%s%s%s%s: a wave of the persistent GraphConv kernel gave up waiting on its LDS ring "
+           "(bound %d sleeps); those calls' outputs were set to NaN",
+           (h & WS_WHO_FWD) ? "grl_graphconv_fwd" : "", (h & WS_WHO_FWD) && (h & ~WS_WHO_FWD) ? ", " : "",
+           (h & WS_WHO_FWD_TRAIN) ? "grl_graphconv_fwd_train" : "",
+           (h & WS_WHO_FWD_TRAIN) && (h & WS_WHO_BWD_DATA) ? ", " : "",
+           (h & WS_WHO_BWD_DATA) ? "grl_graphconv_bwd_data" : "", ws_spin_limit());
+}

@@ -14,6 +14,7 @@ from gnn.data_generator.base_dataloader import BaseDataLoader
 from gnn.inferencer.inference_procedures.base_procedure import BaseProcedure
 from gnn.utils.input_wrapper import cast_label_to_list, handle_single_input
 from grl import TypedGraph
+from grl.graph import device_check
 from grl.layout import edges_to_typed_csr
 
 
@@ -43,6 +44,7 @@ class KVInference(BaseProcedure):
         scores, classes = logits.max(dim=-1)
         classes = classes.reshape(-1).cpu().tolist()
         scores = scores.reshape(-1).cpu().tolist()
+        device_check(self.device)  # synced already: surface a kernel's stream-ordered failure
         if not (len(raw) == len(classes) == len(scores)):
             raise ValueError(f"{len(raw)} boxes but {len(classes)} predictions")
         out = []

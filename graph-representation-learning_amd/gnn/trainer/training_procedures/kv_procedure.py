@@ -23,6 +23,7 @@ from gnn.trainer.training_procedures.base_procedure import BaseProcedure
 from gnn.utils.config import to_plain
 from gnn.utils.metric_tracker import Dictlist
 from grl import TypedGraph
+from grl.graph import device_check
 from grl.layout import edges_to_typed_csr
 
 
@@ -119,6 +120,7 @@ class KVProcedure(BaseProcedure):
         predicts = self.activator(logits).argmax(dim=-1)
         scores, items = self._get_metric_scores(predicts, targets, item_name="Node classification")
         scores["loss"] = loss.item()
+        device_check(self.device)  # the step already synced: surface a kernel's stream-ordered failure
         return loss, scores, items
 
     def _run_train_step(self, batch: Dict[str, Any], **kwargs):
@@ -129,6 +131,7 @@ class KVProcedure(BaseProcedure):
                 predicts = self.activator(logits).argmax(dim=-1)
                 scores, items = self._get_metric_scores(predicts, targets, item_name="Node classification")
                 scores["loss"] = loss.item()
+                device_check(self.device)
                 return scores, items
         self.model.train()
         self.optimizer.zero_grad()
@@ -204,5 +207,6 @@ class KVProcedure(BaseProcedure):
                     self.checkpointer.save_checkpoint(
                         {"epoch": epoch, "config": to_plain(self.config), "meta_data": to_plain(metrics),
                          "state_dict": self.model.state_dict()}, self.model_dir)
+        device_check(self.device)  # the last step's backward
         self.tb_writer.close()
         return metrics["f1-score"]

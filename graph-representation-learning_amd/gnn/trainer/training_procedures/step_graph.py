@@ -80,8 +80,10 @@ class _Bucket:
                     "cvals": torch.zeros(cap, device=device) if vals else None}
         self.graph = TypedGraph(self.rowptr, self.colidx, L, vals=self.vals, num_cols=rows, batch_shape=(B, N),
                                 self_id_base=cap)
-        # no heavy rows in a bucket (checked on load); the CSC lives in the static buffers
-        self.graph._shared.update({"csc": self.csc, "split_csr": None, "split_csc": None})
+        # no heavy rows in a bucket (checked on load); the CSC lives in the static buffers.  The arrays are
+        # refilled every step and nnz here is the capacity, so no typed transpose may be cached on this graph:
+        # static_buffers keeps graph_conv's backward off the one-kernel data gradient (grl.ops)
+        self.graph._shared.update({"csc": self.csc, "split_csr": None, "split_csc": None, "static_buffers": True})
         self.hip_graph: Optional[torch.cuda.CUDAGraph] = None
         self.out: Optional[Tuple[torch.Tensor, torch.Tensor]] = None  # static (loss, logits)
         self.failed = False

@@ -5,7 +5,10 @@ lives in the sibling `gnn` package (gnn.models.GraphCNNDropEdge,
 gnn.models.networks.robust_gcn.GraphConv, gnn.cl_warper.GNNLearningWarper).
 """
 from ._lib import GrlError, version  # noqa: F401
-from .graph import DropEdge, EdgeBlockedGraph, TypedGraph  # noqa: F401
+from .graph import DropEdge, EdgeBlockedGraph, TypedGraph, device_check  # noqa: F401
 from .ops import graph_linear, typed_aggregate  # noqa: F401
 
-__all__ = ["GrlError", "version", "DropEdge", "EdgeBlockedGraph", "TypedGraph", "graph_linear", "typed_aggregate"]
+check = device_check  # grl.check(): surface a persistent kernel's stream-ordered failure (grl_check)
+
+__all__ = ["GrlError", "version", "DropEdge", "EdgeBlockedGraph", "TypedGraph", "check", "device_check",
+           "graph_linear", "typed_aggregate"]

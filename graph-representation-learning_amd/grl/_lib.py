@@ -125,6 +125,7 @@ _P = ctypes.POINTER
 SIGNATURES = {
     "grl_version": (ctypes.c_char_p, []),
     "grl_last_error": (ctypes.c_char_p, []),
+    "grl_check": (_c_i32, [_c_vp]),
     "grl_trace_push": (None, [ctypes.c_char_p]),
     "grl_trace_pop": (None, []),
     "grl_dropedge_init": (_c_i32, [_P(GrlDropEdge), ctypes.c_float, _c_u64, _c_u64, _c_i32]),

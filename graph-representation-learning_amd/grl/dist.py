@@ -526,21 +526,23 @@ class _PipelinedAggregate(torch.autograd.Function):
 
 def _p2p_exchange(sends, recvs, group):
     """Post point-to-point transfers: sends [(tensor, dst)], recvs [(tensor,
-    src)] (group ranks).  RCCL: one batch_isend_irecv, asynchronous (the
-    transfer waits for the work queued on the current stream); returns the
-    works and a finish() that copies host-staged receives back (gloo moves
-    device tensors through host copies)."""
+    src)], peers given as ranks OF `group` (P2POp's group_peer: a subgroup's
+    rank q is not global rank q).  RCCL: one batch_isend_irecv, asynchronous
+    (the transfer waits for the work queued on the current stream); a send
+    to this rank itself pairs with a receive from it (a loopback plan).
+    Returns the works and a finish() that copies host-staged receives back
+    (gloo moves device tensors through host copies)."""
     if not sends and not recvs:
         return [], lambda: None
     staged = _host_staged(group)
     ops, back = [], []
     for t, dst in sends:
-        ops.append(dist.P2POp(dist.isend, t.cpu() if staged and t.is_cuda else t, dst, group))
+        ops.append(dist.P2POp(dist.isend, t.cpu() if staged and t.is_cuda else t, group=group, group_peer=dst))
     for t, src in recvs:
         buf = torch.empty(t.shape, dtype=t.dtype) if staged and t.is_cuda else t
         if buf is not t:
             back.append((t, buf))
-        ops.append(dist.P2POp(dist.irecv, buf, src, group))
+        ops.append(dist.P2POp(dist.irecv, buf, group=group, group_peer=src))
     works = dist.batch_isend_irecv(ops)
 
     def finish():
@@ -548,6 +550,19 @@ def _p2p_exchange(sends, recvs, group):
             t.copy_(buf)
 
     return works, finish
+
+
+def _all_agree(flag: bool, group, device) -> bool:
+    """True iff `flag` holds on every rank of `group` (a MIN all-reduce): a
+    decision that picks between two different collective sequences must be
+    the same on every rank, or the ranks post mismatched collectives and
+    hang."""
+    if _world(group) == 1:
+        return flag
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32,
+                     device="cpu" if _host_staged(group) or device is None else device)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(int(t.item()))
 
 
 class _RowPipelinedGraphConv(torch.autograd.Function):
@@ -641,8 +656,10 @@ def allreduce_gradients(params, group=None, bucket_bytes: int = 64 << 20, averag
     one all_reduce per step completes it (1.8 MB for gcn1 at
     d=256).  Gradients are packed into flat fp32 buckets of <= bucket_bytes
     (one RCCL call each; all of GraphCNNDropEdge's fit one bucket).
-    average=True divides by the world size (data parallelism's mean)."""
-    if _world(group) == 1:
+    average=True divides by the world size (data parallelism's mean).
+    Without a process group nothing runs; a one-rank group runs the real
+    collectives (a sum over one rank: the gradients unchanged)."""
+    if not (dist.is_available() and dist.is_initialized()):
         return
     grads = [p.grad for p in params if p.grad is not None]
     bucket: List[torch.Tensor] = []
@@ -796,15 +813,21 @@ class ShardedGraph:
 
     def halo_blocks(self):
         """[(peer q, r0, r1)]: the X_ext rows holding peer q's rows, for
-        q = rank+1, rank+2, ... (mod P) -- the order rows_backward sends in."""
+        q = rank+1, rank+2, ... (mod P) -- the order rows_backward sends in.
+        A loopback plan (a one-rank group whose sources all come through the
+        exchange, tests/rccl_loopback.py) has one block, its own rows' copy."""
         p, world = self.plan, len(self.plan.bounds) - 1
         out = []
-        for j in range(1, world):
+        for j in range(1, world + 1):
             q = (p.rank + j) % world
             if p.mode == "dense":
+                if q == p.rank:
+                    continue  # own rows: X_ext[:n_loc], not a gathered slot
                 r0 = p.stride * (1 + q)
                 out.append((q, r0, r0 + p.bounds[q + 1] - p.bounds[q]))
             else:
+                if q == p.rank and p.recv_counts[q] == 0:
+                    continue
                 r0 = p.n_loc + sum(p.recv_counts[:q])
                 out.append((q, r0, r0 + p.recv_counts[q]))
         return out
@@ -814,19 +837,25 @@ class ShardedGraph:
         through the ReLU): the one-kernel data gradient in row blocks, each
         peer's halo block posted to that peer as soon as it is computed, the
         own rows last, then the peers' partials for my rows added in peer
-        order.  None when a block is outside the one-kernel path."""
-        from .ops import graph_conv_bwd_data_rows
+        order.  None -- on EVERY rank -- when a block of some rank is outside
+        the one-kernel path: the ranks agree on the choice (one small
+        all-reduce) before any point-to-point transfer is posted, since the
+        fallback runs the unpipelined exchange, another collective sequence."""
+        from .ops import graph_conv_bwd_data_rows, graph_conv_bwd_data_rows_views
 
         p, world = self.plan, len(self.plan.bounds) - 1
         dev = g.device
         blocks = self.halo_blocks()
+        order = [(r0, r1) for _, r0, r1 in blocks] + [(0, p.n_loc)]
+        views = graph_conv_bwd_data_rows_views(g, graph, W, F, order)
+        if not _all_agree(views is not None, self.group, dev):
+            return None
         dX_ext = torch.empty(graph.num_cols, F, dtype=torch.float32, device=dev)
-        # receive buffers: what peer q computed for my rows (dense: all of them; sparse: the ones q referenced)
-        recv = {}
-        for q in range(world):
-            if q != p.rank:
-                n = p.n_loc if p.mode == "dense" else p.send_counts[q]
-                recv[q] = torch.empty(n, F, dtype=torch.float32, device=dev)
+        # receive buffers: the partials for my rows from the peer whose j-th block they are (src_j = rank - j;
+        # dense: all my rows; sparse: the ones that peer referenced)
+        srcs = [(p.rank - j) % world for j in range(1, len(blocks) + 1)]
+        recv = {q: torch.empty(p.n_loc if p.mode == "dense" else p.send_counts[q], F, dtype=torch.float32,
+                               device=dev) for q in srcs}
         pending = []
         step = {"j": 0}
 
@@ -835,17 +864,12 @@ class ShardedGraph:
             j = step["j"]
             if j > len(blocks):
                 return  # the own rows: nothing to send
-            dst = blocks[j - 1][0]
-            src = (p.rank - j) % world
+            dst, src = blocks[j - 1][0], srcs[j - 1]
             sends = [(dX_ext[r0:r1], dst)] if r1 > r0 else []
             recvs = [(recv[src], src)] if recv[src].shape[0] else []
             pending.append(_p2p_exchange(sends, recvs, self.group))
 
-        order = [(r0, r1) for _, r0, r1 in blocks] + [(0, p.n_loc)]
-        if world > 1 and not graph_conv_bwd_data_rows(g, graph, W, F, order, dX_ext, on_block=post):
-            return None
-        if world == 1 and not graph_conv_bwd_data_rows(g, graph, W, F, [(0, p.n_loc)], dX_ext):
-            return None
+        graph_conv_bwd_data_rows(g, graph, W, F, order, dX_ext, on_block=post, views=views)
         for works, finish in pending:
             for w in works:
                 w.wait()
@@ -853,13 +877,12 @@ class ShardedGraph:
         dX_loc = dX_ext[:p.n_loc].clone()
         off = 0
         for q in range(world):  # peer order: the unpipelined exchange's (_HaloExchange.backward)
-            if q == p.rank:
-                continue
-            if p.mode == "dense":
-                dX_loc += recv[q]
-            elif p.send_counts[q]:
-                cnt = p.send_counts[q]
-                dX_loc.index_add_(0, p.send_index[off:off + cnt], recv[q])
+            if q in recv:
+                if p.mode == "dense":
+                    dX_loc += recv[q]
+                elif p.send_counts[q]:
+                    cnt = p.send_counts[q]
+                    dX_loc.index_add_(0, p.send_index[off:off + cnt], recv[q])
             off += p.send_counts[q] if p.mode != "dense" else 0
         return dX_loc
 

@@ -34,6 +34,18 @@ def current_stream_handle(device: torch.device) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 
 
+def device_check(device=None) -> None:
+    """Raise GrlError if a persistent one-kernel GraphConv call on `device`
+    (default: the current one) gave up on its LDS ring since the last check:
+    grl_check reads and clears the sticky status word those calls' follow-up
+    kernels set (their outputs are NaN then).  It waits for the current
+    stream, so call it where the caller syncs anyway (a loss.item())."""
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    if dev.type != "cuda":
+        return  # no device work ran there
+    call("grl_check", current_stream_handle(dev))
+
+
 def _require_device(t: torch.Tensor, what: str) -> None:
     if not t.is_cuda:
         raise _lib.GrlError(
@@ -219,6 +231,14 @@ class TypedGraph:
         self._shared["csc"] = c
         return c
 
+    @property
+    def transpose_ok(self) -> bool:
+        """False for a graph whose arrays are static buffers refilled in place
+        (a captured training step's bucket, step_graph.py): a cached typed
+        transpose would go stale, so the one-kernel data gradient is not
+        used on it."""
+        return not self._shared.get("static_buffers", False)
+
     def typed_transpose(self):
         """(gt, eid): the typed transpose, built once and cached -- gt's row m
         (one per column of this graph: a shard's own and halo rows), segment
@@ -232,6 +252,9 @@ class TypedGraph:
         tt = self._shared.get("typed_transpose")
         if tt is not None:
             return tt
+        if not self.transpose_ok:
+            raise _lib.GrlError("typed_transpose: this graph's arrays are refilled in place (static buffers); "
+                                "a cached transpose would go stale")
         if self.self_rows != self.num_rows or self.num_cols < self.num_rows:
             raise _lib.GrlError("typed_transpose needs every row to own its self loop (self_rows == num_rows) and "
                                 "the rows among the columns")

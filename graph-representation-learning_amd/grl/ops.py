@@ -271,6 +271,14 @@ class _GraphLinear(torch.autograd.Function):
         return dZ, dW, db_pre if db_pre is not None else db, None
 
 
+# Widths of the one-kernel GraphConv (graphconv.hip): the gathered width (the
+# forward's F, or the data gradient's C) and the largest output width of one
+# call (the forward's C, or the data gradient's F; wider dX runs in column
+# blocks).
+FUSED_WIDTHS = (64, 128, 256)
+FUSED_MAX_OUT = 256
+
+
 def _bwd_data_enabled() -> bool:
     return os.environ.get("GRL_GRAPHCONV_FUSED_BWD", "1") != "0"
 
@@ -287,7 +295,7 @@ def graph_conv_bwd_data(g: torch.Tensor, graph: TypedGraph, W: torch.Tensor, F: 
     disables it.  want_aggregate: return (dX, G_agg, g_eff) with G_agg =
     [A_drop,s^T g_eff]_s ([num_cols, segments * C], written by the same
     kernel) and g_eff the gradient through the ReLU, for dW_s = X^T G_agg_s."""
-    if not _bwd_data_enabled() or isinstance(graph, EdgeBlockedGraph):
+    if not _bwd_data_enabled() or isinstance(graph, EdgeBlockedGraph) or not graph.transpose_ok:
         return None
     M, C = g.shape
     L, S = graph.num_types, graph.segments
@@ -328,29 +336,36 @@ def graph_conv_bwd_data(g: torch.Tensor, graph: TypedGraph, W: torch.Tensor, F: 
     return (dX, G_agg, g) if want_aggregate else dX
 
 
-def graph_conv_bwd_data_rows(g: torch.Tensor, graph: TypedGraph, W: torch.Tensor, F: int, blocks, dX: torch.Tensor,
-                             on_block=None) -> bool:
-    """The one-kernel data gradient (graph_conv_bwd_data) computed in row
-    blocks of dX, one grl_graphconv_bwd_data call per block [r0, r1) over a
-    row-range view of the cached typed transpose, so a caller can act on a
-    block (e.g. send a node-range shard's halo rows home) while the next one
-    computes.  Every row is the same arithmetic as in the whole-range call
-    (rows do not mix in the kernel), so dX is bitwise that call's.  A block
-    starting at row 0 carries the self term of rows < graph.num_rows; other
-    blocks must lie at or beyond num_rows (a shard's halo rows: no self term).
-    g: the output gradient already through the ReLU.  dX: [graph.num_cols, F]
-    (written).  on_block(r0, r1) runs after each block's launch.  False (and
-    nothing written) when some block is outside the one-kernel path or F > 256;
-    the caller then takes the whole-range path."""
-    if not _bwd_data_enabled() or isinstance(graph, EdgeBlockedGraph) or F > 256:
-        return False
+def _rows_view(gt: TypedGraph, r0: int, r1: int, dropedge) -> TypedGraph:
+    """Rows [r0, r1) of the typed transpose as a TypedGraph (rowptr a slice,
+    colidx / vals / eid shared), cached on the transpose so its split plan is
+    built once per graph, not once per backward."""
+    cache = gt._shared.setdefault("row_views", {})
+    v = cache.get((r0, r1))
+    if v is None:
+        L = gt.num_types
+        v = TypedGraph(gt.rowptr[r0 * L: r1 * L + 1], gt.colidx, L, vals=gt.vals, has_self=gt.has_self,
+                       num_cols=gt.num_cols, edge_id_base=gt.edge_id_base, self_id_base=gt.self_id_base,
+                       self_rows=r1 - r0)
+        v.split_threshold, v.split_chunk = gt.split_threshold, gt.split_chunk
+        cache[(r0, r1)] = v
+    return v.with_dropedge(dropedge)
+
+
+def graph_conv_bwd_data_rows_views(g: torch.Tensor, graph: TypedGraph, W: torch.Tensor, F: int, blocks):
+    """The per-block launch data of graph_conv_bwd_data_rows -- [(view, csr,
+    workspace bytes) or None for an empty block] -- or None when some block
+    is outside the one-kernel path.  No device work beyond the cached
+    transpose and split plans: a caller that must decide collectively
+    (grl.dist rows_backward) asks this first, agrees, then launches."""
+    if not _bwd_data_enabled() or isinstance(graph, EdgeBlockedGraph) or not graph.transpose_ok:
+        return None
     M, C = g.shape
     L, S = graph.num_types, graph.segments
-    if (C not in (64, 128, 256) or F % 4 or L > 7 or graph.num_cols < graph.num_rows
+    if (C not in FUSED_WIDTHS or F % 4 or F > FUSED_MAX_OUT or L > 7 or graph.num_cols < graph.num_rows
             or graph.self_rows != graph.num_rows or M != graph.num_rows or g.dtype != torch.float32
-            or not g.is_contiguous() or W.dtype != torch.float32 or tuple(W.shape) != (S * F, C)
-            or tuple(dX.shape) != (graph.num_cols, F) or not dX.is_contiguous()):
-        return False
+            or not g.is_contiguous() or W.dtype != torch.float32 or tuple(W.shape) != (S * F, C)):
+        return None
     for r0, r1 in blocks:
         if not (r0 == 0 or r0 >= graph.num_rows) or r1 < r0 or r1 > graph.num_cols:
             raise _lib.GrlError(f"row block [{r0}, {r1}) must start at 0 or at/after row {graph.num_rows}")
@@ -361,17 +376,38 @@ def graph_conv_bwd_data_rows(g: torch.Tensor, graph: TypedGraph, W: torch.Tensor
         if r1 == r0:
             views.append(None)
             continue
-        v = TypedGraph(gt.rowptr[r0 * L: r1 * L + 1], gt.colidx, L, vals=gt.vals, has_self=gt.has_self,
-                       num_cols=gt.num_cols, edge_id_base=gt.edge_id_base, self_id_base=gt.self_id_base,
-                       self_rows=r1 - r0, _shared={"csc": None})
-        v.split_threshold, v.split_chunk = gt.split_threshold, gt.split_chunk
-        v = v.with_dropedge(graph.dropedge)
+        v = _rows_view(gt, r0, r1, graph.dropedge)
         csr = v.csr_c(C)
         ws_bytes = _lib.lib().grl_graphconv_bwd_data_workspace_query(ctypes.byref(csr), g.data_ptr(), g.stride(0),
                                                                      C, Wc.data_ptr(), F)
         if ws_bytes == 0:
-            return False
+            return None
         views.append((v, csr, ws_bytes))
+    return views
+
+
+def graph_conv_bwd_data_rows(g: torch.Tensor, graph: TypedGraph, W: torch.Tensor, F: int, blocks, dX: torch.Tensor,
+                             on_block=None, views=None) -> bool:
+    """The one-kernel data gradient (graph_conv_bwd_data) computed in row
+    blocks of dX, one grl_graphconv_bwd_data call per block [r0, r1) over a
+    row-range view of the cached typed transpose, so a caller can act on a
+    block (e.g. send a node-range shard's halo rows home) while the next one
+    computes.  Every row is the same arithmetic as in the whole-range call
+    (rows do not mix in the kernel), so dX is bitwise that call's.  A block
+    starting at row 0 carries the self term of rows < graph.num_rows; other
+    blocks must lie at or beyond num_rows (a shard's halo rows: no self term).
+    g: the output gradient already through the ReLU.  dX: [graph.num_cols, F]
+    (written).  on_block(r0, r1) runs after each block's launch.  views:
+    graph_conv_bwd_data_rows_views' result for these arguments (else it is
+    computed here).  False (and nothing written) when some block is outside
+    the one-kernel path; the caller then takes the whole-range path."""
+    if views is None:
+        views = graph_conv_bwd_data_rows_views(g, graph, W, F, blocks)
+    if views is None or tuple(dX.shape) != (graph.num_cols, F) or not dX.is_contiguous():
+        return False
+    gt, eid = graph.typed_transpose()
+    Wc = W.contiguous()
+    M, C = g.shape
     de = graph.dropedge.to_c() if graph.dropedge is not None else None
     stream = current_stream_handle(g.device)
     ws = None

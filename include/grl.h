@@ -15,12 +15,13 @@
  *    memory; scratch comes from a caller workspace sized by *_workspace_size.
  *  - Every call is stream-ordered on `stream` (a hipStream_t passed as void*,
  *    NULL = default stream) and never synchronises the device, so calls can
- *    be captured into a hipGraph.  One exception: where grl_graphconv_fwd,
- *    grl_graphconv_fwd_train and grl_graphconv_bwd_data run their
- *    persistent one-kernel form outside a stream capture, they wait for that
- *    kernel and read its status word (GRL_E_TIMEOUT if a bounded wait ran
- *    out); inside a capture they instead enqueue a kernel that fills their
- *    outputs with NaN when the word is set.
+ *    be captured into a hipGraph.  Failures found on the device are
+ *    stream-ordered too: where grl_graphconv_fwd, grl_graphconv_fwd_train
+ *    and grl_graphconv_bwd_data run their persistent one-kernel form, a
+ *    follow-up kernel fills that call's outputs with NaN if a bounded wait
+ *    ran out and records the entry point in a sticky per-device status word;
+ *    grl_check() (the caller's existing sync point: a loss.item(), an event
+ *    wait) reads and clears that word and returns GRL_E_TIMEOUT.
  *  - Return value 0 = success, negative GRL_E_* = failure; grl_last_error()
  *    returns a thread-local message for the last failure on this thread.
  *  - fp32 features, int32 indices.  Sums over a row's edges run in CSR order
@@ -150,6 +151,15 @@ typedef struct GrlDropEdge {
 /* Library identity / errors. */
 const char* grl_version(void);
 const char* grl_last_error(void);
+
+/* Sticky device status of the current device: waits for `stream`, reads the
+ * word the persistent kernels' follow-up kernels set (see Conventions) and
+ * clears it.  GRL_OK, or GRL_E_TIMEOUT naming every entry point whose
+ * outputs were invalidated (NaN) since the last check.  The one call that
+ * synchronises; meant for points where the caller syncs anyway (the
+ * reference's loss.item(), kv_procedure.py:140; an event wait).  Not
+ * capturable.                                                              */
+int grl_check(grl_stream_t stream);
 
 /* roctx ranges (rocprofv3 --marker-trace): the hot entry points push their
  * own; these let a host layer bracket its steps, e.g. the halo exchange of a

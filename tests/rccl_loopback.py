@@ -16,6 +16,11 @@ the same way and the combine adds them, as a peer's partials.  What runs:
     stale rows;
   * _HaloExchange (ShardedGraph.aggregate, autograd) -- the synchronous
     collectives, forward and backward;
+  * ShardedGraph.graphconv(pipeline="rows") -- the one-kernel layer whose
+    backward posts each halo block's partials point to point
+    (batch_isend_irecv, here to the rank itself) while the next block
+    computes: out / dX / dW / db bitwise the unpipelined sharded layer;
+  * allreduce_gradients with small buckets (several RCCL all_reduce calls);
   * the bench's max-over-ranks all_reduce (float64 on the device) and barrier.
 Checked: Z bitwise the one-GPU aggregation; the pipelined dX bitwise the
 unpipelined sharded dX (the loopback combine adds the edge sums to the self
@@ -124,6 +129,53 @@ def main():
             err = float((dXb[i] - ref_dX[i]).abs().max())
             check(f"{mode}_dX_vs_one_gpu[{i}]", err <= 1e-5 * scale, {"max_abs": err, "scale": scale})
         results[f"{mode}_halo_rows"] = sg.plan.n_halo
+
+    # the one-kernel layer on the shard, with the reverse exchange pipelined over row blocks: the block of
+    # the loopback "peer" (the halo rows) is sent home point to point (batch_isend_irecv to this rank itself)
+    # while the own-row block computes -- out, dX, dW, db bitwise the unpipelined sharded layer's
+    class Layer(torch.nn.Module):
+        def __init__(self, K, C):
+            super().__init__()
+            gw = torch.Generator(device=DEV).manual_seed(7)
+            self.h_weights = torch.nn.Parameter(torch.randn(K, C, generator=gw, device=DEV) / K ** 0.5)
+            self.bias = torch.nn.Parameter(torch.randn(C, generator=gw, device=DEV))
+
+    C = 256
+    R = torch.randn(N, C, generator=gen, device=DEV)
+    for mode in ("dense", "sparse"):
+        sg = loopback_shard(g, mode)
+        res = {}
+        for pipeline in (None, "rows"):
+            layer = Layer((L + 1) * F, C)
+            X = Xs[0].clone().requires_grad_(True)
+            out = sg.graphconv(X, layer, de, relu=True, pipeline=pipeline)
+            (out * R).sum().backward()
+            res[pipeline] = (out.detach(), X.grad, layer.h_weights.grad, layer.bias.grad)
+        names = ("out", "dX", "dW", "db")
+        for name, a, b in zip(names, res[None], res["rows"]):
+            check(f"{mode}_rows_pipeline_{name}_bitwise_unpipelined", torch.equal(a, b))
+        from grl.ops import graph_conv
+
+        with torch.no_grad():
+            layer = Layer((L + 1) * F, C)
+            one = graph_conv(Xs[0], g.with_dropedge(de), layer.h_weights, layer.bias, relu=True)
+        check(f"{mode}_rows_pipeline_out_bitwise_one_gpu", torch.equal(res["rows"][0], one))
+        results[f"{mode}_rows_blocks"] = [(q, r1 - r0) for q, r0, r1 in sg.halo_blocks()]
+
+    # the bucketed gradient all-reduce (DP and the captured step): several buckets, each one RCCL all_reduce
+    from grl.dist import allreduce_gradients
+
+    ps = [torch.nn.Parameter(torch.zeros(s, device=DEV)) for s in [(7, 3), (5,), (1000,), (2, 2), (300, 2)]]
+    for i, p in enumerate(ps):
+        p.grad = torch.randn(p.shape, generator=gen, device=DEV)
+    ps[3].grad = None
+    before = [None if p.grad is None else p.grad.clone() for p in ps]
+    allreduce_gradients(ps, bucket_bytes=4 * 40)  # 40-float buckets: every parameter flushes its own
+    check("allreduce_buckets_exact", all((b is None and p.grad is None) or torch.equal(p.grad, b)
+                                         for p, b in zip(ps, before)))
+    allreduce_gradients(ps, average=True)  # one bucket, divided by the world size (1)
+    check("allreduce_average_exact", all((b is None and p.grad is None) or torch.equal(p.grad, b)
+                                         for p, b in zip(ps, before)))
 
     # the bench's max-over-ranks reduction and barriers
     tt = torch.tensor([1.5, 2.5, 3.5], dtype=torch.float64, device=DEV)

@@ -248,3 +248,60 @@ def _allreduce_worker(rank, world, port):
 
 def test_allreduce_gradients_buckets():
     mp.spawn(_allreduce_worker, args=(3, _free_port()), nprocs=3, join=True)
+
+
+def _agree_worker(rank, world, port):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import types
+
+        from grl import dist as gdist
+        from grl import ops
+
+        # rows_backward: one rank's block is outside the one-kernel path -> EVERY rank returns None before any
+        # point-to-point transfer is posted (they then all run the unpipelined exchange: matching collectives)
+        plan = types.SimpleNamespace(bounds=[0, 10, 20, 30], rank=rank, mode="dense", stride=10, n_loc=10,
+                                     recv_counts=[0] * 3, send_counts=[0] * 3)
+        sg = types.SimpleNamespace(plan=plan, group=None)
+        sg.halo_blocks = types.MethodType(gdist.ShardedGraph.halo_blocks, sg)
+        orig_views, orig_rows = ops.graph_conv_bwd_data_rows_views, ops.graph_conv_bwd_data_rows
+        try:
+            ops.graph_conv_bwd_data_rows_views = lambda *a, **k: None if rank == 1 else ["eligible"]
+
+            def no_launch(*a, **k):
+                raise AssertionError("launched although a peer fell back")
+
+            ops.graph_conv_bwd_data_rows = no_launch
+            g = torch.zeros(10, 4)
+            assert gdist.ShardedGraph.rows_backward(sg, g, None, 4, types.SimpleNamespace(num_cols=40)) is None
+        finally:
+            ops.graph_conv_bwd_data_rows_views, ops.graph_conv_bwd_data_rows = orig_views, orig_rows
+        assert gdist._all_agree(True, None, None) and not gdist._all_agree(rank != 2, None, None)
+        # the dense blocks are every peer's gathered slot in rotation order
+        assert [q for q, _, _ in sg.halo_blocks()] == [(rank + 1) % 3, (rank + 2) % 3]
+        # point-to-point inside a SUBGROUP: peers are group ranks (global rank q + 1 here)
+        sub = dist.new_group([1, 2])
+        if rank in (1, 2):
+            me = dist.get_rank(sub)
+            peer = 1 - me
+            send = torch.full((3,), float(rank))
+            recv = torch.empty(3)
+            works, finish = gdist._p2p_exchange([(send, peer)], [(recv, peer)], sub)
+            for w in works:
+                w.wait()
+            finish()
+            assert torch.equal(recv, torch.full((3,), float(3 - rank)))
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rows_backward_fallback_is_collective_and_p2p_uses_group_ranks():
+    """rows_backward's choice between the row-pipelined
+    point-to-point backward and the unpipelined exchange is agreed by all
+    ranks before anything is posted (a rank whose block cannot take the
+    one-kernel path makes every rank fall back), and point-to-point peers are
+    ranks of the shard's group, also under a subgroup."""
+    mp.spawn(_agree_worker, args=(3, _free_port()), nprocs=3, join=True)

@@ -351,10 +351,14 @@ def test_recompute_takes_weight_gradient_from_the_aggregate(de):
 def test_persistent_kernel_timeout_is_an_error(monkeypatch):
     """graphconv_ws_kernel's bounded waits: with a one-sleep bound
     (GRL_WS_SPIN=1) the MFMA waves give up before the gather waves fill the
-    ring.  Eager calls (forward, training forward, data gradient) raise
-    GrlError(GRL_E_TIMEOUT) instead of returning a partly written result; a
-    captured call cannot sync, so its replay fills the outputs with NaN.
-    With the normal bound the next call is correct again (no sticky state)."""
+    ring.  The calls stay stream-ordered (no host sync): a follow-up kernel
+    fills each failed call's outputs with NaN and records the entry point in
+    the sticky device word, and grl.check() -- at the caller's next sync
+    point -- raises GrlError(GRL_E_TIMEOUT) naming every failed entry point,
+    then clears the word.  Replays of a captured call fail the same way.
+    GRL_WS_STATUS=sync keeps the per-call check (the call itself raises).
+    With the normal bound the next call is correct again."""
+    import grl
     from grl.ops import graph_conv_bwd_data
 
     N, L, F, C = 20_011, 6, 256, 256
@@ -368,24 +372,37 @@ def test_persistent_kernel_timeout_is_an_error(monkeypatch):
     G = torch.randn(N, C, device=DEV, generator=gen)
     dX_ref = graph_conv_bwd_data(G, g, W, F)
     assert dX_ref is not None
+    grl.check()  # nothing pending
     monkeypatch.setenv("GRL_WS_SPIN", "1")
+    out = graph_conv_infer(X, g, W, b, True)  # no raise, no sync: the failure is stream-ordered
+    with pytest.raises(_lib.GrlError, match=r"grl_graphconv_fwd: a wave .* gave up waiting"):
+        grl.check()
+    assert bool(torch.isnan(out).all())
+    grl.check()  # cleared
+    Xg = X.clone().requires_grad_(True)
+    out_t = graph_conv(Xg, g, W, b, relu=True)
+    dX = graph_conv_bwd_data(G, g, W, F)
+    with pytest.raises(_lib.GrlError, match="grl_graphconv_fwd_train, grl_graphconv_bwd_data"):
+        grl.check()
+    assert bool(torch.isnan(out_t).all()) and bool(torch.isnan(dX).all())
+    monkeypatch.setenv("GRL_WS_STATUS", "sync")  # debug aid: every eager call checks itself
     with pytest.raises(_lib.GrlError, match="gave up waiting"):
         graph_conv_infer(X, g, W, b, True)
-    with pytest.raises(_lib.GrlError, match="grl_graphconv_fwd_train"):
-        Xg = X.clone().requires_grad_(True)
-        graph_conv(Xg, g, W, b, relu=True)
-    with pytest.raises(_lib.GrlError, match="grl_graphconv_bwd_data"):
-        graph_conv_bwd_data(G, g, W, F)
-    # inside a capture: no sync, the replay's outputs are NaN
+    monkeypatch.delenv("GRL_WS_STATUS")
+    # inside a capture: the replay's outputs are NaN and grl.check() reports it
     hg = torch.cuda.CUDAGraph()
     with torch.cuda.graph(hg):
         out_c = graph_conv_infer(X, g, W, b, True)
     hg.replay()
-    torch.cuda.synchronize()
+    with pytest.raises(_lib.GrlError, match="grl_graphconv_fwd"):
+        grl.check()
     assert bool(torch.isnan(out_c).all())
     monkeypatch.delenv("GRL_WS_SPIN")
     assert torch.equal(graph_conv_infer(X, g, W, b, True), ref)
     assert torch.equal(graph_conv_bwd_data(G, g, W, F), dX_ref)
+    grl.check()
     hg.replay()  # the captured call reads the bound at capture: it still times out
     torch.cuda.synchronize()
     assert bool(torch.isnan(out_c).all())
+    with pytest.raises(_lib.GrlError):
+        grl.check()

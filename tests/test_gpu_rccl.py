@@ -5,7 +5,9 @@ tools/probe_rccl_one_gpu.py), so tests/rccl_loopback.py runs a one-rank RCCL
 group in a child process with a loopback plan: every source row the
 aggregation reads comes through an RCCL collective (dense all-gather or
 sparse all-to-all-v), in HaloPipeline's side-stream / async branch and in
-_HaloExchange's synchronous one.  The child prints its checks as JSON."""
+_HaloExchange's synchronous one; the row-pipelined one-kernel layer, whose
+backward posts the halo block's partials point to point (batch_isend_irecv);
+and the bucketed gradient all-reduce.  The child prints its checks as JSON."""
 import json
 import os
 import subprocess
@@ -30,3 +32,6 @@ def test_halo_exchange_on_rccl_loopback():
     assert not failed and res["ok"] and r.returncode == 0, (failed, r.stderr[-2000:])
     assert res["backend"] == "nccl"
     assert res["dense_halo_rows"] > 0 and res["sparse_halo_rows"] > 0
+    # the row-pipelined backward had a halo block to post point to point (the loopback peer's rows)
+    assert res["dense_rows_blocks"] and res["dense_rows_blocks"][0][1] > 0
+    assert res["sparse_rows_blocks"] and res["sparse_rows_blocks"][0][1] > 0
