@@ -336,7 +336,7 @@ def graph_conv_bwd_data(g: torch.Tensor, graph: TypedGraph, W: torch.Tensor, F: 
     return (dX, G_agg, g) if want_aggregate else dX
 
 
-def _rows_view(gt: TypedGraph, r0: int, r1: int, dropedge) -> TypedGraph:
+def _transpose_rows_view(gt: TypedGraph, r0: int, r1: int, dropedge) -> TypedGraph:
     """Rows [r0, r1) of the typed transpose as a TypedGraph (rowptr a slice,
     colidx / vals / eid shared), cached on the transpose so its split plan is
     built once per graph, not once per backward."""
@@ -376,7 +376,7 @@ def graph_conv_bwd_data_rows_views(g: torch.Tensor, graph: TypedGraph, W: torch.
         if r1 == r0:
             views.append(None)
             continue
-        v = _rows_view(gt, r0, r1, graph.dropedge)
+        v = _transpose_rows_view(gt, r0, r1, graph.dropedge)
         csr = v.csr_c(C)
         ws_bytes = _lib.lib().grl_graphconv_bwd_data_workspace_query(ctypes.byref(csr), g.data_ptr(), g.stride(0),
                                                                      C, Wc.data_ptr(), F)
