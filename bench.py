@@ -317,7 +317,11 @@ def main():
 
     bytes_launch = spmm_bytes(E_loc, n_loc, L, F, args.p)
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
-    traffic = load_traffic(args, n_loc, world)
+    wide = F > 256 and graph.num_cols * F * 4 > (12 << 30)
+    kernel = (f"spmm_kernel<4,{2 if wide else 1},{4 if wide else 8},false,false> (grl_typed_spmm_fwd)" if world == 1
+              else f"spmm_kernel / spmm_pair_kernel (grl_typed_spmm_fwd_slice, {chunks} slices of {F // chunks} "
+                   "columns)")
+    traffic = load_traffic(args, wname, n_loc, world, kernel)
     # achieved counts algorithmic bytes.  On a degree-ordered R-MAT graph hot rows are re-read from
     # the Infinity Cache / L2, so it can exceed what HBM delivers ("cache-amplified"); the PMC
     # traffic rate (L2-miss reads + writes per launch over the same kernel time) is the HBM figure.
@@ -348,11 +352,11 @@ def main():
                      if amplified else "algorithmic bytes (SURVEY.md §8(d))",
                      "traffic_GBps": traffic_rate,
                      "traffic_frac": traffic_rate / HBM_PEAK_GBS if traffic_rate else None,
-                     "kernel": (f"spmm_kernel<4,{2 if F > 256 and graph.num_cols * F * 4 > (12 << 30) else 1},"
-                                f"{4 if F > 256 and graph.num_cols * F * 4 > (12 << 30) else 8},false,false> "
-                                "(grl_typed_spmm_fwd)") if world == 1 else
-                     f"spmm_kernel / spmm_pair_kernel (grl_typed_spmm_fwd_slice, {chunks} slices of "
-                     f"{F // chunks} columns)",
+                     "kernel": kernel,
+                     "traffic_note": None if traffic else
+                     ("no PMC record of this kernel for this workload and world size (a shard's slice kernels over "
+                      "its [own | halo] table were never profiled): traffic unmeasured" if world > 1 else
+                      "no PMC record for this workload: traffic unmeasured"),
                      "kernel_ms": kern_ms, "kernel_ms_min_max": [min(per_step), max(per_step)] if world == 1 else None,
                      "launches": {"timed": args.steps, "warmup": args.warmup,
                                   "other": 5 if wname.startswith("C3") else 0,
@@ -373,8 +377,13 @@ def main():
     if args.graph == "rmat":
         out["config"]["split"] = graph.split_stats()
         out["config"]["max_row_edges"] = int((graph.rowptr[L::L] - graph.rowptr[:-1:L]).max())
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        out["cpu_baseline"], out["parity"] = cpu_baseline(args, g_step, X_loc, Z, L, F)
+    if rank == 0 and args.cpu_seconds > 0:
+        if world == 1:
+            out["cpu_baseline"], out["parity"] = cpu_baseline(args, g_step, X_loc, Z, L, F)
+        else:  # rank 0's node-range shard on the host cores: the same rows, the same [own | halo] table
+            out["cpu_baseline"], out["parity"] = cpu_baseline_shard(args, g_step, pipe, Z, L, F, world)
+    if world > 1:
+        dist.barrier()  # the other ranks wait while rank 0 times the host baseline
     if world == 1 and wname.startswith("C3"):
         out["dropedge_train_p0.3"] = dropedge_train(graph, X_loc, E_loc, 3)
         if args.c4_reference:
@@ -502,19 +511,31 @@ def dropedge_train(graph, X, E, iters):
             "note": "fused DropEdge p=0.3 (seed 2, call 7): forward SpMM + CSC-gather backward"}
 
 
-def load_traffic(args, n_loc, world):
-    """HBM bytes per launch from a committed rocprofv3 PMC summary of the same
-    workload (profiles/pmc_traffic.json, written by tools/pmc_traffic.py),
-    or None."""
+def traffic_key(wname, world, args, n_loc):
+    """Key of a PMC record in profiles/pmc_traffic.json: the workload, the
+    world size and the shard shape (a record is only ever the kernel it was
+    measured on, for that workload at that world size)."""
+    return (f"{wname}_w{world}_{args.graph}_n{n_loc}_deg{args.avg_deg:g}_L{args.types}_d{args.dim}"
+            f"_p{args.p:g}")
+
+
+def load_traffic(args, wname, n_loc, world, kernel):
+    """HBM bytes per launch of `kernel` from a committed rocprofv3 PMC summary
+    of the same workload at the same world size (profiles/pmc_traffic.json,
+    written by tools/pmc_traffic.py), or None when no such record exists --
+    e.g. every N>1 line: a shard runs the slice kernels over its [own | halo]
+    table, which no PMC pass has measured (one GPU's whole-graph bytes are
+    not its traffic)."""
     path = os.path.join(HERE, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
         return None
     try:
-        d = json.load(open(path))
-        key = f"{args.graph}_n{n_loc}_deg{args.avg_deg:g}_L{args.types}_d{args.dim}_p{args.p:g}"
-        return d.get(key, {}).get("hbm_bytes_per_launch")
+        rec = json.load(open(path)).get(traffic_key(wname, world, args, n_loc))
     except (OSError, ValueError):  # unreadable summary: report traffic as unmeasured
         return None
+    if not rec or not str(kernel).startswith(rec.get("kernel", "").replace(" ", "").split("<")[0]):
+        return None
+    return rec.get("hbm_bytes_per_launch")
 
 
 def host_cpu_info():
@@ -603,6 +624,45 @@ def cpu_baseline(args, graph, X, Z, L, F):
            "sample": f"{what} and X, {passes} pass(es) in {dt:.1f}s; oracle/grl_oracle.c OpenMP typed-CSR SpMM, "
                      f"{threads} threads", **info}
     parity = {"rows_checked": int(r1 - r0), "max_abs_diff": diff, "bitwise_equal": equal, "tolerance": 1e-4}
+    return cpu, parity
+
+
+def cpu_baseline_shard(args, graph, pipe, Z, L, F, world):
+    """N>1: the oracle (grl_oracle.c, OpenMP, every usable host core) over
+    rank 0's node-range shard -- its typed-CSR rows with the local / halo
+    column ids and the exchanged [own | halo] feature table the pipeline
+    holds after the timed steps -- and every row of rank 0's Z compared
+    bitwise against it.  edges/s of the shard (E_loc per pass); the whole
+    graph is P such shards, so the host's whole-graph rate is this rate."""
+    from oracle import c_oracle
+
+    info = host_cpu_info()
+    threads = cpu_threads(info)
+    rowptr = graph.rowptr.cpu().numpy()
+    colidx = graph.colidx.cpu().numpy()
+    tables = pipe.tables  # [chunks, rows, F / chunks]: slice c = columns [c Fc, (c + 1) Fc)
+    X_ext = tables.permute(1, 0, 2).reshape(tables.shape[1], F).cpu().numpy()
+    E = int(rowptr[-1])
+    d = None if args.p <= 0 else c_oracle.drop(args.p, 2, 0, True)
+    split = (graph.split_threshold, graph.split_chunk)
+    t0 = time.perf_counter()
+    passes = 0
+    while True:
+        Zc = c_oracle.spmm_fwd(rowptr, colidx, X_ext, L, True, d=d, nthreads=threads, split=split,
+                               edge_base=graph.edge_id_base, self_base=graph.self_id_base)
+        passes += 1
+        if time.perf_counter() - t0 >= args.cpu_seconds:
+            break
+    dt = time.perf_counter() - t0
+    Zg = Z.cpu().numpy()
+    equal = bool(np.array_equal(Zg, Zc))
+    diff = 0.0 if equal else float(np.abs(Zg.astype(np.float64) - Zc).max())
+    cpu = {"value": E * passes / dt, "unit": "edges/s", "cores": threads, "kind": "port",
+           "sample": f"rank 0's node-range shard of {world} ({graph.num_rows} rows, {E} typed edges, "
+                     f"[own | halo] table of {X_ext.shape[0]} rows), {passes} pass(es) in {dt:.1f}s; "
+                     f"oracle/grl_oracle.c OpenMP typed-CSR SpMM, {threads} threads (edges/s of the shard)", **info}
+    parity = {"rows_checked": int(graph.num_rows), "scope": "every row of rank 0's shard", "max_abs_diff": diff,
+              "bitwise_equal": equal, "tolerance": 1e-4}
     return cpu, parity
 
 

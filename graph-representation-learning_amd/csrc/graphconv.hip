@@ -91,19 +91,20 @@ __device__ __forceinline__ void fma4(float4& acc, float w, const float4& x) {
 
 // W [K][C] row-major -> three bf16 planes in MFMA B-fragment order:
 // Wf[ks][cb][q][lane][e] = plane q of W(k = 16 ks + 8 (lane >> 5) + e,
-// n = 32 cb + (lane & 31)), zero for n >= C.  Scalar split as
+// n = 32 cb + (lane & 31)) for cb < cbn (8: C <= 256, 16: C <= 512), zero for
+// n >= C.  Scalar split as
 // split_planes_kernel (linear.hip).
 // t_cin > 0 (the data-gradient form, grl_graphconv_bwd_data): W(k, n) is the
 // block-transposed forward weight, W(s t_cin + c, n) = Wfwd[s C + n][c] for
 // the forward's [(L+1) C][t_cin] h_weights (block s of the result = W_s^T).
 __global__ void fused_w_planes_kernel(const float* __restrict__ W, int64_t K, int C, uint16_t* __restrict__ Wf,
-                                      int64_t t_cin) {
-  const int64_t total = K * FG_CB * 32;
+                                      int64_t t_cin, int cbn) {
+  const int64_t total = K * cbn * 32;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
     const int e = (int)(i & 7), lane = (int)((i >> 3) & 63);
     const int64_t rest = i >> 9;
-    const int cb = (int)(rest % FG_CB);
-    const int64_t ks = rest / FG_CB;
+    const int cb = (int)(rest % cbn);
+    const int64_t ks = rest / cbn;
     const int64_t k = ks * 16 + 8 * (lane >> 5) + e;
     const int n = cb * 32 + (lane & 31);
     const float v = n >= C ? 0.0f : (t_cin > 0 ? W[((k / t_cin) * C + n) * t_cin + k % t_cin] : W[k * C + n]);
@@ -379,71 +380,64 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GRL_FG_WPE,
 
 // ---------------------------------------------------------------------------
 // Warp-specialized persistent form (the default).  One workgroup per CU, 12
-// waves: 8 gather waves produce Z tiles into a 4-slot LDS ring, 4 MFMA waves
-// consume them, so the HBM-bound gather and the matrix cores run at the same
-// time instead of in alternating phases.
+// waves: PROD gather waves produce Z tiles into a 4-slot LDS ring, 12 - PROD
+// MFMA waves consume them, so the HBM-bound gather and the matrix cores run
+// at the same time instead of in alternating phases.
 //  * a tile is 64 destination rows; a ring unit is a 128-column part of one
-//    segment of it, kept fp32 (64 x 128 floats + a pad chunk per row, 33
-//    KB): every W fragment fetched from L2 feeds 64 rows (at 32 rows W's
+//    VIRTUAL segment of it, kept fp32 (64 x 128 floats + a pad chunk per row,
+//    33 KB): every W fragment fetched from L2 feeds 64 rows (at 32 rows W's
 //    re-read stream alone exceeded what L2 delivers to a CU), and the MFMA
 //    waves split their A fragments into the x6 planes as they read them;
+//  * virtual segments: a segment of F <= 256 columns is one; F = 256 FV
+//    (gcn3's 2C-wide input, C5's d = 512 and its gcn3 at 1024) is FV
+//    consecutive 256-column parts, each gathered as its own pass over the
+//    segment's edge list (the list and its first 64 sources are reused, the
+//    rows' 1 KB halves are what is read).  A finished row then fills only the
+//    2 units of its part, so the 4-slot ring keeps a free slot ahead of the
+//    MFMA waves at any F.  K order, and so every product, is unchanged;
 //  * the unit stream: tile it of this workgroup (tile = blockIdx.x + it *
-//    gridDim.x), segment s, part hh -> unit u = (it * S + s) * NH + hh, ring
-//    slot u % 4, generation u / 4;
-//  * gather wave p owns rows 8p..8p+7 of each tile: it streams its rows'
-//    segment-s edges as one list (flushes at row boundaries), gathering
-//    whole rows (one float4 per lane, 1 KB per wave-instruction, up to
-//    WS_U rows in flight), and a finished row goes to the segment's NH
-//    units at once; the next segment's list and first 64 sources load while
-//    this one gathers.  Before its first store to a segment's units it waits
-//    until the MFMA waves released their slots' previous generation
-//    (consumed[slot] >= 4 g); after its last it adds 1 to produced[slot]
-//    (release); gather waves never wait for each other;
+//    gridDim.x), virtual segment v, part hh -> unit u = (it * S FV + v) NH +
+//    hh, ring slot u % 4, generation u / 4;
+//  * gather wave p owns rows RW p..RW p + RW - 1 of each tile (RW = 64 /
+//    PROD): it streams its rows' segment edges as one list (flushes at row
+//    boundaries), gathering one float4 per lane per source row (1 KB per
+//    wave-instruction, up to U rows in flight), and a finished row goes to
+//    the virtual segment's NH units at once; the next segment's list and
+//    first 64 sources load while this one gathers.  Before its first store
+//    to a virtual segment's units it waits until the MFMA waves released
+//    their slots' previous generation (consumed[slot] >= CONS g); after its
+//    last it adds 1 to produced[slot] (release); gather waves never wait for
+//    each other;
 //  * MFMA wave c owns output columns 64c..64c+63 for all 64 rows (2 x 2
-//    MFMA blocks): it waits for produced[slot] >= 8 (g + 1) (acquire), runs
+//    MFMA blocks): it waits for produced[slot] >= PROD (g + 1) (acquire), runs
 //    the unit's K16 steps (24 MFMAs each) with the next step's W fragments
 //    in flight (the W stream crosses unit and tile boundaries: it is
 //    periodic in the segment order), then adds 1 to consumed[slot]; after a
 //    tile's last unit it stores the tile.
+//  * PROD = 8 (C <= 256: 4 MFMA waves) or 4 (C <= 512: 8 MFMA waves, each
+//    gather wave 16 rows with two rowptr-window registers and more rows in
+//    flight, so the bytes in flight per CU stay the same).
 // Every wave walks the same unit sequence and units complete in order, so
 // the waits cannot form a cycle; each spin is bounded anyway (a kernel that
 // could hang the GPU is not an option): a wave whose bound runs out sets the
 // call's status word (vector atomic OR into the caller's workspace) and
-// stops, and the host entry point reports GRL_E_TIMEOUT (graphconv_status).
+// stops; graphconv_status then poisons the call's outputs (stream-ordered).
 // Arithmetic per element is the same as graphconv_fused_kernel's (same
 // chains, split, K order, product order): bitwise the two-kernel result.
-// GRL_WS_PLANES=1: the gather waves store x6 bf16 planes (the MFMA waves only
-// read fragments; 3 ring slots of 52 KB); 0: the ring holds fp32 and each
-// MFMA wave splits the fragments it reads (4 slots of 33 KB)
-#ifndef GRL_WS_PLANES
-#define GRL_WS_PLANES 0
-#endif
-#ifndef GRL_WS_KC
-#define GRL_WS_KC 128
-#endif
 constexpr int WS_R = 64;                   // rows per tile
-constexpr int WS_KC = GRL_WS_KC;           // Z columns per ring unit (F > WS_KC: F / WS_KC units per segment)
-#if GRL_WS_PLANES
-constexpr int WS_LDF = WS_KC + 8;          // bf16 per plane row (+ one 16-B pad chunk: conflict-free)
-constexpr int WS_PLANE = WS_R * WS_LDF;    // bf16 per plane
-constexpr int WS_SLOT = 3 * WS_PLANE / 2;  // ring slot in floats (the ring is declared as float)
-#else
+constexpr int WS_KC = 128;                 // Z columns per ring unit
+constexpr int WS_FV = 256;                 // columns per virtual segment (at most)
 constexpr int WS_LDF = WS_KC + 4;          // floats per ring row (+ one 16-B pad chunk: conflict-free)
 constexpr int WS_SLOT = WS_R * WS_LDF;     // floats per ring slot
-#endif
-constexpr int WS_PROD = 8;                 // gather waves
-#ifndef GRL_WS_CONS
-#define GRL_WS_CONS 4
-#endif
-constexpr int WS_CONS = GRL_WS_CONS;       // MFMA waves (4: 64 output columns each; 8: 32, two per SIMD)
-constexpr int WS_CB = FG_CB / WS_CONS;     // 32-column blocks per MFMA wave
-constexpr int WS_RW = WS_R / WS_PROD;      // rows per gather wave
-// ring slots: as many as ~140 KB hold (fp32 128-col units: 4; bf16 planes of 64-col units: 5)
-constexpr int WS_NB = (GRL_WS_PLANES && WS_KC == 128) ? 3 : (140 * 1024) / (WS_SLOT * 4);
+constexpr int WS_WAVES = 12;               // gather + MFMA waves per workgroup
+constexpr int WS_CB = 2;                   // 32-column blocks per MFMA wave
+constexpr int WS_NB = (140 * 1024) / (WS_SLOT * 4);  // ring slots that ~140 KB hold: 4
 #ifndef GRL_WS_U
 #define GRL_WS_U 12
 #endif
-constexpr int WS_U = GRL_WS_U;             // neighbour rows in flight per gather wave
+#ifndef GRL_WS_U16
+#define GRL_WS_U16 12
+#endif
 constexpr int WS_SPIN = 1 << 24;           // bounded waits (~0.5 s of s_sleep 1); GRL_WS_SPIN overrides
 constexpr int WS_STATUS_TIMEOUT = 1;       // status bit: a bounded wait ran out (results invalid)
 
@@ -463,14 +457,6 @@ constexpr int WS_STATUS_TIMEOUT = 1;       // status bit: a bounded wait ran out
 // MFMA waves only release the slots (the gather alone)
 #ifndef GRL_WS_WHATIF
 #define GRL_WS_WHATIF 0
-#endif
-// GRL_WS_PRIO (A/B aid): 1 = MFMA waves issue at s_setprio 2, 2 = gather waves do
-#ifndef GRL_WS_PRIO
-#define GRL_WS_PRIO 0
-#endif
-// GRL_WS_NTX (A/B aid): 1 = the gather waves load source rows non-temporally
-#ifndef GRL_WS_NTX
-#define GRL_WS_NTX 0
 #endif
 #if GRL_WS_STAMP
 __device__ unsigned long long g_ws_dbg[1024 * 12 * 2];
@@ -502,22 +488,34 @@ __device__ __forceinline__ bool wait_ge(int* p, int target, unsigned long long* 
   return false;
 }
 
+// KS: K16 steps of one virtual segment (its width / 16); FV: virtual segments
+// per segment (F = 16 KS FV); PROD: gather waves (8: C <= 256, 4: C <= 512).
 // EID (the data-gradient form over the typed transpose): entry e's DropEdge
 // id is edge_base + eid[e] (its forward CSR position) instead of edge_base + e.
 // Rows >= self_rows have no self term (a shard's transpose: its halo rows);
 // the forward passes M.
-template <int KS, bool VALS, bool EID = false>
-__global__ __launch_bounds__(64 * (WS_PROD + WS_CONS)) void graphconv_ws_kernel(
+#ifndef GRL_WS_DIAG_LB
+#define GRL_WS_DIAG_LB (64 * WS_WAVES)  // register-use diagnostics: a smaller bound shows the unconstrained demand
+#endif
+template <int KS, bool VALS, bool EID = false, int FV = 1, int PROD = 8>
+__global__ __launch_bounds__(GRL_WS_DIAG_LB) void graphconv_ws_kernel(
     int64_t M, int L, int hs, const int32_t* __restrict__ rowptr, const int32_t* __restrict__ colidx,
     const float* __restrict__ vals, uint64_t edge_base, uint64_t self_base, const float* __restrict__ X,
     int64_t ldx, const uint16_t* __restrict__ Wf, const float* __restrict__ bias, int relu,
     float* __restrict__ out, int C, DropDev de, int64_t num_tiles, float* __restrict__ Zout, int64_t ldz,
     const int32_t* __restrict__ eid, int64_t self_rows, int spin_limit, int* __restrict__ status) {
-  constexpr int F = KS * 16;
-  constexpr int KC = F < WS_KC ? F : WS_KC;  // Z columns per unit
-  constexpr int NH = F / KC;                  // units per segment
+  constexpr int FVW = KS * 16;                // columns per virtual segment
+  constexpr int F = FVW * FV;                 // columns per segment
+  constexpr int KC = FVW < WS_KC ? FVW : WS_KC;  // Z columns per unit
+  constexpr int NH = FVW / KC;                // units per virtual segment
   constexpr int KSU = KC / 16;                // K16 steps per unit
-  static_assert(NH < WS_NB, "a segment's units are distinct ring slots, and one more is free");
+  constexpr int CONS = WS_WAVES - PROD;       // MFMA waves
+  constexpr int CB = CONS * WS_CB;            // 32-column blocks of W's planes (C <= 32 CB)
+  constexpr int RW = WS_R / PROD;             // rows per gather wave
+  constexpr int U = RW > 8 ? GRL_WS_U16 : GRL_WS_U;  // neighbour rows in flight per gather wave
+  static_assert(FV == 1 || FVW == WS_FV, "wide segments are cut into 256-column virtual segments");
+  static_assert(NH < WS_NB, "a virtual segment's units are distinct ring slots, and one more is free");
+  static_assert(PROD == 8 || PROD == 4, "8 gather + 4 MFMA waves, or 4 + 8 (two 8-row groups per gather wave)");
   __shared__ __attribute__((aligned(16))) float ring[WS_NB * WS_SLOT];
   __shared__ int produced[WS_NB], consumed[WS_NB];
   if (threadIdx.x < WS_NB) {
@@ -545,39 +543,45 @@ __global__ __launch_bounds__(64 * (WS_PROD + WS_CONS)) void graphconv_ws_kernel(
 #if GRL_WS_ONLY_ROLE == 2
   if (false) {
 #else
-  if (wave < WS_PROD) {
+  if (wave < PROD) {
 #endif
     // =========================== gather waves ===========================
-#if GRL_WS_PRIO == 2
-    __builtin_amdgcn_s_setprio(2);
+    // A gather wave's RW rows are NG groups of GR = 8; each group's edges of a
+    // segment stream as one list (the rowptr window of 8 rows fits one
+    // register), the groups one after the other.
+    constexpr int GR = 8;
+    constexpr int NG = RW / GR;
+#ifndef GRL_WS_SC
+#define GRL_WS_SC 4
 #endif
-    const int col = lane * 4;            // this lane's 4 columns of the row
-    const bool col_ok = col < F;
-    const int part = col / KC;           // the unit (part of the segment) they belong to
+    constexpr int SC = GRL_WS_SC;        // self rows loaded per step
+    const int col = lane * 4;            // this lane's 4 columns of the virtual segment
+    const bool col_ok = col < FVW;
+    const int part = col / KC;           // the unit (part of the virtual segment) they belong to
     const int ucol = col - part * KC;    // column within that unit
-    int u = 0;                           // first unit of the current segment
-    // segment lists: lanes < WS_RW hold row lane's range start b and the
+    int u = 0;                           // first unit of the current virtual segment
+    // segment lists: lanes < GR hold row lane's range start b and the
     // inclusive count incl; the first 64 entries' source rows / weights are
-    // fetched one segment ahead
+    // fetched one list ahead
     struct List {
       int b, incl, exc, total, sidx;
       float w;
     };
     auto make_list = [&](int rp, int t) {
       List ls;
-      const int r = min(lane, WS_RW - 1);
+      const int r = min(lane, GR - 1);
       ls.b = __shfl(rp, r * L + t);
       const int e1 = __shfl(rp, r * L + t + 1);  // all lanes: ds_bpermute reads active lanes only
-      const int cnt = lane < WS_RW ? e1 - ls.b : 0;
+      const int cnt = lane < GR ? e1 - ls.b : 0;
       int incl = cnt;
 #pragma unroll
-      for (int d = 1; d < WS_RW; d <<= 1) {
+      for (int d = 1; d < GR; d <<= 1) {
         const int v = __shfl_up(incl, d);
         if (lane >= d) incl += v;
       }
       ls.incl = incl;
       ls.exc = incl - cnt;
-      ls.total = readlane_i(incl, WS_RW - 1);
+      ls.total = readlane_i(incl, GR - 1);
       return ls;
     };
     // list entries [c0, c0 + 64): source row and DropEdge weight (0 = dropped / past the end)
@@ -585,7 +589,7 @@ __global__ __launch_bounds__(64 * (WS_PROD + WS_CONS)) void graphconv_ws_kernel(
       const int pp = c0 + lane;
       int sl = 0;
 #pragma unroll
-      for (int i = 0; i < WS_RW - 1; ++i) sl += pp >= readlane_i(ls.incl, i) ? 1 : 0;
+      for (int i = 0; i < GR - 1; ++i) sl += pp >= readlane_i(ls.incl, i) ? 1 : 0;
       const int e = __shfl(ls.b, sl) + (pp - __shfl(ls.exc, sl));  // CSR position of entry pp
       sidx = 0;
       w = 0.0f;
@@ -599,140 +603,137 @@ __global__ __launch_bounds__(64 * (WS_PROD + WS_CONS)) void graphconv_ws_kernel(
       }
     };
     for (int64_t tile = blockIdx.x; tile < num_tiles; tile += gridDim.x) {
-      const int64_t rw0 = tile * WS_R + wave * WS_RW;
-      const int nvalid = (int)max<int64_t>(0, min<int64_t>(WS_RW, M - rw0));
-      const int rp = lane <= WS_RW * L ? rowptr[min<int64_t>(rw0 * L + min(lane, nvalid * L), M * L)] : 0;
-      List cur = make_list(rp, 0);
+      const int64_t rw0 = tile * WS_R + wave * RW;
+      const int nvalid = (int)max<int64_t>(0, min<int64_t>(RW, M - rw0));
+      // rowptr window of each group's rows (lane l: rowptr[(rw0 + 8 g) L + l], l <= 8 L; rows past M read as empty)
+      int rp[NG];
+#pragma unroll
+      for (int gi = 0; gi < NG; ++gi) {
+        const int nv = max(0, min(GR, nvalid - gi * GR));
+        rp[gi] = lane <= GR * L ? rowptr[min<int64_t>((rw0 + gi * GR) * L + min(lane, nv * L), M * L)] : 0;
+      }
+      List cur = make_list(rp[0], 0);
       fetch(cur, 0, cur.sidx, cur.w);
-      for (int s = 0; s < S; ++s, u += NH) {
-        // claim the segment's NH slots (this wave's rows only), once, before the first store
-        bool have = false;
-        auto claim = [&]() -> bool {
-          if (have) return true;
+      for (int s = 0; s < S; ++s) {
+#pragma unroll 1
+        for (int hv = 0; hv < FV; ++hv, u += NH) {
+          // claim the virtual segment's NH slots (this wave's rows only), once, before the first store
+          bool have = false;
+          auto claim = [&]() -> bool {
+            if (have) return true;
 #pragma unroll
-          for (int q = 0; q < NH; ++q)
-            if (!wait_ge(&consumed[(u + q) % WS_NB], WS_CONS * ((u + q) / WS_NB), &waited, spin_limit, status))
-              return false;
-          have = true;
-          return true;
-        };
-#if GRL_WS_PLANES
-        uint16_t* const dst = reinterpret_cast<uint16_t*>(ring + ((u + part) % WS_NB) * WS_SLOT) + ucol;
-        float* const zrow = Zout ? Zout + rw0 * ldz + (int64_t)s * F + col : nullptr;
-        auto flush = [&](int r, const float4& v) {
-          if (col_ok) {
-            uint2 q0, q1, q2;
-            split3(v, q0, q1, q2);
-            uint16_t* d = dst + (wave * WS_RW + r) * WS_LDF;
-            *reinterpret_cast<uint2*>(d) = q0;
-            *reinterpret_cast<uint2*>(d + WS_PLANE) = q1;
-            *reinterpret_cast<uint2*>(d + 2 * WS_PLANE) = q2;
-            if (zrow && r < nvalid) {
-              f32x4_t t = {v.x, v.y, v.z, v.w};
-              __builtin_nontemporal_store(t, reinterpret_cast<f32x4_t*>(zrow + (int64_t)r * ldz));
-            }
-          }
-        };
-#else
-        float* const dst = ring + ((u + part) % WS_NB) * WS_SLOT + ucol;
-        // training forward (Zout): the row also goes to HBM for the weight
-        // gradient, with non-temporal stores as spmm_kernel's
-        float* const zrow = Zout ? Zout + rw0 * ldz + (int64_t)s * F + col : nullptr;
-        auto flush = [&](int r, const float4& v) {
-          if (col_ok) {
-            *reinterpret_cast<float4*>(dst + (wave * WS_RW + r) * WS_LDF) = v;
-            if (zrow && r < nvalid) {
-              f32x4_t t = {v.x, v.y, v.z, v.w};
-              __builtin_nontemporal_store(t, reinterpret_cast<f32x4_t*>(zrow + (int64_t)r * ldz));
-            }
-          }
-        };
-#endif
-        if (s < hs) {
-          // identity block of A_pre (robust_gcn.py:58-65): the rows' own features
-          float4 xv[WS_RW];
-#pragma unroll
-          for (int i = 0; i < WS_RW; ++i)
-            xv[i] = (i < nvalid && rw0 + i < self_rows && col_ok) ? *reinterpret_cast<const float4*>(X + (rw0 + i) * ldx + col)
-                                                                  : zero4();
-          if (!claim()) return;
-#pragma unroll
-          for (int i = 0; i < WS_RW; ++i) {
-            float w = 1.0f;
-            if (de.active && de.drop_self) w = dropedge_weight(de, 1.0f, self_base + (uint64_t)(rw0 + i));
-            flush(i, w != 0.0f ? make_float4(w * xv[i].x, w * xv[i].y, w * xv[i].z, w * xv[i].w) : zero4());
-          }
-        } else {
-          // the next segment's list and first 64 entries load while this one gathers
-          List nxt = cur;
-          if (s + 1 < S) {
-            nxt = make_list(rp, s + 1 - hs);
-            fetch(nxt, 0, nxt.sidx, nxt.w);
-          }
-          int row = 0;
-          int bound = readlane_i(cur.incl, 0);
-          float4 a4 = zero4();
-          for (int c0 = 0; c0 < cur.total; c0 += 64) {
-            int sidx = cur.sidx;
-            float w = cur.w;
-            if (c0 > 0) fetch(cur, c0, sidx, w);  // rows with more than 64 segment edges together
-            uint64_t kept = __ballot(w != 0.0f);
-            if (GRL_WS_WHATIF == 3) kept = 0;
-            while (kept) {
-              int jj[WS_U];
-#pragma unroll
-              for (int q = 0; q < WS_U; ++q) {
-                if (kept) {
-                  jj[q] = __builtin_ctzll(kept);
-                  kept &= kept - 1;
-                } else {
-                  jj[q] = -1;
-                }
+            for (int q = 0; q < NH; ++q)
+              if (!wait_ge(&consumed[(u + q) % WS_NB], CONS * ((u + q) / WS_NB), &waited, spin_limit, status))
+                return false;
+            have = true;
+            return true;
+          };
+          float* const dst = ring + ((u + part) % WS_NB) * WS_SLOT + ucol + wave * RW * WS_LDF;
+          const float* const xs = X + hv * FVW + col;  // this lane's columns of the virtual segment
+          // training forward (Zout): the row also goes to HBM for the weight
+          // gradient, with non-temporal stores as spmm_kernel's
+          float* const zrow = Zout ? Zout + rw0 * ldz + (int64_t)s * F + hv * FVW + col : nullptr;
+          auto flush = [&](int r, const float4& v) {  // r: the wave's row
+            if (col_ok) {
+              *reinterpret_cast<float4*>(dst + r * WS_LDF) = v;
+              if (zrow && r < nvalid) {
+                f32x4_t t = {v.x, v.y, v.z, v.w};
+                __builtin_nontemporal_store(t, reinterpret_cast<f32x4_t*>(zrow + (int64_t)r * ldz));
               }
-              float4 xv[WS_U];
+            }
+          };
+          if (s < hs) {
+            // identity block of A_pre (robust_gcn.py:58-65): the rows' own features, SC rows at a time
+            // (a rolled loop: unrolled, the rows' loads and uniform DropEdge hashes crowd the registers)
+#pragma unroll 1
+            for (int i0 = 0; i0 < RW; i0 += SC) {
+              float4 xv[SC];
 #pragma unroll
-              for (int q = 0; q < WS_U; ++q) {
-                if (jj[q] >= 0) {
-                  const int src = readlane_i(sidx, jj[q]);
-#if GRL_WS_NTX
-                  // A/B aid: streamed source rows, so the W planes stay L2-resident
-                  if (col_ok) {
-                    const f32x4_t t = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(X + (int64_t)src * ldx + col));
-                    xv[q] = make_float4(t[0], t[1], t[2], t[3]);
-                  } else {
-                    xv[q] = zero4();
+              for (int i = 0; i < SC; ++i)
+                xv[i] = (i0 + i < nvalid && rw0 + i0 + i < self_rows && col_ok)
+                            ? *reinterpret_cast<const float4*>(xs + (rw0 + i0 + i) * ldx) : zero4();
+              if (!claim()) return;
+#pragma unroll
+              for (int i = 0; i < SC; ++i) {
+                float w = 1.0f;
+                if (de.active && de.drop_self) w = dropedge_weight(de, 1.0f, self_base + (uint64_t)(rw0 + i0 + i));
+                flush(i0 + i, w != 0.0f ? make_float4(w * xv[i].x, w * xv[i].y, w * xv[i].z, w * xv[i].w) : zero4());
+              }
+            }
+          } else {
+#pragma unroll 1
+            for (int gi = 0; gi < NG; ++gi) {
+              // the next list (next group; else the next segment's first, unless the next virtual part
+              // of this segment re-walks this list) and its first 64 entries load while this one gathers
+              List nxt = cur;
+              if (gi + 1 < NG) {
+                nxt = make_list(rp[NG - 1], s - hs);  // NG <= 2: the next group is the last
+                fetch(nxt, 0, nxt.sidx, nxt.w);
+              } else if (hv + 1 < FV) {
+                if (NG > 1) {
+                  nxt = make_list(rp[0], s - hs);
+                  fetch(nxt, 0, nxt.sidx, nxt.w);
+                }
+              } else if (s + 1 < S) {
+                nxt = make_list(rp[0], s + 1 - hs);
+                fetch(nxt, 0, nxt.sidx, nxt.w);
+              }
+              int row = gi * GR;  // the wave's row being summed
+              int bound = readlane_i(cur.incl, 0);
+              float4 a4 = zero4();
+              for (int c0 = 0; c0 < cur.total; c0 += 64) {
+                int sidx = cur.sidx;
+                float w = cur.w;
+                if (c0 > 0) fetch(cur, c0, sidx, w);  // rows with more than 64 segment edges together
+                uint64_t kept = __ballot(w != 0.0f);
+                if (GRL_WS_WHATIF == 3) kept = 0;
+                while (kept) {
+                  int jj[U];
+#pragma unroll
+                  for (int q = 0; q < U; ++q) {
+                    if (kept) {
+                      jj[q] = __builtin_ctzll(kept);
+                      kept &= kept - 1;
+                    } else {
+                      jj[q] = -1;
+                    }
                   }
-#else
-                  xv[q] = col_ok ? *reinterpret_cast<const float4*>(X + (int64_t)src * ldx + col) : zero4();
-#endif
-                }
-              }
+                  float4 xv[U];
 #pragma unroll
-              for (int q = 0; q < WS_U; ++q) {
-                if (jj[q] >= 0) {
-                  const int pos = c0 + jj[q];
-                  while (pos >= bound) {  // rows finished before this entry (wave-uniform)
-                    if (!claim()) return;
-                    flush(row, a4);
-                    a4 = zero4();
-                    ++row;
-                    bound = readlane_i(cur.incl, row);
+                  for (int q = 0; q < U; ++q) {
+                    if (jj[q] >= 0) {
+                      const int src = readlane_i(sidx, jj[q]);
+                      xv[q] = col_ok ? *reinterpret_cast<const float4*>(xs + (int64_t)src * ldx) : zero4();
+                    }
                   }
-                  fma4(a4, readlane_f(w, jj[q]), xv[q]);
+#pragma unroll
+                  for (int q = 0; q < U; ++q) {
+                    if (jj[q] >= 0) {
+                      const int pos = c0 + jj[q];
+                      while (pos >= bound) {  // rows finished before this entry (wave-uniform)
+                        if (!claim()) return;
+                        flush(row, a4);
+                        a4 = zero4();
+                        ++row;
+                        bound = readlane_i(cur.incl, row - gi * GR);
+                      }
+                      fma4(a4, readlane_f(w, jj[q]), xv[q]);
+                    }
+                  }
                 }
               }
+              if (!claim()) return;
+              for (; row < (gi + 1) * GR; ++row) {
+                flush(row, a4);
+                a4 = zero4();
+              }
+              cur = nxt;
             }
           }
-          if (!claim()) return;
-          for (; row < WS_RW; ++row) {
-            flush(row, a4);
-            a4 = zero4();
-          }
-          cur = nxt;
+          if (lane == 0)
+#pragma unroll
+            for (int q = 0; q < NH; ++q) lds_add_rel(&produced[(u + q) % WS_NB], 1);
         }
-        if (lane == 0)
-#pragma unroll
-          for (int q = 0; q < NH; ++q) lds_add_rel(&produced[(u + q) % WS_NB], 1);
       }
     }
     stamp_out();
@@ -741,13 +742,10 @@ __global__ __launch_bounds__(64 * (WS_PROD + WS_CONS)) void graphconv_ws_kernel(
     return;
 #endif
     // =========================== MFMA waves ===========================
-#if GRL_WS_PRIO == 1
-    __builtin_amdgcn_s_setprio(2);
-#endif
-    const int c = wave - WS_PROD;
+    const int c = wave - PROD;
     const int l32 = lane & 31, h = lane >> 5;
-    constexpr int WSTEP = FG_CB * 3 * FG_FRAG;  // bf16 between K16 steps of W
-    const int nsteps = S * KS;                   // one tile's K16 steps (the W stream's period)
+    constexpr int WSTEP = CB * 3 * FG_FRAG;     // bf16 between K16 steps of W
+    const int nsteps = S * KS * FV;             // one tile's K16 steps (the W stream's period)
     // uniform base (SGPRs) + the lane's 16 B: saddr loads
     const uint16_t* wbase = Wf + (int64_t)(c * WS_CB) * 3 * FG_FRAG;
     const int loff = lane * 8;
@@ -777,7 +775,6 @@ __global__ __launch_bounds__(64 * (WS_PROD + WS_CONS)) void graphconv_ws_kernel(
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0], b[j][0], acc[i][j], 0, 0, 0);
       }
     };
-#if !GRL_WS_PLANES
     // this lane's 8 k (step ks) of row i*32 + l32 of a fp32 ring unit
     auto read_a = [&](const float* zs, int ks, int i, float4& v0, float4& v1) {
       const float* ar = zs + (i * 32 + l32) * WS_LDF + ks * 16 + h * 8;
@@ -805,39 +802,20 @@ __global__ __launch_bounds__(64 * (WS_PROD + WS_CONS)) void graphconv_ws_kernel(
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
       }
     };
-#endif
     bf16x8_t bb[2][WS_CB][3];
     int nxt = 0;  // K16 step (within the tile) of the next W fragments to load
     load_b(bb[0], nxt);
     nxt = nxt + 1 == nsteps ? 0 : nxt + 1;
     int u = 0;
     for (int64_t tile = blockIdx.x; tile < num_tiles; tile += gridDim.x) {
-      for (int su = 0; su < S * NH; ++su, ++u) {
+      for (int su = 0; su < S * FV * NH; ++su, ++u) {
         const int slot = u % WS_NB, g = u / WS_NB;
         const float* zs = ring + slot * WS_SLOT;
-        if (!wait_ge(&produced[slot], WS_PROD * (g + 1), &waited, spin_limit, status)) return;
+        if (!wait_ge(&produced[slot], PROD * (g + 1), &waited, spin_limit, status)) return;
 #if GRL_WS_WHATIF == 4
         if (lane == 0) lds_add_rel(&consumed[slot], 1);
         continue;
 #endif
-#if GRL_WS_PLANES
-#pragma unroll
-        for (int ks = 0; ks < KSU; ++ks) {  // KSU is even: the stage of step ks is ks & 1
-          load_b(bb[(ks + 1) & 1], nxt);
-          nxt = nxt + 1 == nsteps ? 0 : nxt + 1;
-          __builtin_amdgcn_sched_barrier(0);
-          const int st = ks & 1;
-#pragma unroll
-          for (int i = 0; i < 2; ++i) {
-            bf16x8_t a[3];
-            const uint16_t* ar = reinterpret_cast<const uint16_t*>(zs) + (i * 32 + l32) * WS_LDF + ks * 16 + h * 8;
-#pragma unroll
-            for (int q = 0; q < 3; ++q) a[q] = *reinterpret_cast<const bf16x8_t*>(ar + q * WS_PLANE);
-            mma(i, bb[st], a);
-          }
-          __builtin_amdgcn_sched_barrier(0);
-        }
-#else
         // Software-pipelined by row block: the split of the next row block's
         // A fragments (VALU) is interleaved with the current row block's 12
         // MFMAs (an MFMA holds the SIMD's issue for 8 of its 32 cycles; the
@@ -867,7 +845,6 @@ __global__ __launch_bounds__(64 * (WS_PROD + WS_CONS)) void graphconv_ws_kernel(
           interleave();
           __builtin_amdgcn_sched_barrier(0);
         }
-#endif
         // the slot's A fragments are in registers once their reads returned
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         if (lane == 0) lds_add_rel(&consumed[slot], 1);
@@ -937,17 +914,23 @@ bool graphconv_fused_enabled() {
   return !(e && e[0] == '0');
 }
 
-// F in {64, 128, 256}, C <= 256, and one wave register holds a wave's rowptr
-// window (FG_RW * L + 1 <= 64: L <= 7)
+// The gathered width F: one virtual segment (64, 128, 256) or 2 / 4 of 256
+// columns; the output width C <= 512 (C > 256: 4 gather + 8 MFMA waves); L
+// <= 7 (a gather wave's rowptr window holds RW L + 1 entries in 1 or 2
+// registers).  The phase-alternating kernel (GRL_FG_WS=0) takes F <= 256, C
+// <= 256 only; other shapes always run the persistent one.
 bool graphconv_fused_shape_ok(int F, int C, int L) {
-  return (F == 256 || F == 128 || F == 64) && C >= 1 && C <= 256 && L >= 1 && FG_RW * L < 64;
+  return (F == 64 || F == 128 || F == 256 || F == 512 || F == 1024) && C >= 1 && C <= 512 && L >= 1 && L <= 7;
 }
 
-// W's planes, then 256 B whose first word is the call's status
-size_t graphconv_fused_ws_bytes(int64_t K) { return (size_t)K * FG_CB * 32 * 3 * 2 + 256; }
+// 32-column blocks of W's planes: 8 for C <= 256, 16 for C <= 512
+static int planes_cb(int C) { return C <= 256 ? FG_CB : 2 * FG_CB; }
 
-static int* ws_status(void* ws, int64_t K) {
-  return reinterpret_cast<int*>(static_cast<char*>(ws) + (size_t)K * FG_CB * 32 * 3 * 2);
+// W's planes, then 256 B whose first word is the call's status
+size_t graphconv_fused_ws_bytes(int64_t K, int C) { return (size_t)K * planes_cb(C) * 32 * 3 * 2 + 256; }
+
+static int* ws_status(void* ws, int64_t K, int C) {
+  return reinterpret_cast<int*>(static_cast<char*>(ws) + (size_t)K * planes_cb(C) * 32 * 3 * 2);
 }
 
 static int ws_spin_limit() {
@@ -999,14 +982,57 @@ static int graphconv_status(const int* status, float* a, int64_t na, float* b, i
   return GRL_OK;
 }
 
+// One launch of the persistent kernel for gathered width F and output width
+// C: the template instance for (F, C > 256) with or without edge values /
+// eid (the data-gradient form); grid = one workgroup per CU (at most the
+// tiles).
+template <bool EID>
+static void launch_ws(int F, int C, bool v, dim3 grid, hipStream_t st, int64_t M, int L, int hs,
+                      const GrlTypedCsr* g, const float* X, int64_t ldx, const uint16_t* Wf, const float* bias,
+                      int relu, float* out, DropDev d, int64_t tiles, float* Z, int64_t ldz, const int32_t* eid,
+                      int64_t self_rows, int spin, int* status) {
+#define GRL_WS_ARGS                                                                                                \
+  grid, dim3(64 * WS_WAVES), 0, st, M, L, hs, g->rowptr, g->colidx, g->vals, g->edge_id_base, g->self_id_base, X, \
+      ldx, Wf, bias, relu, out, C, d, tiles, Z, ldz, eid, self_rows, spin, status
+#define GRL_WS_ONE(KS_, FV_, PROD_)                                                                                \
+  do {                                                                                                            \
+    if (v)                                                                                                        \
+      hipLaunchKernelGGL((graphconv_ws_kernel<KS_, true, EID, FV_, PROD_>), GRL_WS_ARGS);                         \
+    else                                                                                                          \
+      hipLaunchKernelGGL((graphconv_ws_kernel<KS_, false, EID, FV_, PROD_>), GRL_WS_ARGS);                        \
+  } while (0)
+#define GRL_WS_PRODS(KS_, FV_)       \
+  do {                               \
+    if (C <= 256)                    \
+      GRL_WS_ONE(KS_, FV_, 8);       \
+    else                             \
+      GRL_WS_ONE(KS_, FV_, 4);       \
+  } while (0)
+#ifdef GRL_WS_DIAG_ONE  // register-use diagnostics only: one instance (F = 256 FV, PROD)
+  GRL_WS_ONE(16, GRL_WS_DIAG_FV, GRL_WS_DIAG_PROD);
+#else
+  switch (F) {
+    case 64: GRL_WS_PRODS(4, 1); break;
+    case 128: GRL_WS_PRODS(8, 1); break;
+    case 256: GRL_WS_PRODS(16, 1); break;
+    case 512: GRL_WS_PRODS(16, 2); break;
+    default: GRL_WS_PRODS(16, 4); break;  // 1024
+  }
+#endif
+#undef GRL_WS_PRODS
+#undef GRL_WS_ONE
+#undef GRL_WS_ARGS
+}
+
 int graphconv_fused_fwd(const GrlTypedCsr* g, const float* X, int64_t ldx, int F, const float* W, const float* bias,
                         int C, int relu, float* out, const GrlDropEdge* de, void* ws, hipStream_t st, float* Z) {
   const int hs = g->has_self ? 1 : 0;
   const int64_t K = (int64_t)(g->num_types + hs) * F;
   uint16_t* Wf = static_cast<uint16_t*>(ws);
-  const int64_t n_el = K * FG_CB * 32;
+  const int cbn = planes_cb(C);
+  const int64_t n_el = K * cbn * 32;
   hipLaunchKernelGGL(fused_w_planes_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(n_el, 256), 4096)), dim3(256), 0,
-                     st, W, K, C, Wf, (int64_t)0);
+                     st, W, K, C, Wf, (int64_t)0, cbn);
   GRL_LAUNCH_CHECK();
   const int64_t M = g->num_rows;
   const int64_t tiles = ceil_div(M, FG_R);
@@ -1014,31 +1040,15 @@ int graphconv_fused_fwd(const GrlTypedCsr* g, const float* X, int64_t ldx, int F
   const DropDev d = to_dev(de);
   const bool v = g->vals != nullptr;
   const char* wse = getenv("GRL_FG_WS");
-  if (!(wse && wse[0] == '0') || Z) {  // Z out: the warp-specialized kernel only
+  if (!(wse && wse[0] == '0') || Z || F > 256 || C > 256) {  // the persistent kernel (Z out: only it)
     const int64_t ldz = K;
     const int64_t ws_tiles = ceil_div(M, WS_R);
     const int64_t grid = std::min<int64_t>(ws_tiles, (int64_t)device_cu_count());
-    int* status = ws_status(ws, K);
+    int* status = ws_status(ws, K, C);
     const int spin = ws_spin_limit();
     GRL_HIP(hipMemsetAsync(status, 0, sizeof(int), st));
-#define GRL_WS_LAUNCH(KS_)                                                                                           \
-  do {                                                                                                               \
-    if (v)                                                                                                           \
-      hipLaunchKernelGGL((graphconv_ws_kernel<KS_, true>), dim3((unsigned)grid), dim3(64 * (WS_PROD + WS_CONS)), 0,  \
-                         st, M, g->num_types, hs, g->rowptr, g->colidx, g->vals, g->edge_id_base, g->self_id_base, X, \
-                         ldx, Wf, bias, relu, out, C, d, ws_tiles, Z, ldz, nullptr, M, spin, status);                \
-    else                                                                                                             \
-      hipLaunchKernelGGL((graphconv_ws_kernel<KS_, false>), dim3((unsigned)grid), dim3(64 * (WS_PROD + WS_CONS)), 0, \
-                         st, M, g->num_types, hs, g->rowptr, g->colidx, g->vals, g->edge_id_base, g->self_id_base, X, \
-                         ldx, Wf, bias, relu, out, C, d, ws_tiles, Z, ldz, nullptr, M, spin, status);                \
-  } while (0)
-    if (F == 256)
-      GRL_WS_LAUNCH(16);
-    else if (F == 128)
-      GRL_WS_LAUNCH(8);
-    else
-      GRL_WS_LAUNCH(4);
-#undef GRL_WS_LAUNCH
+    launch_ws<false>(F, C, v, dim3((unsigned)grid), st, M, g->num_types, hs, g, X, ldx, Wf, bias, relu, out, d,
+                     ws_tiles, Z, ldz, nullptr, M, spin, status);
     GRL_LAUNCH_CHECK();
     return graphconv_status(status, out, M * C, Z, M * ldz, st, Z ? WS_WHO_FWD_TRAIN : WS_WHO_FWD);
   }
@@ -1074,9 +1084,10 @@ int graphconv_fused_bwd_data(const GrlTypedCsr* gt, const int32_t* eid, const fl
   const int hs = gt->has_self ? 1 : 0;
   const int64_t K = (int64_t)(gt->num_types + hs) * Cin;
   uint16_t* Wf = static_cast<uint16_t*>(ws);
-  const int64_t n_el = K * FG_CB * 32;
+  const int cbn = planes_cb(Cout);
+  const int64_t n_el = K * cbn * 32;
   hipLaunchKernelGGL(fused_w_planes_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(n_el, 256), 4096)), dim3(256), 0,
-                     st, W, K, Cout, Wf, (int64_t)Cin);
+                     st, W, K, Cout, Wf, (int64_t)Cin, cbn);
   GRL_LAUNCH_CHECK();
   const int64_t M = gt->num_rows;
   const int64_t ws_tiles = ceil_div(M, WS_R);
@@ -1084,29 +1095,11 @@ int graphconv_fused_bwd_data(const GrlTypedCsr* gt, const int32_t* eid, const fl
   const int64_t grid = std::min<int64_t>(ws_tiles, (int64_t)device_cu_count());
   const DropDev d = to_dev(de);
   const bool v = gt->vals != nullptr;
-  int* status = ws_status(ws, K);
+  int* status = ws_status(ws, K, Cout);
   const int spin = ws_spin_limit();
   GRL_HIP(hipMemsetAsync(status, 0, sizeof(int), st));
-#define GRL_WSB_LAUNCH(KS_)                                                                                          \
-  do {                                                                                                               \
-    if (v)                                                                                                           \
-      hipLaunchKernelGGL((graphconv_ws_kernel<KS_, true, true>), dim3((unsigned)grid), dim3(64 * (WS_PROD + WS_CONS)), \
-                         0, st, M, gt->num_types, hs, gt->rowptr, gt->colidx, gt->vals, gt->edge_id_base,             \
-                         gt->self_id_base, G, ldg, Wf, nullptr, 0, dX, Cout, d, ws_tiles, Gagg, K, eid, self_rows,   \
-                         spin, status);                                                                             \
-    else                                                                                                             \
-      hipLaunchKernelGGL((graphconv_ws_kernel<KS_, false, true>), dim3((unsigned)grid),                              \
-                         dim3(64 * (WS_PROD + WS_CONS)), 0, st, M, gt->num_types, hs, gt->rowptr, gt->colidx,         \
-                         gt->vals, gt->edge_id_base, gt->self_id_base, G, ldg, Wf, nullptr, 0, dX, Cout, d, ws_tiles,  \
-                         Gagg, K, eid, self_rows, spin, status);                                                    \
-  } while (0)
-  if (Cin == 256)
-    GRL_WSB_LAUNCH(16);
-  else if (Cin == 128)
-    GRL_WSB_LAUNCH(8);
-  else
-    GRL_WSB_LAUNCH(4);
-#undef GRL_WSB_LAUNCH
+  launch_ws<true>(Cin, Cout, v, dim3((unsigned)grid), st, M, gt->num_types, hs, gt, G, ldg, Wf, nullptr, 0, dX, d,
+                  ws_tiles, Gagg, K, eid, self_rows, spin, status);
   GRL_LAUNCH_CHECK();
   return graphconv_status(status, dX, M * Cout, Gagg, M * K, st, WS_WHO_BWD_DATA);
 }

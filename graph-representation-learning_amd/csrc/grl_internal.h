@@ -72,7 +72,7 @@ int spmm_fwd_rows(const GrlTypedCsr* g, int64_t r0, int64_t rows, const float* X
 // Fused one-kernel GraphConv forward (graphconv.hip), used by grl_graphconv_fwd.
 bool graphconv_fused_enabled();
 bool graphconv_fused_shape_ok(int F, int C, int L);
-size_t graphconv_fused_ws_bytes(int64_t K);
+size_t graphconv_fused_ws_bytes(int64_t K, int C);
 int graphconv_fused_fwd(const GrlTypedCsr* g, const float* X, int64_t ldx, int F, const float* W, const float* bias,
                         int C, int relu, float* out, const GrlDropEdge* de, void* ws, hipStream_t st,
                         float* Z = nullptr);

@@ -1302,7 +1302,7 @@ static size_t ws_align(size_t b) { return (b + 255) & ~(size_t)255; }
 
 // grl_graphconv_fwd takes the fused kernel when its arithmetic equals the
 // two-kernel path's (the linear on the x6 GEMM: large graphs, 16-B aligned W,
-// C % 4 == 0), the shapes fit it (F in {64, 128, 256}, C <= 256), X rows are
+// C % 4 == 0), the shapes fit it (F in {64, 128, 256, 512, 1024}, C <= 512), X rows are
 // float4-aligned and no heavy row is split (the split path sums chunk
 // partials, a different order).
 static bool fused_path(const GrlTypedCsr* g, const float* X, int64_t ldx, int F, const float* W, int C) {
@@ -1316,7 +1316,7 @@ extern "C" size_t grl_graphconv_fwd_workspace_query(const GrlTypedCsr* g, const 
   if (!g || g->num_rows <= 0 || g->num_types < 1 || F <= 0 || C <= 0) return 0;
   const int64_t K = (int64_t)(g->num_types + (g->has_self ? 1 : 0)) * F;
   if (K > 2147483647LL) return 0;
-  if (fused_path(g, X, ldx, F, W, C)) return graphconv_fused_ws_bytes(K);
+  if (fused_path(g, X, ldx, F, W, C)) return graphconv_fused_ws_bytes(K, C);
   return grl_graphconv_fwd_workspace_size(g->num_rows, g->num_types, g->has_self, F, C);
 }
 
@@ -1347,7 +1347,7 @@ extern "C" int grl_graphconv_fwd(const GrlTypedCsr* g, const float* X, int64_t l
   char* ws = static_cast<char*>(workspace);
   GRL_CHECK_ARG(ws == nullptr || al16(ws), "grl_graphconv_fwd: workspace must be 16-B aligned");
   const size_t zfull = ws_align((size_t)M * (size_t)K * 4);
-  if (fused_path(g, X, ldx, F, W, C) && ws && workspace_bytes >= graphconv_fused_ws_bytes(K)) {
+  if (fused_path(g, X, ldx, F, W, C) && ws && workspace_bytes >= graphconv_fused_ws_bytes(K, C)) {
     // one kernel: Z never leaves the CU (graphconv.hip)
     GRL_CHECK_ARG(g->nnz < 2147483647LL, "grl_graphconv_fwd: nnz %lld exceeds int32", (long long)g->nnz);
     return graphconv_fused_fwd(g, X, ldx, F, W, bias, C, relu, out, de, ws, st);
@@ -1401,7 +1401,7 @@ extern "C" int grl_graphconv_fwd(const GrlTypedCsr* g, const float* X, int64_t l
 // The data gradient of one GraphConv layer by reassociation (see grl.h):
 // dX = sum_s (A_drop,s^T G) W_s^T on the one-kernel GraphConv over the typed
 // transpose.  Eligible when the forward's x6 GEMM shape would be (large
-// graphs), C in {64, 128, 256}, F <= 256, L <= 7, G rows float4-aligned and no
+// graphs), C in {64, 128, 256, 512, 1024}, F <= 512, L <= 7, G rows float4-aligned and no
 // heavy-row split plan on the transpose.
 static bool bwd_data_path(const GrlTypedCsr* gt, const float* G, int64_t ldg, int C, const float* W, int F) {
   const int64_t K = (int64_t)(gt->num_types + (gt->has_self ? 1 : 0)) * C;
@@ -1414,7 +1414,7 @@ extern "C" size_t grl_graphconv_bwd_data_workspace_query(const GrlTypedCsr* gt, 
                                                         const float* W, int32_t F) {
   if (!gt || gt->num_rows <= 0 || gt->num_types < 1 || C <= 0 || F <= 0) return 0;
   if (!bwd_data_path(gt, G, ldg, C, W, F)) return 0;
-  return graphconv_fused_ws_bytes((int64_t)(gt->num_types + (gt->has_self ? 1 : 0)) * C);
+  return graphconv_fused_ws_bytes((int64_t)(gt->num_types + (gt->has_self ? 1 : 0)) * C, F);
 }
 
 extern "C" int grl_graphconv_bwd_data(const GrlTypedCsr* gt, const int32_t* eid, const float* G, int64_t ldg,
@@ -1433,7 +1433,7 @@ extern "C" int grl_graphconv_bwd_data(const GrlTypedCsr* gt, const int32_t* eid,
   if (!bwd_data_path(gt, G, ldg, C, W, F))
     GRL_FAIL(GRL_E_UNSUPPORTED, "grl_graphconv_bwd_data: shape outside the one-kernel path (C %d, F %d, L %d, rows "
              "%lld; see grl_graphconv_bwd_data_workspace_query)", C, F, gt->num_types, (long long)gt->num_rows);
-  const size_t need = graphconv_fused_ws_bytes((int64_t)(gt->num_types + (gt->has_self ? 1 : 0)) * C);
+  const size_t need = graphconv_fused_ws_bytes((int64_t)(gt->num_types + (gt->has_self ? 1 : 0)) * C, F);
   if (!workspace || !al16(workspace) || workspace_bytes < need)
     GRL_FAIL(GRL_E_WORKSPACE, "grl_graphconv_bwd_data: workspace %zu < %zu (16-B aligned)", workspace_bytes, need);
   return graphconv_fused_bwd_data(gt, eid, G, ldg, g_rows, C, W, F, dX, G_agg, de, workspace, as_stream(stream));
@@ -1457,7 +1457,7 @@ extern "C" int grl_graphconv_fwd_train(const GrlTypedCsr* g, const float* X, int
   const int32_t K = (int32_t)K64;
   char* ws = static_cast<char*>(workspace);
   GRL_CHECK_ARG(ws == nullptr || al16(ws), "grl_graphconv_fwd_train: workspace must be 16-B aligned");
-  if (fused_path(g, X, ldx, F, W, C) && al16(Z) && ws && workspace_bytes >= graphconv_fused_ws_bytes(K)) {
+  if (fused_path(g, X, ldx, F, W, C) && al16(Z) && ws && workspace_bytes >= graphconv_fused_ws_bytes(K, C)) {
     GRL_CHECK_ARG(g->nnz < 2147483647LL, "grl_graphconv_fwd_train: nnz %lld exceeds int32", (long long)g->nnz);
     return graphconv_fused_fwd(g, X, ldx, F, W, bias, C, relu, out, de, ws, as_stream(stream), Z);
   }

@@ -275,8 +275,8 @@ class _GraphLinear(torch.autograd.Function):
 # forward's F, or the data gradient's C) and the largest output width of one
 # call (the forward's C, or the data gradient's F; wider dX runs in column
 # blocks).
-FUSED_WIDTHS = (64, 128, 256)
-FUSED_MAX_OUT = 256
+FUSED_WIDTHS = (64, 128, 256, 512, 1024)
+FUSED_MAX_OUT = 512
 
 
 def _bwd_data_enabled() -> bool:
@@ -288,9 +288,9 @@ def graph_conv_bwd_data(g: torch.Tensor, graph: TypedGraph, W: torch.Tensor, F: 
     """dX of one GraphConv layer in one kernel (grl_graphconv_bwd_data):
     dX = sum_s (A_drop,s^T g) W_s^T over the graph's typed transpose, for g
     the output gradient ([num_rows, C]; through the ReLU's [relu_out > 0]
-    when relu_out is given).  F > 256 (gcn3's 2C-wide input) runs one call per
-    <= 256-column block of dX (the gather repeats per block; dZ still never
-    exists).  None when the shape is outside the one-kernel path (the caller
+    when relu_out is given).  F > 512 (gcn3's 2C-wide input at C = 512) runs
+    one call per <= 512-column block of dX (the gather repeats per block; dZ
+    still never exists).  None when the shape is outside the one-kernel path (the caller
     then runs dZ = g W^T and the CSC gather).  GRL_GRAPHCONV_FUSED_BWD=0
     disables it.  want_aggregate: return (dX, G_agg, g_eff) with G_agg =
     [A_drop,s^T g_eff]_s ([num_cols, segments * C], written by the same
@@ -299,11 +299,11 @@ def graph_conv_bwd_data(g: torch.Tensor, graph: TypedGraph, W: torch.Tensor, F: 
         return None
     M, C = g.shape
     L, S = graph.num_types, graph.segments
-    nblk = -(-F // 256)
+    nblk = -(-F // FUSED_MAX_OUT)
     wblk = (-(-F // nblk) + 3) // 4 * 4 if nblk > 1 else F  # block width, a multiple of 4
     bounds = [(f0, min(F, f0 + wblk)) for f0 in range(0, F, wblk)]
     # cheap pre-checks before the (cached, once per graph) transpose build; the library decides
-    if (C not in (64, 128, 256) or F % 4 or F > 1024 or L > 7 or graph.num_cols < graph.num_rows
+    if (C not in FUSED_WIDTHS or F % 4 or F > 2 * FUSED_MAX_OUT or L > 7 or graph.num_cols < graph.num_rows
             or graph.self_rows != graph.num_rows or M != graph.num_rows
             or 2.0 * graph.num_cols * S * C * min(b - a for a, b in bounds) < 1.6e10
             or g.dtype != torch.float32 or not g.is_contiguous() or W.dtype != torch.float32

@@ -38,3 +38,23 @@ def test_spawned_ranks_fail_loudly_without_a_gpu():
 def test_gpus_must_be_positive():
     r = _bench(["--gpus", "0"])
     assert r.returncode != 0 and "--gpus must be >= 1" in r.stderr
+
+
+def test_pmc_traffic_is_keyed_by_workload_world_and_kernel():
+    """roofline.traffic comes only from a PMC record of the same workload, at
+    the same world size, on the same kernel family: the C3 one-GPU record is
+    found; a C4 shard (n_loc = 1M at P = 4, the shape that used to collide
+    with C3's key) and every N > 1 line get None (printed as traffic: null)."""
+    import argparse
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    a = argparse.Namespace(graph="er", avg_deg=32.0, types=6, dim=256, p=0.0)
+    one = "spmm_kernel<4,1,8,false,false> (grl_typed_spmm_fwd)"
+    shard = "spmm_kernel / spmm_pair_kernel (grl_typed_spmm_fwd_slice, 2 slices of 128 columns)"
+    assert bench.load_traffic(a, "C3", 1_000_000, 1, one) > 3e10
+    assert bench.load_traffic(a, "C4", 1_000_000, 4, shard) is None
+    assert bench.load_traffic(a, "C4", 2_000_000, 2, shard) is None
+    assert bench.load_traffic(a, "C3", 1_000_000, 1, "gemm_x6_kernel") is None  # another kernel's bytes: never

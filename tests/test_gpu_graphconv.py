@@ -145,7 +145,13 @@ def _ws_query(X, g, W, C):
 @pytest.mark.parametrize("N,L,F,C,has_self,deg", [(20_011, 6, 256, 256, True, 16.0), (50_000, 6, 256, 96, True, 9.0),
                                                   (40_007, 6, 128, 256, True, 16.0), (70_001, 6, 64, 256, True, 12.0),
                                                   (60_001, 3, 256, 200, False, 20.0), (20_000, 6, 256, 256, True, 120.0),
-                                                  (18_001, 7, 256, 256, True, 14.0)])
+                                                  (18_001, 7, 256, 256, True, 14.0),
+                                                  # wide: F = 512 / 1024 as 256-column virtual segments (gcn3's
+                                                  # 2C input, C5's d = 512), C > 256 on 4 gather + 8 MFMA waves
+                                                  (20_011, 6, 512, 256, True, 10.0), (20_011, 6, 512, 512, True, 10.0),
+                                                  (24_001, 6, 256, 512, True, 12.0), (10_007, 6, 1024, 512, True, 8.0),
+                                                  (30_001, 6, 128, 384, True, 12.0), (20_000, 6, 256, 512, True, 120.0),
+                                                  (18_001, 7, 512, 500, True, 14.0), (40_003, 3, 512, 260, False, 9.0)])
 @pytest.mark.parametrize("variant", ["plain", "drop_bias_relu", "drop_spare_self", "strided_relu"])
 @pytest.mark.parametrize("kernel", ["ws", "phases"])
 def test_fused_graphconv_bitwise_equals_two_kernels(N, L, F, C, has_self, deg, variant, kernel, monkeypatch):
@@ -172,7 +178,7 @@ def test_fused_graphconv_bitwise_equals_two_kernels(N, L, F, C, has_self, deg, v
     if deg > 64:  # no heavy-row split plan on this graph: the fused path applies
         assert g.split_stats()["csr"]["heavy_segments"] == 0
     ws = _ws_query(X, g, W, C)
-    assert ws < 3 * 256 * K * 2 + 4096 < N * K * 4, ws  # W planes only: the fused path
+    assert ws < 3 * (256 if C <= 256 else 512) * K * 2 + 4096 < N * K * 4, ws  # W planes only: the fused path
     out = graph_conv_infer(X, g, W, b, relu)
     ref = _two_op(X, g, W, b, relu)
     assert torch.equal(out, ref)
@@ -238,10 +244,35 @@ def test_training_forward_one_kernel_same_bits(de, recompute, monkeypatch):
         assert torch.equal(a, c)
 
 
+@pytest.mark.parametrize("F,C", [(512, 256), (512, 512), (256, 512), (1024, 512)])
+@pytest.mark.parametrize("de", [None, DropEdge(0.3, 4, 2, True)])
+def test_wide_training_forward_one_kernel_same_bits(F, C, de):
+    """The training forward at gcn3's F = 2C and at d = 512 (C5): the one
+    kernel (256-column virtual segments; 8 MFMA waves for C > 256) writes
+    out and Z bitwise those of the two-kernel path, and the layer's
+    gradients through graph_conv equal the chain's (dX within fp32 rounding
+    of the one-kernel reassociation, dW / db bitwise)."""
+    from grl.ops import graph_conv_fwd_train, spmm_forward
+
+    N, L = (12_007 if F == 1024 else 20_011), 6
+    g = TypedGraph.synthetic(N, 10.0, L, seed=2, device=DEV).with_dropedge(de)
+    gen = torch.Generator(device=DEV).manual_seed(F + C)
+    X = torch.randn(N, F, device=DEV, generator=gen)
+    W = torch.randn(7 * F, C, device=DEV, generator=gen) / (7 * F) ** 0.5
+    b = torch.randn(C, device=DEV, generator=gen)
+    out, Z = graph_conv_fwd_train(X, g, W, b, True)
+    Zr = spmm_forward(X, g)
+    assert torch.equal(Z, Zr)
+    assert torch.equal(out, linear_fwd(Zr, W, b, True))
+    assert torch.equal(graph_conv_infer(X, g, W, b, True), out)
+
+
 @pytest.mark.parametrize("N,L,F,C,has_self,deg", [(20_011, 6, 256, 256, True, 16.0), (100_003, 6, 96, 128, True, 9.0),
                                                   (80_000, 6, 256, 64, True, 12.0), (60_001, 3, 200, 256, False, 20.0),
                                                   (20_000, 6, 256, 256, True, 120.0), (18_001, 7, 256, 256, True, 14.0),
-                                                  (20_011, 6, 512, 256, True, 10.0), (40_011, 6, 260, 256, True, 8.0)])
+                                                  (20_011, 6, 512, 256, True, 10.0), (40_011, 6, 260, 256, True, 8.0),
+                                                  (20_011, 6, 512, 512, True, 10.0), (20_011, 6, 256, 512, True, 10.0),
+                                                  (10_007, 6, 1024, 512, True, 8.0), (18_001, 7, 384, 512, True, 12.0)])
 @pytest.mark.parametrize("variant", ["plain", "drop_self", "drop_spare_self_vals"])
 def test_bwd_data_one_kernel(N, L, F, C, has_self, deg, variant, monkeypatch):
     """grl_graphconv_bwd_data: dX = sum_s (A_drop,s^T G) W_s^T in one kernel

@@ -28,10 +28,14 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-fPIC", "-std=c++17", "-I" + os.path.j
 KERNELS = [
     ("spmm.hip", "_ZN3grl12_GLOBAL__N_111spmm_kernelILi4ELi1ELi8ELb0ELb0ELb0EE",
      "C3 headline: typed-SpMM forward, whole 1 KiB rows (bench.py roofline.kernel)"),
-    ("graphconv.hip", "_ZN3grl12_GLOBAL__N_119graphconv_ws_kernelILi16ELb0ELb0EE",
+    ("graphconv.hip", "_ZN3grl12_GLOBAL__N_119graphconv_ws_kernelILi16ELb0ELb0ELi1ELi8EEE",
      "one-kernel GraphConv forward at F=256 (inference / training forward)"),
-    ("graphconv.hip", "_ZN3grl12_GLOBAL__N_119graphconv_ws_kernelILi16ELb0ELb1EE",
+    ("graphconv.hip", "_ZN3grl12_GLOBAL__N_119graphconv_ws_kernelILi16ELb0ELb1ELi1ELi8EEE",
      "one-kernel GraphConv data gradient at C=256 (grl_graphconv_bwd_data)"),
+    ("graphconv.hip", "_ZN3grl12_GLOBAL__N_119graphconv_ws_kernelILi16ELb0ELb0ELi2ELi8EEE",
+     "one-kernel GraphConv forward at F=512, C<=256 (gcn3 at d=256: two 256-column virtual segments)"),
+    ("graphconv.hip", "_ZN3grl12_GLOBAL__N_119graphconv_ws_kernelILi16ELb0ELb0ELi2ELi4EEE",
+     "one-kernel GraphConv forward at F=512, C<=512 (C5 shape: 4 gather + 8 MFMA waves)"),
 ]
 
 

@@ -7,7 +7,10 @@ with the gfx950 corrections of MI355X_MICROARCH.md §HBM:
     read: the factor is the one measured on the SpMM itself
     (profiles/r02_pmc_calibration.json, tools/pmc_calib.py: x1.896);
   * WRITE_SIZE is exact for 16 B/lane streaming stores.
-Writes/updates profiles/pmc_traffic.json under the bench workload key.
+Writes/updates profiles/pmc_traffic.json under the bench workload key
+(bench.traffic_key: workload, world size and shard shape, e.g.
+C3_w1_er_n1000000_deg32_L6_d256_p0); bench.load_traffic returns a record
+only for that workload at that world size and the kernel family named in it.
 
   python tools/pmc_traffic.py KEY FETCH_DIR WRITE_DIR [KERNEL_SUBSTR]
 """

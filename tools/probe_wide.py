@@ -1,0 +1,94 @@
+"""Diagnostic: the one-kernel GraphConv at the wide shapes (verdict r3 item
+1) against the two-kernel chain, on an ER graph (avg_deg 32, L = 6) of
+PROBE_NODES nodes (default 1M, the C3 graph):
+  * gcn3 at d = 256: F = 512 (cat[g1, g2]), C = 256 (drop_robust_gcn.py:84-85);
+  * d = 512 (C5's width): F = C = 512, and gcn3 there: F = 1024, C = 512;
+  * d = 256 -> 512 (F = 256, C = 512).
+Per shape: inference (grl_graphconv_fwd) one kernel vs GRL_GRAPHCONV_FUSED=0
+(SpMM writing Z, then the x6 GEMM), training forward (grl_graphconv_fwd_train)
+vs the same chain, the data gradient (grl_graphconv_bwd_data) vs dZ = g W^T
++ CSC gather, and the layer fwd+bwd through graph_conv with each.  Every
+timed pair is checked: forward bitwise, dX within 1e-5 of the chain on |g|,
+|W|.  PROBE_SHAPES="512x256,512x512" selects shapes; PROBE_P the DropEdge
+rate (default 0.3)."""
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "graph-representation-learning_amd"))
+import torch  # noqa: E402
+
+from grl import DropEdge, TypedGraph  # noqa: E402
+from grl.ops import (graph_conv, graph_conv_bwd_data, graph_conv_fwd_train, graph_conv_infer,  # noqa: E402
+                     linear_bwd_data, linear_fwd, spmm_backward, spmm_forward)
+
+
+def timeit(fn, n=5):
+    fn()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(n):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / n
+
+
+def main():
+    N = int(os.environ.get("PROBE_NODES", "1000000"))
+    p = float(os.environ.get("PROBE_P", "0.3"))
+    shapes = [tuple(int(x) for x in sh.split("x")) for sh in
+              os.environ.get("PROBE_SHAPES", "512x256,512x512,256x512,1024x512").split(",")]
+    dev = torch.device("cuda:0")
+    g0 = TypedGraph.synthetic(N, 32.0, 6, seed=0, device=dev)
+    g0.typed_transpose()
+    g = g0.with_dropedge(DropEdge(p, 2, 1, True) if p else None)
+    gen = torch.Generator(device=dev).manual_seed(3)
+    for F, C in shapes:
+        X = torch.randn(N, F, device=dev, generator=gen)
+        W = torch.randn(7 * F, C, device=dev, generator=gen) / (7 * F) ** 0.5
+        b = torch.randn(C, device=dev, generator=gen)
+        G = torch.randn(N, C, device=dev, generator=gen)
+        res = {"F": F, "C": C, "N": N, "p": p}
+        one = graph_conv_infer(X, g, W, b, True)
+        os.environ["GRL_GRAPHCONV_FUSED"] = "0"
+        two = graph_conv_infer(X, g, W, b, True)
+        res["infer_chain_ms"] = timeit(lambda: graph_conv_infer(X, g, W, b, True))
+        os.environ.pop("GRL_GRAPHCONV_FUSED")
+        res["infer_bitwise"] = bool(torch.equal(one, two))
+        del two
+        res["infer_one_kernel_ms"] = timeit(lambda: graph_conv_infer(X, g, W, b, True))
+        res["train_fwd_one_kernel_ms"] = timeit(lambda: graph_conv_fwd_train(X, g, W, b, True))
+        res["train_fwd_chain_ms"] = timeit(lambda: linear_fwd(spmm_forward(X, g), W, b, True))
+        out, Z = graph_conv_fwd_train(X, g, W, b, True)
+        res["train_fwd_bitwise"] = bool(torch.equal(out, one) and torch.equal(Z, spmm_forward(X, g)))
+        del out, Z, one
+        dX = graph_conv_bwd_data(G, g, W, F)
+        res["bwd_data_one_kernel"] = dX is not None
+        if dX is not None:
+            res["bwd_data_one_kernel_ms"] = timeit(lambda: graph_conv_bwd_data(G, g, W, F))
+            ref = spmm_backward(linear_bwd_data(G, None, W), g, F)
+            bound = spmm_backward(linear_bwd_data(G.abs(), None, W.abs()), g, F)
+            res["bwd_data_rel_err"] = float(((dX - ref).abs() / (bound + 1e-30)).max())
+            del ref, bound
+        del dX
+        res["bwd_data_chain_ms"] = timeit(lambda: spmm_backward(linear_bwd_data(G, None, W), g, F))
+        Xp, Wp, bp = (t.clone().requires_grad_(True) for t in (X, W, b))
+
+        def layer():
+            (graph_conv(Xp, g, Wp, bp, relu=True) * G).sum().backward()
+            Xp.grad = Wp.grad = bp.grad = None
+
+        res["layer_fwd_bwd_ms"] = timeit(layer, 3)
+        os.environ["GRL_GRAPHCONV_FUSED"] = "0"
+        os.environ["GRL_GRAPHCONV_FUSED_BWD"] = "0"
+        res["layer_fwd_bwd_chain_ms"] = timeit(layer, 3)
+        os.environ.pop("GRL_GRAPHCONV_FUSED")
+        os.environ.pop("GRL_GRAPHCONV_FUSED_BWD")
+        print(res, flush=True)
+        del X, W, b, G, Xp, Wp, bp
+        torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
