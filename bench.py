@@ -787,7 +787,55 @@ def extras(args, graph, X_full, L, F, dev, E_loc, n_loc):
                         warm=2)}
     finally:
         del os.environ["GRL_GRAPHCONV_FUSED"]
+    del fused, two, Xe, Xl, Wp, bp
+    torch.cuda.empty_cache()
+    res["graphconv_wide_layers"] = wide_layers(graph, dev, max(3, iters // 2))
     return res
+
+
+def wide_layers(graph, dev, iters):
+    """The wide GraphConv shapes next to their chains, on the headline graph
+    with DropEdge p = 0.3 and ReLU (verdict r3 item 1): gcn3 at d = 256 (F =
+    2C = 512 from cat[g1, g2], drop_robust_gcn.py:84-85) and a d = 512 layer
+    (C5's width; gcn1/gcn2 at F = C = 512).  Per shape: inference (one
+    grl_graphconv_fwd call) and the layer fwd+bwd through graph_conv, one
+    kernel vs GRL_GRAPHCONV_FUSED=0 / GRL_GRAPHCONV_FUSED_BWD=0 (SpMM writing
+    Z + x6 GEMM; dZ GEMM + CSC gather); forward bitwise checked."""
+    from grl import DropEdge
+    from grl.ops import graph_conv, graph_conv_infer
+
+    gl = graph.with_dropedge(DropEdge(0.3, 2, 1, True))
+    gen = torch.Generator(device=dev).manual_seed(11)
+    out = {}
+    for name, F, C in (("gcn3_d256_F512_C256", 512, 256), ("d512_F512_C512", 512, 512)):
+        X = torch.randn(graph.num_cols, F, device=dev, generator=gen)
+        W = torch.randn(graph.segments * F, C, device=dev, generator=gen) / (graph.segments * F) ** 0.5
+        b = torch.randn(C, device=dev, generator=gen)
+        gout = torch.randn(graph.num_rows, C, device=dev, generator=gen)
+        Xp, Wp, bp = (t.clone().requires_grad_(True) for t in (X, W, b))
+
+        def layer():
+            Xp.grad = Wp.grad = bp.grad = None
+            graph_conv(Xp, gl, Wp, bp, relu=True).backward(gout)
+
+        r = {}
+        one = graph_conv_infer(X, gl, W, b, True)
+        r["infer_one_kernel_ms"] = _time(lambda: graph_conv_infer(X, gl, W, b, True), iters)
+        r["layer_fwd_bwd_one_kernel_ms"] = _time(layer, iters, warm=2)
+        os.environ["GRL_GRAPHCONV_FUSED"] = "0"
+        os.environ["GRL_GRAPHCONV_FUSED_BWD"] = "0"
+        try:
+            r["infer_bitwise_equal_to_chain"] = bool(torch.equal(graph_conv_infer(X, gl, W, b, True), one))
+            r["infer_chain_ms"] = _time(lambda: graph_conv_infer(X, gl, W, b, True), iters)
+            r["layer_fwd_bwd_chain_ms"] = _time(layer, iters, warm=1)
+        finally:
+            del os.environ["GRL_GRAPHCONV_FUSED"], os.environ["GRL_GRAPHCONV_FUSED_BWD"]
+        r["kernel"] = ("graphconv_ws_kernel: two 256-column virtual segments per segment" +
+                       (", 4 gather + 8 MFMA waves (C = 512)" if C > 256 else ", 8 gather + 4 MFMA waves"))
+        out[name] = r
+        del X, W, b, gout, Xp, Wp, bp, one
+        torch.cuda.empty_cache()
+    return out
 
 
 def c1_extras(dev, iters=20):

@@ -10,7 +10,8 @@ vs the same chain, the data gradient (grl_graphconv_bwd_data) vs dZ = g W^T
 + CSC gather, and the layer fwd+bwd through graph_conv with each.  Every
 timed pair is checked: forward bitwise, dX within 1e-5 of the chain on |g|,
 |W|.  PROBE_SHAPES="512x256,512x512" selects shapes; PROBE_P the DropEdge
-rate (default 0.3)."""
+rate (default 0.3); PROBE_QUICK=1 times only the one-kernel calls (A/B of
+library builds: GRL_LIB_PATH)."""
 import os
 import sys
 
@@ -49,7 +50,12 @@ def main():
         W = torch.randn(7 * F, C, device=dev, generator=gen) / (7 * F) ** 0.5
         b = torch.randn(C, device=dev, generator=gen)
         G = torch.randn(N, C, device=dev, generator=gen)
-        res = {"F": F, "C": C, "N": N, "p": p}
+        res = {"F": F, "C": C, "N": N, "p": p, "lib": os.environ.get("GRL_LIB_PATH", "default")}
+        if os.environ.get("PROBE_QUICK") == "1":
+            res["infer_one_kernel_ms"] = timeit(lambda: graph_conv_infer(X, g, W, b, True), 10)
+            res["bwd_data_one_kernel_ms"] = timeit(lambda: graph_conv_bwd_data(G, g, W, F), 10)
+            print(res, flush=True)
+            continue
         one = graph_conv_infer(X, g, W, b, True)
         os.environ["GRL_GRAPHCONV_FUSED"] = "0"
         two = graph_conv_infer(X, g, W, b, True)
