@@ -45,11 +45,13 @@ def graphconv_backward(V, A_pre, W, Z, dout):
     return dV, dW, db
 
 
-def dense_edge_ids(A_bnln: np.ndarray):
+def dense_edge_ids(A_bnln: np.ndarray, self_base=None):
     """Global DropEdge ids of A_pre's nonzeros, in the engine's id scheme:
     typed edges numbered in CSR order (b, n, t, m ascending); the self loop of
-    global node b*N+n gets E + b*N + n.  Returns (ids_pre, E) where ids_pre has
-    A_pre's shape and is -1 on structural zeros."""
+    global node b*N+n gets self_base + b*N + n, self_base = E by default (a
+    captured training step's static graph starts them at its edge capacity,
+    step_graph.py).  Returns (ids_pre, E) where ids_pre has A_pre's shape and
+    is -1 on structural zeros."""
     B, N, L, _ = A_bnln.shape
     nz = A_bnln != 0
     E = int(nz.sum())
@@ -58,16 +60,17 @@ def dense_edge_ids(A_bnln: np.ndarray):
     ids_pre = np.full((B, N, L + 1, N), -1, dtype=np.int64)
     ids_pre[:, :, 1:, :] = ids
     g = np.arange(B * N, dtype=np.int64).reshape(B, N)
+    sb = E if self_base is None else int(self_base)
     for n in range(N):
-        ids_pre[:, n, 0, n] = E + g[:, n]
+        ids_pre[:, n, 0, n] = sb + g[:, n]
     return ids_pre.reshape(B, N * (L + 1), N), E
 
 
-def dropedge_weights_pre(A_bnln, p, seed, call, drop_self=True):
+def dropedge_weights_pre(A_bnln, p, seed, call, drop_self=True, self_base=None):
     """Multiplier applied to each A_pre entry by the fused DropEdge:
     keep * float(1/(1-p)) (0 for dropped; 1 on the identity when
     drop_self is False)."""
-    ids_pre, _ = dense_edge_ids(A_bnln)
+    ids_pre, _ = dense_edge_ids(A_bnln, self_base)
     active, _, scale = ohash.dropedge_params(p)
     mult = np.zeros(ids_pre.shape, dtype=np.float32)
     valid = ids_pre >= 0

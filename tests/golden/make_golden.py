@@ -322,7 +322,175 @@ def make_model_variant_fixtures(GraphCNNDropEdge):
           f" effF loss {loss.item():.6f}")
 
 
-def main(parts=("text", "graphconv", "model", "layout", "variants")):
+def _procedure_shims():
+    """Logging-only stand-ins the reference's training procedure imports
+    (gnn/trainer/training_procedures/base_procedure.py:4-7,
+    kv_procedure.py:6): neptune (never the real one: gnn/utils/constant.py
+    opens a remote run at import) and tensorboardX."""
+    if "neptune" not in sys.modules:
+        nep = types.ModuleType("neptune")
+        nep.new = types.ModuleType("neptune.new")
+        nep.init_run = nep.new.init_run = lambda *a, **k: None
+        sys.modules["neptune"], sys.modules["neptune.new"] = nep, nep.new
+    def _mod(name, **attrs):
+        if name not in sys.modules:
+            try:
+                __import__(name)
+                return
+            except ImportError:
+                m = types.ModuleType(name)
+                m.__dict__.update(attrs)
+                sys.modules[name] = m
+
+    # config / IO helpers of gnn/data_generator/base_dataloader.py:3-5 (no arithmetic)
+    import yaml
+
+    _mod("anyconfig", load=lambda path, **k: yaml.safe_load(open(path)))
+    _mod("munch", munchify=lambda d: d, Munch=dict)
+
+    class _Compose:
+        def __init__(self, ts):
+            self.ts = ts
+
+        def __call__(self, x):
+            for t in self.ts:
+                x = t(x)
+            return x
+
+    _mod("torchvision")
+    if not hasattr(sys.modules["torchvision"], "transforms"):
+        tv = types.ModuleType("torchvision.transforms")
+        tv.Compose = _Compose
+        sys.modules["torchvision"].transforms = tv
+        sys.modules["torchvision.transforms"] = tv
+    _mod("cv2")
+    if "tensorboardX" not in sys.modules:
+        tb = types.ModuleType("tensorboardX")
+
+        class SummaryWriter:  # no-op
+            def __init__(self, *a, **k):
+                pass
+
+            def __getattr__(self, name):
+                return lambda *a, **k: None
+
+        tb.SummaryWriter = SummaryWriter
+        sys.modules["tensorboardX"] = tb
+
+
+# the procedure fixture: 3 batches of B = 2 pages of N = 40 text lines, a
+# reduced GraphCNNDropEdge(4369, 15, 6, net_size=32) -- feature dropout off,
+# DropEdge p = 0.3 with the engine's hash masks injected -- and the reference's
+# own KVProcedure._run_train_step (kv_procedure.py:143-164: forward, its
+# CrossEntropyLoss wrapper (ignore_index -100), backward, clip_grad_norm_(5.0),
+# Adam built by its BuitlinOptimizer)
+PROC_SEED, PROC_DROPEDGE_SEED, PROC_B, PROC_N, PROC_STEPS = 21, 5, 2, 40, 3
+
+
+def _step_seed(base: int, step: int) -> int:
+    """The per-step DropEdge seed of a captured training step with a fixed
+    dropedge_seed (gnn/trainer/training_procedures/step_graph.py
+    StepGraph._step_seed), restated."""
+    M = (1 << 64) - 1
+    x = (base * 0x9E3779B97F4A7C15 + step) & M
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & M
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & M
+    return (x ^ (x >> 31)) & ((1 << 62) - 1)
+
+
+def make_procedure_fixtures(GraphCNNDropEdge, HeuristicGraphBuilder, TextlineEncoding):
+    _procedure_shims()
+    from gnn.trainer import losses, optimizers
+    from gnn.trainer.training_procedures.kv_procedure import KVProcedure
+
+    with open(os.path.join(REF, "assets/meta_data/master_charset.json"), encoding="utf-8-sig") as f:
+        charset = json.load(f)["charset"]
+    char_to_id = {c: i for i, c in enumerate(charset)}
+    r = gi.rng(PROC_SEED)
+    batches = []
+    for s in range(PROC_STEPS):
+        Vs, As = [], []
+        for d in range(PROC_B):
+            regions = gi.synthetic_document(300 + 10 * s + d, PROC_N)
+            label = {i: {"polygon": reg["location"], "text": reg["text"], "label": "other"}
+                     for i, reg in enumerate(regions)}
+            enc = TextlineEncoding(is_normalized_text=True)({"label": dict(label), "char_to_id": char_to_id})
+            adj = HeuristicGraphBuilder(num_edges=6, edge_type="normal_binary")({"label": dict(label)})
+            Vs.append(enc["textline_encoding"].astype(np.float32))
+            As.append(adj["adjacency_matrix"])
+        y = r.integers(0, 15, size=(PROC_B, PROC_N))
+        y[r.random((PROC_B, PROC_N)) < 0.1] = -100  # padded / unlabelled nodes (NumpyPadding's -100)
+        batches.append((np.stack(Vs), np.stack(As), y))
+    out = {}
+    for s, (V, A, y) in enumerate(batches):
+        nzr = np.nonzero(V)
+        out[f"batch{s}::V_idx"] = np.stack(nzr).astype(np.int32)
+        out[f"batch{s}::V_vals"] = V[nzr]
+        out[f"batch{s}::A_bits"] = np.packbits(A != 0)
+        out[f"batch{s}::labels"] = y
+    out["V_shape"] = np.array(batches[0][0].shape)
+    out["A_shape"] = np.array(batches[0][1].shape)
+    touched = np.unique(np.concatenate([np.nonzero(V.reshape(-1, V.shape[-1]).any(0))[0] for V, _, _ in batches]))
+    out["emb1_touched_cols"] = touched.astype(np.int32)
+    de = gi.DROPEDGE
+    for mode in ("eager", "captured"):
+        torch.manual_seed(PROC_SEED)
+        model = GraphCNNDropEdge(4369, 15, 6, net_size=32)
+        if mode == "eager":
+            out.update({f"init::{k}": v.detach().clone().numpy() for k, v in model.state_dict().items()
+                        if k != "emb1.0.weight"})
+            out["init::emb1.0.weight::touched"] = model.emb1[0].weight.detach()[:, touched].clone().numpy()
+            out["init_sha256"] = np.array([hashlib.sha256(v.detach().contiguous().numpy().tobytes()).hexdigest()
+                                           for v in model.state_dict().values()])
+        model.dropout.p = 0.0
+        masks = []
+        for s, (V, A, y) in enumerate(batches):
+            A32 = A.astype(np.float32)
+            if mode == "eager":  # the model's EdgeDropout(seed): calls 0, 1, 2, 3, ... across steps
+                masks += [dense_ref.dropedge_weights_pre(A32, de["p"], PROC_DROPEDGE_SEED, 3 * s + c) for c in range(3)]
+            else:  # StepGraph: a per-step seed, calls 0, 1, 2; self loops from the static graph's capacity B N L N
+                cap = PROC_B * PROC_N * 6 * PROC_N
+                masks += [dense_ref.dropedge_weights_pre(A32, de["p"], _step_seed(PROC_DROPEDGE_SEED, s), c,
+                                                         self_base=cap) for c in range(3)]
+
+        class InjectedEdgeDropout(torch.nn.Module):
+            def __init__(self, ms):
+                super().__init__()
+                self.ms, self.i = ms, 0
+
+            def forward(self, a):
+                m = self.ms[self.i]
+                self.i += 1
+                keep = _t((m != 0).astype(np.float32))
+                scale = float(m.max()) if (m != 0).any() else 1.0
+                return a.mul(keep).mul_(scale)
+
+        model.edge_dropout = InjectedEdgeDropout(masks)
+        proc = object.__new__(KVProcedure)  # the reference's step methods on a minimal procedure state
+        proc.model, proc.device = model, torch.device("cpu")
+        proc.criterion = getattr(losses, "CrossEntropyLoss")._from_config({})
+        proc.optimizer = getattr(optimizers, "BuitlinOptimizer")._from_config(
+            {"type_optimizer": "Adam", "lr": 0.001}).get_optimizer(model.parameters())
+        proc.activator = torch.nn.Softmax(dim=2)
+        proc.class_names = tuple(["other"] + [f"c{i}" for i in range(14)])
+        proc.config = types.SimpleNamespace(max_grad_norm=5.0, data_config=types.SimpleNamespace(
+            dataset=types.SimpleNamespace(args=types.SimpleNamespace(node_label_padding_value=-100,
+                                                                     other_class_index=None))))
+        losses_ = []
+        for V, A, y in batches:
+            batch = {"textline_encoding": _t(V), "adjacency_matrix": _t(A), "node_label": torch.from_numpy(y)}
+            scores, _ = KVProcedure._run_train_step(proc, batch)
+            losses_.append(scores["loss"])
+        out[f"{mode}::losses"] = np.array(losses_)
+        sd = model.state_dict()
+        out.update({f"{mode}::final::{k}": v.detach().clone().numpy() for k, v in sd.items()
+                    if k != "emb1.0.weight"})
+        out[f"{mode}::final::emb1.0.weight::touched"] = sd["emb1.0.weight"][:, touched].clone().numpy()
+        print(f"procedure {mode}: losses {losses_}")
+    np.savez_compressed(os.path.join(HERE, "procedure_train.npz"), **out)
+
+
+def main(parts=("text", "graphconv", "model", "layout", "variants", "procedure")):
     GraphConv, GraphCNNDropEdge, HGB, TLE = _import_reference()
     if "text" in parts:
         make_text_fixtures()
@@ -334,7 +502,9 @@ def main(parts=("text", "graphconv", "model", "layout", "variants")):
         make_layout_fixtures(HGB, TLE)
     if "variants" in parts:
         make_model_variant_fixtures(GraphCNNDropEdge)
+    if "procedure" in parts:
+        make_procedure_fixtures(GraphCNNDropEdge, HGB, TLE)
 
 
 if __name__ == "__main__":
-    main(tuple(sys.argv[1:]) or ("text", "graphconv", "model", "layout", "variants"))
+    main(tuple(sys.argv[1:]) or ("text", "graphconv", "model", "layout", "variants", "procedure"))
