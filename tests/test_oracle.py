@@ -228,3 +228,30 @@ def test_oracle_model_efficient_mode_false(golden):
     mults = [dense_ref.dropedge_weights_pre(g["effF::A"], de["p"], de["seed"], c, drop_self=False) for c in range(3)]
     logits = dense_ref.graph_cnn_dropedge_forward(P, g["V"], g["effF::A"], edge_mults=mults)
     _close(logits, g["effF::logits"], 1e-5)
+
+
+def test_oracle_model_matches_reference_procedure_first_loss(golden):
+    """procedure_train.npz (the reference KVProcedure's three steps): the
+    float64 oracle model, from the fixture's initial weights with the eager
+    step's injected DropEdge masks, gives the reference's first-step loss
+    (CrossEntropyLoss over the non-ignored nodes, kv_procedure.py:127 /
+    cross_entropy_loss.py:23-35) -- the fixture's batches, masks and init are
+    consistent with the restated model."""
+    g = golden("procedure_train.npz")
+    touched = g["emb1_touched_cols"]
+    P = {k[len("init::"):]: g[k].astype(np.float64) for k in g.keys() if k.startswith("init::") and "emb1.0.weight" not in k}
+    Vs, As = tuple(g["V_shape"]), tuple(g["A_shape"])
+    W1 = np.zeros((P["emb1.0.bias"].shape[0], Vs[-1]))
+    W1[:, touched] = g["init::emb1.0.weight::touched"]
+    P["emb1.0.weight"] = W1  # V is zero on every other column
+    V = np.zeros(Vs, dtype=np.float32)
+    V[tuple(g["batch0::V_idx"])] = g["batch0::V_vals"]
+    A = np.unpackbits(g["batch0::A_bits"])[: int(np.prod(As))].reshape(As).astype(np.float32)
+    y = g["batch0::labels"]
+    mults = [dense_ref.dropedge_weights_pre(A, 0.3, 5, c) for c in range(3)]
+    logits = dense_ref.graph_cnn_dropedge_forward(P, V, A, edge_mults=mults)
+    keep = y != -100
+    z = logits[keep]
+    lse = np.log(np.exp(z - z.max(-1, keepdims=True)).sum(-1)) + z.max(-1)
+    loss = float((lse - z[np.arange(len(z)), y[keep]]).mean())
+    assert abs(loss - float(g["eager::losses"][0])) <= 1e-5 * abs(loss), (loss, g["eager::losses"][0])
