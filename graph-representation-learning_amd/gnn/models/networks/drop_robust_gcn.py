@@ -22,6 +22,7 @@ from torch.nn import functional as F
 from gnn.models.base_network import BaseNetwork
 from gnn.models.networks.robust_gcn import GraphConv, NodeSelfAtten, make_linear_relu
 from grl import DropEdge, TypedGraph
+from grl.dist import ShardedGraph
 from grl.ops import bag_linear
 
 RP_FACTOR = 10
@@ -78,7 +79,7 @@ class EdgeDropout(nn.Dropout):
         self._calls = 0
 
     def forward(self, A, drop_self: bool = True):
-        if not isinstance(A, TypedGraph):
+        if not isinstance(A, (TypedGraph, ShardedGraph)):
             return super().forward(A)
         if not self.training or self.p == 0.0:
             return A.with_dropedge(None)
@@ -89,6 +90,8 @@ class EdgeDropout(nn.Dropout):
                                             seed_tensor=self.seed_source))
         if self.seed is None:
             seed_t = torch.randint(0, 2**62, (1,), dtype=torch.int64, device=A.device)
+            if isinstance(A, ShardedGraph):  # one draw for the whole graph: rank 0's seed on every rank
+                seed_t = A.broadcast_seed(seed_t)
             return A.with_dropedge(DropEdge(p=float(self.p), seed=0, call=self.stream, drop_self=drop_self,
                                             seed_tensor=seed_t))
         else:
@@ -126,8 +129,13 @@ class GraphCNNDropEdge(BaseNetwork):
         self.classifier = nn.Linear(rp_size, output_dim)
 
     def to_graph(self, A) -> TypedGraph:
-        """Collate-layout dense A (B, N, L, N) -> TypedGraph on the model's device."""
-        if isinstance(A, TypedGraph):
+        """Collate-layout dense A (B, N, L, N) -> TypedGraph on the model's
+        device.  A grl.dist.ShardedGraph (additive: this rank's node-range
+        shard of one large graph, V holding the shard's rows) is used as is:
+        every layer then runs on the shard -- GraphConv with its halo
+        exchange, NodeSelfAtten with the softmax over all nodes -- and the
+        logits are the shard's rows of the one-GPU model's."""
+        if isinstance(A, (TypedGraph, ShardedGraph)):
             return A
         dev = self.gcn1.h_weights.device
         return TypedGraph.from_dense(A if A.device == dev else A.to(dev), layout="bnln")
@@ -151,6 +159,6 @@ class GraphCNNDropEdge(BaseNetwork):
         g3 = self.dropout(self.gcn3.propagate(torch.cat([g1, g2], dim=-1), self.edge_dropout(graph, ds), relu=True))
         new_v = self.emb2(torch.cat([g1, g3], dim=-1))
         if self.use_attention:
-            new_v = self.self_atten(new_v)
+            new_v = self.self_atten(new_v, shard=graph) if isinstance(graph, ShardedGraph) else self.self_atten(new_v)
         new_v = self.dropout(F.relu(self.w_rand(new_v)))
         return self.classifier(new_v)

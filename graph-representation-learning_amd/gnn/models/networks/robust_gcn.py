@@ -18,6 +18,7 @@ import torch
 from torch import nn
 
 from grl import TypedGraph
+from grl.dist import ShardedGraph, sharded_node_attention
 from grl.ops import graph_conv, node_self_attention
 
 
@@ -75,12 +76,22 @@ class GraphConv(nn.Module):
         return TypedGraph.from_dense(self._on_device(A), layout="pre")
 
     # ------------------------------------------------------------- forward
-    def propagate(self, V: torch.Tensor, graph: TypedGraph, relu: bool = False) -> torch.Tensor:
-        """Aggregate + linear (+ fused ReLU) on a ready TypedGraph."""
-        B, N = V.shape[0], V.shape[1]
+    def propagate(self, V: torch.Tensor, graph, relu: bool = False) -> torch.Tensor:
+        """Aggregate + linear (+ fused ReLU) on a ready TypedGraph, or on this
+        rank's node-range shard of a graph (grl.dist.ShardedGraph: V holds the
+        shard's rows; the halo exchange runs inside, the output rows are the
+        shard's, every value the one-GPU layer's -- the forward bitwise)."""
+        lead = V.shape[:-1]
+        if isinstance(graph, ShardedGraph):
+            V2 = V.reshape(-1, V.shape[-1])
+            training = torch.is_grad_enabled() and any(t is not None and t.requires_grad
+                                                       for t in (V, self.h_weights, self.bias))
+            # training: the one-kernel forms both ways, the reverse halo exchange pipelined over row blocks
+            out = graph.graphconv(V2, self, relu=relu, pipeline="rows" if training else None)
+            return out.view(*lead, self.C)
         # new_V = A_pre V (B*N, (L+1)F) then new_V h_weights + bias, one autograd node
         out = graph_conv(V, graph, self.h_weights, self.bias, relu=relu, recompute=self.recompute_aggregation)
-        return out.view(B, N, self.C)
+        return out.view(*lead, self.C)
 
     def forward(self, V: torch.Tensor, A: AdjLike, preprocess_A: bool = True) -> torch.Tensor:
         """V: (B, N, F).  A: TypedGraph, or dense (B, N, N, L) when
@@ -108,7 +119,12 @@ class NodeSelfAtten(nn.Module):
         self.gamma = nn.Parameter(torch.empty(input_dim))
         nn.init.normal_(self.gamma)
 
-    def forward(self, V: torch.Tensor) -> torch.Tensor:
+    def forward(self, V: torch.Tensor, shard=None) -> torch.Tensor:
+        """shard (additive): the grl.dist.ShardedGraph whose rows V holds --
+        the softmax then runs over every node of the graph
+        (grl.dist.sharded_node_attention)."""
+        if shard is not None:
+            return sharded_node_attention(self.f(V), self.g(V), self.h(V), V, self.gamma, shard)
         return node_self_attention(self.f(V), self.g(V), self.h(V), V, self.gamma)
 
     def __repr__(self) -> str:

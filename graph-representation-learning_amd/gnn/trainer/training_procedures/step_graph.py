@@ -18,9 +18,9 @@ What stays outside the graph, every step (host work, or shapes that change):
     [B*N*L+1], colidx / CSC arrays at a capacity `cap` (a power of two >=
     nnz).
   Kernels walk rowptr / colptr, so entries past nnz are never read; the
-  static graph's self-loop DropEdge ids start at `cap` (any fixed id scheme
-  gives i.i.d. masks; eager steps of this procedure use the same static
-  graph, so they draw the same masks);
+  static graph's self-loop DropEdge ids start at SELF_ID_BASE = 2^31 (any
+  fixed id scheme gives i.i.d. masks; eager steps of this procedure use the
+  same static graph, so they draw the same masks);
   * V and the labels, copied into static tensors;
   * the DropEdge seed of the step, written into a device word every
     EdgeDropout reads at launch (`seed_source`), call ids 0, 1, 2 per step;
@@ -51,6 +51,10 @@ from grl._lib import lib as _grl
 from grl.graph import current_stream_handle
 
 MAX_BUCKETS = 32
+# DropEdge id of row 0's self loop in every static graph: past any edge id (edge ids are CSR positions < 2^31),
+# and the same for a batch whatever its edge capacity, so the dense and the typed-edge form of one batch draw the
+# same masks
+SELF_ID_BASE = 1 << 31
 MAX_ROWS = 1 << 14  # larger batches are not launch-bound: they run the normal eager step
 DENSE_IN_GRAPH_MAX = 1 << 22  # B*N*L*N entries: dense batches up to this build their graph inside the replay
 
@@ -79,7 +83,7 @@ class _Bucket:
                     "eid": torch.zeros(cap, dtype=torch.int32, device=device),
                     "cvals": torch.zeros(cap, device=device) if vals else None}
         self.graph = TypedGraph(self.rowptr, self.colidx, L, vals=self.vals, num_cols=rows, batch_shape=(B, N),
-                                self_id_base=cap)
+                                self_id_base=SELF_ID_BASE)
         # no heavy rows in a bucket (checked on load); the CSC lives in the static buffers.  The arrays are
         # refilled every step and nnz here is the capacity, so no typed transpose may be cached on this graph:
         # static_buffers keeps graph_conv's backward off the one-kernel data gradient (grl.ops)

@@ -716,6 +716,8 @@ class ShardedGraph:
         self._init(rowptr, build_halo_plan(colidx_global, row_begin, row_end, group, mode=halo), num_types, vals,
                    group)
 
+    dropedge: Optional[DropEdge] = None  # the edge_dropout draw this view carries (with_dropedge)
+
     def _init(self, rowptr, plan: HaloPlan, num_types: int, vals, group):
         self.group, self.plan = group, plan
         p = plan
@@ -788,6 +790,52 @@ class ShardedGraph:
     @property
     def halo_rows(self) -> int:
         return self.plan.n_halo
+
+    @property
+    def device(self) -> torch.device:
+        return self.graph.device
+
+    def with_dropedge(self, de: Optional[DropEdge]) -> "ShardedGraph":
+        """Shallow copy carrying a DropEdge draw (shares the plan, the local
+        graph and its caches): the sharded counterpart of
+        TypedGraph.with_dropedge, i.e. the reference's edge_dropout(A).  The
+        draw's edge ids are global, so every rank masks its edges exactly as
+        the one-GPU graph would."""
+        sg = ShardedGraph.__new__(ShardedGraph)
+        sg.__dict__.update(self.__dict__)
+        sg.dropedge = de
+        return sg
+
+    def gather_rows(self, X_loc: torch.Tensor) -> torch.Tensor:
+        """Every rank's rows of a node-range-sharded [n_loc, d] tensor, in
+        global node order ([N, d]): one all-gather of shards padded to the
+        largest one (no autograd)."""
+        p = self.plan
+        world = len(p.bounds) - 1
+        if world == 1 or not (dist.is_available() and dist.is_initialized()):
+            return X_loc
+        stride = max(p.bounds[q + 1] - p.bounds[q] for q in range(world))
+        X_loc = X_loc.reshape(-1, X_loc.shape[-1])
+        pad = X_loc.new_zeros(stride, X_loc.shape[1])
+        pad[: X_loc.shape[0]] = X_loc
+        out = X_loc.new_empty(world * stride, X_loc.shape[1])
+        all_gather_into(out, pad, self.group)
+        return torch.cat([out[q * stride: q * stride + p.bounds[q + 1] - p.bounds[q]] for q in range(world)])
+
+    def broadcast_seed(self, seed_t: torch.Tensor) -> torch.Tensor:
+        """Rank 0's value of a 1-element device tensor on every rank of the
+        shard's group (a device-drawn DropEdge seed: the masks of a sharded
+        graph must be the one-GPU graph's on every rank)."""
+        if _world(self.group) == 1:
+            return seed_t
+        src = dist.get_global_rank(self.group, 0) if self.group is not None else 0
+        if _host_staged(self.group):
+            h = seed_t.cpu()
+            dist.broadcast(h, src, group=self.group)
+            seed_t.copy_(h)
+        else:
+            dist.broadcast(seed_t, src, group=self.group)
+        return seed_t
 
     def exchange(self, X_loc: torch.Tensor) -> torch.Tensor:
         return halo_exchange(X_loc, self.plan, self.group)
@@ -899,6 +947,8 @@ class ShardedGraph:
         in the exchange's backward.  pipeline="rows": the one-kernel forms in
         both directions with the reverse exchange pipelined over row blocks
         (_RowPipelinedGraphConv); out and dX bitwise the unpipelined layer's."""
+        if dropedge is None:
+            dropedge = self.dropedge
         if pipeline == "rows":
             return _RowPipelinedGraphConv.apply(X_loc, self, layer.h_weights, layer.bias, relu, dropedge)
         if pipeline is not None:
@@ -908,3 +958,52 @@ class ShardedGraph:
                               relu=relu)
         Z = self.aggregate(X_loc, dropedge, chunks)
         return graph_linear(Z, layer.h_weights, layer.bias, relu=relu)
+
+
+class _ShardedNodeAttention(torch.autograd.Function):
+    """NodeSelfAtten (robust_gcn.py:78-99) over a node-range-sharded graph:
+    out_loc = gamma * softmax(Q K^T) H + V for this rank's rows, the softmax
+    over EVERY node.  The rows of Q, K, H, V are all-gathered (RCCL) and each
+    rank runs the fused attention kernels over the whole graph -- the
+    kernels are deterministic, so every rank computes the same bits as the
+    one-GPU model -- and keeps its rows; the backward all-gathers the output
+    gradient, reruns the fused backward and keeps its rows of dQ, dK, dH
+    (complete: every query's contribution is in them), dgamma from its own
+    rows only (allreduce_gradients adds the ranks' partials, as for every
+    other weight).  The attention's O(N^2) work is replicated, not sharded:
+    the GraphConv layers are what this path distributes."""
+
+    @staticmethod
+    def forward(ctx, Q, K, H, V, gamma, sg):
+        from .ops import node_attention_forward
+
+        p = sg.plan
+        shape = V.shape
+        Qg, Kg, Hg, Vg = (sg.gather_rows(t.detach().reshape(-1, t.shape[-1]).contiguous()) for t in (Q, K, H, V))
+        out, onorm, rmax, rsum = node_attention_forward(Qg[None], Kg[None], Hg[None], Vg[None], gamma, stats=True)
+        rb = p.row_begin if len(p.bounds) > 2 else 0
+        ctx.rows = (rb, rb + p.n_loc)
+        ctx.shapes = (Q.shape, K.shape, H.shape)
+        ctx.sg = sg
+        ctx.save_for_backward(Qg, Kg, Hg, gamma, onorm, rmax, rsum)
+        return out[0, rb: rb + p.n_loc].reshape(shape)
+
+    @staticmethod
+    def backward(ctx, dout):
+        from .ops import node_attention_backward
+
+        Qg, Kg, Hg, gamma, onorm, rmax, rsum = ctx.saved_tensors
+        r0, r1 = ctx.rows
+        d_loc = dout.reshape(-1, dout.shape[-1]).contiguous().float()
+        dg = ctx.sg.gather_rows(d_loc)
+        dQ, dK, dH = node_attention_backward(Qg[None], Kg[None], Hg[None], gamma, onorm, rmax, rsum, dg[None])
+        dgamma = (d_loc * onorm[0, r0:r1]).sum(0)
+        qs, ks, hs = ctx.shapes
+        return (dQ[0, r0:r1].reshape(qs), dK[0, r0:r1].reshape(ks), dH[0, r0:r1].reshape(hs), dout, dgamma, None)
+
+
+def sharded_node_attention(Q: torch.Tensor, K: torch.Tensor, H: torch.Tensor, V: torch.Tensor, gamma: torch.Tensor,
+                           sg: "ShardedGraph") -> torch.Tensor:
+    """gamma * softmax_rows(Q K^T) H + V for this rank's rows of a sharded
+    graph, the softmax over all nodes (_ShardedNodeAttention)."""
+    return _ShardedNodeAttention.apply(Q, K, H, V, gamma, sg)

@@ -664,6 +664,33 @@ def node_attention_forward(Q, K, H, V, gamma, stats: bool = False):
     return (out, onorm, rmax, rsum) if stats else out
 
 
+def node_attention_backward(Q, K, H, gamma, onorm, rmax, rsum, dout):
+    """(dQ, dK, dH) of out = gamma * softmax(Q K^T) H + V for the output
+    gradient dout, from the forward's stats (grl_node_attention_bwd)."""
+    dout = dout.contiguous().float()
+    B, N, dk = Q.shape
+    dv = H.shape[2]
+    dO = dout * gamma
+    dQ = dK = None
+    dHs = []
+    for a, b in _dv_blocks(dk, dv):  # one block unless dv exceeds a call's width
+        dO_b = dO[..., a:b].contiguous()
+        D = (dO_b * onorm[..., a:b]).sum(-1).contiguous()
+        dQ_b, dK_b = torch.empty_like(Q), torch.empty_like(K)
+        dH_b = torch.empty(B, N, b - a, dtype=H.dtype, device=H.device)
+        H_b = H[..., a:b].contiguous()
+        ws, ws_bytes = _attn_workspace(B, N, dk, b - a, Q.device, backward=True)
+        call("grl_node_attention_bwd", Q.data_ptr(), K.data_ptr(), H_b.data_ptr(), dO_b.data_ptr(),
+             rmax.data_ptr(), rsum.data_ptr(), D.data_ptr(), dQ_b.data_ptr(), dK_b.data_ptr(), dH_b.data_ptr(),
+             B, N, dk, b - a, ws.data_ptr() if ws is not None else None, ws_bytes,
+             current_stream_handle(Q.device))
+        dQ = dQ_b if dQ is None else dQ + dQ_b
+        dK = dK_b if dK is None else dK + dK_b
+        dHs.append(dH_b)
+    dH = dHs[0] if len(dHs) == 1 else torch.cat(dHs, -1)
+    return dQ, dK, dH
+
+
 class _NodeAttention(torch.autograd.Function):
     @staticmethod
     def forward(ctx, Q, K, H, V, gamma):
@@ -675,26 +702,7 @@ class _NodeAttention(torch.autograd.Function):
     def backward(ctx, dout):
         Q, K, H, gamma, onorm, rmax, rsum = ctx.saved_tensors
         dout = dout.contiguous().float()
-        B, N, dk = Q.shape
-        dv = H.shape[2]
-        dO = dout * gamma
-        dQ = dK = None
-        dHs = []
-        for a, b in _dv_blocks(dk, dv):  # one block unless dv exceeds a call's width
-            dO_b = dO[..., a:b].contiguous()
-            D = (dO_b * onorm[..., a:b]).sum(-1).contiguous()
-            dQ_b, dK_b = torch.empty_like(Q), torch.empty_like(K)
-            dH_b = torch.empty(B, N, b - a, dtype=H.dtype, device=H.device)
-            H_b = H[..., a:b].contiguous()
-            ws, ws_bytes = _attn_workspace(B, N, dk, b - a, Q.device, backward=True)
-            call("grl_node_attention_bwd", Q.data_ptr(), K.data_ptr(), H_b.data_ptr(), dO_b.data_ptr(),
-                 rmax.data_ptr(), rsum.data_ptr(), D.data_ptr(), dQ_b.data_ptr(), dK_b.data_ptr(), dH_b.data_ptr(),
-                 B, N, dk, b - a, ws.data_ptr() if ws is not None else None, ws_bytes,
-                 current_stream_handle(Q.device))
-            dQ = dQ_b if dQ is None else dQ + dQ_b
-            dK = dK_b if dK is None else dK + dK_b
-            dHs.append(dH_b)
-        dH = dHs[0] if len(dHs) == 1 else torch.cat(dHs, -1)
+        dQ, dK, dH = node_attention_backward(Q, K, H, gamma, onorm, rmax, rsum, dout)
         dgamma = (dout * onorm).sum((0, 1))
         return dQ, dK, dH, dout, dgamma
 

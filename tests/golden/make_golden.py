@@ -448,10 +448,9 @@ def make_procedure_fixtures(GraphCNNDropEdge, HeuristicGraphBuilder, TextlineEnc
             A32 = A.astype(np.float32)
             if mode == "eager":  # the model's EdgeDropout(seed): calls 0, 1, 2, 3, ... across steps
                 masks += [dense_ref.dropedge_weights_pre(A32, de["p"], PROC_DROPEDGE_SEED, 3 * s + c) for c in range(3)]
-            else:  # StepGraph: a per-step seed, calls 0, 1, 2; self loops from the static graph's capacity B N L N
-                cap = PROC_B * PROC_N * 6 * PROC_N
+            else:  # StepGraph: a per-step seed, calls 0, 1, 2; static graphs number self loops from 2^31
                 masks += [dense_ref.dropedge_weights_pre(A32, de["p"], _step_seed(PROC_DROPEDGE_SEED, s), c,
-                                                         self_base=cap) for c in range(3)]
+                                                         self_base=1 << 31) for c in range(3)]
 
         class InjectedEdgeDropout(torch.nn.Module):
             def __init__(self, ms):

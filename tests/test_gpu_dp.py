@@ -110,6 +110,7 @@ def test_dp_step_equals_single_process_on_union_batch(tmp_path):
     from test_data_pipeline import make_config
 
     cfg = make_config(str(tmp_path), epochs=1)
+    cfg.capture_train_step = False  # the eager step: the oracle regenerates its (seed, call) masks
     cfg.dist_backend = "gloo"
     mp.spawn(_worker, args=(2, _free_port(), cfg), nprocs=2, join=True)
 
@@ -210,5 +211,6 @@ def test_dp_dropedge_matches_oracle_with_per_rank_masks(tmp_path):
     from test_data_pipeline import make_config
 
     cfg = make_config(str(tmp_path), epochs=1)
+    cfg.capture_train_step = False  # the eager step: the oracle regenerates its (seed, call) masks
     cfg.dist_backend = "gloo"
     mp.spawn(_worker_random, args=(2, _free_port(), cfg), nprocs=2, join=True)
