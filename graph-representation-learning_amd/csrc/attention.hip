@@ -66,6 +66,10 @@ struct AttnArgs {
   float* qslab;  // bwd_kq: dQ partials [B][ceil(N / 128)][N][16], one row block per key workgroup
   int64_t N;
   int dk, dv;
+  // query rows computed: [q0, q1) of the N (forward and dQ: only these
+  // outputs are written; dK / dH: only these queries contribute) -- a node-
+  // range shard's own queries against every key (grl_node_attention_*_rows)
+  int64_t q0, q1;
 };
 
 __device__ __forceinline__ int kappa(int s, int h) { return (s & 3) + 8 * (s >> 2) + 4 * h; }
@@ -154,13 +158,13 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
   const float* Qb = a.Q + b * N * a.dk;
   const float* Kb = a.K + b * N * a.dk;
   const float* Hb = a.H + b * N * a.dv;
-  const int64_t q = (int64_t)blockIdx.x * 128 + wave * 32 + l32;
+  const int64_t q = a.q0 + (int64_t)blockIdx.x * 128 + wave * 32 + l32;
 
   float qr[KS];
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
     const int d = h * KS + s;
-    qr[s] = (q < N && d < a.dk) ? Qb[q * a.dk + d] : 0.0f;
+    qr[s] = (q < a.q1 && d < a.dk) ? Qb[q * a.dk + d] : 0.0f;
   }
   f32x16 o[NT];
 #pragma unroll
@@ -211,7 +215,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(AttnArgs a) {
     __syncthreads();
   }
 
-  if (q < N) {
+  if (q < a.q1) {
     const float inv = 1.0f / l;
     const int64_t base = (b * N + q) * a.dv;
 #pragma unroll
@@ -242,8 +246,8 @@ __global__ __launch_bounds__(256) void attn_bwd_q_kernel(AttnArgs a) {
   const int64_t N = a.N, b = blockIdx.y;
   const float* Kb = a.K + b * N * a.dk;
   const float* Hb = a.H + b * N * a.dv;
-  const int64_t q = (int64_t)blockIdx.x * 128 + wave * 32 + l32;
-  const bool qv = q < N;
+  const int64_t q = a.q0 + (int64_t)blockIdx.x * 128 + wave * 32 + l32;
+  const bool qv = q < a.q1;
 
   float qr[KS];
 #pragma unroll
@@ -350,17 +354,17 @@ __global__ __launch_bounds__(256) void attn_bwd_kv_kernel(AttnArgs a) {
   auto fetch_stats = [&](int64_t q0) {
     if (tid < 32) {
       const int64_t qq = q0 + tid;
-      const bool v = qq < N;
+      const bool v = qq < a.q1;
       pm = v ? a.smax[b * N + qq] : 0.0f;
       pl = v ? 1.0f / a.ssum[b * N + qq] : 0.0f;  // 0 => P = 0 for padded queries
       pd = v ? a.Drow[b * N + qq] : 0.0f;
     }
   };
-  sq.fetch(Qb, 0, N, a.dk, vq, tid);
-  so.fetch(dOb, 0, N, a.dv, vo, tid);
-  fetch_stats(0);
+  sq.fetch(Qb, a.q0, N, a.dk, vq, tid);
+  so.fetch(dOb, a.q0, N, a.dv, vo, tid);
+  fetch_stats(a.q0);
 
-  for (int64_t q0 = 0; q0 < N; q0 += 32) {
+  for (int64_t q0 = a.q0; q0 < a.q1; q0 += 32) {
     sq.store(Qs, tid);
     so.store(Os, tid);
     if (tid < 32) {
@@ -641,7 +645,7 @@ __global__ __launch_bounds__(256) void attn_fwd_x6_kernel(AttnArgs a) {
   const float* Qb = a.Q + b * N * a.dk;
   const float* Kb = a.K + b * N * a.dk;
   const float* Hb = a.H + b * N * a.dv;
-  const int64_t q = (int64_t)blockIdx.x * 128 + wave * 32 + l32;
+  const int64_t q = a.q0 + (int64_t)blockIdx.x * 128 + wave * 32 + l32;
   // key split blockIdx.z covers keys [k_lo, k_hi) (the whole range when unsplit)
   const int64_t k_lo = SPLIT ? (int64_t)blockIdx.z * a.kr : 0, k_hi = SPLIT ? min<int64_t>(N, k_lo + a.kr) : N;
 
@@ -653,7 +657,7 @@ __global__ __launch_bounds__(256) void attn_fwd_x6_kernel(AttnArgs a) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int d = kc * 16 + 8 * h + j;
-      v[j] = (q < N && d < a.dk) ? Qb[q * a.dk + d] * ALOG2E : 0.0f;  // base-2 scores
+      v[j] = (q < a.q1 && d < a.dk) ? Qb[q * a.dk + d] * ALOG2E : 0.0f;  // base-2 scores
     }
     asplit8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]), qp[kc][0], qp[kc][1],
             qp[kc][2]);
@@ -770,7 +774,7 @@ __global__ __launch_bounds__(256) void attn_fwd_x6_kernel(AttnArgs a) {
     if constexpr (!PRE) __syncthreads();
   }
 
-  if (SPLIT && q < N) {  // key split: unnormalised partials, combined by attn_fwd_combine_kernel
+  if (SPLIT && q < a.q1) {  // key split: unnormalised partials, combined by attn_fwd_combine_kernel
     const int64_t rows = (int64_t)gridDim.y * N, row = b * N + q, zs = blockIdx.z;
     float* po = a.part + zs * rows * a.dv + row * a.dv;
 #pragma unroll
@@ -785,7 +789,7 @@ __global__ __launch_bounds__(256) void attn_fwd_x6_kernel(AttnArgs a) {
       pm[zs * rows + row] = m;
       pm[((int64_t)gridDim.z + zs) * rows + row] = l;
     }
-  } else if (q < N) {
+  } else if (q < a.q1) {
     const float inv = 1.0f / l;
     const int64_t base = (b * N + q) * a.dv;
 #pragma unroll
@@ -827,7 +831,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_x6p_kernel(AttnArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, h = lane >> 5;
   const int64_t N = a.N, b = blockIdx.y;
   const float* Qb = a.Q + b * N * a.dk;
-  const int64_t q = (int64_t)blockIdx.x * (32 * NW) + wave * 32 + l32;
+  const int64_t q = a.q0 + (int64_t)blockIdx.x * (32 * NW) + wave * 32 + l32;
   const int64_t k_lo = SPLIT ? (int64_t)blockIdx.z * a.kr : 0, k_hi = SPLIT ? min<int64_t>(N, k_lo + a.kr) : N;
   const int nblk = (int)((k_hi - k_lo + 31) >> 5);
   const bool partial = ((k_hi - k_lo) & 31) != 0;
@@ -839,7 +843,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_x6p_kernel(AttnArgs a) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int d = kc * 16 + 8 * h + j;
-      v[j] = (q < N && d < a.dk) ? Qb[q * a.dk + d] * ALOG2E : 0.0f;  // base-2 scores
+      v[j] = (q < a.q1 && d < a.dk) ? Qb[q * a.dk + d] * ALOG2E : 0.0f;  // base-2 scores
     }
     asplit8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]), qp[kc][0], qp[kc][1],
             qp[kc][2]);
@@ -1041,7 +1045,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_x6p_kernel(AttnArgs a) {
   rescale(alpha);
   pv(Hp_s + (it & 1) * HST, pp);
 
-  if (SPLIT && q < N) {  // key split: unnormalised partials, combined by attn_fwd_combine_kernel
+  if (SPLIT && q < a.q1) {  // key split: unnormalised partials, combined by attn_fwd_combine_kernel
     const int64_t rows = (int64_t)gridDim.y * N, row = b * N + q, zs = blockIdx.z;
     float* po = a.part + zs * rows * a.dv + row * a.dv;
 #pragma unroll
@@ -1056,7 +1060,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_x6p_kernel(AttnArgs a) {
       pm[zs * rows + row] = m;
       pm[((int64_t)gridDim.z + zs) * rows + row] = l;
     }
-  } else if (q < N) {
+  } else if (q < a.q1) {
     const float inv = 1.0f / l;
     const int64_t base = (b * N + q) * a.dv;
 #pragma unroll
@@ -1131,8 +1135,8 @@ __global__ __launch_bounds__(256, 2) void attn_bwd_q_x6_kernel(AttnArgs a) {
   const int64_t N = a.N, b = blockIdx.y;
   const float* Kb = a.K + b * N * a.dk;
   const float* Hb = a.H + b * N * a.dv;
-  const int64_t q = (int64_t)blockIdx.x * 128 + wave * 32 + l32;
-  const bool qv = q < N;
+  const int64_t q = a.q0 + (int64_t)blockIdx.x * 128 + wave * 32 + l32;
+  const bool qv = q < a.q1;
   const int64_t k_lo = SPLIT ? (int64_t)blockIdx.z * a.kr : 0, k_hi = SPLIT ? min<int64_t>(N, k_lo + a.kr) : N;
   abf16x8_t qp[KC][3], dop[FC][3];
   row_planes<KC>(a.Q + (b * N + q) * a.dk, qv, a.dk, h, qp, ALOG2E);  // base-2 scores
@@ -1246,7 +1250,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_kv_x6_kernel(AttnArg
   const float* dOb = a.dO + b * N * a.dv;
   const int64_t key = (int64_t)blockIdx.x * (32 * NW) + wave * 32 + l32;
   const bool kv = key < N;
-  const int64_t q_lo = SPLIT ? (int64_t)blockIdx.z * a.kr : 0, q_hi = SPLIT ? min<int64_t>(N, q_lo + a.kr) : N;
+  const int64_t q_lo = SPLIT ? (int64_t)blockIdx.z * a.kr : a.q0, q_hi = SPLIT ? min<int64_t>(N, q_lo + a.kr) : a.q1;
   abf16x8_t kp[KC][3];
   row_planes<KC>(a.K + (b * N + key) * a.dk, kv, a.dk, h, kp, ALOG2E);  // base-2 scores
   abf16x8_t hp[WANT_H ? 1 : FC][3];
@@ -1441,7 +1445,7 @@ __global__ __launch_bounds__(64 * KQ_WAVES, 1) void attn_bwd_kq_x6_kernel(AttnAr
   const int64_t N = a.N, b = blockIdx.y;
   const int64_t key = (int64_t)blockIdx.x * KW + wave * 32 + l32;
   const bool kv = key < N;
-  const int64_t q_lo = SPLIT ? (int64_t)blockIdx.z * a.kr : 0, q_hi = SPLIT ? min<int64_t>(N, q_lo + a.kr) : N;
+  const int64_t q_lo = SPLIT ? (int64_t)blockIdx.z * a.kr : a.q0, q_hi = SPLIT ? min<int64_t>(N, q_lo + a.kr) : a.q1;
   abf16x8_t hp[FC][3];
   row_planes<FC>(a.H + (b * N + key) * a.dv, kv, a.dv, h, hp);
   {  // K rows, natural scale (the scores' B operand, and dQ's; zero for padded keys)
@@ -1694,7 +1698,10 @@ int launch_attn(AttnPass pass, const AttnArgs& a0, int64_t B, int S, hipStream_t
     a.part = a.part2 = nullptr;
     a.kr = a.N;
   }
-  const dim3 grid((unsigned)ceil_div(a.N, 128), (unsigned)B, (unsigned)S);
+  // query-stationary passes (forward, dQ) cover the queries [q0, q1); dK / dH every key
+  const int64_t nq = a.q1 - a.q0;
+  if (pass != PASS_BWD_KV && nq <= 0) return GRL_OK;  // no query rows: no forward / dQ work
+  const dim3 grid((unsigned)ceil_div(pass == PASS_BWD_KV ? a.N : nq, 128), (unsigned)B, (unsigned)S);
   const bool pre = pass == PASS_BWD_KV ? (a.Qpl && a.Opl) : (a.Kpl && a.Hpl);
   const int64_t rows = B * a.N;
   const unsigned red = (unsigned)std::min<int64_t>(ceil_div(rows * std::max(a.dv, 1), 256), 8192);
@@ -1718,7 +1725,7 @@ int launch_attn(AttnPass pass, const AttnArgs& a0, int64_t B, int S, hipStream_t
       hipLaunchKernelGGL((attn_bwd_kv_kernel<DKP, NT>), grid, dim3(256), 0, st, a);
   } else if (pass == PASS_FWD && x6) {
     if (pre && attn_pipe_enabled() && attn_fwd8_enabled()) {  // 256 queries per workgroup
-      const dim3 g8((unsigned)ceil_div(a.N, 256), (unsigned)B, (unsigned)S);
+      const dim3 g8((unsigned)ceil_div(nq, 256), (unsigned)B, (unsigned)S);
       if (S > 1)
         hipLaunchKernelGGL((attn_fwd_x6p_kernel<DKP, NT, true, 8>), g8, dim3(512), 0, st, a);
       else
@@ -1910,13 +1917,17 @@ extern "C" size_t grl_node_attention_bwd_workspace_size(int64_t B, int64_t N, in
   return base + (q ? q + attn_plane_bytes(B * N, 16) : 0);
 }
 
-extern "C" int grl_node_attention_fwd(const float* Q, const float* K, const float* H, const float* V,
-                                      const float* gamma, float* out, float* o_norm, float* row_max, float* row_sum,
-                                      int64_t B, int64_t N, int32_t dk, int32_t dv, void* workspace,
-                                      size_t workspace_bytes, grl_stream_t stream) {
+extern "C" int grl_node_attention_fwd_rows(const float* Q, const float* K, const float* H, const float* V,
+                                           const float* gamma, float* out, float* o_norm, float* row_max,
+                                           float* row_sum, int64_t B, int64_t N, int32_t dk, int32_t dv,
+                                           int64_t q_begin, int64_t q_end, void* workspace, size_t workspace_bytes,
+                                           grl_stream_t stream) {
   TraceRange trace_("grl_node_attention_fwd");
   int rc = check_dims("grl_node_attention_fwd", B, N, dk, dv);
   if (rc) return rc;
+  GRL_CHECK_ARG(0 <= q_begin && q_begin <= q_end && q_end <= N, "grl_node_attention_fwd: query rows [%lld, %lld) "
+                "outside [0, %lld)", (long long)q_begin, (long long)q_end, (long long)N);
+  if (q_begin == q_end) return GRL_OK;
   if (B == 0 || N == 0) return GRL_OK;
   GRL_CHECK_ARG((dk == 0 || (Q && K)) && H && V && gamma && out, "grl_node_attention_fwd: NULL pointer");
   GRL_CHECK_ARG((row_max == nullptr) == (row_sum == nullptr), "grl_node_attention_fwd: row_max/row_sum: both or none");
@@ -1933,6 +1944,9 @@ extern "C" int grl_node_attention_fwd(const float* Q, const float* K, const floa
   a.N = N;
   a.dk = dk;
   a.dv = dv;
+  a.q0 = q_begin;
+  a.q1 = q_end;
+  const bool ranged = q_begin != 0 || q_end != N;
   hipStream_t st = as_stream(stream);
   int S = 1;
   // below ~4k rows the per-call split launches cost more than the in-kernel
@@ -1948,7 +1962,7 @@ extern "C" int grl_node_attention_fwd(const float* Q, const float* K, const floa
     }
     GRL_LAUNCH_CHECK();
     int64_t kr;
-    S = attn_splits(B, N, &kr);  // small N: key split with (o, m, l) partials
+    S = ranged ? 1 : attn_splits(B, N, &kr);  // small N: key split with (o, m, l) partials (whole range only)
     if (S > 1 && cur + (size_t)S * B * N * (dv + 2) * 4 <= end) {
       a.part = reinterpret_cast<float*>(cur);
       a.kr = kr;
@@ -1959,13 +1973,16 @@ extern "C" int grl_node_attention_fwd(const float* Q, const float* K, const floa
   return dispatch(PASS_FWD, a, B, S, st);
 }
 
-extern "C" int grl_node_attention_bwd(const float* Q, const float* K, const float* H, const float* dO,
-                                      const float* row_max, const float* row_sum, const float* D, float* dQ,
-                                      float* dK, float* dH, int64_t B, int64_t N, int32_t dk, int32_t dv,
-                                      void* workspace, size_t workspace_bytes, grl_stream_t stream) {
+extern "C" int grl_node_attention_bwd_rows(const float* Q, const float* K, const float* H, const float* dO,
+                                           const float* row_max, const float* row_sum, const float* D, float* dQ,
+                                           float* dK, float* dH, int64_t B, int64_t N, int32_t dk, int32_t dv,
+                                           int64_t q_begin, int64_t q_end, void* workspace, size_t workspace_bytes,
+                                           grl_stream_t stream) {
   TraceRange trace_("grl_node_attention_bwd");
   int rc = check_dims("grl_node_attention_bwd", B, N, dk, dv);
   if (rc) return rc;
+  GRL_CHECK_ARG(0 <= q_begin && q_begin <= q_end && q_end <= N, "grl_node_attention_bwd: query rows [%lld, %lld) "
+                "outside [0, %lld)", (long long)q_begin, (long long)q_end, (long long)N);
   if (B == 0 || N == 0) return GRL_OK;
   GRL_CHECK_ARG((dk == 0 || (Q && K && dQ && dK)) && H && dO && row_max && row_sum && D && dH,
                 "grl_node_attention_bwd: NULL pointer");
@@ -1983,6 +2000,9 @@ extern "C" int grl_node_attention_bwd(const float* Q, const float* K, const floa
   a.N = N;
   a.dk = dk;
   a.dv = dv;
+  a.q0 = q_begin;
+  a.q1 = q_end;
+  const bool ranged = q_begin != 0 || q_end != N;
   hipStream_t st = as_stream(stream);
   int S = 1;
   if (workspace && attn_x6_enabled() && attn_dvp(dv) == 128 && dk <= 32) {  // the x6 backward's operands
@@ -1999,7 +2019,7 @@ extern "C" int grl_node_attention_bwd(const float* Q, const float* K, const floa
     }
     GRL_LAUNCH_CHECK();
     int64_t kr;
-    S = attn_splits(B, N, &kr);  // small N: key / query split with ordered partial sums
+    S = ranged ? 1 : attn_splits(B, N, &kr);  // small N: key / query split with ordered partial sums
     if (S > 1 && cur + (size_t)S * B * N * (dv + dk) * 4 <= end) {
       a.part = reinterpret_cast<float*>(cur);
       a.kr = kr;
@@ -2007,7 +2027,7 @@ extern "C" int grl_node_attention_bwd(const float* Q, const float* K, const floa
     } else {
       S = 1;
     }
-    const size_t qs = attn_qslab_bytes(B, N, dk, dv);
+    const size_t qs = ranged ? 0 : attn_qslab_bytes(B, N, dk, dv);  // ranged: the dQ kernel (no slabs)
     const uint16_t* q16 = nullptr;
     if (qs && a.Qpl && dk > 0 && cur + qs <= end) {
       a.qslab = reinterpret_cast<float*>(cur);
@@ -2025,4 +2045,20 @@ extern "C" int grl_node_attention_bwd(const float* Q, const float* K, const floa
     if (rc) return rc;
   }
   return dispatch(PASS_BWD_KV, a, B, S, st);
+}
+
+extern "C" int grl_node_attention_fwd(const float* Q, const float* K, const float* H, const float* V,
+                                      const float* gamma, float* out, float* o_norm, float* row_max, float* row_sum,
+                                      int64_t B, int64_t N, int32_t dk, int32_t dv, void* workspace,
+                                      size_t workspace_bytes, grl_stream_t stream) {
+  return grl_node_attention_fwd_rows(Q, K, H, V, gamma, out, o_norm, row_max, row_sum, B, N, dk, dv, 0, N, workspace,
+                                     workspace_bytes, stream);
+}
+
+extern "C" int grl_node_attention_bwd(const float* Q, const float* K, const float* H, const float* dO,
+                                      const float* row_max, const float* row_sum, const float* D, float* dQ,
+                                      float* dK, float* dH, int64_t B, int64_t N, int32_t dk, int32_t dv,
+                                      void* workspace, size_t workspace_bytes, grl_stream_t stream) {
+  return grl_node_attention_bwd_rows(Q, K, H, dO, row_max, row_sum, D, dQ, dK, dH, B, N, dk, dv, 0, N, workspace,
+                                     workspace_bytes, stream);
 }

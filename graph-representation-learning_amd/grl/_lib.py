@@ -176,6 +176,10 @@ SIGNATURES = {
                                         _c_i32, _c_i32, _c_vp, _c_size, _c_vp]),
     "grl_node_attention_bwd": (_c_i32, [_c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_i64,
                                         _c_i64, _c_i32, _c_i32, _c_vp, _c_size, _c_vp]),
+    "grl_node_attention_fwd_rows": (_c_i32, [_c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_i64,
+                                             _c_i64, _c_i32, _c_i32, _c_i64, _c_i64, _c_vp, _c_size, _c_vp]),
+    "grl_node_attention_bwd_rows": (_c_i32, [_c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp, _c_vp,
+                                             _c_i64, _c_i64, _c_i32, _c_i32, _c_i64, _c_i64, _c_vp, _c_size, _c_vp]),
     "grl_layout_graph_size": (_c_i32, [_c_vp, _c_i32, _c_vp]),
     "grl_layout_graph_dense": (_c_i32, [_c_vp, _c_i32, _c_i32, _c_i32, _c_vp]),
     "grl_layout_graph_edges": (_c_i32, [_c_vp, _c_i32, _c_i32, _c_vp, _c_i64, _c_vp]),

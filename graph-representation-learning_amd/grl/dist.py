@@ -822,6 +822,24 @@ class ShardedGraph:
         all_gather_into(out, pad, self.group)
         return torch.cat([out[q * stride: q * stride + p.bounds[q + 1] - p.bounds[q]] for q in range(world)])
 
+    def reduce_rows(self, P: torch.Tensor) -> torch.Tensor:
+        """This rank's rows of the sum over ranks of a per-rank [N, d] partial
+        (global node order), added in rank order: every rank sends each peer
+        that peer's row block (all-to-all-v) and adds the P blocks it receives
+        in rank order -- deterministic, the bits independent of the
+        collective's algorithm."""
+        p = self.plan
+        world = len(p.bounds) - 1
+        if world == 1 or not (dist.is_available() and dist.is_initialized()):
+            return P.contiguous()
+        sizes = [p.bounds[q + 1] - p.bounds[q] for q in range(world)]
+        recv = P.new_empty(world * p.n_loc, P.shape[1])
+        all_to_all_v(recv, P.contiguous(), [p.n_loc] * world, sizes, self.group)
+        acc = recv[: p.n_loc].clone()
+        for q in range(1, world):
+            acc += recv[q * p.n_loc: (q + 1) * p.n_loc]
+        return acc
+
     def broadcast_seed(self, seed_t: torch.Tensor) -> torch.Tensor:
         """Rank 0's value of a 1-element device tensor on every rank of the
         shard's group (a device-drawn DropEdge seed: the masks of a sharded
@@ -963,43 +981,52 @@ class ShardedGraph:
 class _ShardedNodeAttention(torch.autograd.Function):
     """NodeSelfAtten (robust_gcn.py:78-99) over a node-range-sharded graph:
     out_loc = gamma * softmax(Q K^T) H + V for this rank's rows, the softmax
-    over EVERY node.  The rows of Q, K, H, V are all-gathered (RCCL) and each
-    rank runs the fused attention kernels over the whole graph -- the
-    kernels are deterministic, so every rank computes the same bits as the
-    one-GPU model -- and keeps its rows; the backward all-gathers the output
-    gradient, reruns the fused backward and keeps its rows of dQ, dK, dH
-    (complete: every query's contribution is in them), dgamma from its own
-    rows only (allreduce_gradients adds the ranks' partials, as for every
-    other weight).  The attention's O(N^2) work is replicated, not sharded:
-    the GraphConv layers are what this path distributes."""
+    over EVERY node.  Forward: K and H of every rank are all-gathered (RCCL)
+    and the fused kernels run this rank's queries only against every key
+    (grl_node_attention_fwd_rows): the O(N^2) work is split P ways.
+    Backward (grl_node_attention_bwd_rows): dQ of the own queries is
+    complete; dK and dH come out for every key as the own queries'
+    contribution, and each key row's owner adds the P partials in rank
+    order (an all-to-all of the row blocks, then an ordered sum:
+    deterministic, unlike a reduce-scatter's); dgamma from the own rows
+    (allreduce_gradients adds the ranks' partials, as for every weight)."""
 
     @staticmethod
     def forward(ctx, Q, K, H, V, gamma, sg):
         from .ops import node_attention_forward
 
         p = sg.plan
-        shape = V.shape
-        Qg, Kg, Hg, Vg = (sg.gather_rows(t.detach().reshape(-1, t.shape[-1]).contiguous()) for t in (Q, K, H, V))
-        out, onorm, rmax, rsum = node_attention_forward(Qg[None], Kg[None], Hg[None], Vg[None], gamma, stats=True)
-        rb = p.row_begin if len(p.bounds) > 2 else 0
-        ctx.rows = (rb, rb + p.n_loc)
-        ctx.shapes = (Q.shape, K.shape, H.shape)
-        ctx.sg = sg
-        ctx.save_for_backward(Qg, Kg, Hg, gamma, onorm, rmax, rsum)
-        return out[0, rb: rb + p.n_loc].reshape(shape)
+        dk, dv = Q.shape[-1], H.shape[-1]
+        Kg = sg.gather_rows(K.detach().reshape(-1, dk).contiguous())
+        Hg = sg.gather_rows(H.detach().reshape(-1, dv).contiguous())
+        N = Kg.shape[0]
+        r0 = p.row_begin - p.bounds[0] if N != p.n_loc else 0
+        r1 = r0 + p.n_loc
+        Qf = Q.new_zeros(1, N, dk)
+        Qf[0, r0:r1] = Q.detach().reshape(-1, dk)
+        Vf = V.new_zeros(1, N, dv)
+        Vf[0, r0:r1] = V.detach().reshape(-1, dv)
+        out, onorm, rmax, rsum = node_attention_forward(Qf, Kg[None], Hg[None], Vf, gamma, stats=True,
+                                                        q_range=(r0, r1))
+        ctx.rows, ctx.shapes, ctx.sg = (r0, r1), (Q.shape, K.shape, H.shape), sg
+        ctx.save_for_backward(Qf, Kg, Hg, gamma, onorm, rmax, rsum)
+        return out[0, r0:r1].reshape(V.shape)
 
     @staticmethod
     def backward(ctx, dout):
         from .ops import node_attention_backward
 
-        Qg, Kg, Hg, gamma, onorm, rmax, rsum = ctx.saved_tensors
+        Qf, Kg, Hg, gamma, onorm, rmax, rsum = ctx.saved_tensors
         r0, r1 = ctx.rows
         d_loc = dout.reshape(-1, dout.shape[-1]).contiguous().float()
-        dg = ctx.sg.gather_rows(d_loc)
-        dQ, dK, dH = node_attention_backward(Qg[None], Kg[None], Hg[None], gamma, onorm, rmax, rsum, dg[None])
+        dOf = d_loc.new_zeros(1, Qf.shape[1], d_loc.shape[1])
+        dOf[0, r0:r1] = d_loc
+        dQ, dK, dH = node_attention_backward(Qf, Kg[None], Hg[None], gamma, onorm, rmax, rsum, dOf, q_range=(r0, r1))
         dgamma = (d_loc * onorm[0, r0:r1]).sum(0)
+        dKH = ctx.sg.reduce_rows(torch.cat([dK[0], dH[0]], 1))
+        dk = dK.shape[-1]
         qs, ks, hs = ctx.shapes
-        return (dQ[0, r0:r1].reshape(qs), dK[0, r0:r1].reshape(ks), dH[0, r0:r1].reshape(hs), dout, dgamma, None)
+        return (dQ[0, r0:r1].reshape(qs), dKH[:, :dk].reshape(ks), dKH[:, dk:].reshape(hs), dout, dgamma, None)
 
 
 def sharded_node_attention(Q: torch.Tensor, K: torch.Tensor, H: torch.Tensor, V: torch.Tensor, gamma: torch.Tensor,

@@ -636,53 +636,62 @@ def _dv_blocks(dk: int, dv: int):
     return [(c0, min(dv, c0 + step)) for c0 in range(0, dv, step)]
 
 
-def node_attention_forward(Q, K, H, V, gamma, stats: bool = False):
+def node_attention_forward(Q, K, H, V, gamma, stats: bool = False, q_range=None):
     """out = gamma * softmax(Q K^T) H + V (robust_gcn.py:90-96), fused.
-    stats=True also returns (o_norm, row_max, row_sum) for the backward."""
+    stats=True also returns (o_norm, row_max, row_sum) for the backward.
+    q_range=(q0, q1): only those query rows are computed (the other rows of
+    the outputs are zeros) -- a node-range shard's queries against every key
+    (grl_node_attention_fwd_rows)."""
     _attn_check(Q, K, H, V, gamma)
     Q, K, H, V, gamma = (t.contiguous() for t in (Q, K, H, V, gamma))
     B, N, dk = Q.shape
     dv = H.shape[2]
+    q0, q1 = (0, N) if q_range is None else (int(q_range[0]), int(q_range[1]))
     blocks = _dv_blocks(dk, dv)
     if len(blocks) > 1:
         parts = [node_attention_forward(Q, K, H[..., a:b].contiguous(), V[..., a:b].contiguous(),
-                                        gamma[a:b].contiguous(), stats=stats) for a, b in blocks]
+                                        gamma[a:b].contiguous(), stats=stats, q_range=q_range) for a, b in blocks]
         if not stats:
             return torch.cat(parts, -1)
         out = torch.cat([p[0] for p in parts], -1)
         onorm = torch.cat([p[1] for p in parts], -1)
         return out, onorm, parts[0][2], parts[0][3]
-    out = torch.empty_like(V)
-    onorm = torch.empty_like(V) if stats else None
-    rmax = torch.empty(B, N, device=V.device) if stats else None
-    rsum = torch.empty(B, N, device=V.device) if stats else None
+    alloc = torch.empty_like if q_range is None else torch.zeros_like  # ranged: rows outside stay defined
+    out = alloc(V)
+    onorm = alloc(V) if stats else None
+    rmax = alloc(V[..., 0]) if stats else None
+    rsum = (torch.ones_like(V[..., 0]) if q_range is not None else torch.empty_like(V[..., 0])) if stats else None
     ptr = (lambda t: t.data_ptr() if t is not None else None)  # noqa: E731
     ws, ws_bytes = _attn_workspace(B, N, dk, dv, V.device)
-    call("grl_node_attention_fwd", Q.data_ptr(), K.data_ptr(), H.data_ptr(), V.data_ptr(), gamma.data_ptr(),
-         out.data_ptr(), ptr(onorm), ptr(rmax), ptr(rsum), B, N, dk, dv, ptr(ws), ws_bytes,
+    call("grl_node_attention_fwd_rows", Q.data_ptr(), K.data_ptr(), H.data_ptr(), V.data_ptr(), gamma.data_ptr(),
+         out.data_ptr(), ptr(onorm), ptr(rmax), ptr(rsum), B, N, dk, dv, q0, q1, ptr(ws), ws_bytes,
          current_stream_handle(V.device))
     return (out, onorm, rmax, rsum) if stats else out
 
 
-def node_attention_backward(Q, K, H, gamma, onorm, rmax, rsum, dout):
+def node_attention_backward(Q, K, H, gamma, onorm, rmax, rsum, dout, q_range=None):
     """(dQ, dK, dH) of out = gamma * softmax(Q K^T) H + V for the output
-    gradient dout, from the forward's stats (grl_node_attention_bwd)."""
+    gradient dout, from the forward's stats (grl_node_attention_bwd).
+    q_range=(q0, q1): only those queries -- dQ of the range (other rows
+    zero), dK / dH of every key from the range's queries alone (partials)."""
     dout = dout.contiguous().float()
     B, N, dk = Q.shape
     dv = H.shape[2]
+    q0, q1 = (0, N) if q_range is None else (int(q_range[0]), int(q_range[1]))
     dO = dout * gamma
     dQ = dK = None
     dHs = []
     for a, b in _dv_blocks(dk, dv):  # one block unless dv exceeds a call's width
         dO_b = dO[..., a:b].contiguous()
         D = (dO_b * onorm[..., a:b]).sum(-1).contiguous()
-        dQ_b, dK_b = torch.empty_like(Q), torch.empty_like(K)
+        dQ_b = torch.empty_like(Q) if q_range is None else torch.zeros_like(Q)
+        dK_b = torch.empty_like(K)
         dH_b = torch.empty(B, N, b - a, dtype=H.dtype, device=H.device)
         H_b = H[..., a:b].contiguous()
         ws, ws_bytes = _attn_workspace(B, N, dk, b - a, Q.device, backward=True)
-        call("grl_node_attention_bwd", Q.data_ptr(), K.data_ptr(), H_b.data_ptr(), dO_b.data_ptr(),
+        call("grl_node_attention_bwd_rows", Q.data_ptr(), K.data_ptr(), H_b.data_ptr(), dO_b.data_ptr(),
              rmax.data_ptr(), rsum.data_ptr(), D.data_ptr(), dQ_b.data_ptr(), dK_b.data_ptr(), dH_b.data_ptr(),
-             B, N, dk, b - a, ws.data_ptr() if ws is not None else None, ws_bytes,
+             B, N, dk, b - a, q0, q1, ws.data_ptr() if ws is not None else None, ws_bytes,
              current_stream_handle(Q.device))
         dQ = dQ_b if dQ is None else dQ + dQ_b
         dK = dK_b if dK is None else dK + dK_b

@@ -454,6 +454,31 @@ int grl_node_attention_bwd(const float* Q, const float* K, const float* H,
                            int32_t dk, int32_t dv, void* workspace,
                            size_t workspace_bytes, grl_stream_t stream);
 
+/* The same two calls over the query rows [q_begin, q_end) only -- a node-
+ * range shard's own queries against EVERY key (NodeSelfAtten on a sharded
+ * graph, robust_gcn.py:90-96; grl/dist.py sharded_node_attention).  All
+ * arrays keep their [B, N, ...] shapes; rows outside the range of Q / V /
+ * dO are read as padding only, and those of out / o_norm / row_max /
+ * row_sum / dQ are not written.  fwd: out, o_norm and the stats of the
+ * range.  bwd: dQ of the range (complete), and dK, dH of EVERY key as the
+ * range's queries' contribution (partials: a shard adds the other shards'
+ * in rank order); row_max / row_sum / D must hold the range's rows (the
+ * whole softmax's statistics).  The whole range (0, N) is exactly
+ * grl_node_attention_fwd / _bwd.  No key split, no folded dQ when ranged. */
+int grl_node_attention_fwd_rows(const float* Q, const float* K, const float* H,
+                                const float* V, const float* gamma, float* out,
+                                float* o_norm, float* row_max, float* row_sum,
+                                int64_t B, int64_t N, int32_t dk, int32_t dv,
+                                int64_t q_begin, int64_t q_end, void* workspace,
+                                size_t workspace_bytes, grl_stream_t stream);
+int grl_node_attention_bwd_rows(const float* Q, const float* K, const float* H,
+                                const float* dO, const float* row_max,
+                                const float* row_sum, const float* D, float* dQ,
+                                float* dK, float* dH, int64_t B, int64_t N,
+                                int32_t dk, int32_t dv, int64_t q_begin,
+                                int64_t q_end, void* workspace,
+                                size_t workspace_bytes, grl_stream_t stream);
+
 /* ---------------------------------------------------------------------- */
 /* Graph formats                                                           */
 /* ---------------------------------------------------------------------- */

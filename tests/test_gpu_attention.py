@@ -185,3 +185,39 @@ def test_eight_wave_workgroups_same_bits(B, N, dk, dv, monkeypatch):
         res[v] = [out.detach()] + [t.grad for t in leaves]
     for a, b in zip(res["1"], res["0"]):
         assert torch.equal(a, b)
+
+
+RANGED = [(1, 20_000, 16, 128, (0, 7000, 13_003, 20_000)), (2, 3000, 16, 100, (0, 1, 1500, 3000)),
+          (1, 5000, 32, 128, (0, 2500, 5000)), (1, 1200, 64, 512, (0, 600, 1200)), (1, 9000, 4, 32, (0, 9000))]
+
+
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("B,N,dk,dv,cuts", RANGED)
+def test_query_ranges_partition_the_attention(B, N, dk, dv, cuts, mode, monkeypatch):
+    """grl_node_attention_fwd_rows / _bwd_rows (a node-range shard's queries
+    against every key, grl.dist sharded_node_attention): over a partition of
+    the queries, each range's output rows match the float64 attention, the
+    ranges' dQ rows are the whole dQ's, and the ranges' dK / dH partials add
+    up (in range order) to the whole dK / dH -- within 1e-5 of fp64.  Rows
+    outside a range stay zero."""
+    from grl.ops import node_attention_backward
+
+    _set_mode(mode, monkeypatch)
+    Q, K, H, V, gamma = _inputs(B, N, dk, dv, seed=N + 7)
+    dout = torch.randn(B, N, dv, generator=torch.Generator().manual_seed(3)).to(DEV)
+    Qd, Kd, Hd, Vd, gd = (t.double().requires_grad_(True) for t in (Q, K, H, V, gamma))
+    ref = _ref(Qd, Kd, Hd, Vd, gd)
+    ref.backward(dout.double())
+    dQ_sum = torch.zeros_like(Q)
+    dK_sum, dH_sum = torch.zeros_like(K), torch.zeros_like(H)
+    for q0, q1 in zip(cuts[:-1], cuts[1:]):
+        out, onorm, rmax, rsum = node_attention_forward(Q, K, H, V, gamma, stats=True, q_range=(q0, q1))
+        torch.testing.assert_close(out[:, q0:q1].double(), ref[:, q0:q1].detach(), rtol=1e-5, atol=1e-5)
+        assert not bool(out[:, :q0].any()) and not bool(out[:, q1:].any())
+        dQ, dK, dH = node_attention_backward(Q, K, H, gamma, onorm, rmax, rsum, dout, q_range=(q0, q1))
+        assert not bool(dQ[:, :q0].any()) and not bool(dQ[:, q1:].any())
+        dQ_sum += dQ
+        dK_sum += dK
+        dH_sum += dH
+    for got, want in ((dQ_sum, Qd.grad), (dK_sum, Kd.grad), (dH_sum, Hd.grad)):
+        torch.testing.assert_close(got.double(), want, rtol=1e-5, atol=1e-5 * max(1.0, float(want.abs().max())))
