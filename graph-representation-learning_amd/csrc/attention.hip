@@ -70,6 +70,10 @@ struct AttnArgs {
   // outputs are written; dK / dH: only these queries contribute) -- a node-
   // range shard's own queries against every key (grl_node_attention_*_rows)
   int64_t q0, q1;
+  // bwd_kq: first key of this launch, and key workgroups per launch (the
+  // fused pass runs in key chunks whose dQ slabs fit the workspace; each
+  // chunk's slabs are added onto dQ in order)
+  int64_t k0, kq_chunk;
 };
 
 __device__ __forceinline__ int kappa(int s, int h) { return (s & 3) + 8 * (s >> 2) + 4 * h; }
@@ -1443,7 +1447,7 @@ __global__ __launch_bounds__(64 * KQ_WAVES, 1) void attn_bwd_kq_x6_kernel(AttnAr
   __shared__ float Ms_s[2 * 32], Ds_s[2 * 32];                         // lse2, D per query
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, h = lane >> 5;
   const int64_t N = a.N, b = blockIdx.y;
-  const int64_t key = (int64_t)blockIdx.x * KW + wave * 32 + l32;
+  const int64_t key = a.k0 + (int64_t)blockIdx.x * KW + wave * 32 + l32;
   const bool kv = key < N;
   const int64_t q_lo = SPLIT ? (int64_t)blockIdx.z * a.kr : a.q0, q_hi = SPLIT ? min<int64_t>(N, q_lo + a.kr) : a.q1;
   abf16x8_t hp[FC][3];
@@ -1593,9 +1597,11 @@ __global__ __launch_bounds__(64 * KQ_WAVES, 1) void attn_bwd_kq_x6_kernel(AttnAr
   }
 }
 
-// dQ[b][q][d] = sum over key workgroups x of qslab[b][x][q][d], in x order
+// dQ[b][q][d] = sum over key workgroups x of qslab[b][x][q][d], in x order;
+// accumulate: start from dQ (a later key chunk: the same chain of fp32 adds
+// as one pass over every chunk's slabs)
 __global__ void attn_qslab_sum_kernel(const float* __restrict__ qslab, int64_t B, int64_t X, int64_t N, int dk,
-                                      float* __restrict__ dQ) {
+                                      float* __restrict__ dQ, int accumulate) {
   const int64_t n_all = B * N * dk;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_all; i += (int64_t)gridDim.x * blockDim.x) {
     // i = (b * dk + d) * N + q: consecutive threads read consecutive q of one slab row
@@ -1603,7 +1609,7 @@ __global__ void attn_qslab_sum_kernel(const float* __restrict__ qslab, int64_t B
     const int d = (int)(bd - b * dk);
     const int64_t npad = (N + 31) & ~(int64_t)31, xs = 16 * npad;  // slab [b][x][d][npad]
     const float* p = qslab + b * X * xs + (int64_t)d * npad + q;
-    float acc = 0.0f;
+    float acc = accumulate ? dQ[(b * N + q) * dk + d] : 0.0f;
     int64_t x = 0;
     for (; x + 4 <= X; x += 4) {
       const float v0 = p[(x + 0) * xs], v1 = p[(x + 1) * xs], v2 = p[(x + 2) * xs], v3 = p[(x + 3) * xs];
@@ -1767,15 +1773,22 @@ int launch_attn(AttnPass pass, const AttnArgs& a0, int64_t B, int S, hipStream_t
       if constexpr (DKP == 16) {
         if (a.qslab && pre) {  // dK with dQ folded in (grl_node_attention_bwd skipped the dQ pass)
           kq = true;
-          const dim3 gkq((unsigned)ceil_div(a.N, KQ_KEYS), (unsigned)B, (unsigned)S);
-          if (S > 1)
-            hipLaunchKernelGGL((attn_bwd_kq_x6_kernel<true>), gkq, dim3(64 * KQ_WAVES), 0, st, a);
-          else
-            hipLaunchKernelGGL((attn_bwd_kq_x6_kernel<false>), gkq, dim3(64 * KQ_WAVES), 0, st, a);
-          GRL_LAUNCH_CHECK();
-          if (a.dk > 0)
-            hipLaunchKernelGGL(attn_qslab_sum_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(rows * a.dk, 256), 8192)),
-                               dim3(256), 0, st, a.qslab, B, (int64_t)gkq.x, a.N, a.dk, a.dQ);
+          // key chunks of xc workgroups, as many slabs as the workspace holds (a.kr_slabs)
+          const int64_t xall = ceil_div(a.N, KQ_KEYS), xc = std::max<int64_t>(1, std::min<int64_t>(xall, a.kq_chunk));
+          for (int64_t x0 = 0; x0 < xall; x0 += xc) {
+            AttnArgs ac = a;
+            ac.k0 = x0 * KQ_KEYS;
+            const dim3 gkq((unsigned)std::min<int64_t>(xc, xall - x0), (unsigned)B, (unsigned)S);
+            if (S > 1)
+              hipLaunchKernelGGL((attn_bwd_kq_x6_kernel<true>), gkq, dim3(64 * KQ_WAVES), 0, st, ac);
+            else
+              hipLaunchKernelGGL((attn_bwd_kq_x6_kernel<false>), gkq, dim3(64 * KQ_WAVES), 0, st, ac);
+            GRL_LAUNCH_CHECK();
+            if (a.dk > 0)
+              hipLaunchKernelGGL(attn_qslab_sum_kernel,
+                                 dim3((unsigned)std::min<int64_t>(ceil_div(rows * a.dk, 256), 8192)), dim3(256), 0, st,
+                                 a.qslab, B, (int64_t)gkq.x, a.N, a.dk, a.dQ, (int)(x0 > 0));
+          }
         }
       }
       if (!kq) GRL_X6L(attn_bwd_kv_x6_kernel, DKP, false);
@@ -1902,13 +1915,25 @@ extern "C" size_t grl_node_attention_workspace_size(int64_t B, int64_t N, int32_
   return planes + part ? planes + part + 512 : 0;
 }
 
-// the backward's dQ slabs (attn_bwd_kq_x6_kernel): dk <= 16, x6 planes, and
-// at most kAttnQslabMax bytes (N^2 / 4 at B = 1: 2.5 GB at N = 100k)
+// the backward's dQ slabs (attn_bwd_kq_x6_kernel): dk <= 16, x6 planes;
+// N^2 / 4 bytes at B = 1 (2.5 GB at N = 100k) in key chunks of at most
+// kAttnQslabMax bytes (N = 500k: 3 chunks of 768 key workgroups)
 constexpr size_t kAttnQslabMax = (size_t)24 << 30;
+static size_t attn_qslab_x_bytes(int64_t B, int64_t N) {  // one key workgroup's slabs
+  return (size_t)B * (size_t)(ceil_div(N, 32) * 32) * 16 * 4;
+}
+static int64_t attn_qslab_chunk(int64_t B, int64_t N) {  // key workgroups per fused launch
+  const char* e = getenv("GRL_ATTN_QSLAB_MAX");  // test aid: a smaller chunk budget (bytes)
+  const size_t cap = e && atoll(e) > 0 ? (size_t)atoll(e) : kAttnQslabMax;
+  const int64_t all = ceil_div(N, KQ_KEYS), fit = (int64_t)(cap / attn_qslab_x_bytes(B, N));
+  if (fit >= all) return all;
+  const int64_t cus = device_cu_count();  // one workgroup per CU: whole rounds of the grid
+  return std::max<int64_t>(1, fit >= cus ? fit / cus * cus : fit);
+}
 static size_t attn_qslab_bytes(int64_t B, int64_t N, int dk, int dv) {
   if (!attn_fused_dq_enabled() || dk > 16 || attn_dvp(dv) != 128 || B * N < kAttnPlaneMinRows) return 0;
-  const size_t n = (size_t)B * (size_t)ceil_div(N, KQ_KEYS) * (size_t)(ceil_div(N, 32) * 32) * 16 * 4;
-  return n <= kAttnQslabMax ? (n + 255) / 256 * 256 : 0;
+  const size_t n = (size_t)attn_qslab_chunk(B, N) * attn_qslab_x_bytes(B, N);
+  return (n + 255) / 256 * 256;
 }
 
 extern "C" size_t grl_node_attention_bwd_workspace_size(int64_t B, int64_t N, int32_t dk, int32_t dv) {
@@ -2031,6 +2056,7 @@ extern "C" int grl_node_attention_bwd_rows(const float* Q, const float* K, const
     const uint16_t* q16 = nullptr;
     if (qs && a.Qpl && dk > 0 && cur + qs <= end) {
       a.qslab = reinterpret_cast<float*>(cur);
+      a.kq_chunk = attn_qslab_chunk(B, N);
       cur += qs;
       if (attn_split(Q, B * N, dk, 16, cur, end, &q16, st)) {
         a.Qpl16 = q16;

@@ -442,8 +442,8 @@ int grl_node_attention_fwd(const float* Q, const float* K, const float* H,
  * key-stationary; dQ is query-stationary, or -- with a workspace of
  * grl_node_attention_bwd_workspace_size bytes, dk <= 16 -- folded into the
  * dK kernel as one partial slab per 256-key workgroup (B ceil(N/256) N 64
- * bytes, at most 24 GiB; larger N keeps the dQ kernel) added in workgroup
- * order.  d gamma = sum(d_out * o_norm) and the residual's d_out are the
+ * bytes; beyond 24 GiB the fused pass runs in key chunks, each chunk's slabs
+ * added onto dQ in order: the same additions) added in workgroup order.  d gamma = sum(d_out * o_norm) and the residual's d_out are the
  * caller's.                                                                  */
 size_t grl_node_attention_bwd_workspace_size(int64_t B, int64_t N, int32_t dk,
                                              int32_t dv);
