@@ -81,14 +81,14 @@ class KVProcedure(BaseProcedure):
         self.global_step = 0
         self.activator = torch.nn.Softmax(dim=2)
         self.train_loader, self.val_loader, self.class_names = self._init_dataloaders()
-        # additive config key capture_train_step: "capture" (the default when the
-        # key is absent) replays each batch shape's training step as one HIP graph
+        # additive config key capture_train_step: "capture" (the default on a ROCm
+        # device when the key is absent) replays each batch shape's training step as one HIP graph
         # from its second occurrence on (step_graph.py; ineligible batches run
         # eagerly); false opts out (the reference's eager step); "static" runs the
         # same static-buffer step eagerly (the replays' parity reference)
         from gnn.trainer.training_procedures.step_graph import StepGraph, as_mode
 
-        mode = as_mode(config.get("capture_train_step", "capture"))
+        mode = as_mode(config.get("capture_train_step", "capture" if self.device.type == "cuda" else None))
         self.step_graph = StepGraph(self, mode) if mode else None
 
     def _init_dataloaders(self):
