@@ -663,6 +663,12 @@ bool x6_stagger() {
   return e && e[0] == '1';
 }
 
+// GRL_X6T_U2 (read per call): 0 = the rolled dW loop (A/B aid)
+bool x6t_u2() {
+  const char* e = getenv("GRL_X6T_U2");
+  return !(e && e[0] == '0');
+}
+
 // GRL_X6_INTERLEAVE (read per call): 1 = the A split interleaved with the MFMAs
 bool x6_interleave() {
   const char* e = getenv("GRL_X6_INTERLEAVE");
@@ -947,7 +953,25 @@ __device__ __forceinline__ bf16x8_t tr_pair(const uint16_t* plane, int k, int co
   return __builtin_bit_cast(bf16x8_t, v);
 }
 
-template <int EPI>
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
+
+// tr_pair on an LDS-space pointer (p0 = plane + k * 256 + swizzled column):
+// the second block row is a constant 2 KB further, so with the stage and the
+// plane also constants both reads fold into one base VGPR + ds offsets
+__device__ __forceinline__ bf16x8_t tr_pair3(const lds_u16* p0) {
+  typedef __attribute__((address_space(3))) i16x4_t lds_v4;
+  const i16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)p0);
+  const i16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(p0 + 4 * 256));
+  typedef short i16x8_t __attribute__((ext_vector_type(8)));
+  const i16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8_t, v);
+}
+
+// GRL_X6T_U2 (read per call; default 1): the K16 loop unrolled over the two
+// stages, fragment reads from per-lane LDS offsets fixed for the kernel (the
+// stage and plane as immediates) -- the rolled loop recomputed ~40 address
+// adds per step.  Same reads, same MFMAs, same bits.
+template <int EPI, bool U2 = false>
 __global__ __launch_bounds__(512) void gemm_x6t_kernel(GemmArgs p) {
   __shared__ __attribute__((aligned(16))) uint16_t smem[2 * X6_STAGE];  // 2 stages x (A, B) x 3 planes x 8 KB
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1025,6 +1049,50 @@ __global__ __launch_bounds__(512) void gemm_x6t_kernel(GemmArgs p) {
     if (nk > 1) X6T_LOAD(1);
   }
   __syncthreads();
+  if (U2) {
+    const lds_u16* s3 = (const lds_u16*)smem;
+    const int sx = (tk & 3) << 5;
+    int oa[4], ob[2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) oa[i] = tk * 256 + ((wm * 128 + i * 32 + tc) ^ sx);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) ob[j] = tk * 256 + ((wn * 64 + j * 32 + tc) ^ sx);
+    auto step = [&](int64_t t, auto stage) {
+      constexpr int S = decltype(stage)::value;
+      const lds_u16* cur = s3 + S * X6_STAGE;
+      bf16x8_t a_[4][3], b_[2][3];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) a_[i][q] = tr_pair3(cur + q * X6_PLANE + oa[i]);
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) b_[j][q] = tr_pair3(cur + (3 + q) * X6_PLANE + ob[j]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_[i][2], b_[j][0], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_[i][1], b_[j][1], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_[i][0], b_[j][2], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_[i][1], b_[j][0], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_[i][0], b_[j][1], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_[i][0], b_[j][0], acc[i][j], 0, 0, 0);
+        }
+      if (t + 1 < nk) {
+        X6T_STASH(smem + (S ^ 1) * X6_STAGE);  // the other stage: last read in step t-1
+        if (t + 2 < nk) X6T_LOAD(t + 2);
+      }
+      __syncthreads();
+    };
+    int64_t t = 0;
+    for (; t + 1 < nk; t += 2) {
+      step(t, std::integral_constant<int, 0>{});
+      step(t + 1, std::integral_constant<int, 1>{});
+    }
+    if (t < nk) step(t, std::integral_constant<int, 0>{});
+  } else
   for (int64_t t = 0; t < nk; ++t) {
     const uint16_t* cur = smem + (t & 1) * X6_STAGE;
     bf16x8_t a_[4][3], b_[2][3];
@@ -1591,10 +1659,14 @@ extern "C" int grl_linear_bwd_weight(const float* Z, int64_t ldz, const float* g
     a.inner_n = 0;
     GRL_CHECK_ARG(a.mt * a.nt * a.zt < 2147483647LL, "gemm: grid too large");
     const dim3 grid((unsigned)(a.mt * a.nt * a.zt));
-    if (used > 1)
-      hipLaunchKernelGGL(gemm_x6t_kernel<EPI_SLAB>, grid, dim3(512), 0, st, a);
-    else
-      hipLaunchKernelGGL(gemm_x6t_kernel<EPI_STORE>, grid, dim3(512), 0, st, a);
+    const bool u2 = x6t_u2();
+    if (used > 1) {
+      if (u2) hipLaunchKernelGGL((gemm_x6t_kernel<EPI_SLAB, true>), grid, dim3(512), 0, st, a);
+      else hipLaunchKernelGGL((gemm_x6t_kernel<EPI_SLAB, false>), grid, dim3(512), 0, st, a);
+    } else {
+      if (u2) hipLaunchKernelGGL((gemm_x6t_kernel<EPI_STORE, true>), grid, dim3(512), 0, st, a);
+      else hipLaunchKernelGGL((gemm_x6t_kernel<EPI_STORE, false>), grid, dim3(512), 0, st, a);
+    }
     GRL_LAUNCH_CHECK();
   } else {
     const int splits = pick_splits(K, C, M);

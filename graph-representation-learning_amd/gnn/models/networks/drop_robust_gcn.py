@@ -154,9 +154,19 @@ class GraphCNNDropEdge(BaseNetwork):
         # efficient_mode=True: dropout covers the identity block of A_pre
         # (:69,:76); False: dropout hits raw A, identity added after (:72-74).
         ds = bool(efficient_mode)
+        sharded = isinstance(graph, ShardedGraph)
+        if sharded:  # gcn3's input cat[g1, g2]: g1's halo rows already came for gcn2
+            graph = graph.with_halo_memo()
         g1 = self.dropout(self.gcn1.propagate(embedding, self.edge_dropout(graph, ds), relu=True))
+        if sharded:
+            graph.remember(g1)
         g2 = self.dropout(self.gcn2.propagate(g1, self.edge_dropout(graph, ds), relu=True))
-        g3 = self.dropout(self.gcn3.propagate(torch.cat([g1, g2], dim=-1), self.edge_dropout(graph, ds), relu=True))
+        x3 = torch.cat([g1, g2], dim=-1)
+        if sharded:
+            graph.note_concat(x3, (g1, g2))
+        g3 = self.dropout(self.gcn3.propagate(x3, self.edge_dropout(graph, ds), relu=True))
+        if sharded:
+            graph.clear_halo_memo()
         new_v = self.emb2(torch.cat([g1, g3], dim=-1))
         if self.use_attention:
             new_v = self.self_atten(new_v, shard=graph) if isinstance(graph, ShardedGraph) else self.self_atten(new_v)

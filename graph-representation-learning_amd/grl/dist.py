@@ -591,8 +591,7 @@ class _RowPipelinedGraphConv(torch.autograd.Function):
         from .ops import graph_conv_fwd_train
 
         with trace("grl.rows_pipeline_fwd"):
-            with torch.no_grad():
-                X_ext = halo_exchange(X_loc.detach().contiguous(), sg.plan, sg.group)
+            X_ext = sg.exchange_table(X_loc)
             graph = sg.graph.with_dropedge(dropedge)
             out, Z = graph_conv_fwd_train(X_ext, graph, W.contiguous(), b.contiguous() if b is not None else None,
                                           relu)
@@ -858,6 +857,71 @@ class ShardedGraph:
     def exchange(self, X_loc: torch.Tensor) -> torch.Tensor:
         return halo_exchange(X_loc, self.plan, self.group)
 
+    # ---- halo tables reused within one forward (GraphCNNDropEdge: gcn3's
+    # input is cat[g1, g2] and g1's table was exchanged for gcn2) ----
+    halo_memo: Optional[dict] = None
+
+    def with_halo_memo(self) -> "ShardedGraph":
+        """Shallow copy (like with_dropedge; its own copies share the memo)
+        whose exchanges consult a per-forward memo: remember(X) keeps X's
+        table once exchanged, note_concat(X, parts) lets a column concat of
+        remembered tensors be assembled from their tables (only the parts
+        not yet exchanged travel).  Same rows, same values as exchanging the
+        concat itself, so every layer's output keeps its bits."""
+        sg = ShardedGraph.__new__(ShardedGraph)
+        sg.__dict__.update(self.__dict__)
+        sg.halo_memo = {"keep": {}, "tables": {}, "concat": {}}
+        return sg
+
+    @staticmethod
+    def _tkey(X: torch.Tensor):
+        """Identity of a contiguous tensor's [rows, cols] view (a (B, n, F)
+        tensor and its 2-D view are one key); None for other layouts."""
+        if not X.is_contiguous() or X.dim() == 0:
+            return None
+        return (X.data_ptr(), X._version, X.numel() // max(X.shape[-1], 1), X.shape[-1], X.dtype)
+
+    def remember(self, X: torch.Tensor) -> None:
+        k = self._tkey(X)
+        if self.halo_memo is not None and k is not None:
+            self.halo_memo["keep"][k] = X  # the reference keeps X's storage from being reused
+
+    def note_concat(self, X: torch.Tensor, parts) -> None:
+        k = self._tkey(X)
+        if self.halo_memo is not None and k is not None:
+            self.halo_memo["concat"][k] = (X, list(parts))
+
+    def clear_halo_memo(self) -> None:
+        if self.halo_memo is not None:
+            for d in self.halo_memo.values():
+                d.clear()
+
+    def exchange_table(self, X_loc: torch.Tensor) -> torch.Tensor:
+        """X_ext = [own | halo] rows of X_loc without autograd (the layers'
+        backward sends the halo gradients home themselves), through the memo
+        when one is attached."""
+        X_loc = X_loc.detach()
+        X_loc = X_loc.reshape(-1, X_loc.shape[-1])
+        memo = self.halo_memo
+        if memo is None:
+            with torch.no_grad():
+                return halo_exchange(X_loc.contiguous(), self.plan, self.group)
+        k = self._tkey(X_loc)
+        if k is None:
+            with torch.no_grad():
+                return halo_exchange(X_loc.contiguous(), self.plan, self.group)
+        hit = memo["tables"].get(k)
+        if hit is not None:
+            return hit
+        cat = memo["concat"].get(k)
+        if cat is not None:
+            return torch.cat([self.exchange_table(part.reshape(-1, part.shape[-1])) for part in cat[1]], dim=1)
+        with torch.no_grad():
+            X_ext = halo_exchange(X_loc.contiguous(), self.plan, self.group)
+        if k in memo["keep"]:
+            memo["tables"][k] = X_ext
+        return X_ext
+
     def pipeline(self, F: int, chunks: int) -> HaloPipeline:
         """The HaloPipeline of this shard for F-wide features in `chunks`
         column slices (built once, buffers reused by every call)."""
@@ -972,6 +1036,9 @@ class ShardedGraph:
         if pipeline is not None:
             raise ValueError(f"pipeline must be None or 'rows', got {pipeline!r}")
         if chunks is None:
+            if not (torch.is_grad_enabled() and X_loc.requires_grad):  # no gradient to send home: memo table
+                return graph_conv(self.exchange_table(X_loc), self.graph.with_dropedge(dropedge), layer.h_weights,
+                                  layer.bias, relu=relu)
             return graph_conv(self.exchange(X_loc), self.graph.with_dropedge(dropedge), layer.h_weights, layer.bias,
                               relu=relu)
         Z = self.aggregate(X_loc, dropedge, chunks)

@@ -305,3 +305,63 @@ def test_rows_backward_fallback_is_collective_and_p2p_uses_group_ranks():
     one-kernel path makes every rank fall back), and point-to-point peers are
     ranks of the shard's group, also under a subgroup."""
     mp.spawn(_agree_worker, args=(3, _free_port()), nprocs=3, join=True)
+
+
+def _memo_worker(rank, world, port, mode):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from grl import dist as gdist
+
+        gen = torch.Generator().manual_seed(11)
+        N, L = 40, 2
+        cols = torch.randint(0, N, (N * L * 3,), generator=gen)
+        rowptr_g = torch.arange(0, N * L * 3 + 1, 3, dtype=torch.int64)
+        rb, re = (0, 22) if rank == 0 else (22, N)
+        e0, e1 = int(rowptr_g[rb * L]), int(rowptr_g[re * L])
+        sg = gdist.ShardedGraph.__new__(gdist.ShardedGraph)  # the exchange needs only the plan (no device graph)
+        sg.group, sg.plan = None, build_halo_plan(cols[e0:e1], rb, re, None, mode=mode)
+        n = re - rb
+        g1 = torch.randn(n, 8, generator=torch.Generator().manual_seed(100 + rank))
+        g2 = torch.randn(n, 8, generator=torch.Generator().manual_seed(200 + rank))
+        calls = {"n": 0}
+        orig_ag, orig_a2a = gdist.all_gather_into, gdist.all_to_all_v
+
+        def count_ag(*a, **k):
+            calls["n"] += 1
+            return orig_ag(*a, **k)
+
+        def count_a2a(*a, **k):
+            calls["n"] += 1
+            return orig_a2a(*a, **k)
+
+        gdist.all_gather_into, gdist.all_to_all_v = count_ag, count_a2a
+        try:
+            x3 = torch.cat([g1, g2], dim=-1)
+            want = sg.exchange(x3)  # the concat exchanged as itself
+            m = sg.with_halo_memo().with_dropedge(None)  # copies share the memo
+            m.remember(g1)
+            t1 = m.exchange_table(g1.view(1, n, 8))  # a 3-D view is the same tensor
+            assert torch.equal(t1, sg.exchange(g1))
+            m.note_concat(x3, (g1, g2))
+            before = calls["n"]
+            t3 = m.exchange_table(x3)
+            assert calls["n"] == before + 1  # only g2's rows travelled
+            assert torch.equal(t3, want)
+            m.clear_halo_memo()
+            before = calls["n"]
+            assert torch.equal(m.exchange_table(x3), want) and calls["n"] == before + 1  # no memo: x3 itself
+            assert sg.halo_memo is None and torch.equal(sg.exchange_table(g1), t1)  # the original has no memo
+        finally:
+            gdist.all_gather_into, gdist.all_to_all_v = orig_ag, orig_a2a
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["dense", "sparse"])
+def test_halo_memo_reuses_concat_parts(mode):
+    """GraphCNNDropEdge's gcn3 input cat[g1, g2] on a shard: with the
+    per-forward halo memo only g2's rows travel (g1's table came for gcn2),
+    and the assembled table equals the concat's own exchange."""
+    mp.spawn(_memo_worker, args=(2, _free_port(), mode), nprocs=2, join=True)
