@@ -825,6 +825,9 @@ __global__ __launch_bounds__(256) void attn_fwd_x6_kernel(AttnArgs a) {
 // and H two.  Same products, same order of every sum as attn_fwd_x6_kernel,
 // hence the same bits.  The last block's partial-key mask is applied in its
 // own instantiation of the iteration (MASK), outside the interleaved body.
+#ifndef GRL_ATTN_HU2
+#define GRL_ATTN_HU2 1
+#endif
 template <int DKP, int NT, bool SPLIT, int NW = 4>
 __global__ __launch_bounds__(64 * NW) void attn_fwd_x6p_kernel(AttnArgs a) {
   constexpr int DV = NT * 32, KC = DKP / 16;
@@ -950,8 +953,12 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_x6p_kernel(AttnArgs a) {
   }
   float alpha = 1.0f;
   // iteration it: block it's P.H with block it+1's softmax in the same body
-  auto iteration = [&](int it, auto masked) {
+  // hs: the H stage (it & 1) as a constant (GRL_ATTN_HU2 unrolls the loop by
+  // two): the 8 NT transposed H reads then take it as an immediate offset
+  // instead of an address add each; -1 = the stage at run time
+  auto iteration = [&](int it, auto masked, auto hs) {
     constexpr bool MASK = decltype(masked)::value;
+    constexpr int HS = decltype(hs)::value;
     const int64_t k0 = k_lo + 32 * (int64_t)it;
     // block it's H and block it+1's K landed; every wave is done with the
     // stages the next DMAs overwrite (H of block it-1, K of block it-1)
@@ -966,7 +973,8 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_x6p_kernel(AttnArgs a) {
     // block it's P.H in 2 NT groups of 6 MFMAs; block it+1's softmax cut into
     // 7 pieces placed after groups 1 .. 2 NT - 1 (group 0 covers the score
     // MFMAs' latency), each group fenced so its VALU fills that group's gaps
-    const uint16_t* Hp = Hp_s + (it & 1) * HST;
+    typedef __attribute__((address_space(3))) uint16_t lds_u16;
+    const lds_u16* Hp = (const lds_u16*)Hp_s + (HS < 0 ? (it & 1) : HS) * HST;
     float mn = 0.0f, an = 1.0f, ps = 0.0f;
     auto piece = [&](int pc) {
       if (pc == 0) {
@@ -1014,10 +1022,10 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_x6p_kernel(AttnArgs a) {
       for (int pl = 0; pl < 3; ++pl) {
         typedef __attribute__((address_space(3))) ai16x4_t lds_v4;
         const int key0 = kappa(8 * u + trq, h), key1 = kappa(8 * u + 4 + trq, h);
-        const uint16_t* p0 = &Hp[pl * HPL + hswz<DV>(key0, t * 32 + trc)];
-        const uint16_t* p1 = &Hp[pl * HPL + hswz<DV>(key1, t * 32 + trc)];
-        const ai16x4_t x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(uintptr_t)(uint32_t)(uintptr_t)p0);
-        const ai16x4_t x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(uintptr_t)(uint32_t)(uintptr_t)p1);
+        const lds_u16* p0 = Hp + pl * HPL + hswz<DV>(key0, t * 32 + trc);
+        const lds_u16* p1 = Hp + pl * HPL + hswz<DV>(key1, t * 32 + trc);
+        const ai16x4_t x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)p0);
+        const ai16x4_t x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)p1);
         const ai16x8_t v = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
         hp[pl] = __builtin_bit_cast(abf16x8_t, v);
       }
@@ -1034,13 +1042,20 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_x6p_kernel(AttnArgs a) {
 #pragma unroll
       for (int pl = 0; pl < 3; ++pl) pp[u][pl] = pn[u][pl];
   };
+  using HRun = std::integral_constant<int, -1>;
   int it = 0;
-  for (; it + 2 < nblk; ++it) iteration(it, std::false_type{});
+#if GRL_ATTN_HU2
+  for (; it + 3 < nblk; it += 2) {  // it even: H stages 0, 1
+    iteration(it, std::false_type{}, std::integral_constant<int, 0>{});
+    iteration(it + 1, std::false_type{}, std::integral_constant<int, 1>{});
+  }
+#endif
+  for (; it + 2 < nblk; ++it) iteration(it, std::false_type{}, HRun{});
   if (it + 1 < nblk) {
     if (partial)
-      iteration(it, std::true_type{});
+      iteration(it, std::true_type{}, HRun{});
     else
-      iteration(it, std::false_type{});
+      iteration(it, std::false_type{}, HRun{});
     ++it;
   }
   // the last block: its P.H only
