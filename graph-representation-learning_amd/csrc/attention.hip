@@ -828,6 +828,7 @@ __global__ __launch_bounds__(256) void attn_fwd_x6_kernel(AttnArgs a) {
 #ifndef GRL_ATTN_HU2
 #define GRL_ATTN_HU2 1
 #endif
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
 template <int DKP, int NT, bool SPLIT, int NW = 4>
 __global__ __launch_bounds__(64 * NW) void attn_fwd_x6p_kernel(AttnArgs a) {
   constexpr int DV = NT * 32, KC = DKP / 16;
@@ -973,7 +974,6 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_x6p_kernel(AttnArgs a) {
     // block it's P.H in 2 NT groups of 6 MFMAs; block it+1's softmax cut into
     // 7 pieces placed after groups 1 .. 2 NT - 1 (group 0 covers the score
     // MFMAs' latency), each group fenced so its VALU fills that group's gaps
-    typedef __attribute__((address_space(3))) uint16_t lds_u16;
     const lds_u16* Hp = (const lds_u16*)Hp_s + (HS < 0 ? (it & 1) : HS) * HST;
     float mn = 0.0f, an = 1.0f, ps = 0.0f;
     auto piece = [&](int pc) {
@@ -1112,6 +1112,15 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_x6p_kernel(AttnArgs a) {
 // ds_read_b128 row reads and the ds_read_b64_tr_b16 reads of 4 consecutive
 // rows.  The 32-column planes (K, Q; dk padded with zeros) are read
 // transposed over 4 consecutive rows of 64 B: conflict-free as they lie.
+// tr8 on LDS-space pointers: constant offsets fold into the reads' immediates
+__device__ __forceinline__ abf16x8_t tr8s(const lds_u16* p0, const lds_u16* p1) {
+  typedef __attribute__((address_space(3))) ai16x4_t lds_v4;
+  const ai16x4_t x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)p0);
+  const ai16x4_t x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)p1);
+  const ai16x8_t v = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
+  return __builtin_bit_cast(abf16x8_t, v);
+}
+
 __device__ __forceinline__ abf16x8_t tr8(const uint16_t* p0, const uint16_t* p1) {
   typedef __attribute__((address_space(3))) ai16x4_t lds_v4;
   const ai16x4_t x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(uintptr_t)(uint32_t)(uintptr_t)p0);
@@ -1316,10 +1325,15 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_kv_x6_kernel(AttnArg
   fetch_stats(q_lo);
   const int trq = (lane & 15) >> 2, trc = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
 
-  for (int64_t q0 = q_lo; q0 < q_hi; q0 += 32) {
-    const int stg = PRE ? (int)(((q0 - q_lo) >> 5) & 1) : 0;
+  // one query block; stc: its stage as a constant (the PRE dH loop unrolled
+  // by two under GRL_ATTN_HU2: transposed reads at immediate LDS offsets), -1 = at run time
+  auto block = [&](int64_t q0, auto stc) {
+    constexpr int SC = decltype(stc)::value;
+    const int stg = SC >= 0 ? SC : (PRE ? (int)(((q0 - q_lo) >> 5) & 1) : 0);
     uint16_t* Qp = Qp_s + stg * 3 * 1024;
     uint16_t* Op = Op_s + stg * 3 * 4096;
+    const lds_u16* Qp3 = (const lds_u16*)Qp_s + stg * 3 * 1024;
+    const lds_u16* Op3 = (const lds_u16*)Op_s + stg * 3 * 4096;
     float* Ms = Ms_s + stg * 32;
     float* Ds = Ds_s + stg * 32;
     if (!PRE) {
@@ -1371,7 +1385,7 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_kv_x6_kernel(AttnArg
           abf16x8_t ot[3];
 #pragma unroll
           for (int pl = 0; pl < 3; ++pl)
-            ot[pl] = tr8(&Op[pl * 4096 + swz128(r0, t * 32 + trc)], &Op[pl * 4096 + swz128(r1, t * 32 + trc)]);
+            ot[pl] = tr8s(Op3 + pl * 4096 + swz128(r0, t * 32 + trc), Op3 + pl * 4096 + swz128(r1, t * 32 + trc));
           MFMA6(acc[t], ot[0], ot[1], ot[2], pp[u][0], pp[u][1], pp[u][2]);
         }
     } else {
@@ -1396,11 +1410,24 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_kv_x6_kernel(AttnArg
         const int r0 = kappa(8 * u + trq, h), r1 = kappa(8 * u + 4 + trq, h);
         abf16x8_t qt[3];
 #pragma unroll
-        for (int pl = 0; pl < 3; ++pl) qt[pl] = tr8(&Qp[pl * 1024 + r0 * 32 + trc], &Qp[pl * 1024 + r1 * 32 + trc]);
+        for (int pl = 0; pl < 3; ++pl) qt[pl] = tr8s(Qp3 + pl * 1024 + r0 * 32 + trc, Qp3 + pl * 1024 + r1 * 32 + trc);
         MFMA6(acc[0], qt[0], qt[1], qt[2], dsp[u][0], dsp[u][1], dsp[u][2]);
       }
     }
     if constexpr (!PRE) __syncthreads();
+    };
+#if GRL_ATTN_HU2
+  if constexpr (PRE && WANT_H) {  // (the dK form has no VGPRs left for the unrolled pair)
+    int64_t q0 = q_lo;
+    for (; q0 + 32 < q_hi; q0 += 64) {
+      block(q0, std::integral_constant<int, 0>{});
+      block(q0 + 32, std::integral_constant<int, 1>{});
+    }
+    if (q0 < q_hi) block(q0, std::integral_constant<int, 0>{});
+  } else
+#endif
+  {
+    for (int64_t q0 = q_lo; q0 < q_hi; q0 += 32) block(q0, std::integral_constant<int, -1>{});
   }
   if (kv) {  // query split: partial dH / dK into slab blockIdx.z (summed in split order afterwards)
     const int64_t rows = (int64_t)gridDim.y * N;
