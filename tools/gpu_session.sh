@@ -1,11 +1,11 @@
 #!/bin/bash
 # One GPU-box session: each GPU step runs under its own time limit; the
-# session stops at the first step that faults, aborts, segfaults or times
-# out (exit 124/134/137/139 or a signal).  Ordinary test failures (pytest
-# rc 1) do not stop later steps.  Usage: tools/gpu_session.sh STEP...
+# session stops at the first step that exits nonzero -- a fault, abort,
+# segfault or time limit, and also an ordinary failure (the steps are
+# chained as with &&).  Usage: tools/gpu_session.sh STEP...
 #   steps: tests smoke bench bench_extras bench_drop bench_c5 bench_c5s prof_bench prof_fwd prof_bwd
 #          prof_linear prof_layer prof_attn prof_c1 pmc_fwd_fetch pmc_fwd_write pmc_list pmc_linear_mfma
-#          pmc_fwd_tlb pmc_c4_tlb
+#          pmc_fwd_tlb pmc_c4_tlb; round 4: ab_dw_u2 ab_attn_hu tests_r4 pmc_infer_l2 pmc_wide_mfma prof_wide
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
 OUT=gpurun_out
@@ -21,6 +21,7 @@ run() {  # name seconds cmd...
   echo "=== $name rc=$rc"
   tail -n 5 "$OUT/$name.log"
   if fatal $rc; then echo "FATAL in $name (rc=$rc): stopping session"; exit $rc; fi
+  if [ "$rc" -ne 0 ]; then echo "$name failed (rc=$rc): stopping session"; exit $rc; fi
   return 0
 }
 
@@ -143,6 +144,20 @@ for step in "$@"; do
     ab_fused_dq) rm -f gpurun_out/ab_fused_dq.log; run ab_fused_dq 900 tools/ab_fused_dq.sh ;;
     prof_attn_fused) run prof_attn_fused 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_attn_fused" -o run \
                   --output-format csv -- python tools/probe_attn.py 100000 ;;
+    ab_dw_u2) rm -f gpurun_out/ab_dw_env.log; run ab_dw_u2 300 tools/ab_dw_env.sh GRL_X6T_U2 ;;
+    ab_attn_hu) export ATTN_N="100000"; rm -f gpurun_out/ab_attn_lib.log; run ab_attn_hu 400 tools/ab_attn_lib.sh attn_hu0 ;;
+    tests_r4) run pytest_gpu_r4 900 python -u -m pytest tests/test_gpu_attention.py tests/test_gpu_procedure_golden.py \
+                  tests/test_gpu_warper.py tests/test_gpu_dp.py tests/test_gpu_sharded_model.py tests/test_gpu_rccl.py \
+                  tests/test_gpu_graph_capture.py -m gpu -q -rf --timeout 300 --timeout-method thread ;;
+    pmc_infer_l2) run pmc_infer_l2 300 timeout -s KILL 240 rocprofv3 --pmc TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum \
+                  GRBM_GUI_ACTIVE --kernel-trace -d "$OUT/pmc_infer_l2" -o run --output-format csv \
+                  -- python bench.py --only infer --steps 5 --warmup 1 ;;
+    pmc_wide_mfma) export PROBE_QUICK=1 PROBE_SHAPES=512x256,512x512; run pmc_wide_mfma 300 timeout -s KILL 240 \
+                  rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CU_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA \
+                  --kernel-trace -d "$OUT/pmc_wide_mfma" -o run --output-format csv -- python tools/probe_wide.py; \
+                  unset PROBE_QUICK PROBE_SHAPES ;;
+    prof_wide) export PROBE_SHAPES=512x256,512x512,1024x512; run prof_wide 400 rocprofv3 --kernel-trace --stats \
+                  -d "$OUT/prof_wide" -o run --output-format csv -- python tools/probe_wide.py; unset PROBE_SHAPES ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
