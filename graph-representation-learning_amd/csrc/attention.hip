@@ -1476,6 +1476,9 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_kv_x6_kernel(AttnArg
 // deterministic.  The scores are natural-scale here (K is shared with dQ)
 // and p = 2^(fma(s, log2 e, -lse2)): the same instruction count as the
 // base-2 kernels' v_sub.  Q comes as 16-wide planes.
+#ifndef GRL_ATTN_TPLANES
+#define GRL_ATTN_TPLANES 1
+#endif
 constexpr int KQ_WAVES = 8, KQ_KEYS = 32 * KQ_WAVES;
 template <bool SPLIT>
 __global__ __launch_bounds__(64 * KQ_WAVES, 1) void attn_bwd_kq_x6_kernel(AttnArgs a) {
@@ -1588,7 +1591,6 @@ __global__ __launch_bounds__(64 * KQ_WAVES, 1) void attn_bwd_kq_x6_kernel(AttnAr
     }
     abf16x8_t dsp[2][3];
     reg_planes(s, dsp);
-    f32x16 dt = zero16();  // dS transposed: lanes = queries, registers = keys kappa(r, h)
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const int r0 = kappa(8 * u + trq, h), r1 = kappa(8 * u + 4 + trq, h);
@@ -1597,6 +1599,34 @@ __global__ __launch_bounds__(64 * KQ_WAVES, 1) void attn_bwd_kq_x6_kernel(AttnAr
       for (int pl = 0; pl < 3; ++pl)
         qt[pl] = tr8(&Qp[pl * 512 + r0 * 16 + (trc & 15)], &Qp[pl * 512 + r1 * 16 + (trc & 15)]);
       MFMA6(acc, qt[0], qt[1], qt[2], dsp[u][0], dsp[u][1], dsp[u][2]);  // dK^T += Q^T dS
+    }
+    // dS transposed (lanes = queries, registers = keys kappa(r, h)) PLANE BY PLANE:
+    // each transposed element is one plane value times 1 plus zeros, so it is
+    // that bf16 value exactly and packs back without a split -- the planes a
+    // split of the transposed sum hi + mid + lo (== dS, exact) would give
+#if GRL_ATTN_TPLANES
+    abf16x8_t dtp[2][3];
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl) {
+      f32x16 dt = zero16();
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        ai16x8_t pv;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pv[j] = u == perm_u ? onehot[j] : (short)0;
+        dt = __builtin_amdgcn_mfma_f32_32x32x16_bf16(dsp[u][pl], __builtin_bit_cast(abf16x8_t, pv), dt, 0, 0, 0);
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+        dtp[u][pl] = __builtin_bit_cast(abf16x8_t, make_uint4(apack(dt[8 * u], dt[8 * u + 1]),
+                                                              apack(dt[8 * u + 2], dt[8 * u + 3]),
+                                                              apack(dt[8 * u + 4], dt[8 * u + 5]),
+                                                              apack(dt[8 * u + 6], dt[8 * u + 7])));
+    }
+#else
+    f32x16 dt = zero16();
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
       ai16x8_t pv;
 #pragma unroll
       for (int j = 0; j < 8; ++j) pv[j] = u == perm_u ? onehot[j] : (short)0;
@@ -1606,6 +1636,7 @@ __global__ __launch_bounds__(64 * KQ_WAVES, 1) void attn_bwd_kq_x6_kernel(AttnAr
     }
     abf16x8_t dtp[2][3];
     reg_planes(dt, dtp);
+#endif
     f32x16 dq = zero16();  // dQ_blk[query][d] over this wave's 32 keys (columns d >= 16 discarded)
 #pragma unroll
     for (int u = 0; u < 2; ++u) {

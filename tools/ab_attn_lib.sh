@@ -4,6 +4,8 @@
 #   tools/ab_attn_lib.sh NAME...   (diag/libgrl_NAME.so built by tools/build_diag.sh)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 L=graph-representation-learning_amd/grl
+rm -f /tmp/ab_attn_ref.pt.*
+export AB_SAVE=/tmp/ab_attn_ref.pt  # out and grads compared bitwise with the first (default) library's
 for rep in 1 2; do
   for lib in $L/libgrl.so $(for n in "$@"; do echo $L/diag/libgrl_$n.so; done); do
     echo "$lib" >> gpurun_out/ab_attn_lib.log

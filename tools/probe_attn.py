@@ -32,5 +32,18 @@ for N in ([int(x) for x in sys.argv[1:]] or (2048, 16384, 65536, 131072)):
     ms_fb = timeit(lambda: node_self_attention(*leaves).sum().backward(), 3)
     # backward = 2 S recomputes (2*N^2*dk each) + 2 dP (2*N^2*dv each) + dQ, dK (2*N^2*dk each) + dH (2*N^2*dv)
     bflops = 2.0 * N * N * (4 * dk + 3 * dv)
+    same = None
+    ref_path = os.environ.get("AB_SAVE")
+    if ref_path:  # bits of out and every gradient against the first library's (A/B of builds)
+        for t in leaves:
+            t.grad = None
+        out = node_self_attention(*leaves)
+        out.backward(torch.ones_like(out))
+        got = torch.cat([out.detach().flatten()] + [t.grad.flatten() for t in leaves]).cpu()
+        path = f"{ref_path}.{N}"
+        if os.path.exists(path):
+            same = bool(torch.equal(torch.load(path, weights_only=True), got))
+        else:
+            torch.save(got, path)
     print(f"N={N:7d} fwd {ms:9.3f} ms {flops / ms / 1e9:7.1f} TFLOP/s | fwd+bwd {ms_fb:9.3f} ms "
-          f"{(flops + bflops) / ms_fb / 1e9:7.1f} TFLOP/s", flush=True)
+          f"{(flops + bflops) / ms_fb / 1e9:7.1f} TFLOP/s bitwise_vs_first={same}", flush=True)
