@@ -196,10 +196,12 @@ RANGED = [(1, 20_000, 16, 128, (0, 7000, 13_003, 20_000)), (2, 3000, 16, 100, (0
 def test_query_ranges_partition_the_attention(B, N, dk, dv, cuts, mode, monkeypatch):
     """grl_node_attention_fwd_rows / _bwd_rows (a node-range shard's queries
     against every key, grl.dist sharded_node_attention): over a partition of
-    the queries, each range's output rows match the float64 attention, the
+    the queries, each range's output rows match the float64 attention (the
+    unranged forward's tolerance: 1e-5, and the fp32 1e-4 at 20k keys), the
     ranges' dQ rows are the whole dQ's, and the ranges' dK / dH partials add
-    up (in range order) to the whole dK / dH -- within 1e-5 of fp64.  Rows
-    outside a range stay zero."""
+    up (in range order) to the whole dK / dH -- within the unranged
+    backward's tolerance per range (each range's partial is one more fp32
+    rounding of the sum).  Rows outside a range stay zero."""
     from grl.ops import node_attention_backward
 
     _set_mode(mode, monkeypatch)
@@ -212,15 +214,18 @@ def test_query_ranges_partition_the_attention(B, N, dk, dv, cuts, mode, monkeypa
     dK_sum, dH_sum = torch.zeros_like(K), torch.zeros_like(H)
     for q0, q1 in zip(cuts[:-1], cuts[1:]):
         out, onorm, rmax, rsum = node_attention_forward(Q, K, H, V, gamma, stats=True, q_range=(q0, q1))
-        torch.testing.assert_close(out[:, q0:q1].double(), ref[:, q0:q1].detach(), rtol=1e-5, atol=1e-5)
+        tol = 1e-4 if N >= 20_000 else 1e-5  # as test_forward_matches_fp64 / test_large_n_rows_sampled
+        torch.testing.assert_close(out[:, q0:q1].double(), ref[:, q0:q1].detach(), rtol=tol, atol=tol)
         assert not bool(out[:, :q0].any()) and not bool(out[:, q1:].any())
         dQ, dK, dH = node_attention_backward(Q, K, H, gamma, onorm, rmax, rsum, dout, q_range=(q0, q1))
         assert not bool(dQ[:, :q0].any()) and not bool(dQ[:, q1:].any())
         dQ_sum += dQ
         dK_sum += dK
         dH_sum += dH
+    ranges = len(cuts) - 1
     for got, want in ((dQ_sum, Qd.grad), (dK_sum, Kd.grad), (dH_sum, Hd.grad)):
-        torch.testing.assert_close(got.double(), want, rtol=1e-5, atol=1e-5 * max(1.0, float(want.abs().max())))
+        scale = float(want.abs().max()) + 1.0  # test_backward_matches_fp64's bound, per range
+        torch.testing.assert_close(got.double(), want, rtol=1e-4, atol=2e-5 * scale * ranges)
 
 
 @pytest.mark.parametrize("B,N,budget_x", [(1, 20_000, 23), (2, 9000, 7), (1, 4500, 1)])
@@ -243,9 +248,10 @@ def test_fused_dq_key_chunks_are_bitwise(B, N, budget_x, monkeypatch):
 
 def test_half_million_nodes_forward_backward():
     """B = 1, N = 500k (the fused pass's dQ slabs, 62 GB in one piece, run in
-    key chunks): fwd + bwd run; out and dQ on sampled queries within 1e-5 of
-    float64 (their softmax statistics recomputed in float64 over every key);
-    dK / dH equal the separate-dQ-kernel path's within 1e-5 of their scale."""
+    key chunks): fwd + bwd run; out on sampled queries within 1e-5 of float64
+    (their softmax statistics recomputed in float64 over every key), dQ within
+    the fp32 1e-4 of its scale (sums over 500k keys); dK / dH equal the
+    separate-dQ-kernel path's within 1e-5 of their scale."""
     import os
 
     from grl.ops import node_attention_backward
@@ -265,7 +271,7 @@ def test_half_million_nodes_forward_backward():
     dP = dO @ Hd.T
     D = (dO * o).sum(-1, keepdim=True)
     dQ_ref = (p * (dP - D)) @ Kd
-    torch.testing.assert_close(dQ[0, rows].double(), dQ_ref, rtol=1e-5, atol=1e-5 * float(dQ_ref.abs().max()))
+    torch.testing.assert_close(dQ[0, rows].double(), dQ_ref, rtol=1e-4, atol=1e-4 * float(dQ_ref.abs().max()))
     os.environ["GRL_ATTN_FUSED_DQ"] = "0"
     try:
         _, dK2, dH2 = node_attention_backward(Q, K, H, gamma, onorm, rmax, rsum, dout)

@@ -24,6 +24,7 @@ def timeit(fn, n=5):
 dev = torch.device("cuda:0")
 for N in ([int(x) for x in sys.argv[1:]] or (2048, 16384, 65536, 131072)):
     dk, dv = 16, 128
+    torch.manual_seed(N)  # the same inputs in every library's run (AB_SAVE bit check)
     Q, K = torch.relu(torch.randn(1, N, dk, device=dev)), torch.relu(torch.randn(1, N, dk, device=dev))
     H, V, g = torch.relu(torch.randn(1, N, dv, device=dev)), torch.randn(1, N, dv, device=dev), torch.randn(dv, device=dev)
     flops = 2.0 * N * N * (dk + dv)
