@@ -829,6 +829,9 @@ __global__ __launch_bounds__(256) void attn_fwd_x6_kernel(AttnArgs a) {
 #define GRL_ATTN_HU2 1
 #endif
 typedef __attribute__((address_space(3))) uint16_t lds_u16;
+#ifndef GRL_ATTN_PIN_PN
+#define GRL_ATTN_PIN_PN 1
+#endif
 template <int DKP, int NT, bool SPLIT, int NW = 4>
 __global__ __launch_bounds__(64 * NW) void attn_fwd_x6p_kernel(AttnArgs a) {
   constexpr int DV = NT * 32, KC = DKP / 16;
@@ -1040,7 +1043,14 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_x6p_kernel(AttnArgs a) {
 #pragma unroll
     for (int u = 0; u < 2; ++u)
 #pragma unroll
-      for (int pl = 0; pl < 3; ++pl) pp[u][pl] = pn[u][pl];
+      for (int pl = 0; pl < 3; ++pl) {
+#if GRL_ATTN_PIN_PN
+        // keep block it+1's split in this body: unrolled, LLVM would sink it
+        // into the next body (where its MFMAs use it), undoing the interleave
+        asm volatile("" : "+v"(pn[u][pl]));
+#endif
+        pp[u][pl] = pn[u][pl];
+      }
   };
   using HRun = std::integral_constant<int, -1>;
   int it = 0;
