@@ -832,13 +832,23 @@ typedef __attribute__((address_space(3))) uint16_t lds_u16;
 #ifndef GRL_ATTN_PIN_PN
 #define GRL_ATTN_PIN_PN 1
 #endif
+#ifndef GRL_ATTN_B2
+#define GRL_ATTN_B2 1
+#endif
 template <int DKP, int NT, bool SPLIT, int NW = 4>
 __global__ __launch_bounds__(64 * NW) void attn_fwd_x6p_kernel(AttnArgs a) {
   constexpr int DV = NT * 32, KC = DKP / 16;
   constexpr int KPL = 32 * DKP, HPL = 32 * DV;  // bf16 per plane
   constexpr int KST = 3 * KPL, HST = 3 * HPL;   // one stage: the three planes
-  __shared__ __attribute__((aligned(16))) uint16_t Kp_s[3 * KST];
-  __shared__ __attribute__((aligned(16))) uint16_t Hp_s[2 * HST];
+  // B2 (GRL_ATTN_B2, 8-wave workgroups): one barrier per TWO key blocks --
+  // four H and four K stages, the next pair's DMAs issued at the pair's
+  // barrier (108 KB of LDS at dv = 128; the 8-wave form runs one workgroup
+  // per CU anyway).  Else one barrier per block, H 2 / K 3 stages deep.
+  constexpr bool B2 = GRL_ATTN_B2 && NW == 8 && NT <= 4;  // dv = 256: 4 H stages exceed the LDS
+  __shared__ __attribute__((aligned(16))) uint16_t Kp_s[(B2 ? 4 : 3) * KST];
+  __shared__ __attribute__((aligned(16))) uint16_t Hp_s[(B2 ? 4 : 2) * HST];
+  auto hstage = [](int j) { return B2 ? (j & 3) : (j & 1); };
+  auto kstage = [](int j) { return B2 ? (j & 3) : (j % 3); };
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, l32 = lane & 31, h = lane >> 5;
   const int64_t N = a.N, b = blockIdx.y;
   const float* Qb = a.Q + b * N * a.dk;
@@ -871,6 +881,8 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_x6p_kernel(AttnArgs a) {
   kd.issue(k_lo, N, Kp_s, wave, lane);
   hd.issue(k_lo, N, Hp_s, wave, lane);
   if (nblk > 1) kd.issue(k_lo + 32, N, Kp_s + KST, wave, lane);
+  if (B2 && nblk > 1) hd.issue(k_lo + 32, N, Hp_s + HST, wave, lane);  // the first pair's H and
+  if (B2 && nblk > 2) kd.issue(k_lo + 64, N, Kp_s + 2 * KST, wave, lane);  // K(2), before its barrier
   const int trq = (lane & 15) >> 2;
   const int trc = 16 * ((lane >> 4) & 1) + 4 * (lane & 3);
 
@@ -964,20 +976,33 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_x6p_kernel(AttnArgs a) {
     constexpr bool MASK = decltype(masked)::value;
     constexpr int HS = decltype(hs)::value;
     const int64_t k0 = k_lo + 32 * (int64_t)it;
-    // block it's H and block it+1's K landed; every wave is done with the
-    // stages the next DMAs overwrite (H of block it-1, K of block it-1)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (it + 1 < nblk) hd.issue(k0 + 32, N, Hp_s + ((it + 1) & 1) * HST, wave, lane);
-    if (it + 2 < nblk) kd.issue(k0 + 64, N, Kp_s + ((it + 2) % 3) * KST, wave, lane);
+    if constexpr (B2) {
+      // even it: blocks it, it+1's H and K(it+1), K(it+2) landed; every wave is
+      // done with blocks it-2, it-1, whose stages the next pair's DMAs take
+      if ((HS >= 0 ? HS : it) % 2 == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (it + 2 < nblk) hd.issue(k0 + 64, N, Hp_s + hstage(it + 2) * HST, wave, lane);
+        if (it + 3 < nblk) hd.issue(k0 + 96, N, Hp_s + hstage(it + 3) * HST, wave, lane);
+        if (it + 3 < nblk) kd.issue(k0 + 96, N, Kp_s + kstage(it + 3) * KST, wave, lane);
+        if (it + 4 < nblk) kd.issue(k0 + 128, N, Kp_s + kstage(it + 4) * KST, wave, lane);
+      }
+    } else {
+      // block it's H and block it+1's K landed; every wave is done with the
+      // stages the next DMAs overwrite (H of block it-1, K of block it-1)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (it + 1 < nblk) hd.issue(k0 + 32, N, Hp_s + hstage(it + 1) * HST, wave, lane);
+      if (it + 2 < nblk) kd.issue(k0 + 64, N, Kp_s + kstage(it + 2) * KST, wave, lane);
+    }
     rescale(alpha);
-    f32x16 sc = scores(Kp_s + ((it + 1) % 3) * KST);
+    f32x16 sc = scores(Kp_s + (B2 && HS >= 0 ? (HS + 1) & 3 : kstage(it + 1)) * KST);
     if constexpr (MASK) mask(sc, k0 + 32);
     abf16x8_t pn[2][3];
     // block it's P.H in 2 NT groups of 6 MFMAs; block it+1's softmax cut into
     // 7 pieces placed after groups 1 .. 2 NT - 1 (group 0 covers the score
     // MFMAs' latency), each group fenced so its VALU fills that group's gaps
-    const lds_u16* Hp = (const lds_u16*)Hp_s + (HS < 0 ? (it & 1) : HS) * HST;
+    const lds_u16* Hp = (const lds_u16*)Hp_s + (HS < 0 ? hstage(it) : HS) * HST;
     float mn = 0.0f, an = 1.0f, ps = 0.0f;
     auto piece = [&](int pc) {
       if (pc == 0) {
@@ -1055,9 +1080,18 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_x6p_kernel(AttnArgs a) {
   using HRun = std::integral_constant<int, -1>;
   int it = 0;
 #if GRL_ATTN_HU2
-  for (; it + 3 < nblk; it += 2) {  // it even: H stages 0, 1
-    iteration(it, std::false_type{}, std::integral_constant<int, 0>{});
-    iteration(it + 1, std::false_type{}, std::integral_constant<int, 1>{});
+  if constexpr (B2) {
+    for (; it + 5 < nblk; it += 4) {  // it % 4 == 0: H stages 0..3
+      iteration(it, std::false_type{}, std::integral_constant<int, 0>{});
+      iteration(it + 1, std::false_type{}, std::integral_constant<int, 1>{});
+      iteration(it + 2, std::false_type{}, std::integral_constant<int, 2>{});
+      iteration(it + 3, std::false_type{}, std::integral_constant<int, 3>{});
+    }
+  } else {
+    for (; it + 3 < nblk; it += 2) {  // it even: H stages 0, 1
+      iteration(it, std::false_type{}, std::integral_constant<int, 0>{});
+      iteration(it + 1, std::false_type{}, std::integral_constant<int, 1>{});
+    }
   }
 #endif
   for (; it + 2 < nblk; ++it) iteration(it, std::false_type{}, HRun{});
@@ -1072,7 +1106,7 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_x6p_kernel(AttnArgs a) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   rescale(alpha);
-  pv(Hp_s + (it & 1) * HST, pp);
+  pv(Hp_s + hstage(it) * HST, pp);
 
   if (SPLIT && q < a.q1) {  // key split: unnormalised partials, combined by attn_fwd_combine_kernel
     const int64_t rows = (int64_t)gridDim.y * N, row = b * N + q, zs = blockIdx.z;

@@ -145,7 +145,7 @@ for step in "$@"; do
     prof_attn_fused) run prof_attn_fused 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_attn_fused" -o run \
                   --output-format csv -- python tools/probe_attn.py 100000 ;;
     ab_dw_u2) rm -f gpurun_out/ab_dw_env.log; run ab_dw_u2 300 tools/ab_dw_env.sh GRL_X6T_U2 ;;
-    ab_attn_hu) export ATTN_N="100000"; rm -f gpurun_out/ab_attn_lib.log; run ab_attn_hu 500 tools/ab_attn_lib.sh attn_pin0 attn_hu0 attn_r3 ;;
+    ab_attn_hu) export ATTN_N="100000"; rm -f gpurun_out/ab_attn_lib.log; run ab_attn_hu 500 tools/ab_attn_lib.sh attn_b20 attn_pin0 attn_hu0 attn_r3 ;;
     tests_r4) run pytest_gpu_r4 900 python -u -m pytest tests/test_gpu_attention.py tests/test_gpu_procedure_golden.py \
                   tests/test_gpu_warper.py tests/test_gpu_dp.py tests/test_gpu_sharded_model.py tests/test_gpu_rccl.py \
                   tests/test_gpu_graph_capture.py -m gpu -q -rf --timeout 300 --timeout-method thread ;;
