@@ -214,7 +214,8 @@ def test_query_ranges_partition_the_attention(B, N, dk, dv, cuts, mode, monkeypa
     dK_sum, dH_sum = torch.zeros_like(K), torch.zeros_like(H)
     for q0, q1 in zip(cuts[:-1], cuts[1:]):
         out, onorm, rmax, rsum = node_attention_forward(Q, K, H, V, gamma, stats=True, q_range=(q0, q1))
-        tol = 1e-4 if N >= 20_000 else 1e-5  # as test_forward_matches_fp64 / test_large_n_rows_sampled
+        # as test_forward_matches_fp64 (N <= 2048) / test_large_n_rows_sampled (the fp32 1e-4 beyond)
+        tol = 1e-4 if N > 2048 and (N >= 20_000 or mode == "f32") else 1e-5
         torch.testing.assert_close(out[:, q0:q1].double(), ref[:, q0:q1].detach(), rtol=tol, atol=tol)
         assert not bool(out[:, :q0].any()) and not bool(out[:, q1:].any())
         dQ, dK, dH = node_attention_backward(Q, K, H, gamma, onorm, rmax, rsum, dout, q_range=(q0, q1))
@@ -225,7 +226,8 @@ def test_query_ranges_partition_the_attention(B, N, dk, dv, cuts, mode, monkeypa
     ranges = len(cuts) - 1
     for got, want in ((dQ_sum, Qd.grad), (dK_sum, Kd.grad), (dH_sum, Hd.grad)):
         scale = float(want.abs().max()) + 1.0  # test_backward_matches_fp64's bound, per range
-        torch.testing.assert_close(got.double(), want, rtol=1e-4, atol=2e-5 * scale * ranges)
+        per = 1e-4 if mode == "f32" and N > 2048 else 2e-5  # the fp32-MFMA kernels' sums over >= 3k queries
+        torch.testing.assert_close(got.double(), want, rtol=1e-4, atol=per * scale * ranges)
 
 
 @pytest.mark.parametrize("B,N,budget_x", [(1, 20_000, 23), (2, 9000, 7), (1, 4500, 1)])

@@ -8,8 +8,10 @@ random projection / the classifier row-local, every GraphConv on the shard
 pipelined over row blocks), NodeSelfAtten with the softmax over every node --
 and backward, then allreduce_gradients.  Against the one-GPU model on the
 whole graph with the same weights and the same DropEdge masks (global edge
-ids): each GraphConv's output rows bitwise, logits within 1e-4, every
-parameter gradient within 1e-4 of its scale."""
+ids): each GraphConv's output rows bitwise on the one-kernel layers (20k
+rows per rank; small graphs' two-kernel layers pick the linear's split-K by
+row count, so there within 1e-5), logits within 1e-4, every parameter
+gradient within 1e-4 of its scale."""
 import os
 import socket
 
@@ -77,7 +79,10 @@ def _worker(rank, world, port, mode, net_size, n_per_rank, balance):
                         "grads": {k: p.grad.detach().clone() for k, p in model.named_parameters() if p.grad is not None}}
         for k in ("gcn1", "gcn2", "gcn3"):
             a, b = res["one"]["gcn"][k], res["sharded"]["gcn"][k]
-            assert torch.equal(a, b), (rank, k, float((a - b).abs().max()))
+            if n_per_rank >= 20_000:  # the one-kernel layer on both sides: every row's sums in the same order
+                assert torch.equal(a, b), (rank, k, float((a - b).abs().max()))
+            else:  # small graphs: the linear's split-K depends on the row count (6000 vs a 3000-row shard)
+                assert float((a - b).abs().max()) <= 1e-5 * max(1.0, float(a.abs().max())), (rank, k)
         a, b = res["one"]["logits"], res["sharded"]["logits"]
         assert float((a - b).abs().max()) <= 1e-4 * max(1.0, float(a.abs().max())), (rank, float((a - b).abs().max()))
         for k, ga in res["one"]["grads"].items():
