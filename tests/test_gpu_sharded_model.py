@@ -64,11 +64,18 @@ def _worker(rank, world, port, mode, net_size, n_per_rank, balance):
         for name in ("gcn1", "gcn2", "gcn3"):
             mod = getattr(model, name)
             mod.propagate = record(name, mod.propagate)
+        pre = {}  # pre-activations ahead of the ReLUs after the GraphConvs (kink flips explain gradient outliers)
+        att = model.self_atten
+        for name, mod in (("w_rand", model.w_rand), ("emb2", model.emb2[0]), ("f", att.f[0]), ("g", att.g[0]),
+                          ("h", att.h[0])):
+            mod.register_forward_hook(lambda m, i, o, name=name: pre.setdefault(name, []).append(o.detach().reshape(
+                -1, o.shape[-1])))
         res = {}
         for tag, (Vin, A, rows) in (("one", (V[None], g, slice(0, N))), ("sharded", (V[rb:re], sg, slice(rb, re)))):
             model.zero_grad(set_to_none=True)
             model.edge_dropout.reset_calls()
             seen.clear()
+            pre.clear()
             logits = model.forward([Vin, A]).reshape(-1, out_dim)
             loss = torch.nn.functional.cross_entropy(logits, y[rows], reduction="sum")
             loss.backward()
@@ -76,6 +83,7 @@ def _worker(rank, world, port, mode, net_size, n_per_rank, balance):
                 allreduce_gradients([p for p in model.parameters() if p.requires_grad])
             res[tag] = {"logits": logits.detach()[(slice(rb, re) if tag == "one" else slice(None))],
                         "gcn": {k: v[0][(slice(rb, re) if tag == "one" else slice(None))] for k, v in seen.items()},
+                        "pre": {k: v[0][(slice(rb, re) if tag == "one" else slice(None))] for k, v in pre.items()},
                         "grads": {k: p.grad.detach().clone() for k, p in model.named_parameters() if p.grad is not None}}
         for k in ("gcn1", "gcn2", "gcn3"):
             a, b = res["one"]["gcn"][k], res["sharded"]["gcn"][k]
@@ -85,10 +93,26 @@ def _worker(rank, world, port, mode, net_size, n_per_rank, balance):
                 assert float((a - b).abs().max()) <= 1e-5 * max(1.0, float(a.abs().max())), (rank, k)
         a, b = res["one"]["logits"], res["sharded"]["logits"]
         assert float((a - b).abs().max()) <= 1e-4 * max(1.0, float(a.abs().max())), (rank, float((a - b).abs().max()))
+        # A ReLU whose input lies within rounding of 0 can switch between the two runs (their GraphConv
+        # rows agree to 1e-7, not bitwise, on the small graphs' two-kernel layers): the loss is then on
+        # another piece, and the gradients differ by that unit's contribution (seen: 1 of 7500 x 128 emb2
+        # units, emb2's weight gradient off by 8e-4 of its scale; both runs match float64 of their own
+        # activations).  So: every parameter's gradient within 1e-4 of its scale when no ReLU input
+        # switched sign on any rank, else within 1e-3 in the Frobenius norm.
+        sites = [(res["one"]["pre"][k], res["sharded"]["pre"][k]) for k in pre] + \
+            [(res["one"]["gcn"][k], res["sharded"]["gcn"][k]) for k in ("gcn1", "gcn2", "gcn3")]  # fused ReLUs
+        flips = torch.tensor([sum(int(((u > 0) != (v > 0)).sum()) for u, v in sites)])
+        dist.all_reduce(flips)
+        bad = []
         for k, ga in res["one"]["grads"].items():
             gb = res["sharded"]["grads"][k]
-            err = float((ga - gb).abs().max())
-            assert err <= 1e-4 * max(1.0, float(ga.abs().max())), (rank, k, err, float(ga.abs().max()))
+            if int(flips) == 0:
+                err, lim = float((ga - gb).abs().max()), 1e-4 * max(1.0, float(ga.abs().max()))
+            else:
+                err, lim = float((ga - gb).norm() / max(float(ga.norm()), 1e-30)), 1e-3
+            if not err <= lim:
+                bad.append((k, err, lim))
+        assert not bad, (rank, bad, "ReLU inputs that switched sign", int(flips))
     finally:
         dist.destroy_process_group()
 
@@ -96,6 +120,9 @@ def _worker(rank, world, port, mode, net_size, n_per_rank, balance):
 @pytest.mark.parametrize("world,mode,net_size,n_per_rank,balance", [
     (2, "dense", 64, 3000, "nodes"),      # small shards: the two-kernel layer, unpipelined reverse exchange
     (3, "sparse", 64, 2500, "edges"),
+    (3, "dense", 64, 2500, "edges"),
+    (3, "sparse", 64, 2500, "nodes"),
+    (2, "sparse", 64, 3000, "edges"),
     (2, "dense", 256, 20_000, "nodes"),   # one-kernel forward / data gradient, p2p row blocks in the backward
     (3, "sparse", 256, 20_000, "nodes"),
 ])
@@ -103,3 +130,57 @@ def test_sharded_model_equals_one_gpu(world, mode, net_size, n_per_rank, balance
     import torch.multiprocessing as mp
 
     mp.spawn(_worker, args=(world, _free_port(), mode, net_size, n_per_rank, balance), nprocs=world, join=True)
+
+
+def _attn_worker(rank, world, port, N, dk, dv, bounds):
+    import torch.distributed as dist
+
+    from grl.dist import ShardedGraph, sharded_node_attention
+    from grl.ops import node_self_attention
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import types
+
+        g = torch.Generator().manual_seed(N)
+        Q = torch.relu(torch.randn(N, dk, generator=g)).to(DEV)
+        K = torch.relu(torch.randn(N, dk, generator=g)).to(DEV)
+        H = torch.relu(torch.randn(N, dv, generator=g)).to(DEV)
+        V = torch.randn(N, dv, generator=g).to(DEV)
+        gm = torch.randn(dv, generator=g).to(DEV)
+        dout = torch.randn(N, dv, generator=g).to(DEV)
+        one = [t.clone().requires_grad_(True) for t in (Q, K, H, V, gm)]
+        out1 = node_self_attention(one[0][None], one[1][None], one[2][None], one[3][None], one[4])[0]
+        out1.backward(dout)
+        rb, re = bounds[rank], bounds[rank + 1]
+        sg = ShardedGraph.__new__(ShardedGraph)  # the attention needs only the row ranges and the group
+        sg.group = None
+        sg.plan = types.SimpleNamespace(bounds=bounds, row_begin=rb, row_end=re, n_loc=re - rb, rank=rank)
+        loc = [t[rb:re].clone().requires_grad_(True) for t in (Q, K, H, V)] + [gm.clone().requires_grad_(True)]
+        out2 = sharded_node_attention(*loc, sg)
+        out2.backward(dout[rb:re])
+        assert float((out2 - out1[rb:re]).abs().max()) <= 1e-5 * max(1.0, float(out1.abs().max())), rank
+        for name, a, b in zip("QKHV", one[:4], loc[:4]):
+            ga, gb = a.grad[rb:re], b.grad
+            err = float((ga - gb).abs().max())
+            assert err <= 2e-5 * (float(ga.abs().max()) + 1.0), (rank, name, err, float(ga.abs().max()))
+        dgam = loc[4].grad.clone()
+        dist.all_reduce(dgam)
+        assert float((dgam - one[4].grad).abs().max()) <= 1e-4 * (float(one[4].grad.abs().max()) + 1.0), rank
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,N,dk,dv,bounds", [(3, 7500, 4, 32, [0, 2500, 5000, 7500]),
+                                                   (3, 7500, 4, 32, [0, 2491, 5003, 7500]),
+                                                   (2, 6000, 16, 128, [0, 3000, 6000])])
+def test_sharded_attention_equals_one_gpu(world, N, dk, dv, bounds):
+    """NodeSelfAtten over node-range shards (grl.dist.sharded_node_attention:
+    all-gathered K / H, ranged kernels, rank-ordered dK / dH reduction)
+    against the one-GPU op on the same rows: out, dQ, dK, dH, dV per row and
+    the summed dgamma."""
+    import torch.multiprocessing as mp
+
+    mp.spawn(_attn_worker, args=(world, _free_port(), N, dk, dv, bounds), nprocs=world, join=True)
