@@ -1646,8 +1646,11 @@ __global__ __launch_bounds__(64 * KQ_WAVES, 1) void attn_bwd_kq_x6_kernel(AttnAr
     }
     // dS transposed (lanes = queries, registers = keys kappa(r, h)) PLANE BY PLANE:
     // each transposed element is one plane value times 1 plus zeros, so it is
-    // that bf16 value exactly and packs back without a split -- the planes a
-    // split of the transposed sum hi + mid + lo (== dS, exact) would give
+    // that bf16 value exactly and packs back without a split: dQ's A operand
+    // is dS's own three planes (the ones dK used).  The previous form summed
+    // the planes in fp32 and split the sum again -- 48 more VALU per block,
+    // and not always the same planes (a re-split of hi + mid + lo can round
+    // differently), so dQ's last bits differ between the two forms
 #if GRL_ATTN_TPLANES
     abf16x8_t dtp[2][3];
 #pragma unroll
