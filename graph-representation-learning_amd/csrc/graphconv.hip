@@ -443,6 +443,11 @@ constexpr int WS_STATUS_TIMEOUT = 1;       // status bit: a bounded wait ran out
 
 // GRL_WS_STAMP=1 (diagnostic builds only): every wave adds up the cycles it
 // spent waiting on the ring and its total, read back with grl_debug_ws_stats
+// GRL_WS_SADDR: gathered rows addressed as a scalar row base + the lane's
+// column offset (0 = the per-lane 64-bit address of rounds 2-3, A/B aid)
+#ifndef GRL_WS_SADDR
+#define GRL_WS_SADDR 1
+#endif
 #ifndef GRL_WS_STAMP
 #define GRL_WS_STAMP 0
 #endif
@@ -703,7 +708,24 @@ __global__ __launch_bounds__(GRL_WS_DIAG_LB) void graphconv_ws_kernel(
                   for (int q = 0; q < U; ++q) {
                     if (jj[q] >= 0) {
                       const int src = readlane_i(sidx, jj[q]);
+#if GRL_WS_SADDR
+                      // the source row's address is wave-uniform: a scalar base + the lane's column
+                      // offset (global_load's saddr form, no 64-bit VALU add per gathered row)
+                      // (src, ldx >= 0 and ldx < 2^30: an unsigned 32 x 32 -> 64-bit product of bytes)
+                      const uint64_t ra = reinterpret_cast<uint64_t>(X + hv * FVW) +
+                                          (uint64_t)(uint32_t)src * (uint32_t)(ldx * 4);
+                      typedef __attribute__((address_space(1))) const float gfloat;
+                      typedef __attribute__((address_space(1))) const f32x4_t gvec4;
+                      gfloat* const rowp = (gfloat*)(((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(ra >> 32)) << 32) |
+                                                     (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)ra));
+                      xv[q] = zero4();
+                      if (col_ok) {
+                        const f32x4_t t = *(gvec4*)(rowp + col);
+                        xv[q] = make_float4(t[0], t[1], t[2], t[3]);
+                      }
+#else
                       xv[q] = col_ok ? *reinterpret_cast<const float4*>(xs + (int64_t)src * ldx) : zero4();
+#endif
                     }
                   }
 #pragma unroll

@@ -1376,7 +1376,8 @@ static size_t ws_align(size_t b) { return (b + 255) & ~(size_t)255; }
 static bool fused_path(const GrlTypedCsr* g, const float* X, int64_t ldx, int F, const float* W, int C) {
   const int64_t K = (int64_t)(g->num_types + (g->has_self ? 1 : 0)) * F;
   return graphconv_fused_enabled() && graphconv_fused_shape_ok(F, C, g->num_types) && x6_shape_ok(g->num_rows, C, K) &&
-         al16(W) && C % 4 == 0 && al16(X) && ldx % 4 == 0 && (!g->split || g->split->num_heavy == 0);
+         al16(W) && C % 4 == 0 && al16(X) && ldx % 4 == 0 && ldx < (1LL << 30) &&  // gather: 32-bit row bytes
+         (!g->split || g->split->num_heavy == 0);
 }
 
 extern "C" size_t grl_graphconv_fwd_workspace_query(const GrlTypedCsr* g, const float* X, int64_t ldx, int32_t F,
@@ -1474,7 +1475,8 @@ extern "C" int grl_graphconv_fwd(const GrlTypedCsr* g, const float* X, int64_t l
 static bool bwd_data_path(const GrlTypedCsr* gt, const float* G, int64_t ldg, int C, const float* W, int F) {
   const int64_t K = (int64_t)(gt->num_types + (gt->has_self ? 1 : 0)) * C;
   return graphconv_fused_enabled() && graphconv_fused_shape_ok(C, F, gt->num_types) && x6_shape_ok(gt->num_rows, F, K) &&
-         al16(W) && F % 4 == 0 && al16(G) && ldg % 4 == 0 && (!gt->split || gt->split->num_heavy == 0) &&
+         al16(W) && F % 4 == 0 && al16(G) && ldg % 4 == 0 && ldg < (1LL << 30) &&
+         (!gt->split || gt->split->num_heavy == 0) &&
          K <= 2147483647LL && gt->nnz < 2147483647LL;
 }
 
