@@ -187,7 +187,7 @@ def test_eight_wave_workgroups_same_bits(B, N, dk, dv, monkeypatch):
         assert torch.equal(a, b)
 
 
-RANGED = [(1, 20_000, 16, 128, (0, 7000, 13_003, 20_000)), (2, 3000, 16, 100, (0, 1, 1500, 3000)),
+RANGED = [(1, 20_000, 16, 128, (0, 7000, 13_003, 20_000)), (2, 3000, 16, 100, (0, 0, 1, 1500, 3000)),
           (1, 5000, 32, 128, (0, 2500, 5000)), (1, 1200, 64, 512, (0, 600, 1200)), (1, 9000, 4, 32, (0, 9000))]
 
 
