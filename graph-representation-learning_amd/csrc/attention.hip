@@ -835,6 +835,9 @@ typedef __attribute__((address_space(3))) uint16_t lds_u16;
 #ifndef GRL_ATTN_B2
 #define GRL_ATTN_B2 1
 #endif
+#ifndef GRL_ATTN_HPF
+#define GRL_ATTN_HPF 1
+#endif
 template <int DKP, int NT, bool SPLIT, int NW = 4>
 __global__ __launch_bounds__(64 * NW) void attn_fwd_x6p_kernel(AttnArgs a) {
   constexpr int DV = NT * 32, KC = DKP / 16;
@@ -1042,10 +1045,9 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_x6p_kernel(AttnArgs a) {
         }
       }
     };
-#pragma unroll
-    for (int g = 0; g < 2 * NT; ++g) {
+    // group g's H fragments (three planes, transposed reads)
+    auto load_h = [&](int g, abf16x8_t (&hp)[3]) {
       const int t = g >> 1, u = g & 1;
-      abf16x8_t hp[3];
 #pragma unroll
       for (int pl = 0; pl < 3; ++pl) {
         typedef __attribute__((address_space(3))) ai16x4_t lds_v4;
@@ -1057,7 +1059,25 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_x6p_kernel(AttnArgs a) {
         const ai16x8_t v = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3]};
         hp[pl] = __builtin_bit_cast(abf16x8_t, v);
       }
-      MFMA6(o[t], hp[0], hp[1], hp[2], pp[u][0], pp[u][1], pp[u][2]);
+    };
+    // HPF: the next group's fragments are read one group ahead (two register
+    // sets): behind the fence each group's reads would otherwise expose the LDS
+    // latency (where the registers allow: 12 more VGPRs)
+    constexpr bool HPF = GRL_ATTN_HPF && NT <= 4 && (DKP <= 16 || NW == 4);
+    abf16x8_t hq[HPF ? 2 : 1][3];
+    if constexpr (HPF) load_h(0, hq[0]);
+    (void)hq;
+#pragma unroll
+    for (int g = 0; g < 2 * NT; ++g) {
+      const int t = g >> 1, u = g & 1;
+      if constexpr (HPF) {
+        if (g + 1 < 2 * NT) load_h(g + 1, hq[(g + 1) & 1]);
+        MFMA6(o[t], hq[g & 1][0], hq[g & 1][1], hq[g & 1][2], pp[u][0], pp[u][1], pp[u][2]);
+      } else {
+        abf16x8_t hp[3];
+        load_h(g, hp);
+        MFMA6(o[t], hp[0], hp[1], hp[2], pp[u][0], pp[u][1], pp[u][2]);
+      }
       // pieces assigned to this group: piece pc runs after group 1 + pc * (2 NT - 1) / 7
 #pragma unroll
       for (int pc = 0; pc < 7; ++pc)
@@ -1069,18 +1089,18 @@ __global__ __launch_bounds__(64 * NW) void attn_fwd_x6p_kernel(AttnArgs a) {
     for (int u = 0; u < 2; ++u)
 #pragma unroll
       for (int pl = 0; pl < 3; ++pl) {
-#if GRL_ATTN_PIN_PN
         // keep block it+1's split in this body: unrolled, LLVM would sink it
         // into the next body (where its MFMAs use it), undoing the interleave
-        asm volatile("" : "+v"(pn[u][pl]));
-#endif
+        if constexpr (GRL_ATTN_PIN_PN && NT <= 4) asm volatile("" : "+v"(pn[u][pl]));
         pp[u][pl] = pn[u][pl];
       }
   };
   using HRun = std::integral_constant<int, -1>;
   int it = 0;
 #if GRL_ATTN_HU2
-  if constexpr (B2) {
+  // (dv = 256, NT = 8: the unrolled bodies spill -- that form keeps the rolled loop)
+  if constexpr (NT > 4) {
+  } else if constexpr (B2) {
     for (; it + 5 < nblk; it += 4) {  // it % 4 == 0: H stages 0..3
       iteration(it, std::false_type{}, std::integral_constant<int, 0>{});
       iteration(it + 1, std::false_type{}, std::integral_constant<int, 1>{});
