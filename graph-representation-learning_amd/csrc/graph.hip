@@ -328,6 +328,8 @@ extern "C" int grl_csr_to_csc(const GrlTypedCsr* g, int64_t num_cols, int32_t* c
   GRL_CHECK_ARG(g != nullptr && num_cols >= 0 && colptr != nullptr, "grl_csr_to_csc: bad arguments");
   GRL_CHECK_ARG(g->num_types >= 1, "grl_csr_to_csc: num_types must be >= 1");
   GRL_CHECK_ARG(g->nnz < 2147483647LL, "grl_csr_to_csc: nnz exceeds int32");
+  GRL_CHECK_ARG(g->self_row0 == 0, "grl_csr_to_csc: a row-range view (self_row0 %lld) has no transpose of its own",
+                (long long)g->self_row0);
   hipStream_t st = as_stream(stream);
   const int64_t nnz = g->nnz;
   const size_t need = grl_csr_to_csc_workspace_size(nnz, num_cols);

@@ -508,7 +508,8 @@ __global__ __launch_bounds__(GRL_WS_DIAG_LB) void graphconv_ws_kernel(
     const float* __restrict__ vals, uint64_t edge_base, uint64_t self_base, const float* __restrict__ X,
     int64_t ldx, const uint16_t* __restrict__ Wf, const float* __restrict__ bias, int relu,
     float* __restrict__ out, int C, DropDev de, int64_t num_tiles, float* __restrict__ Zout, int64_t ldz,
-    const int32_t* __restrict__ eid, int64_t self_rows, int spin_limit, int* __restrict__ status) {
+    const int32_t* __restrict__ eid, int64_t self_rows, int spin_limit, int* __restrict__ status,
+    int64_t self_row0) {
   constexpr int FVW = KS * 16;                // columns per virtual segment
   constexpr int F = FVW * FV;                 // columns per segment
   constexpr int KC = FVW < WS_KC ? FVW : WS_KC;  // Z columns per unit
@@ -656,7 +657,7 @@ __global__ __launch_bounds__(GRL_WS_DIAG_LB) void graphconv_ws_kernel(
 #pragma unroll
               for (int i = 0; i < SC; ++i)
                 xv[i] = (i0 + i < nvalid && rw0 + i0 + i < self_rows && col_ok)
-                            ? *reinterpret_cast<const float4*>(xs + (rw0 + i0 + i) * ldx) : zero4();
+                            ? *reinterpret_cast<const float4*>(xs + (self_row0 + rw0 + i0 + i) * ldx) : zero4();
               if (!claim()) return;
 #pragma unroll
               for (int i = 0; i < SC; ++i) {
@@ -1015,7 +1016,7 @@ static void launch_ws(int F, int C, bool v, dim3 grid, hipStream_t st, int64_t M
                       int64_t self_rows, int spin, int* status) {
 #define GRL_WS_ARGS                                                                                                \
   grid, dim3(64 * WS_WAVES), 0, st, M, L, hs, g->rowptr, g->colidx, g->vals, g->edge_id_base, g->self_id_base, X, \
-      ldx, Wf, bias, relu, out, C, d, tiles, Z, ldz, eid, self_rows, spin, status
+      ldx, Wf, bias, relu, out, C, d, tiles, Z, ldz, eid, self_rows, spin, status, g->self_row0
 #define GRL_WS_ONE(KS_, FV_, PROD_)                                                                                \
   do {                                                                                                            \
     if (v)                                                                                                        \
@@ -1062,7 +1063,8 @@ int graphconv_fused_fwd(const GrlTypedCsr* g, const float* X, int64_t ldx, int F
   const DropDev d = to_dev(de);
   const bool v = g->vals != nullptr;
   const char* wse = getenv("GRL_FG_WS");
-  if (!(wse && wse[0] == '0') || Z || F > 256 || C > 256) {  // the persistent kernel (Z out: only it)
+  // the persistent kernel (Z out, wide shapes and row-range views: only it)
+  if (!(wse && wse[0] == '0') || Z || F > 256 || C > 256 || g->self_row0 != 0) {
     const int64_t ldz = K;
     const int64_t ws_tiles = ceil_div(M, WS_R);
     const int64_t grid = std::min<int64_t>(ws_tiles, (int64_t)device_cu_count());

@@ -1474,7 +1474,7 @@ extern "C" int grl_graphconv_fwd(const GrlTypedCsr* g, const float* X, int64_t l
 // heavy-row split plan on the transpose.
 static bool bwd_data_path(const GrlTypedCsr* gt, const float* G, int64_t ldg, int C, const float* W, int F) {
   const int64_t K = (int64_t)(gt->num_types + (gt->has_self ? 1 : 0)) * C;
-  return graphconv_fused_enabled() && graphconv_fused_shape_ok(C, F, gt->num_types) && x6_shape_ok(gt->num_rows, F, K) &&
+  return gt->self_row0 == 0 && graphconv_fused_enabled() && graphconv_fused_shape_ok(C, F, gt->num_types) && x6_shape_ok(gt->num_rows, F, K) &&
          al16(W) && F % 4 == 0 && al16(G) && ldg % 4 == 0 && ldg < (1LL << 30) &&
          (!gt->split || gt->split->num_heavy == 0) &&
          K <= 2147483647LL && gt->nnz < 2147483647LL;

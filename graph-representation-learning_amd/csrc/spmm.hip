@@ -713,7 +713,7 @@ int spmm_fwd_rows(const GrlTypedCsr* g, int64_t r0, int64_t rows, const float* X
   const int64_t ldz = (int64_t)(g->num_types + hs) * F;
   return launch_spmm<false>(rows, rows, g->num_types, hs, g->rowptr + r0 * g->num_types, g->colidx, nullptr, g->vals,
                             g->edge_id_base, g->self_id_base + (uint64_t)r0, X, ldx, F, Z, ldz, to_dev(de), nullptr,
-                            st, Z, r0, g->num_rows);
+                            st, Z, g->self_row0 + r0, g->num_rows);
 }
 
 }  // namespace grl
@@ -781,11 +781,12 @@ extern "C" int grl_typed_spmm_fwd(const GrlTypedCsr* g, const float* X, int64_t 
   if (g->num_rows == 0) return GRL_OK;
   GRL_CHECK_ARG(X && Z && g->rowptr && (g->nnz == 0 || g->colidx), "grl_typed_spmm_fwd: NULL pointer");
   GRL_CHECK_ARG(g->nnz < 2147483647LL, "grl_typed_spmm_fwd: nnz %lld exceeds int32", (long long)g->nnz);
+  GRL_CHECK_ARG(g->self_row0 >= 0, "grl_typed_spmm_fwd: negative self_row0");
   const int hs = g->has_self ? 1 : 0;
   const int64_t ldz = (int64_t)(g->num_types + hs) * F;
   return launch_spmm<false>(g->num_rows, g->num_rows, g->num_types, hs, g->rowptr, g->colidx, nullptr, g->vals,
                             g->edge_id_base, g->self_id_base, X, ldx, F, Z, ldz, to_dev(de), g->split,
-                            as_stream(stream), Z);
+                            as_stream(stream), Z, g->self_row0);
 }
 
 extern "C" int grl_typed_spmm_fwd_slice(const GrlTypedCsr* g, const float* X, int64_t ldx, int32_t F,
@@ -805,9 +806,10 @@ extern "C" int grl_typed_spmm_fwd_slice(const GrlTypedCsr* g, const float* X, in
   if (g->num_rows == 0) return GRL_OK;
   GRL_CHECK_ARG(X && Z && g->rowptr && (g->nnz == 0 || g->colidx), "grl_typed_spmm_fwd_slice: NULL pointer");
   GRL_CHECK_ARG(g->nnz < 2147483647LL, "grl_typed_spmm_fwd_slice: nnz %lld exceeds int32", (long long)g->nnz);
+  GRL_CHECK_ARG(g->self_row0 >= 0, "grl_typed_spmm_fwd_slice: negative self_row0");
   return launch_spmm<false>(g->num_rows, g->num_rows, g->num_types, hs, g->rowptr, g->colidx, nullptr, g->vals,
                             g->edge_id_base, g->self_id_base, X, ldx, F, Z, ldz, to_dev(de), g->split,
-                            as_stream(stream), Z, self_col0, -1, zseg);
+                            as_stream(stream), Z, self_col0 + g->self_row0, -1, zseg);
 }
 
 // dX columns [0, F) = columns [col0, col0 + F) of A_drop^T dZ, dZ segments

@@ -65,6 +65,7 @@ class GrlTypedCsr(ctypes.Structure):
         ("edge_id_base", _c_u64),
         ("self_id_base", _c_u64),
         ("split", ctypes.POINTER(GrlSplitPlan)),
+        ("self_row0", _c_i64),
     ]
 
 

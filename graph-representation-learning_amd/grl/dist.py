@@ -870,7 +870,7 @@ class ShardedGraph:
         concat itself, so every layer's output keeps its bits."""
         sg = ShardedGraph.__new__(ShardedGraph)
         sg.__dict__.update(self.__dict__)
-        sg.halo_memo = {"keep": {}, "tables": {}, "concat": {}}
+        sg.halo_memo = {"keep": {}, "tables": {}, "concat": {}, "pending": {}}
         return sg
 
     @staticmethod
@@ -893,8 +893,75 @@ class ShardedGraph:
 
     def clear_halo_memo(self) -> None:
         if self.halo_memo is not None:
+            for _, works, _ in self.halo_memo["pending"].values():  # tables still being filled: finish first
+                for w in works:
+                    if w is not None:
+                        w.wait()
             for d in self.halo_memo.values():
                 d.clear()
+
+    # ---- inference: each layer's output streamed to the peers by row blocks ----
+    stream_rows = True   # dense halos under a memo (the drop-in model's forward): see _graphconv_streamed
+    stream_blocks = 2
+
+    def _can_stream(self, X_loc: torch.Tensor) -> bool:
+        p = self.plan
+        return bool(self.stream_rows and self.halo_memo is not None and p.mode == "dense" and len(p.bounds) > 2
+                    and dist.is_available() and dist.is_initialized() and X_loc.is_cuda)
+
+    def _post_block(self, T: torch.Tensor, a0: int, a1: int):
+        """Rows [a0, a1) of every rank's padded own block into every rank's
+        table T (the dense layout [own | pad | P gathered slots]): one
+        all-gather of the block, asynchronous on RCCL (the next blocks compute
+        meanwhile); host-staged and synchronous on gloo."""
+        p, world = self.plan, len(self.plan.bounds) - 1
+        slots = [T[p.stride * (1 + q) + a0: p.stride * (1 + q) + a1] for q in range(world)]
+        if _host_staged(self.group):
+            h = T[a0:a1].cpu()
+            outs = [torch.empty_like(h) for _ in range(world)]
+            dist.all_gather(outs, h, group=self.group)
+            for v, o in zip(slots, outs):
+                v.copy_(o)
+            return None
+        return dist.all_gather(slots, T[a0:a1], group=self.group, async_op=True)
+
+    def _graphconv_streamed(self, X_loc: torch.Tensor, layer, dropedge, relu: bool) -> torch.Tensor:
+        """Inference GraphConv whose output rows go to the peers while the
+        rest of the layer computes: the output is written straight into the
+        NEXT layer's halo table T ([own | pad | P slots], the dense layout),
+        in stream_blocks row blocks (one-kernel forward over row-range views
+        of the shard graph, TypedGraph.rows_view -- every row the whole
+        shard's arithmetic), each block all-gathered into the peers' T as
+        soon as it is written.  The next layer finds T through the memo
+        (exchange_table waits for the blocks' collectives) instead of
+        exchanging its input.  The output is T's own rows: the same values
+        as the unstreamed layer's (bitwise where both take the one-kernel
+        path; small blocks' two-kernel linear picks its split-K by rows)."""
+        from .ops import graph_conv_infer
+
+        p, world = self.plan, len(self.plan.bounds) - 1
+        X_ext = self.exchange_table(X_loc)
+        W, b = layer.h_weights, layer.bias
+        C = W.shape[1]
+        T = X_ext.new_empty(p.stride * (1 + world), C)
+        assert T.shape[0] == self.graph.num_cols, "dense halo layout: [own | pad | P slots]"
+        T[p.n_loc:p.stride].zero_()
+        g = self.graph.with_dropedge(dropedge)
+        nb = max(1, int(self.stream_blocks))
+        bs = -(-p.stride // nb)
+        works = []
+        for j in range(nb):
+            a0, a1 = min(j * bs, p.stride), min((j + 1) * bs, p.stride)
+            if a1 <= a0:
+                continue
+            r0, r1 = min(a0, p.n_loc), min(a1, p.n_loc)
+            if r1 > r0:
+                graph_conv_infer(X_ext, g.rows_view(r0, r1), W, b, relu, out=T[r0:r1])
+            works.append(self._post_block(T, a0, a1))
+        out = T[:p.n_loc]
+        k = self._tkey(out)
+        self.halo_memo["pending"][k[:1] + k[2:]] = (T, works, out)
+        return out
 
     def exchange_table(self, X_loc: torch.Tensor) -> torch.Tensor:
         """X_ext = [own | halo] rows of X_loc without autograd (the layers'
@@ -913,6 +980,15 @@ class ShardedGraph:
         hit = memo["tables"].get(k)
         if hit is not None:
             return hit
+        pend = memo["pending"].pop(k[:1] + k[2:], None)  # a streamed layer's output (its version may have moved)
+        if pend is not None and pend[2].data_ptr() == X_loc.data_ptr():
+            T, works, _ = pend
+            for w in works:
+                if w is not None:
+                    w.wait()
+            if k in memo["keep"]:
+                memo["tables"][k] = T
+            return T
         cat = memo["concat"].get(k)
         if cat is not None:
             return torch.cat([self.exchange_table(part.reshape(-1, part.shape[-1])) for part in cat[1]], dim=1)
@@ -1037,6 +1113,8 @@ class ShardedGraph:
             raise ValueError(f"pipeline must be None or 'rows', got {pipeline!r}")
         if chunks is None:
             if not (torch.is_grad_enabled() and X_loc.requires_grad):  # no gradient to send home: memo table
+                if self._can_stream(X_loc):
+                    return self._graphconv_streamed(X_loc, layer, dropedge, relu)
                 return graph_conv(self.exchange_table(X_loc), self.graph.with_dropedge(dropedge), layer.h_weights,
                                   layer.bias, relu=relu)
             return graph_conv(self.exchange(X_loc), self.graph.with_dropedge(dropedge), layer.h_weights, layer.bias,

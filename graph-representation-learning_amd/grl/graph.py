@@ -130,6 +130,29 @@ class TypedGraph:
         g.dropedge = de
         return g
 
+    self_row0 = 0  # X row of row 0's identity term (row-range views, rows_view)
+
+    def rows_view(self, r0: int, r1: int) -> "TypedGraph":
+        """Rows [r0, r1) as a forward graph of their own: rowptr a slice
+        (edge positions, hence DropEdge ids, stay absolute), colidx / vals
+        shared, the identity term from X row r0 on (GrlTypedCsr.self_row0)
+        and its DropEdge ids from self_id_base + r0 -- every row exactly as in
+        the whole graph.  Cached per graph; carries this graph's DropEdge
+        draw.  Forward entry points only (no transpose of its own)."""
+        if not 0 <= r0 <= r1 <= self.num_rows:
+            raise _lib.GrlError(f"rows [{r0}, {r1}) outside [0, {self.num_rows})")
+        cache = self._shared.setdefault("fwd_row_views", {})
+        v = cache.get((r0, r1))
+        if v is None:
+            L = self.num_types
+            v = TypedGraph(self.rowptr[r0 * L: r1 * L + 1], self.colidx, L, vals=self.vals, has_self=self.has_self,
+                           num_cols=self.num_cols, edge_id_base=self.edge_id_base,
+                           self_id_base=self.self_id_base + r0, self_rows=max(0, min(self.self_rows, r1) - r0))
+            v.self_row0 = self.self_row0 + r0
+            v.split_threshold, v.split_chunk = self.split_threshold, self.split_chunk
+            cache[(r0, r1)] = v
+        return v.with_dropedge(self.dropedge)
+
     def __repr__(self) -> str:
         return (f"TypedGraph(rows={self.num_rows}, cols={self.num_cols}, types={self.num_types}, "
                 f"nnz={self.nnz}, has_self={self.has_self}, vals={'yes' if self.vals is not None else 'ones'}, "
@@ -204,6 +227,7 @@ class TypedGraph:
         g.nnz = self.nnz
         g.edge_id_base = self.edge_id_base
         g.self_id_base = self.self_id_base
+        g.self_row0 = self.self_row0
         plan = self._split("csr", F) if F is not None else None
         g.split = ctypes.pointer(plan) if plan is not None else None
         return g
@@ -236,8 +260,9 @@ class TypedGraph:
         """False for a graph whose arrays are static buffers refilled in place
         (a captured training step's bucket, step_graph.py): a cached typed
         transpose would go stale, so the one-kernel data gradient is not
-        used on it."""
-        return not self._shared.get("static_buffers", False)
+        used on it.  Nor for a row-range view (rows_view): no transpose of its
+        own."""
+        return not self._shared.get("static_buffers", False) and self.self_row0 == 0
 
     def typed_transpose(self):
         """(gt, eid): the typed transpose, built once and cached -- gt's row m

@@ -519,12 +519,13 @@ def graph_conv_fwd_train(X: torch.Tensor, graph: TypedGraph, W: torch.Tensor, b=
 
 
 def graph_conv_infer(X: torch.Tensor, graph: TypedGraph, W: torch.Tensor, b=None, relu: bool = False,
-                     max_workspace_bytes: int = None) -> torch.Tensor:
+                     max_workspace_bytes: int = None, out: torch.Tensor = None) -> torch.Tensor:
     """GraphConv forward for inference through one grl_graphconv_fwd call
     (aggregation + linear [+ReLU]).  On large graphs this is one fused kernel
     and Z never reaches HBM; otherwise Z lives only in the call's workspace
     and max_workspace_bytes bounds it (the call then works in row chunks,
-    bitwise equal to the whole-graph result)."""
+    bitwise equal to the whole-graph result).  out: a contiguous
+    [num_rows, C] float32 tensor to write (e.g. a row block of a halo table)."""
     _require_device(X, "node features")
     if X.dtype != torch.float32 or W.dtype != torch.float32:
         raise _lib.GrlError("graph_conv_infer: features and weights must be float32")
@@ -537,7 +538,11 @@ def graph_conv_infer(X: torch.Tensor, graph: TypedGraph, W: torch.Tensor, b=None
     if Wc.shape[0] != graph.segments * F:
         raise _lib.GrlError(f"weights have {Wc.shape[0]} rows, expected {graph.segments} x {F}")
     bc = b.contiguous() if b is not None else None
-    out = torch.empty(graph.num_rows, C, dtype=torch.float32, device=X.device)
+    if out is None:
+        out = torch.empty(graph.num_rows, C, dtype=torch.float32, device=X.device)
+    elif (tuple(out.shape) != (graph.num_rows, C) or out.dtype != torch.float32 or not out.is_contiguous()
+          or out.device != X.device):
+        raise _lib.GrlError(f"out must be a contiguous float32 ({graph.num_rows}, {C}) tensor on {X.device}")
     csr = graph.csr_c(F)
     # the fused one-kernel path needs only W's planes; else Z whole
     full = _lib.lib().grl_graphconv_fwd_workspace_query(ctypes.byref(csr), X2.data_ptr(), X2.stride(0), F,

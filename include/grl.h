@@ -99,6 +99,11 @@ typedef struct GrlTypedCsr {
   uint64_t edge_id_base; /* global DropEdge id of colidx[0] (node-range shard)*/
   uint64_t self_id_base; /* global DropEdge id of row 0's self loop           */
   const GrlSplitPlan* split; /* heavy-row plan over rowptr, or NULL           */
+  int64_t self_row0;     /* X row of row 0's self term (0; a row-range view of
+                            a graph -- rowptr a slice, the identity rows from
+                            this row on -- sets its first row).  Forward entry
+                            points only: grl_csr_to_csc and
+                            grl_graphconv_bwd_data require 0.               */
 } GrlTypedCsr;
 
 /*

@@ -113,6 +113,23 @@ def _worker(rank, world, port, mode, net_size, n_per_rank, balance):
             if not err <= lim:
                 bad.append((k, err, lim))
         assert not bad, (rank, bad, "ReLU inputs that switched sign", int(flips))
+        # inference: dense halos stream each layer's output rows to the peers by blocks while the rest of the
+        # layer computes (ShardedGraph._graphconv_streamed) -- against the unstreamed exchange and the one GPU
+        model.eval()
+        with torch.no_grad():
+            one = model.forward([V[None], g]).reshape(-1, out_dim)[rb:re]
+            got = {}
+            for tag, on, nb in (("streamed2", True, 2), ("streamed3", True, 3), ("plain", False, 2)):
+                sg.stream_rows, sg.stream_blocks = on, nb
+                got[tag] = model.forward([V[rb:re], sg]).reshape(-1, out_dim)
+            sg.stream_rows, sg.stream_blocks = True, 2
+        scale = max(1.0, float(one.abs().max()))
+        for tag in ("streamed2", "streamed3"):
+            if n_per_rank >= 20_000:  # one-kernel layers on every block: the same bits
+                assert torch.equal(got[tag], got["plain"]), (rank, tag, float((got[tag] - got["plain"]).abs().max()))
+            else:
+                assert float((got[tag] - got["plain"]).abs().max()) <= 1e-5 * scale, (rank, tag)
+            assert float((got[tag] - one).abs().max()) <= 1e-4 * scale, (rank, tag)
     finally:
         dist.destroy_process_group()
 
