@@ -437,3 +437,34 @@ def test_persistent_kernel_timeout_is_an_error(monkeypatch):
     assert bool(torch.isnan(out_c).all())
     with pytest.raises(_lib.GrlError):
         grl.check()
+
+
+@pytest.mark.parametrize("N,F,C,p,cuts", [(20_000, 256, 256, 0.3, (0, 7000, 13_001, 20_000)),
+                                          (20_000, 512, 256, 0.3, (0, 9999, 20_000)),
+                                          (3000, 64, 64, 0.0, (0, 1000, 1001, 3000))])
+def test_row_views_forward_equals_whole_graph(N, F, C, p, cuts):
+    """TypedGraph.rows_view (GrlTypedCsr.self_row0: the sharded inference's
+    row blocks, grl.dist ShardedGraph._graphconv_streamed): the aggregation of
+    a row range is bitwise the whole graph's rows, DropEdge included; the
+    GraphConv forward over row ranges equals the whole-graph call bitwise on
+    the one-kernel path (large views) and within 1e-5 on small views (their
+    linear picks its split-K by row count)."""
+    g = TypedGraph.synthetic(N, 12.0, 6, kind="er", seed=3, device=DEV)
+    gd = g.with_dropedge(DropEdge(p=p, seed=9, call=2) if p else None)
+    gen = torch.Generator().manual_seed(N + F)
+    X = torch.randn(N, F, generator=gen).to(DEV)
+    W = (torch.randn(7 * F, C, generator=gen) * 0.05).to(DEV)
+    b = torch.randn(C, generator=gen).to(DEV)
+    Z = typed_aggregate(X, gd)
+    whole = graph_conv_infer(X, gd, W, b, relu=True)
+    for r0, r1 in zip(cuts[:-1], cuts[1:]):
+        v = gd.rows_view(r0, r1)
+        assert v.num_rows == r1 - r0 and v.self_row0 == r0 and not v.transpose_ok
+        assert torch.equal(typed_aggregate(X, v), Z[r0:r1])
+        part = graph_conv_infer(X, v, W, b, relu=True)
+        if r1 - r0 >= 5000:
+            assert torch.equal(part, whole[r0:r1])
+        else:
+            assert float((part - whole[r0:r1]).abs().max()) <= 1e-5 * max(1.0, float(whole.abs().max()))
+    with pytest.raises(_lib.GrlError):
+        gd.rows_view(5, 10).typed_transpose()
