@@ -565,6 +565,33 @@ def _all_agree(flag: bool, group, device) -> bool:
     return bool(int(t.item()))
 
 
+def stream_chunks(stride: int, n_loc: int, blocks: int, path_ok):
+    """The streamed inference layer's schedule (ShardedGraph._graphconv_streamed):
+    [(r0, r1, posts)] -- compute rows [r0, r1) of the shard, then post the
+    row blocks `posts` ([a0, a1) of the padded own block; the same blocks,
+    in the same order, on every rank: `blocks` equal parts of `stride`).
+    A compute chunk is a run of whole blocks that takes the same GEMM path as
+    the whole shard (path_ok(rows): ops.x6_rows_ok), so the layer's bits do
+    not depend on the blocking; when the whole shard fails path_ok it is one
+    chunk (the unstreamed layer), its blocks posted after it."""
+    nb = max(1, int(blocks))
+    bs = -(-stride // nb)
+    parts = [(j * bs, min((j + 1) * bs, stride)) for j in range(nb) if j * bs < stride]
+    whole_ok = n_loc > 0 and path_ok(n_loc)
+    out, start, held = [], 0, []
+    for j, (a0, a1) in enumerate(parts):
+        held.append((a0, a1))
+        e = min(a1, n_loc)
+        if j + 1 < len(parts):
+            if not (whole_ok and e > start and path_ok(e - start) and (e == n_loc or path_ok(n_loc - e))):
+                continue
+        else:
+            e = n_loc
+        out.append((start, e, held))
+        start, held = e, []
+    return out
+
+
 class _RowPipelinedGraphConv(torch.autograd.Function):
     """One GraphConv layer (robust_gcn.py:45-51) on a node-range shard with
     the one-kernel forms in both directions and the reverse halo exchange
@@ -934,10 +961,11 @@ class ShardedGraph:
         shard's arithmetic), each block all-gathered into the peers' T as
         soon as it is written.  The next layer finds T through the memo
         (exchange_table waits for the blocks' collectives) instead of
-        exchanging its input.  The output is T's own rows: the same values
-        as the unstreamed layer's (bitwise where both take the one-kernel
-        path; small blocks' two-kernel linear picks its split-K by rows)."""
-        from .ops import graph_conv_infer
+        exchanging its input.  The output is T's own rows, bitwise the
+        unstreamed layer's: blocks are computed in runs that take the same
+        GEMM path as the whole shard (x6_rows_ok), a shard too small for the
+        split-bf16 GEMM in one call (its fp32 linear splits K by rows)."""
+        from .ops import graph_conv_infer, x6_rows_ok
 
         p, world = self.plan, len(self.plan.bounds) - 1
         X_ext = self.exchange_table(X_loc)
@@ -947,17 +975,12 @@ class ShardedGraph:
         assert T.shape[0] == self.graph.num_cols, "dense halo layout: [own | pad | P slots]"
         T[p.n_loc:p.stride].zero_()
         g = self.graph.with_dropedge(dropedge)
-        nb = max(1, int(self.stream_blocks))
-        bs = -(-p.stride // nb)
+        K = g.segments * X_ext.shape[1]
         works = []
-        for j in range(nb):
-            a0, a1 = min(j * bs, p.stride), min((j + 1) * bs, p.stride)
-            if a1 <= a0:
-                continue
-            r0, r1 = min(a0, p.n_loc), min(a1, p.n_loc)
+        for r0, r1, posts in stream_chunks(p.stride, p.n_loc, int(self.stream_blocks), lambda m: x6_rows_ok(m, C, K)):
             if r1 > r0:
                 graph_conv_infer(X_ext, g.rows_view(r0, r1), W, b, relu, out=T[r0:r1])
-            works.append(self._post_block(T, a0, a1))
+            works += [self._post_block(T, a0, a1) for a0, a1 in posts]
         out = T[:p.n_loc]
         k = self._tkey(out)
         self.halo_memo["pending"][k[:1] + k[2:]] = (T, works, out)

@@ -279,6 +279,16 @@ FUSED_WIDTHS = (64, 128, 256, 512, 1024)
 FUSED_MAX_OUT = 512
 
 
+def x6_rows_ok(M: int, N: int, K: int) -> bool:
+    """Whether an [M, K] x [K, N] product takes the split-bf16 GEMM (and so a
+    GraphConv the one-kernel forms): the size rule of x6_shape_ok
+    (csrc/linear.hip).  Its per-element arithmetic is independent of M, the
+    fp32-MFMA path's is not (split-K by rows), so row blocks of one layer
+    match the whole call bitwise exactly when both sides pass this."""
+    return (os.environ.get("GRL_GEMM_X6", "1")[:1] != "0" and K > 0 and K % 16 == 0 and M >= 4 and N >= 4
+            and 2.0 * M * N * K >= 1.6e10)
+
+
 def _bwd_data_enabled() -> bool:
     return os.environ.get("GRL_GRAPHCONV_FUSED_BWD", "1") != "0"
 

@@ -365,3 +365,33 @@ def test_halo_memo_reuses_concat_parts(mode):
     per-forward halo memo only g2's rows travel (g1's table came for gcn2),
     and the assembled table equals the concat's own exchange."""
     mp.spawn(_memo_worker, args=(2, _free_port(), mode), nprocs=2, join=True)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_stream_chunks_schedule(seed):
+    """The streamed inference schedule (grl.dist.stream_chunks): compute
+    chunks tile the shard's rows in order, every rank posts the same blocks
+    in the same order, a block is posted only after its rows are computed,
+    and a chunk takes the whole shard's GEMM path (so the layer's bits do
+    not depend on the blocking)."""
+    from grl.dist import stream_chunks
+
+    rng = np.random.default_rng(seed)
+    for _ in range(200):
+        stride = int(rng.integers(1, 400))
+        n_loc = int(rng.integers(0, stride + 1))
+        nb = int(rng.integers(1, 6))
+        thr = int(rng.integers(1, 300))
+        ok = lambda m: m >= thr  # noqa: E731  (x6_rows_ok is monotone in the row count)
+        sched = stream_chunks(stride, n_loc, nb, ok)
+        bs = -(-stride // nb)
+        parts = [(j * bs, min((j + 1) * bs, stride)) for j in range(nb) if j * bs < stride]
+        assert [b for _, _, posts in sched for b in posts] == parts
+        assert sched[0][0] == 0 and sched[-1][1] == n_loc
+        assert all(a[1] == b[0] for a, b in zip(sched, sched[1:]))
+        for r0, r1, posts in sched:
+            assert all(min(a1, n_loc) <= r1 for _, a1 in posts)
+            if r1 > r0:
+                assert ok(r1 - r0) == ok(n_loc)
+        if not ok(n_loc):
+            assert sum(1 for r0, r1, _ in sched if r1 > r0) <= 1

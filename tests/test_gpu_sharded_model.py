@@ -125,10 +125,8 @@ def _worker(rank, world, port, mode, net_size, n_per_rank, balance):
             sg.stream_rows, sg.stream_blocks = True, 2
         scale = max(1.0, float(one.abs().max()))
         for tag in ("streamed2", "streamed3"):
-            if n_per_rank >= 20_000:  # one-kernel layers on every block: the same bits
-                assert torch.equal(got[tag], got["plain"]), (rank, tag, float((got[tag] - got["plain"]).abs().max()))
-            else:
-                assert float((got[tag] - got["plain"]).abs().max()) <= 1e-5 * scale, (rank, tag)
+            # the blocks run in chunks on the whole shard's GEMM path: the same bits at every size
+            assert torch.equal(got[tag], got["plain"]), (rank, tag, float((got[tag] - got["plain"]).abs().max()))
             assert float((got[tag] - one).abs().max()) <= 1e-4 * scale, (rank, tag)
     finally:
         dist.destroy_process_group()
