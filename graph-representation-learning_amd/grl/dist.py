@@ -592,6 +592,21 @@ def stream_chunks(stride: int, n_loc: int, blocks: int, path_ok):
     return out
 
 
+class _Landing:
+    """A collective's handle whose wait() also lands the received rows where
+    they belong (a stream-ordered copy after the collective)."""
+
+    def __init__(self, work, land, keep):
+        self.work, self.land, self.keep = work, land, keep
+
+    def wait(self):
+        if self.work is not None:
+            self.work.wait()
+            self.work = None
+            self.land()
+            self.keep = None
+
+
 class _RowPipelinedGraphConv(torch.autograd.Function):
     """One GraphConv layer (robust_gcn.py:45-51) on a node-range shard with
     the one-kernel forms in both directions and the reverse halo exchange
@@ -928,59 +943,125 @@ class ShardedGraph:
                 d.clear()
 
     # ---- inference: each layer's output streamed to the peers by row blocks ----
-    stream_rows = True   # dense halos under a memo (the drop-in model's forward): see _graphconv_streamed
+    stream_rows = True   # under a memo (the drop-in model's forward): see _graphconv_streamed
     stream_blocks = 2
 
     def _can_stream(self, X_loc: torch.Tensor) -> bool:
         p = self.plan
-        return bool(self.stream_rows and self.halo_memo is not None and p.mode == "dense" and len(p.bounds) > 2
+        return bool(self.stream_rows and self.halo_memo is not None and len(p.bounds) > 2
                     and dist.is_available() and dist.is_initialized() and X_loc.is_cuda)
 
-    def _post_block(self, T: torch.Tensor, a0: int, a1: int):
-        """Rows [a0, a1) of every rank's padded own block into every rank's
-        table T (the dense layout [own | pad | P gathered slots]): one
-        all-gather of the block, asynchronous on RCCL (the next blocks compute
-        meanwhile); host-staged and synchronous on gloo."""
+    def _stream_extent(self) -> int:
+        """Rows of the uniform block grid: the largest shard (every rank
+        posts the same blocks, so each collective matches)."""
+        b = self.plan.bounds
+        return max(b[q + 1] - b[q] for q in range(len(b) - 1))
+
+    def _stream_table(self, C: int, like: torch.Tensor) -> torch.Tensor:
+        """The next layer's X_ext, to be filled by blocks: the dense layout
+        [own | pad | P slots] (pad rows zero) or the sparse [own | halo]."""
         p, world = self.plan, len(self.plan.bounds) - 1
-        slots = [T[p.stride * (1 + q) + a0: p.stride * (1 + q) + a1] for q in range(world)]
+        if p.mode == "dense":
+            T = like.new_empty(p.stride * (1 + world), C)
+            T[p.n_loc:p.stride].zero_()
+        else:
+            T = like.new_empty(p.n_loc + p.n_halo, C)
+        return T
+
+    def _sparse_block_lists(self, a0: int, a1: int):
+        """Sparse halos, block [a0, a1) of every rank's own rows: (rows of my
+        block the peers asked for, concatenated per peer; per-peer send
+        counts; per-peer receive counts; the X_ext rows the received rows go
+        to).  Cached per block; one host read when built."""
+        cache = self.__dict__.setdefault("_stream_lists", {})
+        if (a0, a1) in cache:
+            return cache[(a0, a1)]
+        p, world = self.plan, len(self.plan.bounds) - 1
+        dev = p.send_index.device
+        send_idx, send_counts, recv_counts, dest = [], [], [], []
+        off = roff = 0
+        for q in range(world):
+            seg = p.send_index[off:off + p.send_counts[q]]  # ascending: the peer's halo ids are
+            lo, hi = (int(x) for x in torch.searchsorted(seg, torch.tensor([a0, a1], device=dev)).tolist())
+            send_idx.append(seg[lo:hi])
+            send_counts.append(hi - lo)
+            off += p.send_counts[q]
+            ids = p.halo_ids[roff:roff + p.recv_counts[q]] - p.bounds[q]  # owner q's rows I read, ascending
+            lo, hi = (int(x) for x in torch.searchsorted(ids, torch.tensor([a0, a1], device=ids.device)).tolist())
+            dest.append(torch.arange(p.n_loc + roff + lo, p.n_loc + roff + hi, device=dev))
+            recv_counts.append(hi - lo)
+            roff += p.recv_counts[q]
+        cache[(a0, a1)] = out = (torch.cat(send_idx), send_counts, recv_counts, torch.cat(dest))
+        return out
+
+    def _post_block(self, T: torch.Tensor, a0: int, a1: int):
+        """Rows [a0, a1) of every rank's own block into every peer's table T:
+        dense halos, one all-gather of the padded block into the P slots;
+        sparse halos, one all-to-all-v of the rows each peer asked for (their
+        slots in T written when the handle is waited on).  Asynchronous on
+        RCCL (the next blocks compute meanwhile); host-staged and synchronous
+        on gloo.  Returns a handle with wait(), or None when done."""
+        p, world = self.plan, len(self.plan.bounds) - 1
+        if p.mode == "dense":
+            a1 = min(a1, p.stride)
+            slots = [T[p.stride * (1 + q) + a0: p.stride * (1 + q) + a1] for q in range(world)]
+            if _host_staged(self.group):
+                h = T[a0:a1].cpu()
+                outs = [torch.empty_like(h) for _ in range(world)]
+                dist.all_gather(outs, h, group=self.group)
+                for v, o in zip(slots, outs):
+                    v.copy_(o)
+                return None
+            return dist.all_gather(slots, T[a0:a1], group=self.group, async_op=True)
+        send_idx, sc, rc, dest = self._sparse_block_lists(a0, a1)
+        send = T.index_select(0, send_idx)
+        recv = T.new_empty(sum(rc), T.shape[1])
         if _host_staged(self.group):
-            h = T[a0:a1].cpu()
-            outs = [torch.empty_like(h) for _ in range(world)]
-            dist.all_gather(outs, h, group=self.group)
-            for v, o in zip(slots, outs):
-                v.copy_(o)
+            all_to_all_v(recv, send, rc, sc, self.group)
+            T.index_copy_(0, dest, recv)
             return None
-        return dist.all_gather(slots, T[a0:a1], group=self.group, async_op=True)
+        work = dist.all_to_all_single(recv, send, rc, sc, group=self.group, async_op=True)
+        return _Landing(work, lambda: T.index_copy_(0, dest, recv), (send, recv))
+
+    def _stream_fill(self, T: torch.Tensor, C: int, K: int, compute) -> list:
+        """Fill T's own rows by compute(r0, r1) (writing T[r0:r1]) in the
+        stream_chunks schedule, posting each block as soon as its rows are
+        written; returns the handles."""
+        from .ops import x6_rows_ok
+
+        works = []
+        for r0, r1, posts in stream_chunks(self._stream_extent(), self.plan.n_loc, int(self.stream_blocks),
+                                           lambda m: x6_rows_ok(m, C, K)):
+            if r1 > r0:
+                compute(r0, r1)
+            works += [self._post_block(T, a0, a1) for a0, a1 in posts]
+        return works
 
     def _graphconv_streamed(self, X_loc: torch.Tensor, layer, dropedge, relu: bool) -> torch.Tensor:
         """Inference GraphConv whose output rows go to the peers while the
         rest of the layer computes: the output is written straight into the
-        NEXT layer's halo table T ([own | pad | P slots], the dense layout),
-        in stream_blocks row blocks (one-kernel forward over row-range views
-        of the shard graph, TypedGraph.rows_view -- every row the whole
-        shard's arithmetic), each block all-gathered into the peers' T as
-        soon as it is written.  The next layer finds T through the memo
+        NEXT layer's halo table T (the plan's X_ext layout) in stream_blocks
+        row blocks (one-kernel forward over row-range views of the shard
+        graph, TypedGraph.rows_view -- every row the whole shard's
+        arithmetic), each block sent to the peers as soon as it is written
+        (_post_block).  The next layer finds T through the memo
         (exchange_table waits for the blocks' collectives) instead of
         exchanging its input.  The output is T's own rows, bitwise the
         unstreamed layer's: blocks are computed in runs that take the same
         GEMM path as the whole shard (x6_rows_ok), a shard too small for the
         split-bf16 GEMM in one call (its fp32 linear splits K by rows)."""
-        from .ops import graph_conv_infer, x6_rows_ok
+        from .ops import graph_conv_infer
 
-        p, world = self.plan, len(self.plan.bounds) - 1
+        p = self.plan
         X_ext = self.exchange_table(X_loc)
         W, b = layer.h_weights, layer.bias
         C = W.shape[1]
-        T = X_ext.new_empty(p.stride * (1 + world), C)
-        assert T.shape[0] == self.graph.num_cols, "dense halo layout: [own | pad | P slots]"
-        T[p.n_loc:p.stride].zero_()
+        T = self._stream_table(C, X_ext)
+        assert T.shape[0] == self.graph.num_cols, "T is the next layer's X_ext"
         g = self.graph.with_dropedge(dropedge)
-        K = g.segments * X_ext.shape[1]
-        works = []
-        for r0, r1, posts in stream_chunks(p.stride, p.n_loc, int(self.stream_blocks), lambda m: x6_rows_ok(m, C, K)):
-            if r1 > r0:
-                graph_conv_infer(X_ext, g.rows_view(r0, r1), W, b, relu, out=T[r0:r1])
-            works += [self._post_block(T, a0, a1) for a0, a1 in posts]
+        works = self._stream_fill(T, C, g.segments * X_ext.shape[1],
+                                  lambda r0, r1: graph_conv_infer(X_ext, g.rows_view(r0, r1), W, b, relu,
+                                                                  out=T[r0:r1]))
         out = T[:p.n_loc]
         k = self._tkey(out)
         self.halo_memo["pending"][k[:1] + k[2:]] = (T, works, out)

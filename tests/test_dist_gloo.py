@@ -395,3 +395,47 @@ def test_stream_chunks_schedule(seed):
                 assert ok(r1 - r0) == ok(n_loc)
         if not ok(n_loc):
             assert sum(1 for r0, r1, _ in sched if r1 > r0) <= 1
+
+
+def _stream_worker(rank, world, port, mode):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from grl import dist as gdist
+
+        gen = torch.Generator().manual_seed(5)
+        N, L, deg = 60, 2, 3
+        cols = torch.randint(0, N, (N * L * deg,), generator=gen)
+        bounds = [0, 25, 37, N]  # unequal shards: blocks past a short shard's end carry no rows
+        rb, re = bounds[rank], bounds[rank + 1]
+        e0, e1 = rb * L * deg, re * L * deg
+        sg = gdist.ShardedGraph.__new__(gdist.ShardedGraph)  # the posts need only the plan (no device graph)
+        sg.group, sg.plan = None, build_halo_plan(cols[e0:e1], rb, re, None, mode=mode)
+        assert sg.plan.mode == mode
+        X = torch.randn(re - rb, 8, generator=torch.Generator().manual_seed(100 + rank))
+        want = halo_exchange(X, sg.plan)
+        # K so large that any run of >= 5 rows takes the x6 path: the schedule then cuts into several chunks
+        for nb in (1, 2, 3, 5):
+            sg.stream_blocks = nb
+            T = sg._stream_table(8, X)
+            seen = []
+            works = sg._stream_fill(T, 8, 200_000_000,
+                                    lambda r0, r1: (seen.append((r0, r1)), T[r0:r1].copy_(X[r0:r1])))
+            for w in works:
+                if w is not None:
+                    w.wait()
+            assert torch.equal(T, want), (rank, mode, nb)
+            assert seen[0][0] == 0 and seen[-1][1] == re - rb and (nb == 1 or rank != 0 or len(seen) > 1), seen
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["dense", "sparse"])
+def test_streamed_blocks_fill_the_halo_table(mode):
+    """Streamed inference's posts (ShardedGraph._stream_fill / _post_block):
+    a layer's output rows sent block by block as they are computed -- an
+    all-gather per block (dense halos) or an all-to-all-v of the rows each
+    peer asked for (sparse) -- fill the next layer's table exactly as the
+    whole-tensor halo exchange does, on unequal shards, for 1..5 blocks."""
+    mp.spawn(_stream_worker, args=(3, _free_port(), mode), nprocs=3, join=True)
