@@ -967,6 +967,9 @@ __device__ __forceinline__ bf16x8_t tr_pair3(const lds_u16* p0) {
   return __builtin_bit_cast(bf16x8_t, v);
 }
 
+#ifndef GRL_X6T_WHATIF
+#define GRL_X6T_WHATIF 0
+#endif
 // GRL_X6T_U2 (read per call; default 1): the K16 loop unrolled over the two
 // stages, fragment reads from per-lane LDS offsets fixed for the kernel (the
 // stage and plane as immediates) -- the rolled loop recomputed ~40 address
@@ -1020,14 +1023,33 @@ __global__ __launch_bounds__(512) void gemm_x6t_kernel(GemmArgs p) {
     *reinterpret_cast<uint2*>((base) + X6_PLANE + (off)) = q1_;                                           \
     *reinterpret_cast<uint2*>((base) + 2 * X6_PLANE + (off)) = q2_;                                       \
   } while (0)
+#if GRL_X6T_WHATIF >= 1
+  // timing diagnostics only, WRONG results: B (2: and A) stored as its
+  // truncated top plane, no split (the ceiling of a pre-split g / Z)
+#define X6T_SPLIT_B(v, base, off)                                                                         \
+  do {                                                                                                    \
+    const uint2 q_ = make_uint2(__builtin_amdgcn_perm(__float_as_uint((v).y), __float_as_uint((v).x), 0x07060302u), \
+                                __builtin_amdgcn_perm(__float_as_uint((v).w), __float_as_uint((v).z), 0x07060302u)); \
+    *reinterpret_cast<uint2*>((base) + (off)) = q_;                                                       \
+    *reinterpret_cast<uint2*>((base) + X6_PLANE + (off)) = q_;                                            \
+    *reinterpret_cast<uint2*>((base) + 2 * X6_PLANE + (off)) = q_;                                        \
+  } while (0)
+#else
+#define X6T_SPLIT_B X6T_SPLIT
+#endif
+#if GRL_X6T_WHATIF == 2
+#define X6T_SPLIT_A X6T_SPLIT_B
+#else
+#define X6T_SPLIT_A X6T_SPLIT
+#endif
 #define X6T_STASH(st)                                                                                     \
   do {                                                                                                    \
     if (!in0) ra0 = rb0 = zero4; /* wave-uniform: only a split's last K16 step branches */                \
     if (!in1) ra1 = rb1 = zero4;                                                                          \
-    X6T_SPLIT(ra0, (st), st_off0);                                                                        \
-    X6T_SPLIT(ra1, (st), st_off1);                                                                        \
-    X6T_SPLIT(rb0, (st) + 3 * X6_PLANE, st_off0);                                                         \
-    X6T_SPLIT(rb1, (st) + 3 * X6_PLANE, st_off1);                                                         \
+    X6T_SPLIT_A(ra0, (st), st_off0);                                                                      \
+    X6T_SPLIT_A(ra1, (st), st_off1);                                                                      \
+    X6T_SPLIT_B(rb0, (st) + 3 * X6_PLANE, st_off0);                                                       \
+    X6T_SPLIT_B(rb1, (st) + 3 * X6_PLANE, st_off1);                                                       \
   } while (0)
 
   // this lane's transposed-read coordinates: k = 8h + ((lane & 15) >> 2),
