@@ -1004,12 +1004,18 @@ __global__ __launch_bounds__(512) void gemm_x6t_kernel(GemmArgs p) {
   // made hipcc branch on the loaded registers and wait vmcnt(0) for them
   // there, exposing the whole load latency on every K16 step
   // (cdna_hip_programming.md, "register or load" selects).
+#if GRL_X6T_WHATIF == 3  // timing only: every step re-reads the split's first rows (cache hits)
+#define X6T_ROW(real, fixed) (fixed)
+#else
+#define X6T_ROW(real, fixed) (real)
+#endif
 #define X6T_LOAD(t)                                                                                       \
   do {                                                                                                    \
     const int64_t k_ = kbeg + (t) * X6_K;                                                                 \
     in0 = k_ + kr0 < kend;                                                                                \
     in1 = k_ + kr1 < kend;                                                                                \
-    const int64_t r0_ = in0 ? k_ + kr0 : kbeg, r1_ = in1 ? k_ + kr1 : kbeg;                               \
+    const int64_t r0_ = X6T_ROW(in0 ? k_ + kr0 : kbeg, kbeg + kr0);                                      \
+    const int64_t r1_ = X6T_ROW(in1 ? k_ + kr1 : kbeg, kbeg + kr1);                                      \
     ra0 = *reinterpret_cast<const float4*>(a_base + r0_ * p.lda);                                         \
     ra1 = *reinterpret_cast<const float4*>(a_base + r1_ * p.lda);                                         \
     rb0 = *reinterpret_cast<const float4*>(b_base + r0_ * p.ldb);                                         \
@@ -1023,9 +1029,11 @@ __global__ __launch_bounds__(512) void gemm_x6t_kernel(GemmArgs p) {
     *reinterpret_cast<uint2*>((base) + X6_PLANE + (off)) = q1_;                                           \
     *reinterpret_cast<uint2*>((base) + 2 * X6_PLANE + (off)) = q2_;                                       \
   } while (0)
-#if GRL_X6T_WHATIF >= 1
-  // timing diagnostics only, WRONG results: B (2: and A) stored as its
-  // truncated top plane, no split (the ceiling of a pre-split g / Z)
+#if GRL_X6T_WHATIF == 1 || GRL_X6T_WHATIF == 2
+  // GRL_X6T_WHATIF (timing diagnostics only, WRONG results): 1 = B (2 = and
+  // A) stored as its truncated top plane, no split (the ceiling of a
+  // pre-split g / Z); 3 = every step loads the split's first rows (cache
+  // hits: the price of Z's HBM stream); 5 = no barrier per step (races)
 #define X6T_SPLIT_B(v, base, off)                                                                         \
   do {                                                                                                    \
     const uint2 q_ = make_uint2(__builtin_amdgcn_perm(__float_as_uint((v).y), __float_as_uint((v).x), 0x07060302u), \
@@ -1106,7 +1114,9 @@ __global__ __launch_bounds__(512) void gemm_x6t_kernel(GemmArgs p) {
         X6T_STASH(smem + (S ^ 1) * X6_STAGE);  // the other stage: last read in step t-1
         if (t + 2 < nk) X6T_LOAD(t + 2);
       }
+#if GRL_X6T_WHATIF != 5  // 5: timing only, no barrier (races)
       __syncthreads();
+#endif
     };
     int64_t t = 0;
     for (; t + 1 < nk; t += 2) {
