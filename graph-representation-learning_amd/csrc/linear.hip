@@ -970,6 +970,19 @@ __device__ __forceinline__ bf16x8_t tr_pair3(const lds_u16* p0) {
 #ifndef GRL_X6T_WHATIF
 #define GRL_X6T_WHATIF 0
 #endif
+#ifndef GRL_X6T_NTA
+#define GRL_X6T_NTA 0
+#endif
+// GRL_X6T_NTA: Z (read once) as non-temporal loads, keeping the L2 for g
+// (re-read by every M tile)
+#if GRL_X6T_NTA
+__device__ __forceinline__ float4 x6t_lda(const float* q) {
+  typedef float v4f __attribute__((ext_vector_type(4)));
+  const v4f v = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(q));
+  return make_float4(v[0], v[1], v[2], v[3]);
+}
+#endif
+
 // GRL_X6T_U2 (read per call; default 1): the K16 loop unrolled over the two
 // stages, fragment reads from per-lane LDS offsets fixed for the kernel (the
 // stage and plane as immediates) -- the rolled loop recomputed ~40 address
@@ -1009,6 +1022,11 @@ __global__ __launch_bounds__(512) void gemm_x6t_kernel(GemmArgs p) {
 #else
 #define X6T_ROW(real, fixed) (real)
 #endif
+#if GRL_X6T_NTA
+#define X6T_LDA(q) x6t_lda(q)
+#else
+#define X6T_LDA(q) (*reinterpret_cast<const float4*>(q))
+#endif
 #define X6T_LOAD(t)                                                                                       \
   do {                                                                                                    \
     const int64_t k_ = kbeg + (t) * X6_K;                                                                 \
@@ -1016,8 +1034,8 @@ __global__ __launch_bounds__(512) void gemm_x6t_kernel(GemmArgs p) {
     in1 = k_ + kr1 < kend;                                                                                \
     const int64_t r0_ = X6T_ROW(in0 ? k_ + kr0 : kbeg, kbeg + kr0);                                      \
     const int64_t r1_ = X6T_ROW(in1 ? k_ + kr1 : kbeg, kbeg + kr1);                                      \
-    ra0 = *reinterpret_cast<const float4*>(a_base + r0_ * p.lda);                                         \
-    ra1 = *reinterpret_cast<const float4*>(a_base + r1_ * p.lda);                                         \
+    ra0 = X6T_LDA(a_base + r0_ * p.lda);                                                                  \
+    ra1 = X6T_LDA(a_base + r1_ * p.lda);                                                                  \
     rb0 = *reinterpret_cast<const float4*>(b_base + r0_ * p.ldb);                                         \
     rb1 = *reinterpret_cast<const float4*>(b_base + r1_ * p.ldb);                                         \
   } while (0)
