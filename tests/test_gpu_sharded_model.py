@@ -199,3 +199,54 @@ def test_sharded_attention_equals_one_gpu(world, N, dk, dv, bounds):
     import torch.multiprocessing as mp
 
     mp.spawn(_attn_worker, args=(world, _free_port(), N, dk, dv, bounds), nprocs=world, join=True)
+
+
+def _stream_chain_worker(rank, world, port, mode, nb):
+    import torch.distributed as dist
+
+    from gnn.models.networks.robust_gcn import GraphConv
+    from grl import DropEdge, TypedGraph
+    from grl.dist import ShardedGraph
+    from grl.ops import graph_conv_infer
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        N, deg, L, d = 60_000 * world, 12.0, 6, 256
+        g = TypedGraph.synthetic(N, deg, L, kind="er", seed=8, device=DEV)
+        sg = ShardedGraph.from_graph(g, halo=mode)
+        rb, re = sg.plan.row_begin, sg.plan.row_end
+        X = torch.randn(N, d, generator=torch.Generator().manual_seed(6)).to(DEV)
+        torch.manual_seed(1)
+        layers = [GraphConv(d, d, L).to(DEV) for _ in range(3)]
+        de = [DropEdge(0.3, 11, c) for c in range(3)]
+        with torch.no_grad():
+            ref = X  # the one-GPU chain (one-kernel layers over the whole graph)
+            for lay, e in zip(layers, de):
+                ref = graph_conv_infer(ref, g.with_dropedge(e), lay.h_weights, lay.bias, True)
+            got = {}
+            for tag, on in (("streamed", True), ("plain", False)):
+                m = sg.with_halo_memo()
+                m.stream_rows, m.stream_blocks = on, nb
+                h = X[rb:re]
+                for lay, e in zip(layers, de):
+                    h = m.graphconv(h, lay, e, relu=True)
+                got[tag] = h.clone()
+                m.clear_halo_memo()
+        assert torch.equal(got["streamed"], got["plain"]), (rank, float((got["streamed"] - got["plain"]).abs().max()))
+        assert torch.equal(got["streamed"], ref[rb:re]), (rank, float((got["streamed"] - ref[rb:re]).abs().max()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode,nb", [("dense", 2), ("dense", 3), ("sparse", 2)])
+def test_streamed_layer_chain_equals_one_gpu(mode, nb):
+    """Three inference GraphConv layers over 2 shards of 60k rows (one-kernel
+    blocks of >= 17.5k rows: the blocks really split): each layer's rows
+    streamed to the peers by blocks as they are written (dense all-gather /
+    sparse all-to-all-v per block) and the next layer reading the filled
+    table -- bitwise the unstreamed sharded chain and the one-GPU chain."""
+    import torch.multiprocessing as mp
+
+    mp.spawn(_stream_chain_worker, args=(2, _free_port(), mode, nb), nprocs=2, join=True)
