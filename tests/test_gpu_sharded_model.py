@@ -234,6 +234,8 @@ def _stream_chain_worker(rank, world, port, mode, nb):
                     h = m.graphconv(h, lay, e, relu=True)
                 got[tag] = h.clone()
                 m.clear_halo_memo()
+        views = sg.graph._shared.get("fwd_row_views", {})
+        assert sum(1 for r0, _ in views if r0 > 0) >= nb - 1, sorted(views)  # the layers ran in row blocks
         assert torch.equal(got["streamed"], got["plain"]), (rank, float((got["streamed"] - got["plain"]).abs().max()))
         assert torch.equal(got["streamed"], ref[rb:re]), (rank, float((got["streamed"] - ref[rb:re]).abs().max()))
     finally:
