@@ -164,7 +164,9 @@ class GraphCNNDropEdge(BaseNetwork):
         x3 = torch.cat([g1, g2], dim=-1)
         if sharded:
             graph.note_concat(x3, (g1, g2))
-        g3 = self.dropout(self.gcn3.propagate(x3, self.edge_dropout(graph, ds), relu=True))
+        # (sharded inference: gcn3's rows feed no later GraphConv, so they are not streamed)
+        g3 = self.dropout(self.gcn3.propagate(x3, self.edge_dropout(graph.without_streaming() if sharded else graph,
+                                                                     ds), relu=True))
         if sharded:
             graph.clear_halo_memo()
         new_v = self.emb2(torch.cat([g1, g3], dim=-1))

@@ -946,6 +946,15 @@ class ShardedGraph:
     stream_rows = True   # under a memo (the drop-in model's forward): see _graphconv_streamed
     stream_blocks = 2
 
+    def without_streaming(self) -> "ShardedGraph":
+        """Shallow copy (the memo shared) whose GraphConv does not stream its
+        output: for a layer whose output no later GraphConv reads (the
+        model's gcn3), whose rows would travel for nothing."""
+        sg = ShardedGraph.__new__(ShardedGraph)
+        sg.__dict__.update(self.__dict__)
+        sg.stream_rows = False
+        return sg
+
     def _can_stream(self, X_loc: torch.Tensor) -> bool:
         p = self.plan
         return bool(self.stream_rows and self.halo_memo is not None and len(p.bounds) > 2
