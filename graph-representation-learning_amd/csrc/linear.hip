@@ -1623,9 +1623,12 @@ bool x6t_shape_ok(int64_t M, int64_t K, int64_t C) {  // M nodes, K = rows of dW
 // K splits of the x6t dW: at most two 256 x 256 workgroups per CU (one is
 // resident per CU at 96 KB of LDS, so the grid runs in two full rounds rather
 // than two and a sliver), >= 16 K16 steps each
+#ifndef GRL_X6T_ROUNDS
+#define GRL_X6T_ROUNDS 2
+#endif
 int x6t_splits(int64_t M, int64_t K, int64_t C) {
   const int64_t tiles = ceil_div(K, LB_M) * ceil_div(C, LB_N);
-  int64_t s = (2 * (int64_t)device_cu_count()) / tiles;
+  int64_t s = (GRL_X6T_ROUNDS * (int64_t)device_cu_count()) / tiles;
   s = std::min<int64_t>(s, ceil_div(M, 16 * X6_K));
   return (int)std::max<int64_t>(1, std::min<int64_t>(s, 512));
 }
