@@ -123,6 +123,20 @@ def _events(n):
     return [torch.cuda.Event(enable_timing=True) for _ in range(n)]
 
 
+def surface(what: str, dev) -> None:
+    """grl.check() after a timed region: a persistent GraphConv kernel that
+    gave up waiting on its LDS ring poisons its outputs (NaN) and sets a
+    sticky word instead of raising at the call (stream-ordered, no host
+    sync); a poisoned run must not be reported as a timing.  Exits non-zero
+    naming the section and the entry point."""
+    from grl import GrlError, device_check
+
+    try:
+        device_check(dev)
+    except GrlError as err:
+        raise SystemExit(f"bench.py: {what}: {err}")
+
+
 def _free_port():
     import socket
 
@@ -217,11 +231,14 @@ def main():
             dist.init_process_group(args.dist_backend)
 
     if args.only == "c1":
-        print(json.dumps({"c1_debug_json": c1_extras(dev, max(3, args.steps))}), flush=True)
+        res = {"c1_debug_json": c1_extras(dev, max(3, args.steps))}
+        surface("c1", dev)
+        print(json.dumps(res), flush=True)
         return
     if args.only == "model":
-        print(json.dumps({"model_one_graph_100k": model_extras(dev),
-                          "model_dense_A_mid_n": model_mid_extras(dev)}), flush=True)
+        res = {"model_one_graph_100k": model_extras(dev), "model_dense_A_mid_n": model_mid_extras(dev)}
+        surface("model", dev)
+        print(json.dumps(res), flush=True)
         return
 
     from grl import DropEdge
@@ -300,6 +317,7 @@ def main():
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t_start
+    surface("timed region", dev)
     per_step = [a.elapsed_time(b) for a, b in zip(ev_s, ev_e)]
     step_ev_ms = float(np.mean(per_step))
     halo = None
@@ -386,15 +404,21 @@ def main():
         dist.barrier()  # the other ranks wait while rank 0 times the host baseline
     if world == 1 and wname.startswith("C3"):
         out["dropedge_train_p0.3"] = dropedge_train(graph, X_loc, E_loc, 3)
+        surface("dropedge_train_p0.3", dev)
         if args.c4_reference:
             out["C4_one_gpu"] = c4_one_gpu(dev, max(3, min(10, args.steps)))
+            surface("C4_one_gpu", dev)
     if args.extras and world == 1:
         out["extras"] = extras(args, graph, X_loc, L, F, dev, E_loc, n_loc)
+        surface("extras (layers)", dev)
         del X_loc, X_full, Z
         torch.cuda.empty_cache()  # C1 is a small-graph workload: time it without C3's 8 GB resident
         out["extras"]["c1_debug_json"] = c1_extras(dev)
+        surface("extras c1_debug_json", dev)
         out["extras"]["model_one_graph_100k"] = model_extras(dev)
+        surface("extras model_one_graph_100k", dev)
         out["extras"]["model_dense_A_mid_n"] = model_mid_extras(dev)
+        surface("extras model_dense_A_mid_n", dev)
     if rank == 0:
         print(json.dumps(out), flush=True)
     if world > 1:

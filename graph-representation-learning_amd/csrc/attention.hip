@@ -1789,6 +1789,8 @@ __global__ void attn_fwd_combine_kernel(AttnArgs a, int64_t rows, int S) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_all; i += (int64_t)gridDim.x * blockDim.x) {
     const int64_t row = i / a.dv;
     const int f = (int)(i - row * a.dv);
+    const int64_t q = row % a.N;
+    if (q < a.q0 || q >= a.q1) continue;  // a query range (grl_node_attention_fwd_rows): its rows only
     float M = -INFINITY;
     for (int s = 0; s < S; ++s) M = fmaxf(M, pm[s * rows + row]);
     float L = 0.0f, O = 0.0f;
@@ -2127,7 +2129,6 @@ extern "C" int grl_node_attention_fwd_rows(const float* Q, const float* K, const
   a.dv = dv;
   a.q0 = q_begin;
   a.q1 = q_end;
-  const bool ranged = q_begin != 0 || q_end != N;
   hipStream_t st = as_stream(stream);
   int S = 1;
   // below ~4k rows the per-call split launches cost more than the in-kernel
@@ -2143,7 +2144,9 @@ extern "C" int grl_node_attention_fwd_rows(const float* Q, const float* K, const
     }
     GRL_LAUNCH_CHECK();
     int64_t kr;
-    S = ranged ? 1 : attn_splits(B, N, &kr);  // small N: key split with (o, m, l) partials (whole range only)
+    // small N: key split with (o, m, l) partials.  The split depends on N alone, not on the query range, so
+    // a node-range shard's query rows (grl.dist sharded attention) are bitwise the whole-range call's rows.
+    S = attn_splits(B, N, &kr);
     if (S > 1 && cur + (size_t)S * B * N * (dv + 2) * 4 <= end) {
       a.part = reinterpret_cast<float*>(cur);
       a.kr = kr;

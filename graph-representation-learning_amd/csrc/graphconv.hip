@@ -1130,16 +1130,36 @@ int graphconv_fused_bwd_data(const GrlTypedCsr* gt, const int32_t* eid, const fl
 
 }  // namespace grl
 
+namespace grl {
+namespace {
+// grl_check's read-and-clear in ONE atomic exchange, its old value written
+// to a pinned host word: a poison kernel on another stream that lands
+// between a read and a separate clear would lose its report.
+__global__ void sticky_take_kernel(int* __restrict__ host_word) {
+  if (threadIdx.x == 0) {
+    const int old = __hip_atomic_exchange(&g_grl_sticky, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(host_word, old, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+}  // namespace
+}  // namespace grl
+
 extern "C" int grl_check(grl_stream_t stream) {
   using namespace grl;
   hipStream_t st = as_stream(stream);
-  int h = 0;
-  GRL_HIP(hipMemcpyFromSymbolAsync(&h, HIP_SYMBOL(g_grl_sticky), sizeof(int), 0, hipMemcpyDeviceToHost, st));
+  // one pinned word per host thread (virtual ranks check concurrently), allocated once
+  thread_local int* word = nullptr;
+  if (!word) {
+    void* p = nullptr;
+    GRL_HIP(hipHostMalloc(&p, sizeof(int), hipHostMallocCoherent));
+    word = static_cast<int*>(p);
+  }
+  *reinterpret_cast<volatile int*>(word) = 0;
+  hipLaunchKernelGGL(sticky_take_kernel, dim3(1), dim3(64), 0, st, word);
+  GRL_LAUNCH_CHECK();
   GRL_HIP(hipStreamSynchronize(st));
+  const int h = *reinterpret_cast<volatile int*>(word);
   if (h == 0) return GRL_OK;
-  const int zero = 0;
-  GRL_HIP(hipMemcpyToSymbolAsync(HIP_SYMBOL(g_grl_sticky), &zero, sizeof(int), 0, hipMemcpyHostToDevice, st));
-  GRL_HIP(hipStreamSynchronize(st));
   GRL_FAIL(GRL_E_TIMEOUT, "%s%s%s%s%s: a wave of the persistent GraphConv kernel gave up waiting on its LDS ring "
            "(bound %d sleeps); those calls' outputs were set to NaN",
            (h & WS_WHO_FWD) ? "grl_graphconv_fwd" : "", (h & WS_WHO_FWD) && (h & ~WS_WHO_FWD) ? ", " : "",

@@ -56,6 +56,15 @@ struct GemmArgs {
   // launched as one dimension; inner_n: which tile index runs fastest
   int64_t mt, nt, zt;
   int inner_n;
+  // M-invariant fp32 path (run_output_gemm): K is summed in fixed chunks of
+  // k_chunk_tiles K tiles each, the chunk sums added in chunk order --
+  // across K splits (one chunk per split, slabs added in split order) or
+  // inside one workgroup (CHUNKED gemm_kernel).  Either way every output
+  // element is the same fp32 operations whatever M is.
+  int64_t k_chunk_tiles;
+  // rows the x6-vs-fp32 path choice is made for (0: M): a node-range shard
+  // passes the whole graph's row count, so it takes the one-GPU call's path
+  int64_t path_rows;
 };
 
 #ifndef GRL_GEMM_XCD
@@ -167,7 +176,7 @@ struct Operand {
 
 // A(m, k): A_KC ? A[m*lda + k] : A[k*lda + m]
 // B(k, n): B_KC ? B[n*ldb + k] : B[k*ldb + n]
-template <bool A_KC, bool B_KC, int EPI, bool ALIGNED, bool MASK_A, bool MASK_B, int BK>
+template <bool A_KC, bool B_KC, int EPI, bool ALIGNED, bool MASK_A, bool MASK_B, int BK, bool CHUNKED = false>
 __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs p) {
   using OA = Operand<A_KC, ALIGNED, MASK_A, BK>;
   using OB = Operand<B_KC, ALIGNED, MASK_B, BK>;
@@ -201,13 +210,14 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs p) {
   ob.row0 = n0;
   const bool rows_in = ALIGNED && (m0 + BM <= p.M) && (n0 + BN <= p.N);
 
-  f32x16 acc[2][2];
+  f32x16 acc[2][2], tot[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = tot[i][j][r] = 0.0f;
+  int64_t kt = 0;  // CHUNKED: K tiles into the current chunk
 
   auto mma_step = [&](const float* As, const float* Bs) {
 #pragma unroll
@@ -260,7 +270,27 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs p) {
       ob.fetch(tid, kn, kend, in);
     }
     mma_step(smem, smem + OA::lds_floats());
+    if constexpr (CHUNKED) {  // chunk done: add its sum to the total, in chunk order (= the split-K slabs)
+      if (++kt == p.k_chunk_tiles || kn >= kend) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              tot[i][j][r] += acc[i][j][r];
+              acc[i][j][r] = 0.0f;
+            }
+        kt = 0;
+      }
+    }
     __syncthreads();
+  }
+  if constexpr (CHUNKED) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = tot[i][j];
   }
 
   // ---- epilogue: C/D map col = lane&31, row = (r&3) + 8(r>>2) + 4h --------
@@ -1196,7 +1226,7 @@ bool al16(const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; }
 #endif
 constexpr int GEMM_BK = GRL_GEMM_BK;
 
-template <bool A_KC, bool B_KC, int EPI>
+template <bool A_KC, bool B_KC, int EPI, bool CHUNKED = false>
 int launch_gemm(GemmArgs a, int splits, bool aligned, hipStream_t st) {
   if (a.M == 0 || a.N == 0) return GRL_OK;
   a.mt = ceil_div(a.M, BM);
@@ -1209,7 +1239,7 @@ int launch_gemm(GemmArgs a, int splits, bool aligned, hipStream_t st) {
   const dim3 grid((unsigned)(a.mt * a.nt * a.zt));
   const bool ma = a.Amask != nullptr, mb = a.Bmask != nullptr;
 #define GRL_GEMM(AL, MA, MB) \
-  hipLaunchKernelGGL((gemm_kernel<A_KC, B_KC, EPI, AL, MA, MB, GEMM_BK>), grid, dim3(256), 0, st, a)
+  hipLaunchKernelGGL((gemm_kernel<A_KC, B_KC, EPI, AL, MA, MB, GEMM_BK, CHUNKED>), grid, dim3(256), 0, st, a)
   if (aligned) {
     if (ma) GRL_GEMM(true, true, false); else if (mb) GRL_GEMM(true, false, true); else GRL_GEMM(true, false, false);
   } else {
@@ -1228,19 +1258,35 @@ int pick_splits(int64_t M, int64_t N, int64_t K) {
   return (int)std::max<int64_t>(1, std::min<int64_t>(s, 256));
 }
 
-// Split-K for an output-stationary GEMM (forward, data gradient) whose tiles
-// alone cannot fill the chip -- small graphs (a 74-node page is one 128-row
-// tile): a lone workgroup walking all of K is bound by load latency, not by
-// the matrix cores.  Large M (>= one tile per CU) never splits.
+// The output-stationary fp32 GEMM (forward, data gradient; the x6 path's
+// fallback) sums K in fixed chunks whose size depends on K alone: at most
+// 16 chunks of whole K tiles.  Small M (tiles that cannot fill the chip: a
+// 74-node page is one 128-row tile) runs one chunk per K split into fp32
+// slabs that a second pass adds in chunk order -- a lone workgroup walking
+// all of K is bound by load latency, not by the matrix cores; larger M runs
+// unsplit, each workgroup adding its chunk sums in the same order
+// (gemm_kernel<..., CHUNKED>).  Both give every element the same operations,
+// so a row's result does not depend on M: a node-range shard's rows equal
+// the whole graph's.
+constexpr int64_t kFp32MaxChunks = 16;
+constexpr size_t kFp32SlabCap = (size_t)256 << 20;  // slab bytes above which the unsplit form runs
+
+int64_t fp32_chunk_tiles(int64_t K) {
+  const int64_t tiles = std::max<int64_t>(1, ceil_div(K, GEMM_BK));
+  return ceil_div(tiles, kFp32MaxChunks);
+}
+
+int fp32_chunks(int64_t K) {
+  return (int)ceil_div(std::max<int64_t>(1, ceil_div(K, GEMM_BK)), fp32_chunk_tiles(K));
+}
+
+// K splits of the fp32 output GEMM: the chunk count (slabs) or 1 (unsplit)
 int pick_splits_small(int64_t M, int64_t N, int64_t K) {
   const int64_t tiles = ceil_div(M, BM) * ceil_div(N, BN);
-  const int64_t cus = device_cu_count();
-  if (tiles >= cus) return 1;
-  int64_t s = (2 * cus) / std::max<int64_t>(tiles, 1);
-  s = std::min<int64_t>(s, ceil_div(K, GEMM_BK));  // >= one K tile per split
-  const char* e = getenv("GRL_GEMM_SMALL_SPLITS");  // A/B aid: force the split count
-  if (e && atoi(e) > 0) s = std::min<int64_t>(atoi(e), ceil_div(K, GEMM_BK));
-  return (int)std::max<int64_t>(1, std::min<int64_t>(s, 64));
+  const int s = fp32_chunks(K);
+  if (s <= 1 || tiles >= (int64_t)device_cu_count()) return 1;
+  if ((size_t)s * (size_t)M * (size_t)N * 4 > kFp32SlabCap) return 1;
+  return s;
 }
 
 // row blocks of the db column sum: ~64 rows each (>= 1 block, <= 1024)
@@ -1298,6 +1344,18 @@ size_t x6_ws_bytes(int64_t M, int64_t N, int64_t K) {
   return x6_shape_ok(M, N, K) ? (size_t)3 * (size_t)x6_np(N) * (size_t)K * 2 + 256 : 0;
 }
 
+// The path choice for an M-row call made on behalf of `path_rows` rows (a
+// node-range shard's rows of a graph of path_rows nodes; 0: M itself): the
+// size floor is the whole call's, so every shard takes the one-GPU path.
+// (The x6 kernels clamp their A rows, so any M >= 1 is safe on them.)
+int64_t path_rows_of(int64_t M, int64_t path_rows) { return std::max<int64_t>(M, path_rows); }
+bool x6_path_ok(int64_t M, int64_t path_rows, int64_t N, int64_t K) {
+  return M >= 1 && x6_shape_ok(path_rows_of(M, path_rows), N, K);
+}
+size_t x6_ws_bytes_p(int64_t M, int64_t path_rows, int64_t N, int64_t K) {
+  return M >= 1 ? x6_ws_bytes(path_rows_of(M, path_rows), N, K) : 0;
+}
+
 template <bool B_KC>
 int split_b_planes(const GemmArgs& a, uint16_t* planes, hipStream_t st) {
   const int64_t Np = x6_np(a.N);
@@ -1348,10 +1406,10 @@ int launch_x6(GemmArgs a, void* ws, hipStream_t st) {
 // [split][M][N], then one ordered reduce applying bias / ReLU).
 template <bool A_KC, bool B_KC>
 int run_output_gemm(GemmArgs a, bool aligned, const char* who, void* ws, size_t ws_bytes, hipStream_t st) {
-  if (A_KC && aligned && !a.Amask && !a.Bmask && x6_shape_ok(a.M, a.N, a.K) && ws && al16(ws) &&
-      ws_bytes >= x6_ws_bytes(a.M, a.N, a.K))  // large M: fp32 on the bf16 matrix cores
+  if (A_KC && aligned && !a.Amask && !a.Bmask && x6_path_ok(a.M, a.path_rows, a.N, a.K) && ws && al16(ws) &&
+      ws_bytes >= x6_ws_bytes_p(a.M, a.path_rows, a.N, a.K))  // large M: fp32 on the bf16 matrix cores
     return launch_x6<B_KC>(a, ws, st);
-  if (big_ok(a, aligned)) {  // forward and dZ at large M: the pipelined 256^2 LDS-DMA tile
+  if (a.path_rows == 0 && big_ok(a, aligned)) {  // forward and dZ at large M: the pipelined 256^2 LDS-DMA tile
     a.k_per_split = std::max<int64_t>(a.K, 1);
     return a.bias || a.relu ? launch_gemm256p<A_KC, B_KC, EPI_BIAS>(a, 1, st)
                             : launch_gemm256p<A_KC, B_KC, EPI_STORE>(a, 1, st);
@@ -1359,8 +1417,9 @@ int run_output_gemm(GemmArgs a, bool aligned, const char* who, void* ws, size_t 
   const int splits = pick_splits_small(a.M, a.N, a.K);
   if (splits == 1) {
     a.k_per_split = std::max<int64_t>(a.K, 1);
-    return a.bias || a.relu ? launch_gemm<A_KC, B_KC, EPI_BIAS>(a, 1, aligned, st)
-                            : launch_gemm<A_KC, B_KC, EPI_STORE>(a, 1, aligned, st);
+    a.k_chunk_tiles = fp32_chunk_tiles(a.K);
+    return a.bias || a.relu ? launch_gemm<A_KC, B_KC, EPI_BIAS, true>(a, 1, aligned, st)
+                            : launch_gemm<A_KC, B_KC, EPI_STORE, true>(a, 1, aligned, st);
   }
   const size_t need = small_ws_bytes(a.M, a.N, a.K);
   if (!ws || ws_bytes < need) GRL_FAIL(GRL_E_WORKSPACE, "%s: workspace %zu < %zu", who, ws_bytes, need);
@@ -1372,8 +1431,8 @@ int run_output_gemm(GemmArgs a, bool aligned, const char* who, void* ws, size_t 
   a.ldc = a.N;
   a.bias = nullptr;
   a.relu = 0;
-  a.k_per_split = ceil_div(ceil_div(a.K, splits), GEMM_BK) * GEMM_BK;
-  const int used = (int)ceil_div(a.K, a.k_per_split);  // trailing splits may be empty
+  a.k_per_split = fp32_chunk_tiles(a.K) * GEMM_BK;  // one chunk per split
+  const int used = (int)ceil_div(a.K, a.k_per_split);
   int rc = launch_gemm<A_KC, B_KC, EPI_SLAB>(a, used, aligned, st);
   if (rc) return rc;
   const int64_t n = a.M * a.N;
@@ -1388,23 +1447,28 @@ int run_output_gemm(GemmArgs a, bool aligned, const char* who, void* ws, size_t 
 
 using namespace grl;
 
-extern "C" size_t grl_linear_fwd_workspace_size(int64_t M, int32_t K, int32_t C) {
-  return M > 0 && K > 0 && C > 0 ? std::max(small_ws_bytes(M, C, K), x6_ws_bytes(M, C, K)) : 0;
+extern "C" size_t grl_linear_fwd_ex_workspace_size(int64_t M, int32_t K, int32_t C, int64_t path_rows) {
+  return M > 0 && K > 0 && C > 0 ? std::max(small_ws_bytes(M, C, K), x6_ws_bytes_p(M, path_rows, C, K)) : 0;
 }
 
-extern "C" int grl_linear_fwd(const float* Z, int64_t ldz, const float* W, const float* bias, float* out, int64_t M,
-                              int32_t K, int32_t C, int32_t relu, void* workspace, size_t workspace_bytes,
-                              grl_stream_t stream) {
+extern "C" size_t grl_linear_fwd_workspace_size(int64_t M, int32_t K, int32_t C) {
+  return grl_linear_fwd_ex_workspace_size(M, K, C, 0);
+}
+
+extern "C" int grl_linear_fwd_ex(const float* Z, int64_t ldz, const float* W, int32_t w_layout, const float* bias,
+                                 float* out, int64_t M, int32_t K, int32_t C, int32_t relu, int64_t path_rows,
+                                 void* workspace, size_t workspace_bytes, grl_stream_t stream) {
   TraceRange trace_("grl_linear_fwd");
-  GRL_CHECK_ARG(M >= 0 && K >= 0 && C >= 0, "grl_linear_fwd: negative size");
+  GRL_CHECK_ARG(M >= 0 && K >= 0 && C >= 0 && path_rows >= 0, "grl_linear_fwd: negative size");
   GRL_CHECK_ARG(ldz >= K, "grl_linear_fwd: ldz (%lld) < K (%d)", (long long)ldz, K);
+  GRL_CHECK_ARG(w_layout == 0 || w_layout == 1, "grl_linear_fwd: w_layout must be 0 ([K][C]) or 1 ([C][K])");
   if (M == 0 || C == 0) return GRL_OK;
   GRL_CHECK_ARG(Z && W && out, "grl_linear_fwd: NULL pointer");
   GemmArgs a{};
   a.A = Z;
   a.lda = ldz;
   a.B = W;
-  a.ldb = C;
+  a.ldb = w_layout ? K : C;
   a.C = out;
   a.ldc = C;
   a.bias = bias;
@@ -1412,11 +1476,27 @@ extern "C" int grl_linear_fwd(const float* Z, int64_t ldz, const float* W, const
   a.N = C;
   a.K = K;
   a.relu = relu;
+  a.path_rows = path_rows;
   const bool aligned = al16(Z) && al16(W) && ldz % 4 == 0 && C % 4 == 0 && K % 4 == 0;
-  return run_output_gemm<true, false>(a, aligned, "grl_linear_fwd", workspace, workspace_bytes, as_stream(stream));
+  hipStream_t st = as_stream(stream);
+  return w_layout ? run_output_gemm<true, true>(a, aligned, "grl_linear_fwd", workspace, workspace_bytes, st)
+                  : run_output_gemm<true, false>(a, aligned, "grl_linear_fwd", workspace, workspace_bytes, st);
+}
+
+extern "C" int grl_linear_fwd(const float* Z, int64_t ldz, const float* W, const float* bias, float* out, int64_t M,
+                              int32_t K, int32_t C, int32_t relu, void* workspace, size_t workspace_bytes,
+                              grl_stream_t stream) {
+  return grl_linear_fwd_ex(Z, ldz, W, 0, bias, out, M, K, C, relu, 0, workspace, workspace_bytes, stream);
 }
 
 static size_t ws_align(size_t b) { return (b + 255) & ~(size_t)255; }
+
+// the two-kernel form's workspace for a graph whose GEMM path is chosen for path_rows rows
+static size_t graphconv_two_kernel_ws(const GrlTypedCsr* g, int F, int C) {
+  const int64_t K = (int64_t)(g->num_types + (g->has_self ? 1 : 0)) * F;
+  return ws_align((size_t)g->num_rows * (size_t)K * 4) +
+         grl_linear_fwd_ex_workspace_size(g->num_rows, (int32_t)K, C, g->path_rows);
+}
 
 // grl_graphconv_fwd takes the fused kernel when its arithmetic equals the
 // two-kernel path's (the linear on the x6 GEMM: large graphs, 16-B aligned W,
@@ -1425,7 +1505,8 @@ static size_t ws_align(size_t b) { return (b + 255) & ~(size_t)255; }
 // partials, a different order).
 static bool fused_path(const GrlTypedCsr* g, const float* X, int64_t ldx, int F, const float* W, int C) {
   const int64_t K = (int64_t)(g->num_types + (g->has_self ? 1 : 0)) * F;
-  return graphconv_fused_enabled() && graphconv_fused_shape_ok(F, C, g->num_types) && x6_shape_ok(g->num_rows, C, K) &&
+  return graphconv_fused_enabled() && graphconv_fused_shape_ok(F, C, g->num_types) &&
+         x6_path_ok(g->num_rows, g->path_rows, C, K) &&
          al16(W) && C % 4 == 0 && al16(X) && ldx % 4 == 0 && ldx < (1LL << 30) &&  // gather: 32-bit row bytes
          (!g->split || g->split->num_heavy == 0);
 }
@@ -1436,7 +1517,7 @@ extern "C" size_t grl_graphconv_fwd_workspace_query(const GrlTypedCsr* g, const 
   const int64_t K = (int64_t)(g->num_types + (g->has_self ? 1 : 0)) * F;
   if (K > 2147483647LL) return 0;
   if (fused_path(g, X, ldx, F, W, C)) return graphconv_fused_ws_bytes(K, C);
-  return grl_graphconv_fwd_workspace_size(g->num_rows, g->num_types, g->has_self, F, C);
+  return graphconv_two_kernel_ws(g, F, C);
 }
 
 extern "C" size_t grl_graphconv_fwd_workspace_size(int64_t num_rows, int32_t num_types, int32_t has_self, int32_t F,
@@ -1446,6 +1527,7 @@ extern "C" size_t grl_graphconv_fwd_workspace_size(int64_t num_rows, int32_t num
   if (K > 2147483647LL) return 0;
   return ws_align((size_t)num_rows * (size_t)K * 4) + grl_linear_fwd_workspace_size(num_rows, (int32_t)K, C);
 }
+
 
 extern "C" int grl_graphconv_fwd(const GrlTypedCsr* g, const float* X, int64_t ldx, int32_t F, const float* W,
                                  const float* bias, int32_t C, int32_t relu, float* out, const GrlDropEdge* de,
@@ -1471,21 +1553,22 @@ extern "C" int grl_graphconv_fwd(const GrlTypedCsr* g, const float* X, int64_t l
     GRL_CHECK_ARG(g->nnz < 2147483647LL, "grl_graphconv_fwd: nnz %lld exceeds int32", (long long)g->nnz);
     return graphconv_fused_fwd(g, X, ldx, F, W, bias, C, relu, out, de, ws, st);
   }
-  if (ws && workspace_bytes >= grl_graphconv_fwd_workspace_size(M, g->num_types, hs, F, C)) {
+  if (ws && workspace_bytes >= graphconv_two_kernel_ws(g, F, C)) {
     // whole graph: Z in the workspace, then the linear (its workspace behind Z)
     float* Z = reinterpret_cast<float*>(ws);
     int rc = grl_typed_spmm_fwd(g, X, ldx, F, Z, de, stream);
     if (rc) return rc;
-    return grl_linear_fwd(Z, K, W, bias, out, M, K, C, relu, ws + zfull, workspace_bytes - zfull, stream);
+    return grl_linear_fwd_ex(Z, K, W, 0, bias, out, M, K, C, relu, g->path_rows, ws + zfull, workspace_bytes - zfull,
+                             stream);
   }
   // Row chunks: Z for R rows at a time (bounded memory), on the x6 GEMM only,
   // whose per-element arithmetic does not depend on M -- so the result is
   // bitwise that of the whole-graph call.
-  const bool x6 = x6_shape_ok(M, C, K) && al16(W) && C % 4 == 0;
+  const bool x6 = x6_path_ok(M, g->path_rows, C, K) && al16(W) && C % 4 == 0;
   if (!x6 || (g->split && g->split->num_heavy > 0) || !ws)
     GRL_FAIL(GRL_E_WORKSPACE, "grl_graphconv_fwd: workspace %zu < %zu (row chunking needs the x6 GEMM shape and no "
              "heavy-row split plan)", workspace_bytes, grl_graphconv_fwd_workspace_size(M, g->num_types, hs, F, C));
-  const size_t planes_bytes = ws_align(x6_ws_bytes(M, C, K));
+  const size_t planes_bytes = ws_align(x6_ws_bytes_p(M, g->path_rows, C, K));
   const int64_t per_row = (int64_t)K * 4;
   int64_t R = workspace_bytes > planes_bytes ? (int64_t)((workspace_bytes - planes_bytes) / per_row) : 0;
   R = R / LB_M * LB_M;
@@ -1582,7 +1665,8 @@ extern "C" int grl_graphconv_fwd_train(const GrlTypedCsr* g, const float* X, int
     return graphconv_fused_fwd(g, X, ldx, F, W, bias, C, relu, out, de, ws, as_stream(stream), Z);
   }
   const int rc = grl_typed_spmm_fwd(g, X, ldx, F, Z, de, stream);
-  return rc ? rc : grl_linear_fwd(Z, K, W, bias, out, M, K, C, relu, workspace, workspace_bytes, stream);
+  return rc ? rc : grl_linear_fwd_ex(Z, K, W, 0, bias, out, M, K, C, relu, g->path_rows, workspace, workspace_bytes,
+                                     stream);
 }
 
 extern "C" size_t grl_linear_bwd_data_workspace_size(int64_t M, int32_t K, int32_t C) {

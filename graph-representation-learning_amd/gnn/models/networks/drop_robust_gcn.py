@@ -17,13 +17,12 @@ from typing import Optional
 
 import torch
 from torch import nn
-from torch.nn import functional as F
 
 from gnn.models.base_network import BaseNetwork
-from gnn.models.networks.robust_gcn import GraphConv, NodeSelfAtten, make_linear_relu
+from gnn.models.networks.robust_gcn import GraphConv, NodeSelfAtten, apply_linear, make_linear_relu
 from grl import DropEdge, TypedGraph
 from grl.dist import ShardedGraph
-from grl.ops import bag_linear
+from grl.ops import bag_linear, feature_dropout
 
 RP_FACTOR = 10
 
@@ -100,6 +99,76 @@ class EdgeDropout(nn.Dropout):
         return A.with_dropedge(DropEdge(p=float(self.p), seed=seed, call=call, drop_self=drop_self))
 
 
+class FeatureDropout(nn.Dropout):
+    """nn.Dropout(p) on node-feature rows (drop_robust_gcn.py:64,77,81,86,100)
+    whose mask is a counter hash of (seed, call, global row, column)
+    (grl_feature_dropout): the mask of a row does not depend on where the
+    row is computed, so a node-range shard draws exactly the one-GPU model's
+    mask for its rows, and a row block's mask is computable on its own.
+    The distribution is the reference's (i.i.d. keep(1-p), scaled by
+    1/(1-p)); the draws are not torch's generator stream.
+
+    Seeds, as EdgeDropout's: `seed_source` (a device word a captured training
+    step writes) takes precedence; else a fixed `seed` with calls numbered
+    0, 1, 2, ... (reset_calls()); else begin_forward() draws one device seed
+    per forward (torch's CUDA generator, so torch.manual_seed reproduces
+    runs; broadcast from rank 0 on a sharded graph) and numbers that
+    forward's calls from 0.  `stream` (data-parallel rank) keeps the ranks'
+    masks independent.  Host tensors get plain nn.Dropout."""
+
+    STREAM_SHIFT = 32
+    DOMAIN = 1 << 48  # call ids apart from EdgeDropout's (which may share the seed)
+
+    def __init__(self, p: float = 0.5, seed: Optional[int] = None):
+        super().__init__(p=p)
+        self.seed = seed
+        self.stream = 0
+        self.seed_source: Optional[torch.Tensor] = None
+        self._calls = 0
+        self._seed_t: Optional[torch.Tensor] = None
+        self.row0 = 0
+
+    def reset_calls(self) -> None:
+        self._calls = 0
+
+    def begin_forward(self, device, shard: Optional[ShardedGraph] = None) -> None:
+        """Per-forward state: the global row of this rank's first row, and
+        (device-drawn seeds) the forward's seed."""
+        self.row0 = shard.plan.row_begin if shard is not None else 0
+        if self.seed_source is not None or self.seed is not None or not self.training or self.p == 0.0 \
+                or torch.device(device).type != "cuda":
+            return
+        seed_t = torch.randint(0, 2**62, (1,), dtype=torch.int64, device=device)
+        self._seed_t = shard.broadcast_seed(seed_t) if shard is not None else seed_t
+        self._calls = 0
+
+    def record(self, device) -> Optional[DropEdge]:
+        """The next call's draw (p, seed, call id) as a DropEdge record, or
+        None when the dropout is the identity (eval, p == 0) or runs on the
+        host; consumes a call id.  A layer that fuses this dropout
+        (GraphConv.propagate on a shard) applies it with row0."""
+        if not self.training or self.p == 0.0 or torch.device(device).type != "cuda":
+            return None
+        call = self.DOMAIN + self._calls + (self.stream << self.STREAM_SHIFT)
+        self._calls += 1
+        if self.seed_source is not None:
+            return DropEdge(p=float(self.p), seed=0, call=call, seed_tensor=self.seed_source)
+        if self.seed is not None:
+            return DropEdge(p=float(self.p), seed=self.seed, call=call)
+        if self._seed_t is None or self._seed_t.device != torch.device(device):
+            self.begin_forward(device)
+            call = self.DOMAIN + (self.stream << self.STREAM_SHIFT)
+            self._calls = 1
+        return DropEdge(p=float(self.p), seed=0, call=call, seed_tensor=self._seed_t)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        if not self.training or self.p == 0.0:
+            return x
+        if not x.is_cuda:
+            return super().forward(x)
+        return feature_dropout(x.float(), self.record(x.device), self.row0)
+
+
 # grl_bag_linear_fwd keeps one output row per wave in registers (include/grl.h)
 BAG_LINEAR_MAX_C = 512
 
@@ -114,7 +183,7 @@ class GraphCNNDropEdge(BaseNetwork):
         # emb1's input is a bag-of-characters row (~7 nonzeros of 4369): run it
         # as a sparse-row gather (grl_bag_linear_fwd); False = dense torch Linear
         self.sparse_emb1 = True
-        self.dropout = nn.Dropout(p=0.5)
+        self.dropout = FeatureDropout(p=0.5, seed=dropedge_seed)
         self.edge_dropout = EdgeDropout(p=0.3, seed=dropedge_seed)
         self.gcn1 = GraphConv(self.net_size, self.net_size, num_edges)
         self.gcn2 = GraphConv(self.net_size, self.net_size, num_edges)
@@ -150,27 +219,32 @@ class GraphCNNDropEdge(BaseNetwork):
     def forward(self, inputs, efficient_mode: bool = True):
         V, A = inputs
         graph = self.to_graph(A)
+        sharded = isinstance(graph, ShardedGraph)
+        # row-local layers of a shard take the one-GPU model's GEMM path (bitwise its rows)
+        pr = graph.global_rows if sharded else 0
+        self.dropout.begin_forward(V.device, graph if sharded else None)
         embedding = self.dropout(self._embed(V))
         # efficient_mode=True: dropout covers the identity block of A_pre
         # (:69,:76); False: dropout hits raw A, identity added after (:72-74).
         ds = bool(efficient_mode)
-        sharded = isinstance(graph, ShardedGraph)
         if sharded:  # gcn3's input cat[g1, g2]: g1's halo rows already came for gcn2
             graph = graph.with_halo_memo()
-        g1 = self.dropout(self.gcn1.propagate(embedding, self.edge_dropout(graph, ds), relu=True))
+        # each GraphConv's feature dropout (:77,:81,:86) rides in propagate: on a shard in training it is fused
+        # into the layer, whose output rows then stream to the peers while the rest of the layer computes
+        g1 = self.gcn1.propagate(embedding, self.edge_dropout(graph, ds), relu=True, dropout=self.dropout)
         if sharded:
             graph.remember(g1)
-        g2 = self.dropout(self.gcn2.propagate(g1, self.edge_dropout(graph, ds), relu=True))
+        g2 = self.gcn2.propagate(g1, self.edge_dropout(graph, ds), relu=True, dropout=self.dropout)
         x3 = torch.cat([g1, g2], dim=-1)
         if sharded:
             graph.note_concat(x3, (g1, g2))
         # (sharded inference: gcn3's rows feed no later GraphConv, so they are not streamed)
-        g3 = self.dropout(self.gcn3.propagate(x3, self.edge_dropout(graph.without_streaming() if sharded else graph,
-                                                                     ds), relu=True))
+        g3 = self.gcn3.propagate(x3, self.edge_dropout(graph.without_streaming() if sharded else graph, ds),
+                                 relu=True, dropout=self.dropout)
         if sharded:
             graph.clear_halo_memo()
-        new_v = self.emb2(torch.cat([g1, g3], dim=-1))
+        new_v = apply_linear(self.emb2, torch.cat([g1, g3], dim=-1), path_rows=pr)
         if self.use_attention:
-            new_v = self.self_atten(new_v, shard=graph) if isinstance(graph, ShardedGraph) else self.self_atten(new_v)
-        new_v = self.dropout(F.relu(self.w_rand(new_v)))
-        return self.classifier(new_v)
+            new_v = self.self_atten(new_v, shard=graph) if sharded else self.self_atten(new_v)
+        new_v = self.dropout(apply_linear(self.w_rand.projection, new_v, relu=True, path_rows=pr))
+        return apply_linear(self.classifier, new_v, path_rows=pr)

@@ -19,12 +19,27 @@ from torch import nn
 
 from grl import TypedGraph
 from grl.dist import ShardedGraph, sharded_node_attention
-from grl.ops import graph_conv, node_self_attention
+from grl.ops import graph_conv, node_self_attention, row_linear
 
 
 def make_linear_relu(input_dim: int, output_dim: int) -> nn.Sequential:
     """Linear + ReLU block (robust_gcn.py:10-11); state_dict keys `0.weight`, `0.bias`."""
     return nn.Sequential(nn.Linear(input_dim, output_dim), nn.ReLU())
+
+
+def apply_linear(mod: nn.Module, x: torch.Tensor, relu: bool = False, path_rows: int = 0) -> torch.Tensor:
+    """An nn.Linear (or a make_linear_relu block, its ReLU fused) over the rows
+    of x.  On the device: the libgrl GEMM (grl.ops.row_linear), whose row
+    results do not depend on the row count -- with path_rows (a node-range
+    shard's whole-graph row count) a shard's rows are bitwise the one-GPU
+    model's; on the host: torch."""
+    lin = mod[0] if isinstance(mod, nn.Sequential) else mod
+    if isinstance(mod, nn.Sequential):
+        relu = True
+    if x.is_cuda:
+        return row_linear(x.float(), lin.weight, lin.bias, relu=relu, path_rows=path_rows)
+    y = lin(x)
+    return torch.relu(y) if relu else y
 
 
 AdjLike = Union[TypedGraph, torch.Tensor]
@@ -76,22 +91,31 @@ class GraphConv(nn.Module):
         return TypedGraph.from_dense(self._on_device(A), layout="pre")
 
     # ------------------------------------------------------------- forward
-    def propagate(self, V: torch.Tensor, graph, relu: bool = False) -> torch.Tensor:
+    def propagate(self, V: torch.Tensor, graph, relu: bool = False, dropout=None) -> torch.Tensor:
         """Aggregate + linear (+ fused ReLU) on a ready TypedGraph, or on this
         rank's node-range shard of a graph (grl.dist.ShardedGraph: V holds the
         shard's rows; the halo exchange runs inside, the output rows are the
-        shard's, every value the one-GPU layer's -- the forward bitwise)."""
+        shard's, every value the one-GPU layer's -- the forward bitwise).
+        dropout: the feature dropout the model applies to the layer's output
+        (drop_robust_gcn.py:77,81,86); on a shard in training it is fused into
+        the layer, whose output rows then stream to the peers as they are
+        written."""
         lead = V.shape[:-1]
         if isinstance(graph, ShardedGraph):
             V2 = V.reshape(-1, V.shape[-1])
             training = torch.is_grad_enabled() and any(t is not None and t.requires_grad
                                                        for t in (V, self.h_weights, self.bias))
-            # training: the one-kernel forms both ways, the reverse halo exchange pipelined over row blocks
-            out = graph.graphconv(V2, self, relu=relu, pipeline="rows" if training else None)
+            if training:  # the one-kernel forms both ways, the reverse halo exchange pipelined over row blocks
+                fd = dropout.record(V.device) if dropout is not None else None
+                out = graph.graphconv(V2, self, relu=relu, pipeline="rows", fdrop=fd)
+            else:
+                out = graph.graphconv(V2, self, relu=relu)
+                out = dropout(out) if dropout is not None else out
             return out.view(*lead, self.C)
         # new_V = A_pre V (B*N, (L+1)F) then new_V h_weights + bias, one autograd node
         out = graph_conv(V, graph, self.h_weights, self.bias, relu=relu, recompute=self.recompute_aggregation)
-        return out.view(*lead, self.C)
+        out = out.view(*lead, self.C)
+        return dropout(out) if dropout is not None else out
 
     def forward(self, V: torch.Tensor, A: AdjLike, preprocess_A: bool = True) -> torch.Tensor:
         """V: (B, N, F).  A: TypedGraph, or dense (B, N, N, L) when
@@ -123,9 +147,11 @@ class NodeSelfAtten(nn.Module):
         """shard (additive): the grl.dist.ShardedGraph whose rows V holds --
         the softmax then runs over every node of the graph
         (grl.dist.sharded_node_attention)."""
+        pr = shard.global_rows if shard is not None else 0
+        f, g, h = (apply_linear(m, V, path_rows=pr) for m in (self.f, self.g, self.h))
         if shard is not None:
-            return sharded_node_attention(self.f(V), self.g(V), self.h(V), V, self.gamma, shard)
-        return node_self_attention(self.f(V), self.g(V), self.h(V), V, self.gamma)
+            return sharded_node_attention(f, g, h, V, self.gamma, shard)
+        return node_self_attention(f, g, h, V, self.gamma)
 
     def __repr__(self) -> str:
         return f"NodeSelfAttention(input_dim={self.F})"

@@ -76,10 +76,10 @@ class BaseProcedure:
         return torch.device("cuda:0" if n_gpu_use > 0 else "cpu"), list(range(n_gpu_use))
 
     def _independent_dropout_streams(self) -> None:
-        from gnn.models.networks.drop_robust_gcn import EdgeDropout
+        from gnn.models.networks.drop_robust_gcn import EdgeDropout, FeatureDropout
 
         for m in self.model.modules():
-            if isinstance(m, EdgeDropout):
+            if isinstance(m, (EdgeDropout, FeatureDropout)):
                 m.stream = self.rank
         if self.device.type == "cuda":
             torch.cuda.manual_seed(torch.initial_seed() + self.rank)

@@ -141,6 +141,7 @@ class KVProcedure(BaseProcedure):
             loss, scores, items = self._step_process(batch, **kwargs)
             loss.backward()
             self._sync_gradients()
+            device_check(self.device)  # a poisoned (NaN) backward must not reach the weights
             nn.utils.clip_grad_norm_(self.model.parameters(), self.config.max_grad_norm)
             self.optimizer.step()
         return scores, items

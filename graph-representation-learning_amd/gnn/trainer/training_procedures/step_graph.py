@@ -145,7 +145,7 @@ class StepGraph:
     def __init__(self, procedure, mode: str = "capture"):
         if mode not in ("capture", "static"):
             raise ValueError(f"capture_train_step must be true/'capture' or 'static', got {mode!r}")
-        from gnn.models.networks.drop_robust_gcn import EdgeDropout
+        from gnn.models.networks.drop_robust_gcn import EdgeDropout, FeatureDropout
 
         self.proc, self.mode = procedure, mode
         dev = procedure.device
@@ -155,7 +155,8 @@ class StepGraph:
         self.buckets: "OrderedDict[tuple, _Bucket]" = OrderedDict()
         self.seen: Dict[tuple, int] = {}
         self.seed_t = torch.zeros(1, dtype=torch.int64, device=dev)
-        self.edge_dropouts = [m for m in procedure.model.modules() if isinstance(m, EdgeDropout)]
+        # every hash-masked dropout (DropEdge and the feature dropout) reads the step's seed word
+        self.edge_dropouts = [m for m in procedure.model.modules() if isinstance(m, (EdgeDropout, FeatureDropout))]
         for m in self.edge_dropouts:
             m.seed_source = self.seed_t
         fixed = [m.seed for m in self.edge_dropouts if m.seed is not None]

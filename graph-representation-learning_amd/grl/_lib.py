@@ -66,6 +66,7 @@ class GrlTypedCsr(ctypes.Structure):
         ("self_id_base", _c_u64),
         ("split", ctypes.POINTER(GrlSplitPlan)),
         ("self_row0", _c_i64),
+        ("path_rows", _c_i64),
     ]
 
 
@@ -132,6 +133,7 @@ SIGNATURES = {
     "grl_dropedge_init": (_c_i32, [_P(GrlDropEdge), ctypes.c_float, _c_u64, _c_u64, _c_i32]),
     "grl_dropedge_init_device": (_c_i32, [_P(GrlDropEdge), ctypes.c_float, _c_vp, _c_u64, _c_i32]),
     "grl_dropedge_mask": (_c_i32, [_P(GrlDropEdge), _c_u64, _c_i64, _c_vp, _c_vp]),
+    "grl_feature_dropout": (_c_i32, [_c_vp, _c_i64, _c_vp, _c_i64, _c_i64, _c_i32, _c_i64, _P(GrlDropEdge), _c_vp]),
     "grl_typed_spmm_fwd": (_c_i32, [_P(GrlTypedCsr), _c_vp, _c_i64, _c_i32, _c_vp, _P(GrlDropEdge), _c_vp]),
     "grl_typed_spmm_fwd_slice": (_c_i32, [_P(GrlTypedCsr), _c_vp, _c_i64, _c_i32, _c_i64, _c_vp, _c_i64, _c_i32,
                                           _P(GrlDropEdge), _c_vp]),
@@ -151,6 +153,9 @@ SIGNATURES = {
     "grl_linear_fwd_workspace_size": (_c_size, [_c_i64, _c_i32, _c_i32]),
     "grl_linear_fwd": (_c_i32, [_c_vp, _c_i64, _c_vp, _c_vp, _c_vp, _c_i64, _c_i32, _c_i32, _c_i32, _c_vp, _c_size,
                                 _c_vp]),
+    "grl_linear_fwd_ex_workspace_size": (_c_size, [_c_i64, _c_i32, _c_i32, _c_i64]),
+    "grl_linear_fwd_ex": (_c_i32, [_c_vp, _c_i64, _c_vp, _c_i32, _c_vp, _c_vp, _c_i64, _c_i32, _c_i32, _c_i32, _c_i64,
+                                   _c_vp, _c_size, _c_vp]),
     "grl_linear_bwd_data_workspace_size": (_c_size, [_c_i64, _c_i32, _c_i32]),
     "grl_linear_bwd_data": (_c_i32, [_c_vp, _c_vp, _c_vp, _c_vp, _c_i64, _c_i64, _c_i32, _c_i32, _c_vp, _c_size,
                                      _c_vp]),

@@ -28,9 +28,21 @@ Two exchange layouts, chosen collectively per graph (HaloPlan.mode):
 Both layouts give the same Z bitwise (the kernel reads the same values in the
 same edge order) and the same dX values (peer-order sums; a peer's rows that
 no edge referenced contribute +0.0).
+
+Communication goes through one dispatch layer (the `_c_*` functions below),
+whose `group` is either a torch.distributed group -- RCCL ("nccl"), the
+product; gloo, whose device tensors are staged through the host -- or a
+LocalGroup member: P virtual ranks driven as threads of one process, with
+torch.distributed's asynchronous stream semantics emulated by device copies
+(LocalGroup).  Every function above the dispatch layer runs unchanged on
+all three, so the code RCCL runs on a multi-GPU node -- async handles, slot
+views, landing copies, peer-order combines -- also runs, with P > 1, on a
+one-GPU box (RCCL refuses two ranks on one device), and the RCCL calls
+themselves run on a one-rank "nccl" group (tests/rccl_loopback.py).
 """
 from __future__ import annotations
 
+import threading
 from dataclasses import dataclass
 from typing import List, Optional
 
@@ -42,18 +54,313 @@ from .graph import DropEdge, TypedGraph
 from .ops import graph_conv, graph_linear, typed_aggregate
 
 
+# ------------------------------------------------------------ virtual ranks
+class _LocalWork:
+    """A LocalGroup transfer's handle: wait() orders the caller's current
+    stream after the transfer on every rank it involves (a collective
+    completes on all ranks), as a torch.distributed work handle does."""
+
+    def __init__(self, events=(), ready=None):
+        self.events, self.ready = list(events), ready
+
+    def wait(self):
+        if self.ready is not None:  # a send: the receiver's copy must have been queued
+            self.events += self.ready()
+            self.ready = None
+        if self.events:
+            cur = torch.cuda.current_stream(self.events[0][1])
+            for ev, _ in self.events:
+                cur.wait_event(ev)
+        self.events = []
+        return True
+
+
+class LocalGroup:
+    """P virtual ranks in one process: the stand-in for a P-rank process
+    group when the ranks are threads (one GPU can hold one RCCL rank only).
+
+    Each member(r) is passed as `group` to the functions of this module.  A
+    collective on rank r records an event on r's current stream (its inputs
+    as queued); after every rank has issued it, rank r's receive side runs
+    on r's own transfer stream once every rank's event has fired, and the
+    handle's wait() makes the caller's stream wait for every rank's transfer
+    -- torch.distributed's async contract (the transfer starts after the work
+    queued before it; inputs must not change until wait()).  Reductions add
+    in rank order.  Ranks must issue the same collectives in the same order:
+    a mismatch raises instead of hanging.  Point-to-point transfers
+    (batch_isend_irecv) match sends and receives per (source, destination)
+    in posting order.  Host (CPU) tensors are copied at once."""
+
+    def __init__(self, world: int, timeout: float = 120.0):
+        self.world = int(world)
+        self.timeout = timeout
+        self.barrier = threading.Barrier(self.world, timeout=timeout)
+        self.slots = [[None] * self.world for _ in range(2)]  # double-buffered per collective sequence number
+        self.done = [[None] * self.world for _ in range(2)]
+        self.cond = threading.Condition()
+        self.mail = {}
+
+    def member(self, rank: int) -> "LocalRank":
+        return LocalRank(self, rank)
+
+    def abort(self) -> None:
+        self.barrier.abort()
+        with self.cond:
+            self.cond.notify_all()
+
+
+class LocalRank:
+    def __init__(self, grp: LocalGroup, rank: int):
+        self.g, self.rank, self.world = grp, int(rank), grp.world
+        self.seq = 0
+        self._stream = {}
+
+    def _side(self, device):
+        s = self._stream.get(device)
+        if s is None:
+            s = self._stream[device] = torch.cuda.Stream(device)
+        return s
+
+    @staticmethod
+    def _ready_event(t):
+        if not t.is_cuda:
+            return None
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(t.device))
+        return ev, t.device
+
+    def _run(self, kind: str, payload, recv, like, async_op: bool, phases: int = 1):
+        """One collective: post `payload`; when every rank has posted, run
+        recv(payloads, phase) for phase 0..phases-1 on this rank's transfer
+        stream (phase 0 after every rank's inputs are ready, phase p after
+        every rank's phase p-1: a later phase may overwrite what an earlier
+        one read).  Sequence numbers alternate between two slot sets: a rank
+        can post collective n+2 only after every rank has left collective n."""
+        g, r = self.g, self.rank
+        k = self.seq % 2
+        self.seq += 1
+        ev = self._ready_event(like)
+        g.slots[k][r] = (kind, payload, ev)
+        g.done[k][r] = {}
+        g.barrier.wait()
+        kinds = {g.slots[k][q][0] for q in range(self.world)}
+        if len(kinds) != 1:
+            g.abort()
+            raise RuntimeError(f"LocalGroup: ranks issued different collectives {sorted(kinds)}")
+        pays = [g.slots[k][q][1] for q in range(self.world)]
+        waits = [g.slots[k][q][2] for q in range(self.world) if g.slots[k][q][2] is not None]
+        for ph in range(phases):
+            if ev is not None:
+                side = self._side(ev[1])
+                for e, _ in waits:
+                    side.wait_event(e)
+                with torch.cuda.stream(side):
+                    recv(pays, ph)
+                d = torch.cuda.Event()
+                d.record(side)
+                g.done[k][r][ph] = (d, ev[1])
+            else:
+                recv(pays, ph)
+            g.barrier.wait()  # every rank's phase is queued (its event posted)
+            if ev is not None:
+                waits = [g.done[k][q][ph] for q in range(self.world)]
+        work = _LocalWork(waits if ev is not None else [])
+        if not async_op:
+            work.wait()
+            return None
+        return work
+
+    # -- the collectives of torch.distributed this module uses --
+    def all_gather(self, outs, inp, async_op=False):
+        r = self.rank
+
+        def recv(pays, ph):
+            for q in range(self.world):
+                outs[q].copy_(pays[q])
+                _keep_for_stream(outs[q], pays[q])
+        return self._run("all_gather", inp, recv, inp, async_op)
+
+    def all_gather_into_tensor(self, out, inp, async_op=False):
+        n = inp.shape[0]
+
+        def recv(pays, ph):
+            for q in range(self.world):
+                out[q * n:(q + 1) * n].copy_(pays[q])
+                _keep_for_stream(pays[q])
+            _keep_for_stream(out)
+        return self._run("all_gather_into", inp, recv, inp, async_op)
+
+    def all_to_all_single(self, out, inp, out_splits=None, in_splits=None, async_op=False):
+        W, r = self.world, self.rank
+        osp = list(out_splits) if out_splits is not None else [out.shape[0] // W] * W
+        isp = list(in_splits) if in_splits is not None else [inp.shape[0] // W] * W
+
+        def recv(pays, ph):
+            off = 0
+            for q in range(W):
+                t_q, isp_q = pays[q]
+                if isp_q[r] != osp[q]:
+                    raise RuntimeError(f"LocalGroup all_to_all: rank {q} sends {isp_q[r]} rows, rank {r} expects {osp[q]}")
+                o = sum(isp_q[:r])
+                if osp[q]:
+                    out[off:off + osp[q]].copy_(t_q[o:o + osp[q]])
+                _keep_for_stream(t_q)
+                off += osp[q]
+            _keep_for_stream(out)
+        return self._run("all_to_all", (inp, isp), recv, inp, async_op)
+
+    def all_reduce(self, t, op="sum", async_op=False):
+        tmp = torch.empty_like(t)
+        name = op if isinstance(op, str) else {dist.ReduceOp.SUM: "sum", dist.ReduceOp.MIN: "min",
+                                                dist.ReduceOp.MAX: "max"}[op]
+
+        def recv(pays, ph):
+            if ph == 0:  # reduce everyone's input in rank order into tmp (inputs untouched)
+                tmp.copy_(pays[0])
+                for q in range(1, self.world):
+                    if name == "sum":
+                        tmp.add_(pays[q])
+                    elif name == "min":
+                        torch.minimum(tmp, pays[q], out=tmp)
+                    else:
+                        torch.maximum(tmp, pays[q], out=tmp)
+                _keep_for_stream(tmp, *pays)
+            else:  # every rank has read every input: overwrite mine
+                t.copy_(tmp)
+                _keep_for_stream(t)
+        return self._run("all_reduce_" + name, t, recv, t, async_op, phases=2)
+
+    def broadcast(self, t, src=0, async_op=False):
+        r = self.rank
+
+        def recv(pays, ph):
+            if r != src:
+                t.copy_(pays[src])
+                _keep_for_stream(t, pays[src])
+        return self._run("broadcast", t, recv, t, async_op)
+
+    def barrier(self):
+        self.g.barrier.wait()
+
+    def batch_isend_irecv(self, sends, recvs):
+        """sends [(tensor, dst)], recvs [(tensor, src)] -> works."""
+        g, r = self.g, self.rank
+        works = []
+        for t, dst in sends:
+            box = {"ev": self._ready_event(t), "t": t, "done": None}
+            with g.cond:
+                g.mail.setdefault((r, dst), []).append(box)
+                g.cond.notify_all()
+
+            def ready(box=box):
+                with g.cond:
+                    if not g.cond.wait_for(lambda: box["done"] is not None, timeout=g.timeout):
+                        raise RuntimeError(f"LocalGroup: rank {r}'s send was never received")
+                return [box["done"]] if box["done"][0] is not None else []
+            works.append(_LocalWork([], ready))
+        for t, src in recvs:
+            with g.cond:
+                if not g.cond.wait_for(lambda: g.mail.get((src, r)), timeout=g.timeout):
+                    raise RuntimeError(f"LocalGroup: rank {r} waited for a send from rank {src} that never came")
+                box = g.mail[(src, r)].pop(0)
+            if box["t"].shape != t.shape:
+                raise RuntimeError(f"LocalGroup p2p: rank {src} sent {tuple(box['t'].shape)}, rank {r} receives "
+                                   f"{tuple(t.shape)}")
+            if t.is_cuda:
+                side = self._side(t.device)
+                side.wait_event(box["ev"][0])
+                with torch.cuda.stream(side):
+                    t.copy_(box["t"])
+                    _keep_for_stream(t, box["t"])
+                d = torch.cuda.Event()
+                d.record(side)
+                done = (d, t.device)
+                works.append(_LocalWork([done]))
+            else:
+                t.copy_(box["t"])
+                done = (None, None)
+            with g.cond:
+                box["done"] = done
+                g.cond.notify_all()
+        return works
+
+
+def _keep_for_stream(*ts) -> None:
+    """The caching allocator must not hand these tensors' memory out again
+    before the current (transfer) stream's work on them has run -- what
+    ProcessGroupNCCL's recordStream does for RCCL transfers."""
+    for t in ts:
+        if t is not None and t.is_cuda:
+            t.record_stream(torch.cuda.current_stream(t.device))
+
+
+def _local(group) -> bool:
+    return isinstance(group, LocalRank)
+
+
+def _comm_on(group) -> bool:
+    """A group to communicate over: a LocalGroup member or an initialised
+    torch.distributed process group (a one-rank group included)."""
+    return _local(group) or (dist.is_available() and dist.is_initialized())
+
+
 def _world(group) -> int:
+    if _local(group):
+        return group.world
     return dist.get_world_size(group) if dist.is_available() and dist.is_initialized() else 1
 
 
 def _rank(group) -> int:
+    if _local(group):
+        return group.rank
     return dist.get_rank(group) if dist.is_available() and dist.is_initialized() else 0
 
 
 def _host_staged(group) -> bool:
     """gloo moves device tensors only through host copies (used to smoke-test
     the N>1 path with several ranks on one GPU; production uses RCCL)."""
-    return dist.is_available() and dist.is_initialized() and dist.get_backend(group) == "gloo"
+    return not _local(group) and dist.is_available() and dist.is_initialized() and dist.get_backend(group) == "gloo"
+
+
+# ---- the dispatch layer: each function is the one place its collective is
+# issued (RCCL / gloo through torch.distributed, or the LocalGroup) ----
+def _c_all_gather(outs, inp, group, async_op=False):
+    if _local(group):
+        return group.all_gather(outs, inp, async_op)
+    return dist.all_gather(outs, inp, group=group, async_op=async_op)
+
+
+def _c_all_gather_into_tensor(out, inp, group, async_op=False):
+    if _local(group):
+        return group.all_gather_into_tensor(out, inp, async_op)
+    return dist.all_gather_into_tensor(out, inp, group=group, async_op=async_op)
+
+
+def _c_all_to_all_single(out, inp, out_splits, in_splits, group, async_op=False):
+    if _local(group):
+        return group.all_to_all_single(out, inp, out_splits, in_splits, async_op)
+    return dist.all_to_all_single(out, inp, out_splits, in_splits, group=group, async_op=async_op)
+
+
+def _c_all_reduce(t, op, group, async_op=False):
+    if _local(group):
+        return group.all_reduce(t, op, async_op)
+    return dist.all_reduce(t, op=op, group=group, async_op=async_op)
+
+
+def _c_broadcast(t, src_in_group, group):
+    if _local(group):
+        return group.broadcast(t, src_in_group)
+    src = dist.get_global_rank(group, src_in_group) if group is not None else src_in_group
+    return dist.broadcast(t, src, group=group)
+
+
+def _c_p2p(sends, recvs, group):
+    if _local(group):
+        return group.batch_isend_irecv(sends, recvs)
+    ops = [dist.P2POp(dist.isend, t, group=group, group_peer=dst) for t, dst in sends]
+    ops += [dist.P2POp(dist.irecv, t, group=group, group_peer=src) for t, src in recvs]
+    return dist.batch_isend_irecv(ops)
 
 
 def all_to_all_v(out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits, group=None) -> None:
@@ -62,7 +369,7 @@ def all_to_all_v(out: torch.Tensor, inp: torch.Tensor, out_splits, in_splits, gr
         dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits, group=group)
         out.copy_(o)
     else:
-        dist.all_to_all_single(out, inp, out_splits, in_splits, group=group)
+        _c_all_to_all_single(out, inp, out_splits, in_splits, group)
 
 
 def all_gather_into(out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
@@ -71,13 +378,13 @@ def all_gather_into(out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
         parts = all_gather_list(inp, group)
         out.copy_(torch.cat(parts, 0))
     else:
-        dist.all_gather_into_tensor(out, inp, group=group)
+        _c_all_gather_into_tensor(out, inp, group)
 
 
 def all_gather_list(t: torch.Tensor, group=None) -> List[torch.Tensor]:
     src = t.cpu() if _host_staged(group) else t
     outs = [torch.empty_like(src) for _ in range(_world(group))]
-    dist.all_gather(outs, src, group=group)
+    _c_all_gather(outs, src, group)
     return outs
 
 
@@ -295,7 +602,7 @@ def halo_exchange_into(X_loc: torch.Tensor, X_ext: torch.Tensor, send_buf: torch
     X_ext[:n_loc] must already alias or hold X_loc; fills X_ext[n_loc:]
     (dense plans: the pad rows X_ext[n_loc:stride] travel as they are and are
     never read by the kernel; send_buf is unused and may be empty)."""
-    if _world(group) == 1:
+    if _world(group) == 1 and plan.n_halo == 0:
         return
     if plan.mode == "dense":
         all_gather_into(X_ext[plan.stride:], X_ext[: plan.stride], group)
@@ -381,12 +688,12 @@ class HaloPipeline:
             if self.side is None:
                 all_gather_into(t[p.stride:], t[:p.stride], self.group)
                 return None
-            return dist.all_gather_into_tensor(t[p.stride:], t[:p.stride], group=self.group, async_op=True)
+            return _c_all_gather_into_tensor(t[p.stride:], t[:p.stride], self.group, async_op=True)
         if self.side is None:
             all_to_all_v(t[p.n_loc:], self.send[c], p.recv_counts, p.send_counts, self.group)
             return None
-        return dist.all_to_all_single(t[p.n_loc:], self.send[c], p.recv_counts, p.send_counts, group=self.group,
-                                      async_op=True)
+        return _c_all_to_all_single(t[p.n_loc:], self.send[c], p.recv_counts, p.send_counts, self.group,
+                                    async_op=True)
 
     def run(self, X_loc: torch.Tensor, Z: torch.Tensor, dropedge: Optional[DropEdge] = None,
             aggregate_slice=None) -> torch.Tensor:
@@ -444,12 +751,12 @@ class HaloPipeline:
                 if not async_op:
                     all_to_all_v(back, g[p.stride:], splits, splits, self.group)
                     return None
-                return dist.all_to_all_single(back, g[p.stride:], splits, splits, group=self.group, async_op=True)
+                return _c_all_to_all_single(back, g[p.stride:], splits, splits, self.group, async_op=True)
             if not async_op:
                 all_to_all_v(back, g[p.n_loc:], p.send_counts, p.recv_counts, self.group)
                 return None
-            return dist.all_to_all_single(back, g[p.n_loc:], p.send_counts, p.recv_counts, group=self.group,
-                                          async_op=True)
+            return _c_all_to_all_single(back, g[p.n_loc:], p.send_counts, p.recv_counts, self.group,
+                                        async_op=True)
 
     def _combine(self, c: int, dX_loc: torch.Tensor) -> None:
         """dX_loc's columns of slice c = my own rows' gradient + every peer's
@@ -535,15 +842,15 @@ def _p2p_exchange(sends, recvs, group):
     if not sends and not recvs:
         return [], lambda: None
     staged = _host_staged(group)
-    ops, back = [], []
+    snd, rcv, back = [], [], []
     for t, dst in sends:
-        ops.append(dist.P2POp(dist.isend, t.cpu() if staged and t.is_cuda else t, group=group, group_peer=dst))
+        snd.append((t.cpu() if staged and t.is_cuda else t, dst))
     for t, src in recvs:
         buf = torch.empty(t.shape, dtype=t.dtype) if staged and t.is_cuda else t
         if buf is not t:
             back.append((t, buf))
-        ops.append(dist.P2POp(dist.irecv, buf, group=group, group_peer=src))
-    works = dist.batch_isend_irecv(ops)
+        rcv.append((buf, src))
+    works = _c_p2p(snd, rcv, group)
 
     def finish():
         for t, buf in back:
@@ -556,12 +863,12 @@ def _all_agree(flag: bool, group, device) -> bool:
     """True iff `flag` holds on every rank of `group` (a MIN all-reduce): a
     decision that picks between two different collective sequences must be
     the same on every rank, or the ranks post mismatched collectives and
-    hang."""
-    if _world(group) == 1:
+    hang.  Runs on any communicating group, a one-rank one included."""
+    if not _comm_on(group):
         return flag
     t = torch.tensor([1 if flag else 0], dtype=torch.int32,
                      device="cpu" if _host_staged(group) or device is None else device)
-    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    _c_all_reduce(t, dist.ReduceOp.MIN, group)
     return bool(int(t.item()))
 
 
@@ -629,27 +936,37 @@ class _RowPipelinedGraphConv(torch.autograd.Function):
     exchange but runs the two-kernel layer."""
 
     @staticmethod
-    def forward(ctx, X_loc: torch.Tensor, sg: "ShardedGraph", W: torch.Tensor, b, relu: bool, dropedge):
-        from .ops import graph_conv_fwd_train
+    def forward(ctx, X_loc: torch.Tensor, sg: "ShardedGraph", W: torch.Tensor, b, relu: bool, dropedge,
+                fdrop=None, stream: bool = False):
+        from .ops import feature_dropout_apply, graph_conv_fwd_train
 
         with trace("grl.rows_pipeline_fwd"):
             X_ext = sg.exchange_table(X_loc)
             graph = sg.graph.with_dropedge(dropedge)
-            out, Z = graph_conv_fwd_train(X_ext, graph, W.contiguous(), b.contiguous() if b is not None else None,
-                                          relu)
+            Wc, bc = W.contiguous(), b.contiguous() if b is not None else None
+            row0 = sg.plan.row_begin
+            if stream:  # the output streamed to the peers by row blocks as it is written (training forward)
+                out, D, Z = sg._graphconv_train_streamed(X_ext, graph, Wc, bc, relu, fdrop)
+            else:
+                out, Z = graph_conv_fwd_train(X_ext, graph, Wc, bc, relu)
+                D = out if fdrop is None else feature_dropout_apply(out, fdrop, row0)
         ctx.sg, ctx.graph, ctx.relu, ctx.has_b, ctx.F = sg, graph, relu, b is not None, X_loc.shape[1]
-        ctx.save_for_backward(Z, W.contiguous(), out if relu else None)
-        return out
+        ctx.fdrop, ctx.row0 = fdrop, row0
+        ctx.save_for_backward(Z, Wc, out if relu else None)
+        return D
 
     @staticmethod
     def backward(ctx, g: torch.Tensor):
-        from .ops import graph_conv_bwd_data, linear_bwd_weight, relu_grad
+        from .ops import feature_dropout_apply, graph_conv_bwd_data, linear_bwd_weight, relu_grad
 
         Z, W, out = ctx.saved_tensors
         sg, graph, F = ctx.sg, ctx.graph, ctx.F
+        g = g.contiguous().float()
+        if ctx.fdrop is not None:  # the fused feature dropout's backward: the same mask on the gradient
+            g = feature_dropout_apply(g, ctx.fdrop, ctx.row0)
         # the ReLU handling of ops._GraphConv.backward (same kernels, same bits)
         want_w, want_b = ctx.needs_input_grad[2], ctx.has_b and ctx.needs_input_grad[3]
-        g, mask, db_pre = relu_grad(g.contiguous().float(), out if ctx.relu else None, want_b)
+        g, mask, db_pre = relu_grad(g, out if ctx.relu else None, want_b)
         dW = db = None
         if want_w or (want_b and db_pre is None):
             dW, db = linear_bwd_weight(Z, g, mask, want_b and db_pre is None)
@@ -667,7 +984,7 @@ class _RowPipelinedGraphConv(torch.autograd.Function):
 
                     dX_ext = spmm_backward(linear_bwd_data(g_data, None, W), graph, F)
                 dX_loc = _HaloExchange.backward(types_ns(plan=sg.plan, group=sg.group), dX_ext)[0]
-        return dX_loc, None, dW if want_w else None, db, None, None
+        return dX_loc, None, dW if want_w else None, db, None, None, None, None
 
 
 def types_ns(**kw):
@@ -680,13 +997,14 @@ def broadcast_module(module: torch.nn.Module, src: int = 0, group=None) -> None:
     """Copy `src`'s parameters and buffers to every rank (replica start)."""
     if _world(group) == 1:
         return
+    src_in_group = src if _local(group) or group is None else dist.get_group_rank(group, src)
     for t in list(module.parameters()) + list(module.buffers()):
         if _host_staged(group) and t.is_cuda:
             h = t.detach().cpu()
-            dist.broadcast(h, src, group=group)
+            _c_broadcast(h, src_in_group, group)
             t.data.copy_(h)
         else:
-            dist.broadcast(t.data, src, group=group)
+            _c_broadcast(t.data, src_in_group, group)
 
 
 def allreduce_gradients(params, group=None, bucket_bytes: int = 64 << 20, average: bool = False) -> None:
@@ -700,7 +1018,7 @@ def allreduce_gradients(params, group=None, bucket_bytes: int = 64 << 20, averag
     average=True divides by the world size (data parallelism's mean).
     Without a process group nothing runs; a one-rank group runs the real
     collectives (a sum over one rank: the gradients unchanged)."""
-    if not (dist.is_available() and dist.is_initialized()):
+    if not _comm_on(group):
         return
     grads = [p.grad for p in params if p.grad is not None]
     bucket: List[torch.Tensor] = []
@@ -715,10 +1033,10 @@ def allreduce_gradients(params, group=None, bucket_bytes: int = 64 << 20, averag
             flat.div_(_world(group))
         if _host_staged(group) and flat.is_cuda:
             h = flat.cpu()
-            dist.all_reduce(h, group=group)
+            _c_all_reduce(h, dist.ReduceOp.SUM, group)
             flat.copy_(h)
         else:
-            dist.all_reduce(flat, group=group)
+            _c_all_reduce(flat, dist.ReduceOp.SUM, group)
         off = 0
         for g in bucket:
             g.copy_(flat[off:off + g.numel()].view_as(g))
@@ -765,14 +1083,26 @@ class ShardedGraph:
         self.graph = TypedGraph(rowptr, p.colidx_local, num_types, vals=vals, has_self=True,
                                 num_cols=p.n_loc + p.n_halo, edge_id_base=p.edge_id_base,
                                 self_id_base=p.num_edges_total + p.row_begin, self_rows=p.n_loc)
+        # the GEMM path of every layer is chosen for the whole graph's rows: a shard's rows are bitwise the
+        # one-GPU layer's (GrlTypedCsr.path_rows)
+        self.graph.path_rows = self.global_rows
+
+    @property
+    def global_rows(self) -> int:
+        """Rows of the whole graph this shard belongs to."""
+        return self.plan.bounds[-1] - self.plan.bounds[0]
 
     @classmethod
-    def in_process(cls, graph: TypedGraph, bounds: List[int], halo: str = "auto") -> List["ShardedGraph"]:
-        """All P node-range shards of `graph` in this process (no process
-        group): shard r is what ShardedGraph.from_graph builds on rank r of a
-        P-rank group with these bounds.  For driving several shards from one
-        process (their exchanges then go through a HaloPipeline `exchange`
-        object instead of collectives)."""
+    def in_process(cls, graph: TypedGraph, bounds: List[int], halo: str = "auto",
+                   group: Optional[LocalGroup] = None) -> List["ShardedGraph"]:
+        """All P node-range shards of `graph` in this process: shard r is what
+        ShardedGraph.from_graph builds on rank r of a P-rank group with these
+        bounds.  For driving several shards from one process: group, a
+        LocalGroup of P virtual ranks (shard r communicates as its member r,
+        each driven by its own thread), or None (the exchanges then go
+        through a HaloPipeline `exchange` object)."""
+        if group is not None and group.world != len(bounds) - 1:
+            raise ValueError(f"a LocalGroup of {group.world} ranks for {len(bounds) - 1} node ranges")
         L = graph.num_types
         parts = []
         for r in range(len(bounds) - 1):
@@ -783,7 +1113,7 @@ class ShardedGraph:
         out = []
         for (rowptr, _, vals), plan in zip(parts, plans):
             sg = cls.__new__(cls)
-            sg._init(rowptr, plan, L, vals, None)
+            sg._init(rowptr, plan, L, vals, None if group is None else group.member(len(out)))
             sg.graph.split_threshold, sg.graph.split_chunk = graph.split_threshold, graph.split_chunk
             out.append(sg)
         return out
@@ -853,7 +1183,7 @@ class ShardedGraph:
         largest one (no autograd)."""
         p = self.plan
         world = len(p.bounds) - 1
-        if world == 1 or not (dist.is_available() and dist.is_initialized()):
+        if not _comm_on(self.group):  # (a one-rank group still runs the collective)
             return X_loc
         stride = max(p.bounds[q + 1] - p.bounds[q] for q in range(world))
         X_loc = X_loc.reshape(-1, X_loc.shape[-1])
@@ -871,7 +1201,7 @@ class ShardedGraph:
         collective's algorithm."""
         p = self.plan
         world = len(p.bounds) - 1
-        if world == 1 or not (dist.is_available() and dist.is_initialized()):
+        if not _comm_on(self.group):  # (a one-rank group still runs the collective)
             return P.contiguous()
         sizes = [p.bounds[q + 1] - p.bounds[q] for q in range(world)]
         recv = P.new_empty(world * p.n_loc, P.shape[1])
@@ -885,15 +1215,14 @@ class ShardedGraph:
         """Rank 0's value of a 1-element device tensor on every rank of the
         shard's group (a device-drawn DropEdge seed: the masks of a sharded
         graph must be the one-GPU graph's on every rank)."""
-        if _world(self.group) == 1:
+        if not _comm_on(self.group):
             return seed_t
-        src = dist.get_global_rank(self.group, 0) if self.group is not None else 0
         if _host_staged(self.group):
             h = seed_t.cpu()
-            dist.broadcast(h, src, group=self.group)
+            _c_broadcast(h, 0, self.group)
             seed_t.copy_(h)
         else:
-            dist.broadcast(seed_t, src, group=self.group)
+            _c_broadcast(seed_t, 0, self.group)
         return seed_t
 
     def exchange(self, X_loc: torch.Tensor) -> torch.Tensor:
@@ -957,8 +1286,9 @@ class ShardedGraph:
 
     def _can_stream(self, X_loc: torch.Tensor) -> bool:
         p = self.plan
-        return bool(self.stream_rows and self.halo_memo is not None and len(p.bounds) > 2
-                    and dist.is_available() and dist.is_initialized() and X_loc.is_cuda)
+        # peers, or a one-rank loopback plan whose sources all come through the exchange (tests/rccl_loopback.py)
+        return bool(self.stream_rows and self.halo_memo is not None and (len(p.bounds) > 2 or p.n_halo > 0)
+                    and _comm_on(self.group) and X_loc.is_cuda)
 
     def _stream_extent(self) -> int:
         """Rows of the uniform block grid: the largest shard (every rank
@@ -1017,11 +1347,11 @@ class ShardedGraph:
             if _host_staged(self.group):
                 h = T[a0:a1].cpu()
                 outs = [torch.empty_like(h) for _ in range(world)]
-                dist.all_gather(outs, h, group=self.group)
+                _c_all_gather(outs, h, self.group)
                 for v, o in zip(slots, outs):
                     v.copy_(o)
                 return None
-            return dist.all_gather(slots, T[a0:a1], group=self.group, async_op=True)
+            return _c_all_gather(slots, T[a0:a1], self.group, async_op=True)
         send_idx, sc, rc, dest = self._sparse_block_lists(a0, a1)
         send = T.index_select(0, send_idx)
         recv = T.new_empty(sum(rc), T.shape[1])
@@ -1029,7 +1359,7 @@ class ShardedGraph:
             all_to_all_v(recv, send, rc, sc, self.group)
             T.index_copy_(0, dest, recv)
             return None
-        work = dist.all_to_all_single(recv, send, rc, sc, group=self.group, async_op=True)
+        work = _c_all_to_all_single(recv, send, rc, sc, self.group, async_op=True)
         return _Landing(work, lambda: T.index_copy_(0, dest, recv), (send, recv))
 
     def _stream_fill(self, T: torch.Tensor, C: int, K: int, compute) -> list:
@@ -1039,8 +1369,9 @@ class ShardedGraph:
         from .ops import x6_rows_ok
 
         works = []
+        pr = self.global_rows
         for r0, r1, posts in stream_chunks(self._stream_extent(), self.plan.n_loc, int(self.stream_blocks),
-                                           lambda m: x6_rows_ok(m, C, K)):
+                                           lambda m: x6_rows_ok(m, C, K, pr)):
             if r1 > r0:
                 compute(r0, r1)
             works += [self._post_block(T, a0, a1) for a0, a1 in posts]
@@ -1076,6 +1407,42 @@ class ShardedGraph:
         self.halo_memo["pending"][k[:1] + k[2:]] = (T, works, out)
         return out
 
+    def _graphconv_train_streamed(self, X_ext: torch.Tensor, graph: TypedGraph, W: torch.Tensor, b, relu: bool,
+                                  fdrop):
+        """Training forward of a GraphConv whose output (through the feature
+        dropout that follows it in the model, fused: drop_robust_gcn.py:77,
+        81) goes to the peers while the rest of the layer computes.  Row
+        blocks [r0, r1) of the shard run the one-kernel training forward over
+        row-range views (out and Z rows, the whole shard's arithmetic: the
+        GEMM path is pinned by path_rows); each block's dropout mask is the
+        hash of its global element ids (feature_dropout), so the block is
+        final as soon as it is written: D[r0:r1] = dropout(out[r0:r1]) is
+        copied into the NEXT layer's halo table T and posted (_post_block),
+        exactly as streamed inference does.  Returns (out, D, Z): the ReLU
+        output (the backward's mask), the layer's output D (its own storage,
+        not a view of T, whose halo rows the collectives write in place: a
+        view would tie the autograd output to those writes) and Z."""
+        from .ops import feature_dropout_apply, graph_conv_fwd_train
+
+        p = self.plan
+        C = W.shape[1]
+        K = graph.segments * X_ext.shape[1]
+        out = X_ext.new_empty(p.n_loc, C)
+        Z = X_ext.new_empty(p.n_loc, K)
+        D = X_ext.new_empty(p.n_loc, C) if fdrop is not None else out
+        T = self._stream_table(C, X_ext)
+
+        def compute(r0, r1):
+            graph_conv_fwd_train(X_ext, graph.rows_view(r0, r1), W, b, relu, out=out[r0:r1], Z=Z[r0:r1])
+            if fdrop is not None:
+                feature_dropout_apply(out[r0:r1], fdrop, p.row_begin + r0, out=D[r0:r1])
+            T[r0:r1].copy_(D[r0:r1])
+
+        works = self._stream_fill(T, C, K, compute)
+        k = self._tkey(D)
+        self.halo_memo["pending"][k[:1] + k[2:]] = (T, works, D)
+        return out, D, Z
+
     def exchange_table(self, X_loc: torch.Tensor) -> torch.Tensor:
         """X_ext = [own | halo] rows of X_loc without autograd (the layers'
         backward sends the halo gradients home themselves), through the memo
@@ -1099,8 +1466,11 @@ class ShardedGraph:
             for w in works:
                 if w is not None:
                     w.wait()
+            # landing the received rows (T.index_copy_) bumped the version X shares with T: re-key
+            k1 = self._tkey(X_loc)
             if k in memo["keep"]:
-                memo["tables"][k] = T
+                memo["keep"][k1] = memo["keep"].pop(k)
+                memo["tables"][k1] = T
             return T
         cat = memo["concat"].get(k)
         if cat is not None:
@@ -1167,8 +1537,17 @@ class ShardedGraph:
         blocks = self.halo_blocks()
         order = [(r0, r1) for _, r0, r1 in blocks] + [(0, p.n_loc)]
         views = graph_conv_bwd_data_rows_views(g, graph, W, F, order)
-        if not _all_agree(views is not None, self.group, dev):
+        # the ranks agree once per layer shape (the choice depends on static shapes and the plan only), not
+        # in every backward: the all-reduce's host read would drain the launch queue
+        agreed = self.graph._shared.setdefault("rows_backward_agreed", {})
+        key = (F, tuple(g.shape), None if W is None else tuple(W.shape))
+        if key not in agreed:
+            agreed[key] = _all_agree(views is not None, self.group, dev)
+        if not agreed[key]:
             return None
+        if views is None:
+            raise RuntimeError("rows_backward: the ranks agreed on the one-kernel path, but this rank's blocks "
+                               "no longer qualify for it")
         dX_ext = torch.empty(graph.num_cols, F, dtype=torch.float32, device=dev)
         # receive buffers: the partials for my rows from the peer whose j-th block they are (src_j = rank - j;
         # dense: all my rows; sparse: the ones that peer referenced)
@@ -1206,7 +1585,8 @@ class ShardedGraph:
         return dX_loc
 
     def graphconv(self, X_loc: torch.Tensor, layer, dropedge: Optional[DropEdge] = None,
-                  relu: bool = False, chunks: Optional[int] = None, pipeline: Optional[str] = None) -> torch.Tensor:
+                  relu: bool = False, chunks: Optional[int] = None, pipeline: Optional[str] = None,
+                  fdrop: Optional[DropEdge] = None) -> torch.Tensor:
         """One GraphConv (gnn.models.GraphConv or anything with h_weights /
         bias) over this shard: halo exchange -> typed SpMM -> MFMA linear
         (+ fused ReLU).  Output rows = this rank's nodes.  After backward,
@@ -1217,11 +1597,18 @@ class ShardedGraph:
         over the shard's typed transpose, whose halo rows then travel home
         in the exchange's backward.  pipeline="rows": the one-kernel forms in
         both directions with the reverse exchange pipelined over row blocks
-        (_RowPipelinedGraphConv); out and dX bitwise the unpipelined layer's."""
+        (_RowPipelinedGraphConv); out and dX bitwise the unpipelined layer's.
+        fdrop (pipeline="rows"): the feature dropout that follows the layer
+        (drop_robust_gcn.py:77,81,86), fused into it; with a halo memo and
+        peers the output is then streamed to them by row blocks as it is
+        written (_graphconv_train_streamed), bitwise the unstreamed layer."""
         if dropedge is None:
             dropedge = self.dropedge
         if pipeline == "rows":
-            return _RowPipelinedGraphConv.apply(X_loc, self, layer.h_weights, layer.bias, relu, dropedge)
+            return _RowPipelinedGraphConv.apply(X_loc, self, layer.h_weights, layer.bias, relu, dropedge, fdrop,
+                                                self._can_stream(X_loc))
+        if fdrop is not None:
+            raise ValueError("fdrop (a fused feature dropout) needs pipeline='rows'")
         if pipeline is not None:
             raise ValueError(f"pipeline must be None or 'rows', got {pipeline!r}")
         if chunks is None:

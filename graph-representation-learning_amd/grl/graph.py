@@ -43,7 +43,8 @@ def device_check(device=None) -> None:
     dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
     if dev.type != "cuda":
         return  # no device work ran there
-    call("grl_check", current_stream_handle(dev))
+    with torch.cuda.device(dev):  # the sticky word is per device: the library reads the current device's
+        call("grl_check", current_stream_handle(dev))
 
 
 def _require_device(t: torch.Tensor, what: str) -> None:
@@ -131,6 +132,10 @@ class TypedGraph:
         return g
 
     self_row0 = 0  # X row of row 0's identity term (row-range views, rows_view)
+    # rows the GEMM path is chosen for (GrlTypedCsr.path_rows; 0 = num_rows): a
+    # node-range shard carries the whole graph's row count, a row-range view its
+    # parent's, so their rows take the one-GPU layer's path (bitwise its rows)
+    path_rows = 0
 
     def rows_view(self, r0: int, r1: int) -> "TypedGraph":
         """Rows [r0, r1) as a forward graph of their own: rowptr a slice
@@ -149,6 +154,7 @@ class TypedGraph:
                            num_cols=self.num_cols, edge_id_base=self.edge_id_base,
                            self_id_base=self.self_id_base + r0, self_rows=max(0, min(self.self_rows, r1) - r0))
             v.self_row0 = self.self_row0 + r0
+            v.path_rows = self.path_rows or self.num_rows
             v.split_threshold, v.split_chunk = self.split_threshold, self.split_chunk
             cache[(r0, r1)] = v
         return v.with_dropedge(self.dropedge)
@@ -228,6 +234,7 @@ class TypedGraph:
         g.edge_id_base = self.edge_id_base
         g.self_id_base = self.self_id_base
         g.self_row0 = self.self_row0
+        g.path_rows = self.path_rows
         plan = self._split("csr", F) if F is not None else None
         g.split = ctypes.pointer(plan) if plan is not None else None
         return g

@@ -279,14 +279,16 @@ FUSED_WIDTHS = (64, 128, 256, 512, 1024)
 FUSED_MAX_OUT = 512
 
 
-def x6_rows_ok(M: int, N: int, K: int) -> bool:
-    """Whether an [M, K] x [K, N] product takes the split-bf16 GEMM (and so a
-    GraphConv the one-kernel forms): the size rule of x6_shape_ok
-    (csrc/linear.hip).  Its per-element arithmetic is independent of M, the
-    fp32-MFMA path's is not (split-K by rows), so row blocks of one layer
-    match the whole call bitwise exactly when both sides pass this."""
-    return (os.environ.get("GRL_GEMM_X6", "1")[:1] != "0" and K > 0 and K % 16 == 0 and M >= 4 and N >= 4
-            and 2.0 * M * N * K >= 1.6e10)
+def x6_rows_ok(M: int, N: int, K: int, path_rows: int = 0) -> bool:
+    """Whether an [M, K] x [K, N] product, chosen for max(M, path_rows) rows,
+    takes the split-bf16 GEMM (and so a GraphConv the one-kernel forms): the
+    size rule of x6_path_ok (csrc/linear.hip).  Both GEMM paths' per-element
+    arithmetic is independent of M (the fp32 one sums K in fixed chunks), so
+    row blocks of one layer match the whole call bitwise when both take the
+    same path -- which path_rows (the whole call's rows) guarantees."""
+    rows = max(M, path_rows)
+    return (os.environ.get("GRL_GEMM_X6", "1")[:1] != "0" and K > 0 and K % 16 == 0 and M >= 1 and rows >= 4
+            and N >= 4 and 2.0 * rows * N * K >= 1.6e10)
 
 
 def _bwd_data_enabled() -> bool:
@@ -498,10 +500,13 @@ class _GraphConv(torch.autograd.Function):
         return dX, None, dW if want_w else None, db, None, None
 
 
-def graph_conv_fwd_train(X: torch.Tensor, graph: TypedGraph, W: torch.Tensor, b=None, relu: bool = False):
+def graph_conv_fwd_train(X: torch.Tensor, graph: TypedGraph, W: torch.Tensor, b=None, relu: bool = False,
+                         out: torch.Tensor = None, Z: torch.Tensor = None):
     """(out, Z) of one GraphConv layer through grl_graphconv_fwd_train: the
     one-kernel path writes Z as a by-product (for the backward's dW); the
-    result is bitwise spmm_forward then linear_fwd."""
+    result is bitwise spmm_forward then linear_fwd.  out / Z: contiguous
+    [num_rows, C] / [num_rows, segments * F] fp32 tensors to write (e.g. the
+    row block of a streamed layer)."""
     _require_device(X, "node features")
     if X.dtype != torch.float32 or W.dtype != torch.float32:
         raise _lib.GrlError("graph_conv_fwd_train: features and weights must be float32")
@@ -515,10 +520,15 @@ def graph_conv_fwd_train(X: torch.Tensor, graph: TypedGraph, W: torch.Tensor, b=
     if Wc.shape[0] != K:
         raise _lib.GrlError(f"weights have {Wc.shape[0]} rows, expected {graph.segments} x {F}")
     bc = b.contiguous() if b is not None else None
-    out = torch.empty(graph.num_rows, C, dtype=torch.float32, device=X.device)
-    Z = torch.empty(graph.num_rows, K, dtype=torch.float32, device=X.device)
+    for t, shape, what in ((out, (graph.num_rows, C), "out"), (Z, (graph.num_rows, K), "Z")):
+        if t is not None and (tuple(t.shape) != shape or t.dtype != torch.float32 or not t.is_contiguous()):
+            raise _lib.GrlError(f"graph_conv_fwd_train: {what} must be a contiguous float32 {shape} tensor")
+    if out is None:
+        out = torch.empty(graph.num_rows, C, dtype=torch.float32, device=X.device)
+    if Z is None:
+        Z = torch.empty(graph.num_rows, K, dtype=torch.float32, device=X.device)
     csr = graph.csr_c(F)
-    ws_bytes = _lib.lib().grl_linear_fwd_workspace_size(graph.num_rows, K, C)
+    ws_bytes = _lib.lib().grl_linear_fwd_ex_workspace_size(graph.num_rows, K, C, graph.path_rows)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=X.device) if ws_bytes else None
     de = graph.dropedge.to_c() if graph.dropedge is not None else None
     call("grl_graphconv_fwd_train", ctypes.byref(csr), X2.data_ptr(), X2.stride(0), F, Wc.data_ptr(),
@@ -605,6 +615,106 @@ def graph_linear(Z: torch.Tensor, W: torch.Tensor, b=None, relu: bool = False) -
     """out = Z W + b (optionally ReLU) on MFMA; Z rows x (L+1)F."""
     _require_device(Z, "aggregated features")
     return _GraphLinear.apply(Z, W, b, relu)
+
+
+# -------------------------------------------------------- feature dropout
+def feature_dropout_apply(x2: torch.Tensor, de, row0: int, out: torch.Tensor = None) -> torch.Tensor:
+    """out = x2 * keep * 1/(1-p) for the element ids (row0 + r) * cols + c
+    (grl_feature_dropout); x2 a 2-D fp32 row view."""
+    _require_device(x2, "dropout input")
+    if x2.dtype != torch.float32 or x2.dim() != 2 or x2.stride(1) != 1:
+        raise _lib.GrlError("feature_dropout: a 2-D float32 tensor with unit column stride")
+    if out is None:
+        out = torch.empty(x2.shape, dtype=torch.float32, device=x2.device)
+    dc = de.to_c()
+    call("grl_feature_dropout", x2.data_ptr(), x2.stride(0), out.data_ptr(), out.stride(0), x2.shape[0], x2.shape[1],
+         int(row0), ctypes.byref(dc), current_stream_handle(x2.device))
+    return out
+
+
+class _FeatureDropout(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x2, de, row0: int):
+        ctx.de, ctx.row0 = de, row0
+        return feature_dropout_apply(x2, de, row0)
+
+    @staticmethod
+    def backward(ctx, g):
+        return feature_dropout_apply(_rows_view(g.contiguous()), ctx.de, ctx.row0), None, None
+
+
+def feature_dropout(x: torch.Tensor, de, row0: int = 0) -> torch.Tensor:
+    """nn.Dropout(p) over node-feature rows with the mask of element (global
+    row, column) a counter hash under the DropEdge record `de` (its p, seed
+    / seed tensor and call id): drop_robust_gcn.py:64,77,81,86,100.  row0:
+    the global row of x's first row (a node-range shard's row_begin), so a
+    shard's rows get the one-GPU model's mask."""
+    lead = x.shape[:-1]
+    x2 = _rows_view(x)
+    return _FeatureDropout.apply(x2, de, int(row0)).view(*lead, x.shape[-1])
+
+
+# ------------------------------------------------------- row-local linears
+def linear_fwd_ex(X2: torch.Tensor, W: torch.Tensor, w_layout: int, b, relu: bool, path_rows: int = 0,
+                  out: torch.Tensor = None) -> torch.Tensor:
+    """out = X2 W (+ b) [ReLU] through grl_linear_fwd_ex; W [K, C]
+    (w_layout 0) or [C, K] (1, nn.Linear.weight); the path chosen for
+    max(M, path_rows) rows."""
+    M, K = X2.shape
+    C = W.shape[1] if w_layout == 0 else W.shape[0]
+    if out is None:
+        out = torch.empty(M, C, dtype=torch.float32, device=X2.device)
+    ws_bytes = _lib.lib().grl_linear_fwd_ex_workspace_size(M, K, C, int(path_rows))
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=X2.device) if ws_bytes else None
+    call("grl_linear_fwd_ex", X2.data_ptr(), X2.stride(0), W.data_ptr(), int(w_layout),
+         b.data_ptr() if b is not None else None, out.data_ptr(), M, K, C, int(relu), int(path_rows),
+         ws.data_ptr() if ws is not None else None, ws_bytes, current_stream_handle(X2.device))
+    return out
+
+
+class _RowLinear(torch.autograd.Function):
+    """nn.Linear (+ ReLU) on the libgrl GEMM: out = X W^T + b.  Every output
+    row is the same fp32 operations whatever the row count (both GEMM paths
+    are M-invariant and path_rows pins the choice), so a node-range shard's
+    rows are bitwise the one-GPU model's."""
+
+    @staticmethod
+    def forward(ctx, X2, W, b, relu: bool, path_rows: int):
+        Wc = W.contiguous()
+        out = linear_fwd_ex(X2, Wc, 1, b.contiguous() if b is not None else None, relu, path_rows)
+        ctx.relu, ctx.path_rows = relu, path_rows
+        ctx.save_for_backward(X2, Wc, out if relu else None)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        X2, W, out = ctx.saved_tensors
+        g = g.contiguous().float()
+        if ctx.relu:
+            g = torch.where(out > 0, g, torch.zeros((), dtype=g.dtype, device=g.device))
+        dX = dW = db = None
+        if ctx.needs_input_grad[0]:
+            dX = linear_fwd_ex(g, W, 0, None, False, ctx.path_rows)  # g [M, C] x W [C, K]
+        want_b = ctx.needs_input_grad[2]
+        if ctx.needs_input_grad[1] or want_b:
+            dWt, db = linear_bwd_weight(X2, g, None, want_b)  # X^T g [K, C]
+            dW = dWt.t() if ctx.needs_input_grad[1] else None
+        return dX, dW, db, None, None
+
+
+def row_linear(X: torch.Tensor, W: torch.Tensor, b=None, relu: bool = False, path_rows: int = 0) -> torch.Tensor:
+    """nn.Linear(K, C) [+ ReLU] over the rows of X [..., K] (W [C, K], b [C])
+    on the libgrl GEMM (grl_linear_fwd_ex): the row-local linears of
+    GraphCNNDropEdge (drop_robust_gcn.py:36-58, robust_gcn.py:81-83).
+    path_rows: the row count the GEMM path is chosen for (a node-range
+    shard passes the whole graph's)."""
+    _require_device(X, "linear input")
+    if X.dtype != torch.float32 or W.dtype != torch.float32:
+        raise _lib.GrlError("row_linear: float32 input and weight required")
+    lead = X.shape[:-1]
+    X2 = _rows_view(X)
+    out = _RowLinear.apply(X2, W, b, relu, int(path_rows))
+    return out.view(*lead, W.shape[0])
 
 
 # ---------------------------------------------------------------- attention

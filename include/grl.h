@@ -104,6 +104,13 @@ typedef struct GrlTypedCsr {
                             this row on -- sets its first row).  Forward entry
                             points only: grl_csr_to_csc and
                             grl_graphconv_bwd_data require 0.               */
+  int64_t path_rows;     /* rows the GEMM path (split-bf16 x6 or fp32) is
+                            chosen for; 0 = num_rows.  A node-range shard (or
+                            a row-range view) passes the whole graph's row
+                            count, so its rows take the one-GPU layer's path:
+                            with it, every output row is bitwise the whole
+                            graph's (both paths' per-row arithmetic is
+                            independent of the row count).                   */
 } GrlTypedCsr;
 
 /*
@@ -186,6 +193,17 @@ int grl_dropedge_init(GrlDropEdge* de, float p, uint64_t seed, uint64_t call_id,
 int grl_dropedge_init_device(GrlDropEdge* de, float p, const uint64_t* seed_dev,
                              uint64_t call_id, int32_t drop_self);
 
+/* Feature dropout on node rows (nn.Dropout(p) at drop_robust_gcn.py:64,77,81,
+ * 86,100): out[r][c] = x[r][c] * scale if element id (row0 + r) * cols + c
+ * survives `de` (the DropEdge hash and keep rule above; the caller gives the
+ * feature draws their own call ids), else 0.  row0 = the global row of x's
+ * first row (a node-range shard's row_begin), so every row's mask is the
+ * one-GPU model's wherever the row is computed.  The backward is the same
+ * call on the gradient.  x / out [rows][ld*] fp32 (out may alias x).      */
+int grl_feature_dropout(const float* x, int64_t ldx, float* out, int64_t ldo,
+                        int64_t rows, int32_t cols, int64_t row0,
+                        const GrlDropEdge* de, grl_stream_t stream);
+
 /* keep[i] = 1 if id_base + i survives DropEdge `de`, else 0 (i < count).
  * Exposes the fused mask for parity checks against the dense reference
  * (the mask nn.Dropout would draw over A_pre, drop_robust_gcn.py:76).    */
@@ -266,7 +284,10 @@ int grl_typed_spmm_bwd_slice(const GrlTypedCsc* g, const float* dZ,
  * When the output tiles cannot fill the chip (small graphs: a 74-node page
  * is one 128-row tile) K is split over workgroups into fp32 slabs in
  * `workspace`, added in split order (deterministic) with bias/ReLU applied
- * once.  grl_linear_fwd_workspace_size() is 0 when neither applies (the
+ * once; larger M sums K in the same fixed chunks inside each workgroup, so
+ * every element is the same fp32 operations whatever M is (a row of a
+ * node-range shard equals the whole graph's row on the same path).
+ * grl_linear_fwd_workspace_size() is 0 when neither applies (the
  * workspace may then be NULL), else the bytes the call requires; a large-M
  * call given less falls back to the fp32-MFMA kernel.                    */
 size_t grl_linear_fwd_workspace_size(int64_t M, int32_t K, int32_t C);
@@ -274,6 +295,22 @@ int grl_linear_fwd(const float* Z, int64_t ldz, const float* W,
                    const float* bias, float* out, int64_t M, int32_t K,
                    int32_t C, int32_t relu, void* workspace,
                    size_t workspace_bytes, grl_stream_t stream);
+
+/* grl_linear_fwd with the weight's layout and the path's row count explicit:
+ * w_layout 0: W [K, C] row-major (GraphConv.h_weights); 1: W [C, K]
+ * row-major (nn.Linear.weight: out = Z W^T + bias, the row-local linears of
+ * GraphCNNDropEdge -- emb2, NodeSelfAtten's f / g / h, the RanPAC projection,
+ * the classifier -- drop_robust_gcn.py:36-58, robust_gcn.py:81-83).
+ * path_rows: the row count the x6-vs-fp32 choice is made for (0 = M); a
+ * node-range shard passes the whole graph's, so its rows are bitwise the
+ * one-GPU call's.  Workspace: grl_linear_fwd_ex_workspace_size().          */
+size_t grl_linear_fwd_ex_workspace_size(int64_t M, int32_t K, int32_t C,
+                                        int64_t path_rows);
+int grl_linear_fwd_ex(const float* Z, int64_t ldz, const float* W,
+                      int32_t w_layout, const float* bias, float* out,
+                      int64_t M, int32_t K, int32_t C, int32_t relu,
+                      int64_t path_rows, void* workspace,
+                      size_t workspace_bytes, grl_stream_t stream);
 
 /* One GraphConv layer forward in one call (inference):
  *   out = relu?( (A_drop X) W + bias )       robust_gcn.py:45-51 (+ the F.relu

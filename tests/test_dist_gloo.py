@@ -264,7 +264,7 @@ def _agree_worker(rank, world, port):
         # point-to-point transfer is posted (they then all run the unpipelined exchange: matching collectives)
         plan = types.SimpleNamespace(bounds=[0, 10, 20, 30], rank=rank, mode="dense", stride=10, n_loc=10,
                                      recv_counts=[0] * 3, send_counts=[0] * 3)
-        sg = types.SimpleNamespace(plan=plan, group=None)
+        sg = types.SimpleNamespace(plan=plan, group=None, graph=types.SimpleNamespace(_shared={}))
         sg.halo_blocks = types.MethodType(gdist.ShardedGraph.halo_blocks, sg)
         orig_views, orig_rows = ops.graph_conv_bwd_data_rows_views, ops.graph_conv_bwd_data_rows
         try:

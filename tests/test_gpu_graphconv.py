@@ -439,6 +439,65 @@ def test_persistent_kernel_timeout_is_an_error(monkeypatch):
         grl.check()
 
 
+def test_timeout_report_is_never_lost_between_checks(monkeypatch):
+    """grl_check takes the sticky word with ONE atomic exchange (its old value
+    written to a pinned host word): a poisoned call on another stream that
+    lands while checks run on this stream is reported by exactly one check
+    -- never lost between a read and a separate clear, never twice."""
+    import grl
+
+    N, L, F, C = 20_011, 6, 256, 256
+    g = TypedGraph.synthetic(N, 16.0, L, seed=3, device=DEV)
+    gen = torch.Generator(device=DEV).manual_seed(9)
+    X = torch.randn(N, F, device=DEV, generator=gen)
+    W = torch.randn(7 * F, C, device=DEV, generator=gen) / 40
+    b = torch.randn(C, device=DEV, generator=gen)
+    graph_conv_infer(X, g, W, b, True)
+    grl.check()
+    monkeypatch.setenv("GRL_WS_SPIN", "1")
+    reports = 0
+    for delay in (0, 2_000_000, 20_000_000):  # the poison lands before, during, after the checks below
+        side = torch.cuda.Stream(DEV)
+        side.wait_stream(torch.cuda.current_stream(DEV))
+        with torch.cuda.stream(side):
+            if delay:
+                torch.cuda._sleep(delay)
+            out = graph_conv_infer(X, g, W, b, True)
+        for _ in range(50):
+            try:
+                grl.check()
+            except _lib.GrlError:
+                reports += 1
+        side.synchronize()
+        try:
+            grl.check()
+        except _lib.GrlError:
+            reports += 1
+        assert bool(torch.isnan(out).all())
+    assert reports == 3  # one per poisoned call
+    monkeypatch.delenv("GRL_WS_SPIN")
+    grl.check()
+
+
+def test_bench_surfaces_a_poisoned_timed_region(monkeypatch):
+    """bench.py checks after every timed region (bench.surface): a poisoned
+    run exits non-zero naming the section and the entry point instead of
+    being reported as a timing."""
+    import bench
+
+    N, L, F, C = 20_011, 6, 256, 256
+    g = TypedGraph.synthetic(N, 16.0, L, seed=3, device=DEV)
+    X = torch.randn(N, F, device=DEV)
+    W = torch.randn(7 * F, C, device=DEV) / 40
+    bench.surface("clean", DEV)
+    monkeypatch.setenv("GRL_WS_SPIN", "1")
+    graph_conv_infer(X, g, W, None, True)
+    with pytest.raises(SystemExit, match=r"bench.py: extras \(layers\): .*grl_graphconv_fwd"):
+        bench.surface("extras (layers)", DEV)
+    monkeypatch.delenv("GRL_WS_SPIN")
+    bench.surface("clean again", DEV)
+
+
 @pytest.mark.parametrize("N,F,C,p,cuts", [(40_000, 256, 256, 0.3, (0, 17_500, 25_000, 40_000)),
                                           (20_000, 512, 256, 0.3, (0, 9999, 20_000)),
                                           (3000, 64, 64, 0.0, (0, 1000, 1001, 3000))])

@@ -35,3 +35,22 @@ def test_halo_exchange_on_rccl_loopback():
     # the row-pipelined backward had a halo block to post point to point (the loopback peer's rows)
     assert res["dense_rows_blocks"] and res["dense_rows_blocks"][0][1] > 0
     assert res["sparse_rows_blocks"] and res["sparse_rows_blocks"][0][1] > 0
+
+
+def test_sharded_model_on_rccl_loopback():
+    """tests/loopback_model.py: the drop-in model's training step and streamed
+    inference over a loopback shard with every grl.dist collective on a
+    one-rank RCCL group -- bitwise the same steps over a one-rank LocalGroup
+    (the emulator the multi-rank GPU tests run), the forward bitwise the
+    one-GPU model's -- and each kind of collective actually issued to RCCL."""
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, "-u", os.path.join(HERE, "loopback_model.py")], env=env,
+                       capture_output=True, text=True, timeout=400)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert lines, f"rc {r.returncode}\nstdout:\n{r.stdout[-3000:]}\nstderr:\n{r.stderr[-3000:]}"
+    res = json.loads(lines[-1])
+    failed = {k: v for k, v in res["checks"].items() if not (v is True or (isinstance(v, dict) and v["ok"]))}
+    assert not failed and res["ok"] and r.returncode == 0, (failed, res["calls"], r.stderr[-2000:])
+    assert res["backend"] == "nccl"
