@@ -81,6 +81,12 @@ def run(m, V, A, y, group):
                             bucket_bytes=1 << 16)  # several buckets
     res = {"logits": logits.detach(), **{k: v for k, v in seen.items()},
            **{"grad " + k: p.grad.detach().clone() for k, p in m.named_parameters() if p.grad is not None}}
+    # device-drawn DropEdge / feature-dropout seeds (the production default): rank 0's draw is broadcast
+    # (ShardedGraph.broadcast_seed); the generator reseeded so both runs draw the same seeds
+    m.edge_dropout.seed = m.dropout.seed = None
+    torch.manual_seed(11)
+    with torch.no_grad():
+        res["logits_device_seeds"] = m.forward([V, A]).reshape(-1, OUT)
     m.eval()
     with torch.no_grad():
         if isinstance(A, ShardedGraph):
@@ -135,7 +141,7 @@ def main():
             tag = f"N{N}_{mode}"
             diff = [k for k in rccl if not torch.equal(rccl[k], loc[k])]
             check(f"{tag}_localgroup_bitwise_rccl", not diff, {"differ": diff[:8]})
-            for k in ("logits", "gcn1", "gcn2", "gcn3", "eval_plain"):
+            for k in ("logits", "gcn1", "gcn2", "gcn3", "eval_plain", "logits_device_seeds"):
                 check(f"{tag}_{k}_bitwise_one_gpu", torch.equal(rccl[k], one[k]))
             for k in ("eval_streamed2", "eval_streamed3"):
                 check(f"{tag}_{k}_bitwise_one_gpu", torch.equal(rccl[k], one["eval_plain"]))

@@ -196,7 +196,7 @@ def _worker_random(rank, world, port, cfg):
         dp2.model.train()
         de = dp2.model.edge_dropout(g).dropedge
         assert de.call == rank and de.seed_tensor is not None
-        fmask = torch.nn.functional.dropout(torch.ones(256, device=dp2.device), 0.5).cpu()
+        fmask = dp2.model.dropout(torch.ones(4, 256, device=dp2.device)).cpu()  # the model's hash-keyed dropout
         draws = [(de.seed_tensor.cpu(), fmask) for _ in range(world)]
         dist.all_gather_object(draws, (de.seed_tensor.cpu(), fmask))
         assert int(draws[0][0]) != int(draws[1][0])  # DropEdge seeds drawn on the device
