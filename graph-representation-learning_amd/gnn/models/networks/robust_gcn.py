@@ -27,18 +27,35 @@ def make_linear_relu(input_dim: int, output_dim: int) -> nn.Sequential:
     return nn.Sequential(nn.Linear(input_dim, output_dim), nn.ReLU())
 
 
+# Row count from which the row-local linears run on the libgrl GEMM (whose row
+# results do not depend on the row count: what a node-range shard needs to
+# reproduce the one-GPU model's rows bitwise).  Below it -- document pages
+# such as debug.json's 74 nodes, graphs far too small to shard -- torch's
+# single-launch GEMM is faster (tools/probe_row_linear.py).  The choice is
+# made on the WHOLE graph's rows (path_rows), so a shard and its one-GPU
+# model always take the same one.
+ROW_LINEAR_MIN_ROWS = 4096
+
+
+def _on_grl(x: torch.Tensor, path_rows: int) -> bool:
+    return x.is_cuda and max(x.numel() // max(x.shape[-1], 1), path_rows) > ROW_LINEAR_MIN_ROWS
+
+
 def apply_linear(mod: nn.Module, x: torch.Tensor, relu: bool = False, path_rows: int = 0) -> torch.Tensor:
     """An nn.Linear (or a make_linear_relu block, its ReLU fused) over the rows
-    of x.  On the device: the libgrl GEMM (grl.ops.row_linear), whose row
-    results do not depend on the row count -- with path_rows (a node-range
-    shard's whole-graph row count) a shard's rows are bitwise the one-GPU
-    model's; on the host: torch."""
+    of x: on the libgrl GEMM (grl.ops.row_linear, rows independent of the row
+    count; path_rows: a node-range shard's whole-graph row count) from
+    ROW_LINEAR_MIN_ROWS rows, else torch."""
     lin = mod[0] if isinstance(mod, nn.Sequential) else mod
     if isinstance(mod, nn.Sequential):
         relu = True
-    if x.is_cuda:
-        return row_linear(x.float(), lin.weight, lin.bias, relu=relu, path_rows=path_rows)
-    y = lin(x)
+    return linear_rows(x, lin.weight, lin.bias, relu, path_rows)
+
+
+def linear_rows(x: torch.Tensor, W: torch.Tensor, b, relu: bool, path_rows: int = 0) -> torch.Tensor:
+    if _on_grl(x, path_rows):
+        return row_linear(x.float(), W, b, relu=relu, path_rows=path_rows)
+    y = torch.nn.functional.linear(x, W, b)
     return torch.relu(y) if relu else y
 
 
@@ -148,7 +165,14 @@ class NodeSelfAtten(nn.Module):
         the softmax then runs over every node of the graph
         (grl.dist.sharded_node_attention)."""
         pr = shard.global_rows if shard is not None else 0
-        f, g, h = (apply_linear(m, V, path_rows=pr) for m in (self.f, self.g, self.h))
+        # f, g, h read the same V: one GEMM over their concatenated weights (2 x F/8 + F columns; a column's
+        # result does not depend on the others)
+        lins = (self.f[0], self.g[0], self.h[0])
+        W = torch.cat([m.weight for m in lins])
+        b = torch.cat([m.bias for m in lins])
+        fgh = linear_rows(V, W, b, True, pr)
+        dk = self.f[0].out_features
+        f, g, h = fgh[..., :dk], fgh[..., dk:2 * dk], fgh[..., 2 * dk:]
         if shard is not None:
             return sharded_node_attention(f, g, h, V, self.gamma, shard)
         return node_self_attention(f, g, h, V, self.gamma)

@@ -680,16 +680,22 @@ class _RowLinear(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, X2, W, b, relu: bool, path_rows: int):
-        Wc = W.contiguous()
-        out = linear_fwd_ex(X2, Wc, 1, b.contiguous() if b is not None else None, relu, path_rows)
-        ctx.relu, ctx.path_rows = relu, path_rows
+        C = W.shape[0]
+        pad = -C % 4  # an output width off the float4 grid (the classifier's 53) runs padded with zero rows of W
+        Wc = W.contiguous() if not pad else torch.nn.functional.pad(W, (0, 0, 0, pad))
+        bc = None if b is None else (b.contiguous() if not pad else torch.nn.functional.pad(b, (0, pad)))
+        out = linear_fwd_ex(X2, Wc, 1, bc, relu, path_rows)
+        ctx.relu, ctx.path_rows, ctx.C = relu, path_rows, C
         ctx.save_for_backward(X2, Wc, out if relu else None)
-        return out
+        return out if not pad else out[:, :C].contiguous()
 
     @staticmethod
     def backward(ctx, g):
         X2, W, out = ctx.saved_tensors
         g = g.contiguous().float()
+        C, Cp = ctx.C, W.shape[0]
+        if Cp != C:
+            g = torch.nn.functional.pad(g, (0, Cp - C))
         if ctx.relu:
             g = torch.where(out > 0, g, torch.zeros((), dtype=g.dtype, device=g.device))
         dX = dW = db = None
@@ -698,7 +704,8 @@ class _RowLinear(torch.autograd.Function):
         want_b = ctx.needs_input_grad[2]
         if ctx.needs_input_grad[1] or want_b:
             dWt, db = linear_bwd_weight(X2, g, None, want_b)  # X^T g [K, C]
-            dW = dWt.t() if ctx.needs_input_grad[1] else None
+            dW = dWt.t()[:C] if ctx.needs_input_grad[1] else None
+            db = db[:C] if db is not None else None
         return dX, dW, db, None, None
 
 
