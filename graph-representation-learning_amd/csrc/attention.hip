@@ -1543,12 +1543,6 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_kv_x6_kernel(AttnArg
 #ifndef GRL_ATTN_TPLANES
 #define GRL_ATTN_TPLANES 1
 #endif
-// GRL_KQ_WHATIF (timing diagnostics only, WRONG results): 1 = no dQ side
-// (no transpose / dQ MFMAs, partial stores or slab reduction); 2 = dS = dP
-// (no exp / softmax-derivative VALU); 3 = no per-block barrier (races)
-#ifndef GRL_KQ_WHATIF
-#define GRL_KQ_WHATIF 0
-#endif
 constexpr int KQ_WAVES = 8, KQ_KEYS = 32 * KQ_WAVES;
 template <bool SPLIT>
 __global__ __launch_bounds__(64 * KQ_WAVES, 1) void attn_bwd_kq_x6_kernel(AttnArgs a) {
@@ -1626,15 +1620,13 @@ __global__ __launch_bounds__(64 * KQ_WAVES, 1) void attn_bwd_kq_x6_kernel(AttnAr
       Ds[tid] = pd;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#if GRL_KQ_WHATIF != 3
     __syncthreads();
-#endif
     if (q0 + 32 < q_hi) {
       dma_block<16, PL_PLAIN, NW>(Qpb, qps, q0 + 32, N, Qp_s + (stg ^ 1) * 3 * 512, wave, lane);
       dma_block<128, PL_SWZ128, NW>(Opb, ops, q0 + 32, N, Op_s + (stg ^ 1) * 3 * 4096, wave, lane);
       fetch_stats(q0 + 32);
     }
-    if (GRL_KQ_WHATIF != 1 && q0 > q_lo) reduce(q0 - 32);
+    if (q0 > q_lo) reduce(q0 - 32);
     // S[query][key]: lanes = keys, registers = queries kappa(r, h)
     f32x16 s = zero16();  // natural-scale scores q.k (base 2 applied in the exponent's fma)
     {
@@ -1656,16 +1648,11 @@ __global__ __launch_bounds__(64 * KQ_WAVES, 1) void attn_bwd_kq_x6_kernel(AttnAr
       const abf16x8_t o2 = *reinterpret_cast<const abf16x8_t*>(&Op[8192 + off]);
       MFMA6(dp, o0, o1, o2, hp[fc][0], hp[fc][1], hp[fc][2]);
     }
-#if GRL_KQ_WHATIF == 2
-#pragma unroll
-    for (int r = 0; r < 16; ++r) s[r] = dp[r];
-#else
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int qi = kappa(r, h);
       s[r] = aexp2(fmaf(s[r], ALOG2E, -Ms[qi])) * (dp[r] - Ds[qi]);  // dS
     }
-#endif
     abf16x8_t dsp[2][3];
     reg_planes(s, dsp);
 #pragma unroll
@@ -1677,9 +1664,6 @@ __global__ __launch_bounds__(64 * KQ_WAVES, 1) void attn_bwd_kq_x6_kernel(AttnAr
         qt[pl] = tr8(&Qp[pl * 512 + r0 * 16 + (trc & 15)], &Qp[pl * 512 + r1 * 16 + (trc & 15)]);
       MFMA6(acc, qt[0], qt[1], qt[2], dsp[u][0], dsp[u][1], dsp[u][2]);  // dK^T += Q^T dS
     }
-#if GRL_KQ_WHATIF == 1
-    continue;
-#endif
     // dS transposed (lanes = queries, registers = keys kappa(r, h)) PLANE BY PLANE:
     // each transposed element is one plane value times 1 plus zeros, so it is
     // that bf16 value exactly and packs back without a split: dQ's A operand
@@ -1997,8 +1981,6 @@ int attn_splits(int64_t B, int64_t N, int64_t* kr) {
       S = s;
     }
   }
-  const char* e = getenv("GRL_ATTN_SPLITS");  // A/B aid: force the split count
-  if (e && atoi(e) > 0) S = std::min<int64_t>(atoi(e), std::max<int64_t>(1, N / 256));
   S = std::max<int64_t>(1, std::min<int64_t>(S, 64));
   *kr = ceil_div(ceil_div(N, S), 32) * 32;
   return (int)ceil_div(N, *kr);

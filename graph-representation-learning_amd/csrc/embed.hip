@@ -300,8 +300,6 @@ __global__ void bag_dw_reduce_kernel(const float* __restrict__ part, int S, int 
 // budget is 1 GiB (S = 128: 573 MB at C = 256; C = 512: S = 120, 1.07 GB).
 constexpr int64_t DW_PART_BUDGET = 1ll << 30;
 int bag_dw_splits(int64_t M, int64_t Keff, int64_t C) {
-  const char* e = getenv("GRL_BAG_DW_SPLITS");  // A/B aid (read by the size query and the call alike)
-  if (e && atoi(e) > 0) return (int)std::max<int64_t>(1, std::min<int64_t>(atoi(e), M));
   const int64_t by_mem = std::max<int64_t>(1, DW_PART_BUDGET / std::max<int64_t>(1, Keff * C * 4));
   return (int)std::max<int64_t>(1, std::min<int64_t>(std::min<int64_t>(128, by_mem), ceil_div(M, 512)));
 }

@@ -443,11 +443,6 @@ constexpr int WS_STATUS_TIMEOUT = 1;       // status bit: a bounded wait ran out
 
 // GRL_WS_STAMP=1 (diagnostic builds only): every wave adds up the cycles it
 // spent waiting on the ring and its total, read back with grl_debug_ws_stats
-// GRL_WS_SADDR: gathered rows addressed as a scalar row base + the lane's
-// column offset (0 = the per-lane 64-bit address of rounds 2-3, A/B aid)
-#ifndef GRL_WS_SADDR
-#define GRL_WS_SADDR 1
-#endif
 #ifndef GRL_WS_STAMP
 #define GRL_WS_STAMP 0
 #endif
@@ -455,13 +450,6 @@ constexpr int WS_STATUS_TIMEOUT = 1;       // status bit: a bounded wait ran out
 // 1 = compile the gather role alone, 2 = the MFMA role alone
 #ifndef GRL_WS_ONLY_ROLE
 #define GRL_WS_ONLY_ROLE 0
-#endif
-// GRL_WS_WHATIF (timing diagnostics only, WRONG results): 1 = the MFMA waves
-// load W fragments once per unit instead of per step; 2 = they skip the A
-// split; 3 = the gather waves skip the neighbour rows (own row only); 4 = the
-// MFMA waves only release the slots (the gather alone)
-#ifndef GRL_WS_WHATIF
-#define GRL_WS_WHATIF 0
 #endif
 #if GRL_WS_STAMP
 __device__ unsigned long long g_ws_dbg[1024 * 12 * 2];
@@ -692,7 +680,6 @@ __global__ __launch_bounds__(GRL_WS_DIAG_LB) void graphconv_ws_kernel(
                 float w = cur.w;
                 if (c0 > 0) fetch(cur, c0, sidx, w);  // rows with more than 64 segment edges together
                 uint64_t kept = __ballot(w != 0.0f);
-                if (GRL_WS_WHATIF == 3) kept = 0;
                 while (kept) {
                   int jj[U];
 #pragma unroll
@@ -709,7 +696,6 @@ __global__ __launch_bounds__(GRL_WS_DIAG_LB) void graphconv_ws_kernel(
                   for (int q = 0; q < U; ++q) {
                     if (jj[q] >= 0) {
                       const int src = readlane_i(sidx, jj[q]);
-#if GRL_WS_SADDR
                       // the source row's address is wave-uniform: a scalar base + the lane's column
                       // offset (global_load's saddr form, no 64-bit VALU add per gathered row)
                       // (src, ldx >= 0 and ldx < 2^30: an unsigned 32 x 32 -> 64-bit product of bytes)
@@ -724,9 +710,6 @@ __global__ __launch_bounds__(GRL_WS_DIAG_LB) void graphconv_ws_kernel(
                         const f32x4_t t = *(gvec4*)(rowp + col);
                         xv[q] = make_float4(t[0], t[1], t[2], t[3]);
                       }
-#else
-                      xv[q] = col_ok ? *reinterpret_cast<const float4*>(xs + (int64_t)src * ldx) : zero4();
-#endif
                     }
                   }
 #pragma unroll
@@ -805,10 +788,6 @@ __global__ __launch_bounds__(GRL_WS_DIAG_LB) void graphconv_ws_kernel(
       v1 = *reinterpret_cast<const float4*>(ar + 4);
     };
     auto split_a = [&](const float4& v0, const float4& v1, bf16x8_t (&a)[3]) {
-#if GRL_WS_WHATIF == 2
-      a[0] = a[1] = a[2] = __builtin_bit_cast(bf16x8_t, make_float4(v0.x, v0.y, v1.x, v1.y));
-      return;
-#endif
       uint2 p0, p1, p2, r0, r1, r2;
       split3(v0, p0, p1, p2);
       split3(v1, r0, r1, r2);
@@ -835,10 +814,6 @@ __global__ __launch_bounds__(GRL_WS_DIAG_LB) void graphconv_ws_kernel(
         const int slot = u % WS_NB, g = u / WS_NB;
         const float* zs = ring + slot * WS_SLOT;
         if (!wait_ge(&produced[slot], PROD * (g + 1), &waited, spin_limit, status)) return;
-#if GRL_WS_WHATIF == 4
-        if (lane == 0) lds_add_rel(&consumed[slot], 1);
-        continue;
-#endif
         // Software-pipelined by row block: the split of the next row block's
         // A fragments (VALU) is interleaved with the current row block's 12
         // MFMAs (an MFMA holds the SIMD's issue for 8 of its 32 cycles; the
@@ -851,7 +826,7 @@ __global__ __launch_bounds__(GRL_WS_DIAG_LB) void graphconv_ws_kernel(
         }
 #pragma unroll
         for (int ks = 0; ks < KSU; ++ks) {  // KSU is even: the stage of step ks is ks & 1
-          if (GRL_WS_WHATIF != 1 || ks == 0) load_b(bb[(ks + 1) & 1], nxt);
+          load_b(bb[(ks + 1) & 1], nxt);
           nxt = nxt + 1 == nsteps ? 0 : nxt + 1;
           const int st = ks & 1;
           float4 v0, v1;

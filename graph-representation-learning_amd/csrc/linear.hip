@@ -29,12 +29,6 @@ using f32x16 = __attribute__((ext_vector_type(16))) float;
 
 constexpr int BM = 128, BN = 128;
 
-#ifndef GRL_GEMM_VEC_EPI
-#define GRL_GEMM_VEC_EPI 1
-#endif
-#ifndef GRL_GEMM_INTERLEAVE
-#define GRL_GEMM_INTERLEAVE 1
-#endif
 
 
 enum Epilogue { EPI_STORE = 0, EPI_BIAS = 1, EPI_SLAB = 2 };
@@ -67,9 +61,6 @@ struct GemmArgs {
   int64_t path_rows;
 };
 
-#ifndef GRL_GEMM_XCD
-#define GRL_GEMM_XCD 1
-#endif
 
 // XCD-aware tile order.  Workgroups are dealt to the 8 XCDs round-robin
 // (blockIdx % 8; speed only, never relied on for correctness), and each XCD
@@ -80,13 +71,8 @@ struct GemmArgs {
 __device__ __forceinline__ void tile_of(const GemmArgs& p, int64_t& mi, int64_t& ni, int64_t& zi) {
   const int64_t T = p.mt * p.nt * p.zt;
   const int64_t L = blockIdx.x;
-#if GRL_GEMM_XCD
   const int64_t q = T / 8, r = T % 8, x = L % 8, s = L / 8;
   const int64_t u = x * q + (x < r ? x : r) + s;
-#else
-  const int64_t u = L;
-  (void)T;
-#endif
   if (p.inner_n) {
     ni = u % p.nt;
     mi = (u / p.nt) % p.mt;
@@ -227,7 +213,6 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs p) {
       for (int i = 0; i < 2; ++i) a[i] = OA::frag(As, wm * 64 + i * 32 + l32, kk, h);
 #pragma unroll
       for (int j = 0; j < 2; ++j) b[j] = OB::frag(Bs, wn * 64 + j * 32 + l32, kk, h);
-#if GRL_GEMM_INTERLEAVE
       // component-major: consecutive MFMAs hit the four independent
       // accumulators, so none waits on the previous one's result (the
       // per-accumulator k order is unchanged: results are bitwise the same)
@@ -240,17 +225,6 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs p) {
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(reinterpret_cast<const float*>(&a[i])[c],
                                                              reinterpret_cast<const float*>(&b[j])[c], acc[i][j],
                                                              0, 0, 0);
-#else
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].x, b[j].x, acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].y, b[j].y, acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].z, b[j].z, acc[i][j], 0, 0, 0);
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i].w, b[j].w, acc[i][j], 0, 0, 0);
-        }
-#endif
     }
   };
 
@@ -295,7 +269,6 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs p) {
 
   // ---- epilogue: C/D map col = lane&31, row = (r&3) + 8(r>>2) + 4h --------
   float* Cz = p.C + (EPI == EPI_SLAB ? zi * p.M * p.ldc : 0);
-#if GRL_GEMM_VEC_EPI
   // Through LDS, one 64 x 32 half of the wave's sub-tile at a time, so that
   // every lane stores whole float4 rows (a register holds one column of four
   // rows; scalar stores cost 4x the store instructions on a 7 GB output).
@@ -335,7 +308,6 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs p) {
     }
     return;
   }
-#endif
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int64_t gn = n0 + wn * 64 + j * 32 + l32;
@@ -637,12 +609,6 @@ __global__ __launch_bounds__(512) void gemm256p_kernel(GemmArgs p) {
 // Preconditions (x6_shape_ok + aligned): K % 16 == 0, 16-B aligned A,
 // lda % 4 == 0, no operand masks.
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-#ifndef GRL_X6_PRIO
-#define GRL_X6_PRIO 0
-#endif
-#ifndef GRL_X6_ORDER
-#define GRL_X6_ORDER 0
-#endif
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
 
@@ -687,24 +653,6 @@ __global__ void split_planes_kernel(const float* __restrict__ B, int64_t ldb, in
   }
 }
 
-// GRL_X6_STAGGER (read per call): 1 = the staggered x6 forward / dZ kernel
-bool x6_stagger() {
-  const char* e = getenv("GRL_X6_STAGGER");
-  return e && e[0] == '1';
-}
-
-// GRL_X6T_U2 (read per call): 0 = the rolled dW loop (A/B aid)
-bool x6t_u2() {
-  const char* e = getenv("GRL_X6T_U2");
-  return !(e && e[0] == '0');
-}
-
-// GRL_X6_INTERLEAVE (read per call): 1 = the A split interleaved with the MFMAs
-bool x6_interleave() {
-  const char* e = getenv("GRL_X6_INTERLEAVE");
-  return e && e[0] == '1';
-}
-
 // global -> LDS DMA of one 16 B chunk per lane (lane l lands at lds_base + 16 l).
 // Issued from asm so that hipcc's waitcnt pass neither sees nor waits on it;
 // completion is ordered by the kernel's counted `s_waitcnt vmcnt`.
@@ -731,20 +679,7 @@ __device__ __forceinline__ void dma16(const void* src, const void* lds_base) {
 // A's loads get two compute phases to land, B's (L2-resident planes) one.
 constexpr int X6_SLOT = 512 * 8;  // floats per landing slot (16 KB)
 
-// STAGGER: the two waves sharing a SIMD (w and w + 4) take the step's two
-// non-MFMA phases in opposite order -- waves 0-3 multiply then split A(t+1)
-// into the next stage, waves 4-7 split first and multiply after -- so one
-// partner's split (VALU + LDS writes, its DMA wait) runs under the other's
-// MFMAs instead of both splitting while the matrix core idles
-// (MI355X_MICROARCH.md, two waves per SIMD: stagger).  Same arithmetic,
-// same bits.
-// INTERLEAVE: the split of A(t+1) into the next stage (2 landing-slot reads,
-// ~44 VALU, 6 LDS writes per wave) is scheduled between step t's 48 MFMAs
-// (sched_group_barrier) instead of after them: an MFMA holds the SIMD's issue
-// for 8 of its 32 cycles and the split fits in the rest.  A(t+1) landed one
-// step earlier, so its wait moves before the MFMAs; B(t+1)'s DMA is waited
-// for at the end of the step, before the next barrier.  Same bits.
-template <int EPI, bool STAGGER = false, bool INTERLEAVE = false>
+template <int EPI>
 __global__ __launch_bounds__(512) void gemm_x6_kernel(GemmArgs p, const uint16_t* __restrict__ Bp, int64_t Np) {
   __shared__ __attribute__((aligned(16))) uint16_t smem[2 * X6_STAGE];  // 2 plane stages x 48 KB
   __shared__ __attribute__((aligned(16))) float land[3 * X6_SLOT];      // 3 landing slots x 16 KB
@@ -843,35 +778,7 @@ __global__ __launch_bounds__(512) void gemm_x6_kernel(GemmArgs p, const uint16_t
 #pragma unroll
         for (int q = 0; q < 3; ++q)
           b_[j][q] = *reinterpret_cast<const bf16x8_t*>(cur + (3 + q) * X6_PLANE + sw(wn * 64 + j * 32 + l32, h * 8));
-      if (INTERLEAVE && t + 1 < nk) {  // A(t+1) is older than B(t+1) (3 DMAs) and A(t+2) (2)
-        if (t + 2 < nk)
-          asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-        else
-          asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-      }
-      if (STAGGER && wm == 1 && t + 1 < nk) {  // the late half: split A(t+1) before its MFMAs
-        // B(t+1) (3 DMAs) and A(t+2) (2) were just issued and may stay in flight; A(t+1) is older
-        if (t + 2 < nk)
-          asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
-        else
-          asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-        stash_a(t + 1, nxt);
-      }
       // small terms first (i + j = 2, then 1, then the leading product)
-#if GRL_X6_PRIO
-      __builtin_amdgcn_s_setprio(1);
-#endif
-#if GRL_X6_ORDER
-      // product-major: eight independent accumulators between two uses of one
-      constexpr int PA[6] = {2, 1, 0, 1, 0, 0}, PB[6] = {0, 1, 2, 0, 1, 0};
-#pragma unroll
-      for (int pr = 0; pr < 6; ++pr)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_[i][PA[pr]], b_[j][PB[pr]], acc[i][j], 0, 0, 0);
-#else
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -883,39 +790,13 @@ __global__ __launch_bounds__(512) void gemm_x6_kernel(GemmArgs p, const uint16_t
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_[i][0], b_[j][1], acc[i][j], 0, 0, 0);
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_[i][0], b_[j][0], acc[i][j], 0, 0, 0);
         }
-#endif
-#if GRL_X6_PRIO
-      __builtin_amdgcn_s_setprio(0);
-#endif
-      if (INTERLEAVE && t + 1 < nk) {
-        stash_a(t + 1, nxt);
-        // fragment and landing reads first, then 2 MFMAs / 2 VALU, the stores last
-        __builtin_amdgcn_sched_group_barrier(0x100, 20, 0);
-#pragma unroll
-        for (int q = 0; q < 22; ++q) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
-          __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
-        }
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          __builtin_amdgcn_sched_group_barrier(0x200, 2, 0);
-        }
-      }
     }
-    if (INTERLEAVE) {
-      if (t + 1 < nk) {  // B(t+1) landed before the next barrier
-        if (t + 2 < nk)
-          asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
-        else
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-    } else if (t + 1 < nk) {
+    if (t + 1 < nk) {
       if (t + 2 < nk)
         asm volatile("s_waitcnt vmcnt(2)" ::: "memory");  // A(t+2) may stay in flight
       else
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (!STAGGER || wm == 0) stash_a(t + 1, nxt);
+      stash_a(t + 1, nxt);
     }
   }
   float* Cz = p.C;
@@ -970,19 +851,6 @@ __global__ __launch_bounds__(512) void gemm_x6_kernel(GemmArgs p, const uint16_t
 // aligned operands, lda, ldb, M, N multiples of 4.
 typedef short i16x4_t __attribute__((ext_vector_type(4)));
 
-__device__ __forceinline__ bf16x8_t tr_pair(const uint16_t* plane, int k, int col) {
-  // k = 8h + qq for this lane's first block row (qq = (lane & 15) >> 2); the
-  // second read is the same block 4 k further
-  typedef __attribute__((address_space(3))) i16x4_t lds_v4;
-  const uint16_t* p0 = plane + k * 256 + (col ^ ((k & 3) << 5));
-  const uint16_t* p1 = plane + (k + 4) * 256 + (col ^ ((k & 3) << 5));
-  const i16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(uintptr_t)(uint32_t)(uintptr_t)p0);
-  const i16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(uintptr_t)(uint32_t)(uintptr_t)p1);
-  typedef short i16x8_t __attribute__((ext_vector_type(8)));
-  const i16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8_t, v);
-}
-
 typedef __attribute__((address_space(3))) uint16_t lds_u16;
 
 // tr_pair on an LDS-space pointer (p0 = plane + k * 256 + swizzled column):
@@ -997,27 +865,11 @@ __device__ __forceinline__ bf16x8_t tr_pair3(const lds_u16* p0) {
   return __builtin_bit_cast(bf16x8_t, v);
 }
 
-#ifndef GRL_X6T_WHATIF
-#define GRL_X6T_WHATIF 0
-#endif
-#ifndef GRL_X6T_NTA
-#define GRL_X6T_NTA 0
-#endif
-// GRL_X6T_NTA: Z (read once) as non-temporal loads, keeping the L2 for g
-// (re-read by every M tile)
-#if GRL_X6T_NTA
-__device__ __forceinline__ float4 x6t_lda(const float* q) {
-  typedef float v4f __attribute__((ext_vector_type(4)));
-  const v4f v = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(q));
-  return make_float4(v[0], v[1], v[2], v[3]);
-}
-#endif
-
-// GRL_X6T_U2 (read per call; default 1): the K16 loop unrolled over the two
-// stages, fragment reads from per-lane LDS offsets fixed for the kernel (the
-// stage and plane as immediates) -- the rolled loop recomputed ~40 address
-// adds per step.  Same reads, same MFMAs, same bits.
-template <int EPI, bool U2 = false>
+// The K16 loop is unrolled over the two stages, fragment reads from per-lane
+// LDS offsets fixed for the kernel (the stage and plane as immediates): the
+// rolled loop recomputed ~40 address adds per step (round 4,
+// profiles/r04_ab_dw_u2.txt).
+template <int EPI>
 __global__ __launch_bounds__(512) void gemm_x6t_kernel(GemmArgs p) {
   __shared__ __attribute__((aligned(16))) uint16_t smem[2 * X6_STAGE];  // 2 stages x (A, B) x 3 planes x 8 KB
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1047,25 +899,15 @@ __global__ __launch_bounds__(512) void gemm_x6t_kernel(GemmArgs p) {
   // made hipcc branch on the loaded registers and wait vmcnt(0) for them
   // there, exposing the whole load latency on every K16 step
   // (cdna_hip_programming.md, "register or load" selects).
-#if GRL_X6T_WHATIF == 3  // timing only: every step re-reads the split's first rows (cache hits)
-#define X6T_ROW(real, fixed) (fixed)
-#else
-#define X6T_ROW(real, fixed) (real)
-#endif
-#if GRL_X6T_NTA
-#define X6T_LDA(q) x6t_lda(q)
-#else
-#define X6T_LDA(q) (*reinterpret_cast<const float4*>(q))
-#endif
 #define X6T_LOAD(t)                                                                                       \
   do {                                                                                                    \
     const int64_t k_ = kbeg + (t) * X6_K;                                                                 \
     in0 = k_ + kr0 < kend;                                                                                \
     in1 = k_ + kr1 < kend;                                                                                \
-    const int64_t r0_ = X6T_ROW(in0 ? k_ + kr0 : kbeg, kbeg + kr0);                                      \
-    const int64_t r1_ = X6T_ROW(in1 ? k_ + kr1 : kbeg, kbeg + kr1);                                      \
-    ra0 = X6T_LDA(a_base + r0_ * p.lda);                                                                  \
-    ra1 = X6T_LDA(a_base + r1_ * p.lda);                                                                  \
+    const int64_t r0_ = in0 ? k_ + kr0 : kbeg;                                                            \
+    const int64_t r1_ = in1 ? k_ + kr1 : kbeg;                                                            \
+    ra0 = *reinterpret_cast<const float4*>(a_base + r0_ * p.lda);                                         \
+    ra1 = *reinterpret_cast<const float4*>(a_base + r1_ * p.lda);                                         \
     rb0 = *reinterpret_cast<const float4*>(b_base + r0_ * p.ldb);                                         \
     rb1 = *reinterpret_cast<const float4*>(b_base + r1_ * p.ldb);                                         \
   } while (0)
@@ -1077,35 +919,14 @@ __global__ __launch_bounds__(512) void gemm_x6t_kernel(GemmArgs p) {
     *reinterpret_cast<uint2*>((base) + X6_PLANE + (off)) = q1_;                                           \
     *reinterpret_cast<uint2*>((base) + 2 * X6_PLANE + (off)) = q2_;                                       \
   } while (0)
-#if GRL_X6T_WHATIF == 1 || GRL_X6T_WHATIF == 2
-  // GRL_X6T_WHATIF (timing diagnostics only, WRONG results): 1 = B (2 = and
-  // A) stored as its truncated top plane, no split (the ceiling of a
-  // pre-split g / Z); 3 = every step loads the split's first rows (cache
-  // hits: the price of Z's HBM stream); 5 = no barrier per step (races)
-#define X6T_SPLIT_B(v, base, off)                                                                         \
-  do {                                                                                                    \
-    const uint2 q_ = make_uint2(__builtin_amdgcn_perm(__float_as_uint((v).y), __float_as_uint((v).x), 0x07060302u), \
-                                __builtin_amdgcn_perm(__float_as_uint((v).w), __float_as_uint((v).z), 0x07060302u)); \
-    *reinterpret_cast<uint2*>((base) + (off)) = q_;                                                       \
-    *reinterpret_cast<uint2*>((base) + X6_PLANE + (off)) = q_;                                            \
-    *reinterpret_cast<uint2*>((base) + 2 * X6_PLANE + (off)) = q_;                                        \
-  } while (0)
-#else
-#define X6T_SPLIT_B X6T_SPLIT
-#endif
-#if GRL_X6T_WHATIF == 2
-#define X6T_SPLIT_A X6T_SPLIT_B
-#else
-#define X6T_SPLIT_A X6T_SPLIT
-#endif
 #define X6T_STASH(st)                                                                                     \
   do {                                                                                                    \
     if (!in0) ra0 = rb0 = zero4; /* wave-uniform: only a split's last K16 step branches */                \
     if (!in1) ra1 = rb1 = zero4;                                                                          \
-    X6T_SPLIT_A(ra0, (st), st_off0);                                                                      \
-    X6T_SPLIT_A(ra1, (st), st_off1);                                                                      \
-    X6T_SPLIT_B(rb0, (st) + 3 * X6_PLANE, st_off0);                                                       \
-    X6T_SPLIT_B(rb1, (st) + 3 * X6_PLANE, st_off1);                                                       \
+    X6T_SPLIT(ra0, (st), st_off0);                                                                        \
+    X6T_SPLIT(ra1, (st), st_off1);                                                                        \
+    X6T_SPLIT(rb0, (st) + 3 * X6_PLANE, st_off0);                                                         \
+    X6T_SPLIT(rb1, (st) + 3 * X6_PLANE, st_off1);                                                         \
   } while (0)
 
   // this lane's transposed-read coordinates: k = 8h + ((lane & 15) >> 2),
@@ -1127,7 +948,7 @@ __global__ __launch_bounds__(512) void gemm_x6t_kernel(GemmArgs p) {
     if (nk > 1) X6T_LOAD(1);
   }
   __syncthreads();
-  if (U2) {
+  {
     const lds_u16* s3 = (const lds_u16*)smem;
     const int sx = (tk & 3) << 5;
     int oa[4], ob[2];
@@ -1162,9 +983,7 @@ __global__ __launch_bounds__(512) void gemm_x6t_kernel(GemmArgs p) {
         X6T_STASH(smem + (S ^ 1) * X6_STAGE);  // the other stage: last read in step t-1
         if (t + 2 < nk) X6T_LOAD(t + 2);
       }
-#if GRL_X6T_WHATIF != 5  // 5: timing only, no barrier (races)
       __syncthreads();
-#endif
     };
     int64_t t = 0;
     for (; t + 1 < nk; t += 2) {
@@ -1172,34 +991,6 @@ __global__ __launch_bounds__(512) void gemm_x6t_kernel(GemmArgs p) {
       step(t + 1, std::integral_constant<int, 1>{});
     }
     if (t < nk) step(t, std::integral_constant<int, 0>{});
-  } else
-  for (int64_t t = 0; t < nk; ++t) {
-    const uint16_t* cur = smem + (t & 1) * X6_STAGE;
-    bf16x8_t a_[4][3], b_[2][3];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int q = 0; q < 3; ++q) a_[i][q] = tr_pair(cur + q * X6_PLANE, tk, wm * 128 + i * 32 + tc);
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int q = 0; q < 3; ++q) b_[j][q] = tr_pair(cur + (3 + q) * X6_PLANE, tk, wn * 64 + j * 32 + tc);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_[i][2], b_[j][0], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_[i][1], b_[j][1], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_[i][0], b_[j][2], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_[i][1], b_[j][0], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_[i][0], b_[j][1], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_[i][0], b_[j][0], acc[i][j], 0, 0, 0);
-      }
-    if (t + 1 < nk) {
-      X6T_STASH(smem + ((t + 1) & 1) * X6_STAGE);  // the other stage: last read in step t-1
-      if (t + 2 < nk) X6T_LOAD(t + 2);
-    }
-    __syncthreads();
   }
 #undef X6T_LOAD
 #undef X6T_SPLIT
@@ -1221,10 +1012,7 @@ __global__ __launch_bounds__(512) void gemm_x6t_kernel(GemmArgs p) {
 
 bool al16(const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; }
 
-#ifndef GRL_GEMM_BK
-#define GRL_GEMM_BK 32
-#endif
-constexpr int GEMM_BK = GRL_GEMM_BK;
+constexpr int GEMM_BK = 32;
 
 template <bool A_KC, bool B_KC, int EPI, bool CHUNKED = false>
 int launch_gemm(GemmArgs a, int splits, bool aligned, hipStream_t st) {
@@ -1297,17 +1085,9 @@ size_t small_ws_bytes(int64_t M, int64_t N, int64_t K) {
   return s > 1 ? (size_t)s * (size_t)M * (size_t)N * 4 + 256 : 0;
 }
 
-// Large-tile path selection.  GRL_GEMM_BIG=0 disables it (A/B aid).
-bool big_enabled() {
-  static const bool v = [] {
-    const char* e = getenv("GRL_GEMM_BIG");
-    return !(e && e[0] == '0');
-  }();
-  return v;
-}
-
+// Large-tile path selection (the fp32 fallback when the x6 path is off).
 bool big_ok(const GemmArgs& a, bool aligned) {
-  return big_enabled() && aligned && !a.Amask && !a.Bmask && a.K % LP_K == 0 && a.M >= 4 && a.N >= 4 &&
+  return aligned && !a.Amask && !a.Bmask && a.K % LP_K == 0 && a.M >= 4 && a.N >= 4 &&
          2.0 * (double)a.M * (double)a.N * (double)a.K >= 1.6e10;
 }
 
@@ -1376,21 +1156,10 @@ int launch_x6_gemm(GemmArgs a, const uint16_t* planes, hipStream_t st) {
   a.k_per_split = a.K;
   GRL_CHECK_ARG(a.mt * a.nt < 2147483647LL, "gemm: grid too large");
   const dim3 grid((unsigned)(a.mt * a.nt));
-  const bool il = x6_interleave();
   if (a.bias || a.relu)
-    if (x6_stagger())
-      hipLaunchKernelGGL((gemm_x6_kernel<EPI_BIAS, true>), grid, dim3(512), 0, st, a, planes, Np);
-    else if (il)
-      hipLaunchKernelGGL((gemm_x6_kernel<EPI_BIAS, false, true>), grid, dim3(512), 0, st, a, planes, Np);
-    else
-      hipLaunchKernelGGL(gemm_x6_kernel<EPI_BIAS>, grid, dim3(512), 0, st, a, planes, Np);
+    hipLaunchKernelGGL(gemm_x6_kernel<EPI_BIAS>, grid, dim3(512), 0, st, a, planes, Np);
   else
-    if (x6_stagger())
-      hipLaunchKernelGGL((gemm_x6_kernel<EPI_STORE, true>), grid, dim3(512), 0, st, a, planes, Np);
-    else if (il)
-      hipLaunchKernelGGL((gemm_x6_kernel<EPI_STORE, false, true>), grid, dim3(512), 0, st, a, planes, Np);
-    else
-      hipLaunchKernelGGL(gemm_x6_kernel<EPI_STORE>, grid, dim3(512), 0, st, a, planes, Np);
+    hipLaunchKernelGGL(gemm_x6_kernel<EPI_STORE>, grid, dim3(512), 0, st, a, planes, Np);
   GRL_LAUNCH_CHECK();
   return GRL_OK;
 }
@@ -1706,13 +1475,12 @@ bool x6t_shape_ok(int64_t M, int64_t K, int64_t C) {  // M nodes, K = rows of dW
 
 // K splits of the x6t dW: at most two 256 x 256 workgroups per CU (one is
 // resident per CU at 96 KB of LDS, so the grid runs in two full rounds rather
-// than two and a sliver), >= 16 K16 steps each
-#ifndef GRL_X6T_ROUNDS
-#define GRL_X6T_ROUNDS 2
-#endif
+// than two and a sliver), >= 16 K16 steps each (1, 3 and 4 rounds were
+// measured slower, profiles/r04_ab_dw_split_whatif.txt)
+constexpr int64_t X6T_ROUNDS = 2;
 int x6t_splits(int64_t M, int64_t K, int64_t C) {
   const int64_t tiles = ceil_div(K, LB_M) * ceil_div(C, LB_N);
-  int64_t s = (GRL_X6T_ROUNDS * (int64_t)device_cu_count()) / tiles;
+  int64_t s = (X6T_ROUNDS * (int64_t)device_cu_count()) / tiles;
   s = std::min<int64_t>(s, ceil_div(M, 16 * X6_K));
   return (int)std::max<int64_t>(1, std::min<int64_t>(s, 512));
 }
@@ -1798,14 +1566,10 @@ extern "C" int grl_linear_bwd_weight(const float* Z, int64_t ldz, const float* g
     a.inner_n = 0;
     GRL_CHECK_ARG(a.mt * a.nt * a.zt < 2147483647LL, "gemm: grid too large");
     const dim3 grid((unsigned)(a.mt * a.nt * a.zt));
-    const bool u2 = x6t_u2();
-    if (used > 1) {
-      if (u2) hipLaunchKernelGGL((gemm_x6t_kernel<EPI_SLAB, true>), grid, dim3(512), 0, st, a);
-      else hipLaunchKernelGGL((gemm_x6t_kernel<EPI_SLAB, false>), grid, dim3(512), 0, st, a);
-    } else {
-      if (u2) hipLaunchKernelGGL((gemm_x6t_kernel<EPI_STORE, true>), grid, dim3(512), 0, st, a);
-      else hipLaunchKernelGGL((gemm_x6t_kernel<EPI_STORE, false>), grid, dim3(512), 0, st, a);
-    }
+    if (used > 1)
+      hipLaunchKernelGGL(gemm_x6t_kernel<EPI_SLAB>, grid, dim3(512), 0, st, a);
+    else
+      hipLaunchKernelGGL(gemm_x6t_kernel<EPI_STORE>, grid, dim3(512), 0, st, a);
     GRL_LAUNCH_CHECK();
   } else {
     const int splits = pick_splits(K, C, M);

@@ -89,19 +89,6 @@ __device__ __forceinline__ void vstore(float* p, const float& v) {
 #endif
 }
 
-// GRL_SPMM_WIDE_U=8 (read on every launch): whole 2 KB rows (F in (256, 512])
-// issued 8 at a time instead of 4 (more bytes in flight, fewer waves).
-int wide_rows_in_flight() {
-  const char* e = getenv("GRL_SPMM_WIDE_U");
-  return e && e[0] == '8' ? 8 : 4;
-}
-
-// GRL_SPMM_PAIR=0 (read on every launch) sends narrow forward rows to the
-// whole-row kernel instead of spmm_pair_kernel (A/B aid and tests).
-bool pair_rows_enabled() {
-  const char* e = getenv("GRL_SPMM_PAIR");
-  return !(e && e[0] == '0');
-}
 
 // Whole-row (F <= 256) gathers in flight per wave (A/B builds: -DGRL_SPMM_U=n).
 #ifndef GRL_SPMM_U
@@ -649,7 +636,7 @@ int launch_spmm(int64_t num_rows, int64_t self_rows, int S, int hs, const int32_
                          zseg, de, sp);                                                                    \
   } while (0)
   if (sh.vec == 4) {
-    if (sh.nv == 1 && F <= 128 && !(BWD && accum) && pair_rows_enabled()) {
+    if (sh.nv == 1 && F <= 128 && !(BWD && accum)) {
       // narrow rows (column slices of a pipelined halo): two edges per gather instruction
       if (v)
         hipLaunchKernelGGL((spmm_pair_kernel<8, true, BWD>), grid, block, 0, stream, num_rows, S, hs, ptr, idx, vals,
@@ -660,9 +647,7 @@ int launch_spmm(int64_t num_rows, int64_t self_rows, int S, int hs, const int32_
                            self_rows);
     } else if (sh.nv == 1) {
       if (v) GRL_SPMM_LAUNCH(4, 1, GRL_SPMM_U, true); else GRL_SPMM_LAUNCH(4, 1, GRL_SPMM_U, false);
-    } else if (!BWD && wide_rows_in_flight() == 8) {  // A/B aid: twice the whole rows in flight per wave
-      if (v) GRL_SPMM_LAUNCH(4, 2, 8, true); else GRL_SPMM_LAUNCH(4, 2, 8, false);
-    } else {
+    } else {  // whole 2 KB rows (F in (256, 512]) 4 at a time (8 in flight measured no faster, round 4)
       if (v) GRL_SPMM_LAUNCH(4, 2, 4, true); else GRL_SPMM_LAUNCH(4, 2, 4, false);
     }
   } else {

@@ -5,7 +5,7 @@
 # chained as with &&).  Usage: tools/gpu_session.sh STEP...
 #   steps: tests smoke bench bench_extras bench_drop bench_c5 bench_c5s prof_bench prof_fwd prof_bwd
 #          prof_linear prof_layer prof_attn prof_c1 pmc_fwd_fetch pmc_fwd_write pmc_list pmc_linear_mfma
-#          pmc_fwd_tlb pmc_c4_tlb; round 4: ab_dw_u2 ab_attn_hu tests_r4 pmc_infer_l2 pmc_wide_mfma prof_wide
+#          pmc_fwd_tlb pmc_c4_tlb; round 4: ab_attn_hu tests_r4 pmc_infer_l2 pmc_wide_mfma prof_wide
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
 OUT=gpurun_out
@@ -76,7 +76,6 @@ for step in "$@"; do
                   SQ_LDS_CMD_FIFO_FULL SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_WAIT_INST_ANY SQ_INSTS_VALU_MFMA_MOPS_BF16 \
                   --kernel-trace -d "$OUT/pmc_x6_b" -o run --output-format csv \
                   -- python bench.py --only linear --steps 5 --warmup 1 ;;
-    probe_slices) run probe_slices 300 python tools/probe_slices.py ;;
     tests_dist) run pytest_gpu_dist 600 python -u -m pytest tests/test_gpu_dist.py -m gpu -v -rf --timeout 300 \
                   --timeout-method thread ;;
     tests_configs) run pytest_gpu_configs 1000 python -u -m pytest tests/test_gpu_configs.py -m gpu -v -s -rf \
@@ -100,7 +99,6 @@ for step in "$@"; do
     pmc_c5_fetch) run pmc_c5_fetch 600 rocprofv3 --pmc FETCH_SIZE TCC_HIT_sum --kernel-trace -d "$OUT/pmc_c5_fetch" \
                   -o run --output-format csv -- python bench.py --workload C5 --only fwd --steps 3 --warmup 1 ;;
     probe_cumask) run probe_cumask 400 python tools/probe_cumask.py ;;
-    probe_c5) run probe_c5 600 python tools/probe_c5.py ;;
     tests_relabel) run pytest_gpu_relabel 300 python -u -m pytest tests/test_gpu_relabel.py -m gpu -v -rf \
                   --timeout 240 --timeout-method thread ;;
     bench_c5full) run bench_c5full 900 python bench.py --workload C5 --steps 5 --warmup 2 ;;
@@ -110,10 +108,6 @@ for step in "$@"; do
                   --output-format csv -- python bench.py --workload C5 --only fwd --steps 3 --warmup 1 ;;
     prof_c5b) run prof_c5b 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c5b" -o run --output-format csv \
                   -- python bench.py --workload C5 --only fwd --steps 5 --warmup 1 ;;
-    probe_stagger) run probe_stagger 400 python tools/probe_stagger.py ;;
-    pmc_x6_stagger) export GRL_X6_STAGGER=1; run pmc_x6_stagger 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES \
-                  GRBM_GUI_ACTIVE SQ_BUSY_CU_CYCLES --kernel-trace -d "$OUT/pmc_x6_stagger" -o run --output-format csv \
-                  -- python bench.py --only linear --steps 5 --warmup 1; unset GRL_X6_STAGGER ;;
     probe_contig) run probe_contig 300 python tools/probe_contig.py ;;
     ab_ws_status) run ab_ws_status 900 tools/ab_ws_status.sh r2gc ;;
     tests_warper) run pytest_gpu_warper 600 python -u -m pytest tests/test_gpu_warper.py tests/test_gpu_graph_capture.py \
@@ -144,7 +138,6 @@ for step in "$@"; do
     ab_fused_dq) rm -f gpurun_out/ab_fused_dq.log; run ab_fused_dq 900 tools/ab_fused_dq.sh ;;
     prof_attn_fused) run prof_attn_fused 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_attn_fused" -o run \
                   --output-format csv -- python tools/probe_attn.py 100000 ;;
-    ab_dw_u2) rm -f gpurun_out/ab_dw_env.log; run ab_dw_u2 300 tools/ab_dw_env.sh GRL_X6T_U2 ;;
     ab_attn_hu) export ATTN_N="100000"; rm -f gpurun_out/ab_attn_lib.log; run ab_attn_hu 500 tools/ab_attn_lib.sh attn_b20 attn_pin0 attn_hu0 attn_r3 ;;
     tests_r4) run pytest_gpu_r4 900 python -u -m pytest tests/test_gpu_attention.py tests/test_gpu_procedure_golden.py \
                   tests/test_gpu_warper.py tests/test_gpu_dp.py tests/test_gpu_sharded_model.py tests/test_gpu_rccl.py \
