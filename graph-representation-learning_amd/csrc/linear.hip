@@ -1010,200 +1010,6 @@ __global__ __launch_bounds__(512) void gemm_x6t_kernel(GemmArgs p) {
   }
 }
 
-// ---------------------------------------------------------------------------
-// dW = Z^T g on v_mfma_f32_16x16x32_bf16 (gemm_x6t16_kernel).  The same x6
-// arithmetic as gemm_x6t_kernel (three exact bf16 planes per operand, six
-// partial products, small terms first) on the 16x16x32 shape, which holds a
-// higher clock than 32x32x16 under load at equal cycles per FLOP
-// (MI355X_MICROARCH.md, DVFS item 7: 1.12-1.15x in bare MFMA loops).  Each
-// MFMA consumes 32 k (nodes), so a step stages 32 node rows: a 128 (feature
-// columns) x 256 (C) block tile keeps the two stages at 72 KB each and every
-// Z element read once (the M tiles partition Z's columns; g, the smaller
-// operand, is re-read per M tile from L2).  8 waves of 64 x 64 (4 x 4 MFMA
-// blocks, 64 accumulators).  Planes lie [32 k][W columns] with the 32-byte
-// chunk c of row r at c ^ f(r), f(r) = (r & 3) | ((r >> 3) & 1) << 2: the
-// transposed reads (ds_read_b64_tr_b16: per 16-lane group 4 k x 16 columns,
-// the two groups of a 32-lane half 8 rows apart) hit 8 distinct chunk slots
-// of one 256-byte bank window -- conflict-free.
-constexpr int T16_BM = 128, T16_BN = 256, T16_K = 32;
-constexpr int T16_APL = T16_K * T16_BM;                   // bf16 per A plane (8 KB)
-constexpr int T16_BPL = T16_K * T16_BN;                   // bf16 per B plane (16 KB)
-constexpr int T16_STAGE = 3 * T16_APL + 3 * T16_BPL;      // 72 KB
-
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ int t16_sw(int r) { return (r & 3) | (((r >> 3) & 1) << 2); }
-template <int W>
-__device__ __forceinline__ int t16_off(int r, int c) {
-  return r * W + ((((c >> 4) ^ t16_sw(r)) << 4) | (c & 15));
-}
-// rows k0..k0+3 and k0+4..k0+7 of a 16-column block, transposed: lane i of a
-// 16-lane group gets column i, k = 8 g + 0..7 (the 16x16x32 operand)
-template <int W>
-__device__ __forceinline__ bf16x8_t t16_frag(const lds_u16* p0) {
-  typedef __attribute__((address_space(3))) i16x4_t lds_v4;
-  const i16x4_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)p0);
-  const i16x4_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4*)(p0 + 4 * W));
-  typedef short i16x8_t __attribute__((ext_vector_type(8)));
-  const i16x8_t v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-  return __builtin_bit_cast(bf16x8_t, v);
-}
-
-// IL: the next stage's stash interleaved with this step's MFMA groups (two
-// register sets: step t loads rows t+2 into the set step t's rows left, at
-// the start of the step, while the set holding rows t+1 is split into the
-// other stage between the column blocks' MFMAs).
-template <int EPI, bool IL = false>
-__global__ __launch_bounds__(512) void gemm_x6t16_kernel(GemmArgs p) {
-  __shared__ __attribute__((aligned(16))) uint16_t smem[2 * T16_STAGE];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 2, wn = wave & 3;
-  int64_t mi, ni, zi;
-  tile_of(p, mi, ni, zi);
-  const int64_t m0 = mi * T16_BM, n0 = ni * T16_BN;
-  const int64_t kbeg = zi * p.k_per_split;
-  const int64_t kend = min(p.K, kbeg + p.k_per_split);
-  const int64_t nk = kend > kbeg ? (kend - kbeg + T16_K - 1) / T16_K : 0;
-
-  // A staging (128 columns of Z): float4 f = tid + 512 i: row (f >> 5) = (tid >> 5) + 16 i, 4 columns at
-  // (tid & 31) * 4.  B staging (256 columns of g): row (f >> 6) = wave + 8 i (wave-uniform), (tid & 63) * 4
-  const int ar = tid >> 5, acol = (tid & 31) * 4;
-  const int br = __builtin_amdgcn_readfirstlane(wave), bcol = (tid & 63) * 4;
-  const float* __restrict__ a_base = p.A + min<int64_t>(m0 + acol, p.M - 4);
-  const float* __restrict__ b_base = p.B + min<int64_t>(n0 + bcol, p.N - 4);
-  int sa[2], sb[4];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) sa[i] = t16_off<T16_BM>(ar + 16 * i, acol);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) sb[i] = 3 * T16_APL + t16_off<T16_BN>(br + 8 * i, bcol);
-  constexpr int NSET = IL ? 2 : 1;
-  float4 ra[NSET][2], rb[NSET][4];
-  bool ia[NSET][2], ib[NSET][4];
-  const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
-  // rows past the split's end load clamped (from kbeg) and are zeroed when stashed (gemm_x6t_kernel)
-  auto load = [&](int64_t t, auto set) {
-    constexpr int X = decltype(set)::value;
-    const int64_t k_ = kbeg + t * T16_K;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      ia[X][i] = k_ + ar + 16 * i < kend;
-      ra[X][i] = *reinterpret_cast<const float4*>(a_base + (ia[X][i] ? k_ + ar + 16 * i : kbeg) * p.lda);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      ib[X][i] = k_ + br + 8 * i < kend;
-      rb[X][i] = *reinterpret_cast<const float4*>(b_base + (ib[X][i] ? k_ + br + 8 * i : kbeg) * p.ldb);
-    }
-  };
-  auto put = [&](uint16_t* st, int off, int plane_elems, float4 v) {
-    uint2 q0, q1, q2;
-    split3(v, q0, q1, q2);
-    *reinterpret_cast<uint2*>(st + off) = q0;
-    *reinterpret_cast<uint2*>(st + plane_elems + off) = q1;
-    *reinterpret_cast<uint2*>(st + 2 * plane_elems + off) = q2;
-  };
-  // part pt of the stash of register set X: 0 = A's two rows, 1 / 2 = two of B's four
-  auto stash_part = [&](uint16_t* st, auto set, int pt) {
-    constexpr int X = decltype(set)::value;
-    if (pt == 0) {
-#pragma unroll
-      for (int i = 0; i < 2; ++i) put(st, sa[i], T16_APL, ia[X][i] ? ra[X][i] : zero4);
-    } else {
-#pragma unroll
-      for (int i = 2 * (pt - 1); i < 2 * pt; ++i) put(st, sb[i], T16_BPL, ib[X][i] ? rb[X][i] : zero4);
-    }
-  };
-  auto stash = [&](uint16_t* st, auto set) {
-    stash_part(st, set, 0);
-    stash_part(st, set, 1);
-    stash_part(st, set, 2);
-  };
-  using Set0 = std::integral_constant<int, 0>;
-
-  // this lane's transposed reads: block rows 8 g + q (q = (lane & 15) >> 2), columns 4 (lane & 3) of a block
-  const int g = lane >> 4, tq = 8 * g + ((lane & 15) >> 2), tc = 4 * (lane & 3);
-  int oa[4], ob[4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i) oa[i] = t16_off<T16_BM>(tq, wm * 64 + i * 16 + tc);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) ob[j] = 3 * T16_APL + t16_off<T16_BN>(tq, wn * 64 + j * 16 + tc);
-
-  f32x4 acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  if (nk > 0) {
-    load(0, Set0{});
-    stash(smem, Set0{});
-    if (nk > 1) load(1, std::integral_constant<int, IL ? 1 : 0>{});
-  }
-  __syncthreads();
-  const lds_u16* s3 = (const lds_u16*)smem;
-  auto step = [&](int64_t t, auto stage) {
-    constexpr int S = decltype(stage)::value;
-    // IL: rows t+1 sit in set (t+1) & 1 = S ^ 1; rows t+2 go to set S (whose rows t were stashed in step t-1)
-    using Next = std::integral_constant<int, IL ? (S ^ 1) : 0>;
-    using Cur = std::integral_constant<int, IL ? S : 0>;
-    if constexpr (IL) {
-      if (t + 2 < nk) load(t + 2, Cur{});
-    }
-    const lds_u16* cur = s3 + S * T16_STAGE;
-    bf16x8_t a_[4][3];
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int q = 0; q < 3; ++q) a_[i][q] = t16_frag<T16_BM>(cur + q * T16_APL + oa[i]);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      bf16x8_t b_[3];
-#pragma unroll
-      for (int q = 0; q < 3; ++q) b_[q] = t16_frag<T16_BN>(cur + q * T16_BPL + ob[j]);
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_[i][2], b_[0], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_[i][1], b_[1], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_[i][0], b_[2], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_[i][1], b_[0], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_[i][0], b_[1], acc[i][j], 0, 0, 0);
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a_[i][0], b_[0], acc[i][j], 0, 0, 0);
-      }
-      if constexpr (IL) {  // a third of the next stage's split after each of the first three column blocks
-        if (j < 3 && t + 1 < nk) stash_part(smem + (S ^ 1) * T16_STAGE, Next{}, j);
-      }
-    }
-    if constexpr (!IL) {
-      if (t + 1 < nk) {
-        stash(smem + (S ^ 1) * T16_STAGE, Next{});  // the other stage: last read in step t-1
-        if (t + 2 < nk) load(t + 2, Next{});
-      }
-    }
-    __syncthreads();
-  };
-  int64_t t = 0;
-  for (; t + 1 < nk; t += 2) {
-    step(t, std::integral_constant<int, 0>{});
-    step(t + 1, std::integral_constant<int, 1>{});
-  }
-  if (t < nk) step(t, std::integral_constant<int, 0>{});
-
-  // D of a 16 x 16 block: lane l holds column l & 15, rows 4 (l >> 4) + v
-  float* Cz = p.C + (EPI == EPI_SLAB ? zi * p.M * p.ldc : 0);
-#pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int64_t gn = n0 + wn * 64 + j * 16 + (lane & 15);
-    if (gn >= p.N) continue;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int64_t gm = m0 + wm * 64 + i * 16 + 4 * (lane >> 4) + v;
-        if (gm < p.M) Cz[gm * p.ldc + gn] = acc[i][j][v];
-      }
-  }
-}
-
 bool al16(const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; }
 
 constexpr int GEMM_BK = 32;
@@ -1679,29 +1485,10 @@ int x6t_splits(int64_t M, int64_t K, int64_t C) {
   return (int)std::max<int64_t>(1, std::min<int64_t>(s, 512));
 }
 
-// the 16x16x32 form (gemm_x6t16_kernel, 128 x 256 tiles, K32 steps): the same rule
-int x6t16_splits(int64_t M, int64_t K, int64_t C) {
-  const int64_t tiles = ceil_div(K, T16_BM) * ceil_div(C, T16_BN);
-  int64_t s = (X6T_ROUNDS * (int64_t)device_cu_count()) / tiles;
-  s = std::min<int64_t>(s, ceil_div(M, 16 * T16_K));
-  return (int)std::max<int64_t>(1, std::min<int64_t>(s, 512));
-}
-
-// GRL_X6T16 (read per call; A/B aid until measured): 1 = the 16x16x32 dW
-// kernel, 2 = the same with the interleaved stash; unset / 0 = 32x32x16
-bool x6t16_enabled() {
-  const char* e = getenv("GRL_X6T16");
-  return e && (e[0] == '1' || e[0] == '2');
-}
-bool x6t16_il() {
-  const char* e = getenv("GRL_X6T16");
-  return e && e[0] == '2';
-}
-
 // slabs reserved in the dW workspace: enough for whichever path runs
 int wgt_slab_splits(int64_t M, int64_t K, int64_t C) {
   int s = pick_splits(K, C, M);
-  if (x6t_shape_ok(M, K, C)) s = std::max(s, std::max(x6t_splits(M, K, C), x6t16_splits(M, K, C)));
+  if (x6t_shape_ok(M, K, C)) s = std::max(s, x6t_splits(M, K, C));
   return s;
 }
 
@@ -1769,34 +1556,23 @@ extern "C" int grl_linear_bwd_weight(const float* Z, int64_t ldz, const float* g
   const bool aligned = al16(Z) && al16(g) && (!relu_out || al16(relu_out)) && ldz % 4 == 0 && C % 4 == 0 && K % 4 == 0;
   int used;
   if (aligned && !relu_out && x6t_shape_ok(M, K, C)) {  // large M: fp32 on the bf16 matrix cores
-    const bool t16 = x6t16_enabled();
-    const int splits = t16 ? x6t16_splits(M, K, C) : x6t_splits(M, K, C);
-    const int kq = t16 ? T16_K : X6_K;
-    const bool il = t16 && x6t16_il();
+    // (a v_mfma_f32_16x16x32_bf16 form -- 128 x 256 tiles, 32-deep stages, conflict-free transposed reads,
+    // with or without the next stage's split interleaved -- was 10 % slower at C3: 5.31 / 5.38 vs 4.81 ms,
+    // profiles/r05_ab_dw16.txt; 16 x 16 fragments cost a third more LDS reads per flop here)
+    const int splits = x6t_splits(M, K, C);
     a.C = splits > 1 ? slab : dW;
-    a.k_per_split = ceil_div(ceil_div(M, splits), kq) * kq;
+    a.k_per_split = ceil_div(ceil_div(M, splits), X6_K) * X6_K;
     used = (int)ceil_div(M, a.k_per_split);
-    a.mt = ceil_div(a.M, t16 ? T16_BM : LB_M);
-    a.nt = ceil_div(a.N, t16 ? T16_BN : LB_N);
+    a.mt = ceil_div(a.M, LB_M);
+    a.nt = ceil_div(a.N, LB_N);
     a.zt = used;
     a.inner_n = 0;
     GRL_CHECK_ARG(a.mt * a.nt * a.zt < 2147483647LL, "gemm: grid too large");
     const dim3 grid((unsigned)(a.mt * a.nt * a.zt));
-    if (t16 && il) {
-      if (used > 1)
-        hipLaunchKernelGGL((gemm_x6t16_kernel<EPI_SLAB, true>), grid, dim3(512), 0, st, a);
-      else
-        hipLaunchKernelGGL((gemm_x6t16_kernel<EPI_STORE, true>), grid, dim3(512), 0, st, a);
-    } else if (t16) {
-      if (used > 1)
-        hipLaunchKernelGGL(gemm_x6t16_kernel<EPI_SLAB>, grid, dim3(512), 0, st, a);
-      else
-        hipLaunchKernelGGL(gemm_x6t16_kernel<EPI_STORE>, grid, dim3(512), 0, st, a);
-    } else if (used > 1) {
+    if (used > 1)
       hipLaunchKernelGGL(gemm_x6t_kernel<EPI_SLAB>, grid, dim3(512), 0, st, a);
-    } else {
+    else
       hipLaunchKernelGGL(gemm_x6t_kernel<EPI_STORE>, grid, dim3(512), 0, st, a);
-    }
     GRL_LAUNCH_CHECK();
   } else {
     const int splits = pick_splits(K, C, M);
