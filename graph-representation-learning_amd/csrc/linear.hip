@@ -50,12 +50,6 @@ struct GemmArgs {
   // launched as one dimension; inner_n: which tile index runs fastest
   int64_t mt, nt, zt;
   int inner_n;
-  // M-invariant fp32 path (run_output_gemm): K is summed in fixed chunks of
-  // k_chunk_tiles K tiles each, the chunk sums added in chunk order --
-  // across K splits (one chunk per split, slabs added in split order) or
-  // inside one workgroup (CHUNKED gemm_kernel).  Either way every output
-  // element is the same fp32 operations whatever M is.
-  int64_t k_chunk_tiles;
   // rows the x6-vs-fp32 path choice is made for (0: M): a node-range shard
   // passes the whole graph's row count, so it takes the one-GPU call's path
   int64_t path_rows;
@@ -162,7 +156,7 @@ struct Operand {
 
 // A(m, k): A_KC ? A[m*lda + k] : A[k*lda + m]
 // B(k, n): B_KC ? B[n*ldb + k] : B[k*ldb + n]
-template <bool A_KC, bool B_KC, int EPI, bool ALIGNED, bool MASK_A, bool MASK_B, int BK, bool CHUNKED = false>
+template <bool A_KC, bool B_KC, int EPI, bool ALIGNED, bool MASK_A, bool MASK_B, int BK>
 __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs p) {
   using OA = Operand<A_KC, ALIGNED, MASK_A, BK>;
   using OB = Operand<B_KC, ALIGNED, MASK_B, BK>;
@@ -196,14 +190,13 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs p) {
   ob.row0 = n0;
   const bool rows_in = ALIGNED && (m0 + BM <= p.M) && (n0 + BN <= p.N);
 
-  f32x16 acc[2][2], tot[2][2];
+  f32x16 acc[2][2];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = tot[i][j][r] = 0.0f;
-  int64_t kt = 0;  // CHUNKED: K tiles into the current chunk
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
 
   auto mma_step = [&](const float* As, const float* Bs) {
 #pragma unroll
@@ -244,27 +237,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs p) {
       ob.fetch(tid, kn, kend, in);
     }
     mma_step(smem, smem + OA::lds_floats());
-    if constexpr (CHUNKED) {  // chunk done: add its sum to the total, in chunk order (= the split-K slabs)
-      if (++kt == p.k_chunk_tiles || kn >= kend) {
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              tot[i][j][r] += acc[i][j][r];
-              acc[i][j][r] = 0.0f;
-            }
-        kt = 0;
-      }
-    }
     __syncthreads();
-  }
-  if constexpr (CHUNKED) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) acc[i][j] = tot[i][j];
   }
 
   // ---- epilogue: C/D map col = lane&31, row = (r&3) + 8(r>>2) + 4h --------
@@ -1014,7 +987,7 @@ bool al16(const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; }
 
 constexpr int GEMM_BK = 32;
 
-template <bool A_KC, bool B_KC, int EPI, bool CHUNKED = false>
+template <bool A_KC, bool B_KC, int EPI>
 int launch_gemm(GemmArgs a, int splits, bool aligned, hipStream_t st) {
   if (a.M == 0 || a.N == 0) return GRL_OK;
   a.mt = ceil_div(a.M, BM);
@@ -1027,7 +1000,7 @@ int launch_gemm(GemmArgs a, int splits, bool aligned, hipStream_t st) {
   const dim3 grid((unsigned)(a.mt * a.nt * a.zt));
   const bool ma = a.Amask != nullptr, mb = a.Bmask != nullptr;
 #define GRL_GEMM(AL, MA, MB) \
-  hipLaunchKernelGGL((gemm_kernel<A_KC, B_KC, EPI, AL, MA, MB, GEMM_BK, CHUNKED>), grid, dim3(256), 0, st, a)
+  hipLaunchKernelGGL((gemm_kernel<A_KC, B_KC, EPI, AL, MA, MB, GEMM_BK>), grid, dim3(256), 0, st, a)
   if (aligned) {
     if (ma) GRL_GEMM(true, true, false); else if (mb) GRL_GEMM(true, false, true); else GRL_GEMM(true, false, false);
   } else {
@@ -1047,17 +1020,18 @@ int pick_splits(int64_t M, int64_t N, int64_t K) {
 }
 
 // The output-stationary fp32 GEMM (forward, data gradient; the x6 path's
-// fallback) sums K in fixed chunks whose size depends on K alone: at most
-// 16 chunks of whole K tiles.  Small M (tiles that cannot fill the chip: a
-// 74-node page is one 128-row tile) runs one chunk per K split into fp32
-// slabs that a second pass adds in chunk order -- a lone workgroup walking
-// all of K is bound by load latency, not by the matrix cores; larger M runs
-// unsplit, each workgroup adding its chunk sums in the same order
-// (gemm_kernel<..., CHUNKED>).  Both give every element the same operations,
-// so a row's result does not depend on M: a node-range shard's rows equal
-// the whole graph's.
+// fallback) sums K in fixed chunks whose size depends on K alone -- at most
+// 16 chunks of whole K tiles -- one chunk per K split into fp32 slabs that a
+// second pass adds in chunk order with the bias / ReLU epilogue.  So every
+// element is the same fp32 operations whatever M is, and a node-range
+// shard's rows equal the whole graph's.  Small M gets the
+// chunks' parallelism (a lone workgroup walking all of K is bound by load
+// latency: a 74-node page is one 128-row tile); M whose slabs would exceed
+// kFp32SlabCap runs in row blocks that fit.  (Summing the chunks inside one
+// workgroup instead -- a second accumulator set -- cost 1 wave per SIMD at
+// 225-251 VGPRs: the classifier's 100k rows ran 5x slower than hipBLASLt.)
 constexpr int64_t kFp32MaxChunks = 16;
-constexpr size_t kFp32SlabCap = (size_t)256 << 20;  // slab bytes above which the unsplit form runs
+constexpr size_t kFp32SlabCap = (size_t)256 << 20;
 
 int64_t fp32_chunk_tiles(int64_t K) {
   const int64_t tiles = std::max<int64_t>(1, ceil_div(K, GEMM_BK));
@@ -1068,13 +1042,18 @@ int fp32_chunks(int64_t K) {
   return (int)ceil_div(std::max<int64_t>(1, ceil_div(K, GEMM_BK)), fp32_chunk_tiles(K));
 }
 
-// K splits of the fp32 output GEMM: the chunk count (slabs) or 1 (unsplit)
+// rows per slab pass: all of M, or the BM-multiple whose slabs fit kFp32SlabCap
+int64_t fp32_block_rows(int64_t M, int64_t N, int64_t K) {
+  const int64_t per_row = (int64_t)fp32_chunks(K) * std::max<int64_t>(N, 1) * 4;
+  const int64_t cap = std::max<int64_t>(BM, (int64_t)kFp32SlabCap / per_row / BM * BM);
+  return std::min<int64_t>(M, cap);
+}
+
+// K splits of the fp32 output GEMM: the chunk count (1: one chunk, no slabs)
 int pick_splits_small(int64_t M, int64_t N, int64_t K) {
-  const int64_t tiles = ceil_div(M, BM) * ceil_div(N, BN);
-  const int s = fp32_chunks(K);
-  if (s <= 1 || tiles >= (int64_t)device_cu_count()) return 1;
-  if ((size_t)s * (size_t)M * (size_t)N * 4 > kFp32SlabCap) return 1;
-  return s;
+  (void)M;
+  (void)N;
+  return fp32_chunks(K);
 }
 
 // row blocks of the db column sum: ~64 rows each (>= 1 block, <= 1024)
@@ -1082,7 +1061,7 @@ int colsum_splits(int64_t M) { return (int)std::max<int64_t>(1, std::min<int64_t
 
 size_t small_ws_bytes(int64_t M, int64_t N, int64_t K) {
   const int s = pick_splits_small(M, N, K);
-  return s > 1 ? (size_t)s * (size_t)M * (size_t)N * 4 + 256 : 0;
+  return s > 1 ? (size_t)s * (size_t)fp32_block_rows(M, N, K) * (size_t)N * 4 + 256 : 0;
 }
 
 // Large-tile path selection (the fp32 fallback when the x6 path is off).
@@ -1186,28 +1165,38 @@ int run_output_gemm(GemmArgs a, bool aligned, const char* who, void* ws, size_t 
   const int splits = pick_splits_small(a.M, a.N, a.K);
   if (splits == 1) {
     a.k_per_split = std::max<int64_t>(a.K, 1);
-    a.k_chunk_tiles = fp32_chunk_tiles(a.K);
-    return a.bias || a.relu ? launch_gemm<A_KC, B_KC, EPI_BIAS, true>(a, 1, aligned, st)
-                            : launch_gemm<A_KC, B_KC, EPI_STORE, true>(a, 1, aligned, st);
+    return a.bias || a.relu ? launch_gemm<A_KC, B_KC, EPI_BIAS>(a, 1, aligned, st)
+                            : launch_gemm<A_KC, B_KC, EPI_STORE>(a, 1, aligned, st);
   }
   const size_t need = small_ws_bytes(a.M, a.N, a.K);
   if (!ws || ws_bytes < need) GRL_FAIL(GRL_E_WORKSPACE, "%s: workspace %zu < %zu", who, ws_bytes, need);
-  float* out = a.C;
+  float* const out = a.C;
   const int64_t ldo = a.ldc;
-  const float* bias = a.bias;
+  const float* const bias = a.bias;
   const int relu = a.relu;
+  const float* const A0 = a.A;
+  const float* const Amask0 = a.Amask;
+  const int64_t M = a.M;
+  const int64_t R = fp32_block_rows(M, a.N, a.K);
   a.C = static_cast<float*>(ws);
   a.ldc = a.N;
   a.bias = nullptr;
   a.relu = 0;
   a.k_per_split = fp32_chunk_tiles(a.K) * GEMM_BK;  // one chunk per split
   const int used = (int)ceil_div(a.K, a.k_per_split);
-  int rc = launch_gemm<A_KC, B_KC, EPI_SLAB>(a, used, aligned, st);
-  if (rc) return rc;
-  const int64_t n = a.M * a.N;
-  hipLaunchKernelGGL(slab_reduce_epi_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(n, 256), 4096)), dim3(256), 0,
-                     st, a.C, a.M, a.N, used, out, ldo, bias, relu);
-  GRL_LAUNCH_CHECK();
+  for (int64_t r0 = 0; r0 < M; r0 += R) {  // row blocks: the same chunks, so the same bits, as one pass
+    const int64_t rows = std::min<int64_t>(R, M - r0);
+    // A(m, k) = A_KC ? A[m * lda + k] : A[k * lda + m]: row m of the block is m + r0
+    a.A = A0 + (A_KC ? r0 * a.lda : r0);
+    a.Amask = Amask0 ? Amask0 + (A_KC ? r0 * a.lda : r0) : nullptr;
+    a.M = rows;
+    int rc = launch_gemm<A_KC, B_KC, EPI_SLAB>(a, used, aligned, st);
+    if (rc) return rc;
+    const int64_t n = rows * a.N;
+    hipLaunchKernelGGL(slab_reduce_epi_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(n, 256), 4096)), dim3(256),
+                       0, st, a.C, rows, a.N, used, out + r0 * ldo, ldo, bias, relu);
+    GRL_LAUNCH_CHECK();
+  }
   return GRL_OK;
 }
 
