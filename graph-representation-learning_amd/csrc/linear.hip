@@ -1169,7 +1169,16 @@ int run_output_gemm(GemmArgs a, bool aligned, const char* who, void* ws, size_t 
                             : launch_gemm<A_KC, B_KC, EPI_STORE>(a, 1, aligned, st);
   }
   const size_t need = small_ws_bytes(a.M, a.N, a.K);
-  if (!ws || ws_bytes < need) GRL_FAIL(GRL_E_WORKSPACE, "%s: workspace %zu < %zu", who, ws_bytes, need);
+  if (!ws || ws_bytes < need) {
+    // an x6-sized call whose operands turned out unaligned (its workspace was sized for W's planes):
+    // one pass over all of K (its rows' bits then follow this kernel, not the chunked form's)
+    if (ceil_div(a.M, BM) * ceil_div(a.N, BN) >= (int64_t)device_cu_count() && x6_path_ok(a.M, a.path_rows, a.N, a.K)) {
+      a.k_per_split = std::max<int64_t>(a.K, 1);
+      return a.bias || a.relu ? launch_gemm<A_KC, B_KC, EPI_BIAS>(a, 1, aligned, st)
+                              : launch_gemm<A_KC, B_KC, EPI_STORE>(a, 1, aligned, st);
+    }
+    GRL_FAIL(GRL_E_WORKSPACE, "%s: workspace %zu < %zu", who, ws_bytes, need);
+  }
   float* const out = a.C;
   const int64_t ldo = a.ldc;
   const float* const bias = a.bias;
@@ -1205,8 +1214,10 @@ int run_output_gemm(GemmArgs a, bool aligned, const char* who, void* ws, size_t 
 
 using namespace grl;
 
+// x6-sized calls need W's planes; the others the fp32 path's slabs (at most kFp32SlabCap)
 extern "C" size_t grl_linear_fwd_ex_workspace_size(int64_t M, int32_t K, int32_t C, int64_t path_rows) {
-  return M > 0 && K > 0 && C > 0 ? std::max(small_ws_bytes(M, C, K), x6_ws_bytes_p(M, path_rows, C, K)) : 0;
+  if (M <= 0 || K <= 0 || C <= 0) return 0;
+  return x6_path_ok(M, path_rows, C, K) ? x6_ws_bytes_p(M, path_rows, C, K) : small_ws_bytes(M, C, K);
 }
 
 extern "C" size_t grl_linear_fwd_workspace_size(int64_t M, int32_t K, int32_t C) {
@@ -1428,7 +1439,8 @@ extern "C" int grl_graphconv_fwd_train(const GrlTypedCsr* g, const float* X, int
 }
 
 extern "C" size_t grl_linear_bwd_data_workspace_size(int64_t M, int32_t K, int32_t C) {
-  return M > 0 && K > 0 && C > 0 ? std::max(small_ws_bytes(M, K, C), x6_ws_bytes(M, K, C)) : 0;
+  if (M <= 0 || K <= 0 || C <= 0) return 0;
+  return x6_shape_ok(M, K, C) ? x6_ws_bytes(M, K, C) : small_ws_bytes(M, K, C);
 }
 
 extern "C" int grl_linear_bwd_data(const float* g, const float* relu_out, const float* W, float* dZ, int64_t lddz,
