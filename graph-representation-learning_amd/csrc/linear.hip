@@ -85,16 +85,17 @@ __device__ __forceinline__ float4 masked(float4 v, float4 mk) {
   return v;
 }
 
-// One operand tile (ROWS x BK) staged as 1024*BK/32 float4 slots, SLOTS per
+// One operand tile (ROWS x BK) staged as ROWS*BK/4 float4 slots, SLOTS per
 // thread.  KC: image [row][k] (k contiguous, stride LDK); RC: image [k][row]
 // (row contiguous, stride LDR).  Global addresses are per-thread pointers
 // advanced by one K tile per step; interior tiles load with no per-element
 // branches (clamped + selected loads only on edge tiles).
-template <bool KC, bool ALIGNED, bool MASK, int BK>
+template <bool KC, bool ALIGNED, bool MASK, int BK, int ROWS = BM>
 struct Operand {
   static constexpr int LDK = BK + 4;
-  static constexpr int LDR = BM + 4;
-  static constexpr int SLOTS = BK / 8;  // (128 * BK / 4) / 256
+  static constexpr int LDR = ROWS + 4;
+  static constexpr int RQ = ROWS / 4;  // float4 slots per k row of the [k][row] image
+  static constexpr int SLOTS = ROWS * BK / 4 / 256;
   const float* base;
   const float* mask;
   int64_t ld, rows_total, row0;
@@ -106,12 +107,12 @@ struct Operand {
       row = row0 + idx / (BK / 4);
       kin = (idx % (BK / 4)) * 4;
     } else {
-      row = row0 + (idx % 32) * 4;
-      kin = idx / 32;
+      row = row0 + (idx % RQ) * 4;
+      kin = idx / RQ;
     }
   }
   __device__ __forceinline__ int lds_off(int idx) const {
-    return KC ? (idx / (BK / 4)) * LDK + (idx % (BK / 4)) * 4 : (idx / 32) * LDR + (idx % 32) * 4;
+    return KC ? (idx / (BK / 4)) * LDK + (idx % (BK / 4)) * 4 : (idx / RQ) * LDR + (idx % RQ) * 4;
   }
   __device__ __forceinline__ void fetch(int tid, int64_t k0, int64_t kend, bool interior) {
 #pragma unroll
@@ -145,24 +146,31 @@ struct Operand {
 #pragma unroll
     for (int it = 0; it < SLOTS; ++it) *reinterpret_cast<float4*>(&lds[lds_off(tid + it * 256)]) = reg[it];
   }
-  // fragment of row `row` (0..127 within the tile) for k = kk + 4h + s, s = 0..3
+  // fragment of row `row` (0..ROWS-1 within the tile) for k = kk + 4h + s, s = 0..3
   __device__ __forceinline__ static float4 frag(const float* lds, int row, int kk, int h) {
     if (KC) return *reinterpret_cast<const float4*>(&lds[row * LDK + kk + 4 * h]);
     const float* c = &lds[(kk + 4 * h) * LDR + row];
     return make_float4(c[0], c[LDR], c[2 * LDR], c[3 * LDR]);
   }
-  static constexpr int lds_floats() { return KC ? BM * LDK : BK * LDR; }
+  static constexpr int lds_floats() { return KC ? ROWS * LDK : BK * LDR; }
 };
 
 // A(m, k): A_KC ? A[m*lda + k] : A[k*lda + m]
 // B(k, n): B_KC ? B[n*ldb + k] : B[k*ldb + n]
-template <bool A_KC, bool B_KC, int EPI, bool ALIGNED, bool MASK_A, bool MASK_B, int BK>
+// TBN: the tile's columns, 128 (four 64 x 64 wave tiles) or 64 (four 64 x 32:
+// narrow outputs -- the classifier's 56, f/g/h's 160 -- compute half the
+// padding).  Every element's accumulation is the same either way (one
+// accumulator, k in the same order): the choice never changes bits.
+template <bool A_KC, bool B_KC, int EPI, bool ALIGNED, bool MASK_A, bool MASK_B, int BK, int TBN = BN>
 __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs p) {
   using OA = Operand<A_KC, ALIGNED, MASK_A, BK>;
-  using OB = Operand<B_KC, ALIGNED, MASK_B, BK>;
+  using OB = Operand<B_KC, ALIGNED, MASK_B, BK, TBN>;
+  constexpr int NJ = TBN / 64;  // 32-column accumulators per wave
+  constexpr int WN = 32 * NJ;   // wave tile columns
   constexpr int STAGE = OA::lds_floats() + OB::lds_floats();
-  __shared__ __attribute__((aligned(16))) float smem[STAGE];
-  static_assert(STAGE >= 4 * 64 * 32, "epilogue staging must fit the operand LDS");
+  constexpr int SMEM = STAGE > 4 * 64 * 32 ? STAGE : 4 * 64 * 32;  // epilogue staging: 64 x 32 per wave
+  __shared__ __attribute__((aligned(16))) float smem[SMEM];
+  static_assert(TBN == 64 || TBN == 128, "tile columns: 64 or 128");
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -172,7 +180,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs p) {
   int64_t mi, ni, zi;
   tile_of(p, mi, ni, zi);
   const int64_t m0 = mi * BM;
-  const int64_t n0 = ni * BN;
+  const int64_t n0 = ni * TBN;
   const int64_t kbeg = zi * p.k_per_split;
   const int64_t kend = min(p.K, kbeg + p.k_per_split);
 
@@ -188,24 +196,24 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs p) {
   ob.ld = p.ldb;
   ob.rows_total = p.N;
   ob.row0 = n0;
-  const bool rows_in = ALIGNED && (m0 + BM <= p.M) && (n0 + BN <= p.N);
+  const bool rows_in = ALIGNED && (m0 + BM <= p.M) && (n0 + TBN <= p.N);
 
-  f32x16 acc[2][2];
+  f32x16 acc[2][NJ];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < NJ; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
 
   auto mma_step = [&](const float* As, const float* Bs) {
 #pragma unroll
     for (int kk = 0; kk < BK; kk += 8) {
-      float4 a[2], b[2];
+      float4 a[2], b[NJ];
 #pragma unroll
       for (int i = 0; i < 2; ++i) a[i] = OA::frag(As, wm * 64 + i * 32 + l32, kk, h);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) b[j] = OB::frag(Bs, wn * 64 + j * 32 + l32, kk, h);
+      for (int j = 0; j < NJ; ++j) b[j] = OB::frag(Bs, wn * WN + j * 32 + l32, kk, h);
       // component-major: consecutive MFMAs hit the four independent
       // accumulators, so none waits on the previous one's result (the
       // per-accumulator k order is unchanged: results are bitwise the same)
@@ -214,7 +222,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs p) {
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j)
+          for (int j = 0; j < NJ; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(reinterpret_cast<const float*>(&a[i])[c],
                                                              reinterpret_cast<const float*>(&b[j])[c], acc[i][j],
                                                              0, 0, 0);
@@ -246,9 +254,9 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs p) {
   // every lane stores whole float4 rows (a register holds one column of four
   // rows; scalar stores cost 4x the store instructions on a 7 GB output).
   if ((p.ldc & 3) == 0 && (reinterpret_cast<uintptr_t>(Cz) & 15) == 0) {
-    float* stage = smem + wave * (64 * 32);  // 4 x 2048 floats <= operand buffers
+    float* stage = smem + wave * (64 * 32);  // 4 x 2048 floats
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < NJ; ++j) {
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -258,7 +266,7 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs p) {
       for (int it = 0; it < 8; ++it) {
         const int row = (lane >> 3) + 8 * it, c4 = (lane & 7) * 4;
         const int64_t gm = m0 + wm * 64 + row;
-        const int64_t gn = n0 + wn * 64 + j * 32 + c4;
+        const int64_t gn = n0 + wn * WN + j * 32 + c4;
         if (gm >= p.M || gn >= p.N) continue;
         float4 v = *reinterpret_cast<const float4*>(&stage[row * 32 + c4]);
         float* vp = reinterpret_cast<float*>(&v);
@@ -282,8 +290,8 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs p) {
     return;
   }
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int64_t gn = n0 + wn * 64 + j * 32 + l32;
+  for (int j = 0; j < NJ; ++j) {
+    const int64_t gn = n0 + wn * WN + j * 32 + l32;
     if (gn >= p.N) continue;
     const float bv = (EPI == EPI_BIAS && p.bias) ? p.bias[gn] : 0.0f;
 #pragma unroll
@@ -987,11 +995,11 @@ bool al16(const void* p) { return reinterpret_cast<uintptr_t>(p) % 16 == 0; }
 
 constexpr int GEMM_BK = 32;
 
-template <bool A_KC, bool B_KC, int EPI>
+template <bool A_KC, bool B_KC, int EPI, int TBN = BN>
 int launch_gemm(GemmArgs a, int splits, bool aligned, hipStream_t st) {
   if (a.M == 0 || a.N == 0) return GRL_OK;
   a.mt = ceil_div(a.M, BM);
-  a.nt = ceil_div(a.N, BN);
+  a.nt = ceil_div(a.N, TBN);
   a.zt = splits;
   // the operand worth sharing is the one with more rows per tile: A (M x K
   // rows of Z / g) for the forward and dZ, B (the K x N slab of g) for dW
@@ -1000,7 +1008,7 @@ int launch_gemm(GemmArgs a, int splits, bool aligned, hipStream_t st) {
   const dim3 grid((unsigned)(a.mt * a.nt * a.zt));
   const bool ma = a.Amask != nullptr, mb = a.Bmask != nullptr;
 #define GRL_GEMM(AL, MA, MB) \
-  hipLaunchKernelGGL((gemm_kernel<A_KC, B_KC, EPI, AL, MA, MB, GEMM_BK>), grid, dim3(256), 0, st, a)
+  hipLaunchKernelGGL((gemm_kernel<A_KC, B_KC, EPI, AL, MA, MB, GEMM_BK, TBN>), grid, dim3(256), 0, st, a)
   if (aligned) {
     if (ma) GRL_GEMM(true, true, false); else if (mb) GRL_GEMM(true, false, true); else GRL_GEMM(true, false, false);
   } else {
@@ -1030,8 +1038,14 @@ int pick_splits(int64_t M, int64_t N, int64_t K) {
 // kFp32SlabCap runs in row blocks that fit.  (Summing the chunks inside one
 // workgroup instead -- a second accumulator set -- cost 1 wave per SIMD at
 // 225-251 VGPRs: the classifier's 100k rows ran 5x slower than hipBLASLt.)
+// Calls made for at least kFp32OnePassTiles output tiles -- counted on the
+// whole graph's rows (path_rows), so every shard and row block of that graph
+// decides alike -- fill the chip without the chunks and walk all of K in one
+// accumulator instead: the slabs of K = 512 at 100k rows were 16 chunks of
+// one K tile each, 1.6 GB of slab traffic for a 13 GFLOP GEMM.
 constexpr int64_t kFp32MaxChunks = 16;
 constexpr size_t kFp32SlabCap = (size_t)256 << 20;
+constexpr int64_t kFp32OnePassTiles = 256;
 
 int64_t fp32_chunk_tiles(int64_t K) {
   const int64_t tiles = std::max<int64_t>(1, ceil_div(K, GEMM_BK));
@@ -1049,18 +1063,20 @@ int64_t fp32_block_rows(int64_t M, int64_t N, int64_t K) {
   return std::min<int64_t>(M, cap);
 }
 
-// K splits of the fp32 output GEMM: the chunk count (1: one chunk, no slabs)
-int pick_splits_small(int64_t M, int64_t N, int64_t K) {
-  (void)M;
-  (void)N;
+int64_t path_rows_of(int64_t M, int64_t path_rows) { return std::max<int64_t>(M, path_rows); }
+
+// K splits of the fp32 output GEMM: 1 (one pass, no slabs) for calls of
+// kFp32OnePassTiles tiles, else the chunk count
+int pick_splits_small(int64_t M, int64_t path_rows, int64_t N, int64_t K) {
+  if (ceil_div(path_rows_of(M, path_rows), BM) * ceil_div(std::max<int64_t>(N, 1), BN) >= kFp32OnePassTiles) return 1;
   return fp32_chunks(K);
 }
 
 // row blocks of the db column sum: ~64 rows each (>= 1 block, <= 1024)
 int colsum_splits(int64_t M) { return (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(M, 64), 1024)); }
 
-size_t small_ws_bytes(int64_t M, int64_t N, int64_t K) {
-  const int s = pick_splits_small(M, N, K);
+size_t small_ws_bytes(int64_t M, int64_t path_rows, int64_t N, int64_t K) {
+  const int s = pick_splits_small(M, path_rows, N, K);
   return s > 1 ? (size_t)s * (size_t)fp32_block_rows(M, N, K) * (size_t)N * 4 + 256 : 0;
 }
 
@@ -1107,7 +1123,6 @@ size_t x6_ws_bytes(int64_t M, int64_t N, int64_t K) {
 // node-range shard's rows of a graph of path_rows nodes; 0: M itself): the
 // size floor is the whole call's, so every shard takes the one-GPU path.
 // (The x6 kernels clamp their A rows, so any M >= 1 is safe on them.)
-int64_t path_rows_of(int64_t M, int64_t path_rows) { return std::max<int64_t>(M, path_rows); }
 bool x6_path_ok(int64_t M, int64_t path_rows, int64_t N, int64_t K) {
   return M >= 1 && x6_shape_ok(path_rows_of(M, path_rows), N, K);
 }
@@ -1150,6 +1165,15 @@ int launch_x6(GemmArgs a, void* ws, hipStream_t st) {
   return rc ? rc : launch_x6_gemm(a, planes, st);
 }
 
+// The output GEMM on 64-column tiles when that computes less padding (N mod
+// 128 in 1..64: the classifier's 56 columns, f/g/h's 160); same bits.
+template <bool A_KC, bool B_KC, int EPI>
+int launch_out_gemm(const GemmArgs& a, int splits, bool aligned, hipStream_t st) {
+  const int64_t rem = a.N % BN;
+  return rem != 0 && rem <= 64 ? launch_gemm<A_KC, B_KC, EPI, 64>(a, splits, aligned, st)
+                               : launch_gemm<A_KC, B_KC, EPI, BN>(a, splits, aligned, st);
+}
+
 // Output-stationary GEMM with optional split-K through `ws` (slab layout
 // [split][M][N], then one ordered reduce applying bias / ReLU).
 template <bool A_KC, bool B_KC>
@@ -1162,23 +1186,14 @@ int run_output_gemm(GemmArgs a, bool aligned, const char* who, void* ws, size_t 
     return a.bias || a.relu ? launch_gemm256p<A_KC, B_KC, EPI_BIAS>(a, 1, st)
                             : launch_gemm256p<A_KC, B_KC, EPI_STORE>(a, 1, st);
   }
-  const int splits = pick_splits_small(a.M, a.N, a.K);
+  const int splits = pick_splits_small(a.M, a.path_rows, a.N, a.K);
   if (splits == 1) {
     a.k_per_split = std::max<int64_t>(a.K, 1);
-    return a.bias || a.relu ? launch_gemm<A_KC, B_KC, EPI_BIAS>(a, 1, aligned, st)
-                            : launch_gemm<A_KC, B_KC, EPI_STORE>(a, 1, aligned, st);
+    return a.bias || a.relu ? launch_out_gemm<A_KC, B_KC, EPI_BIAS>(a, 1, aligned, st)
+                            : launch_out_gemm<A_KC, B_KC, EPI_STORE>(a, 1, aligned, st);
   }
-  const size_t need = small_ws_bytes(a.M, a.N, a.K);
-  if (!ws || ws_bytes < need) {
-    // an x6-sized call whose operands turned out unaligned (its workspace was sized for W's planes):
-    // one pass over all of K (its rows' bits then follow this kernel, not the chunked form's)
-    if (ceil_div(a.M, BM) * ceil_div(a.N, BN) >= (int64_t)device_cu_count() && x6_path_ok(a.M, a.path_rows, a.N, a.K)) {
-      a.k_per_split = std::max<int64_t>(a.K, 1);
-      return a.bias || a.relu ? launch_gemm<A_KC, B_KC, EPI_BIAS>(a, 1, aligned, st)
-                              : launch_gemm<A_KC, B_KC, EPI_STORE>(a, 1, aligned, st);
-    }
-    GRL_FAIL(GRL_E_WORKSPACE, "%s: workspace %zu < %zu", who, ws_bytes, need);
-  }
+  const size_t need = small_ws_bytes(a.M, a.path_rows, a.N, a.K);
+  if (!ws || ws_bytes < need) GRL_FAIL(GRL_E_WORKSPACE, "%s: workspace %zu < %zu", who, ws_bytes, need);
   float* const out = a.C;
   const int64_t ldo = a.ldc;
   const float* const bias = a.bias;
@@ -1199,7 +1214,7 @@ int run_output_gemm(GemmArgs a, bool aligned, const char* who, void* ws, size_t 
     a.A = A0 + (A_KC ? r0 * a.lda : r0);
     a.Amask = Amask0 ? Amask0 + (A_KC ? r0 * a.lda : r0) : nullptr;
     a.M = rows;
-    int rc = launch_gemm<A_KC, B_KC, EPI_SLAB>(a, used, aligned, st);
+    int rc = launch_out_gemm<A_KC, B_KC, EPI_SLAB>(a, used, aligned, st);
     if (rc) return rc;
     const int64_t n = rows * a.N;
     hipLaunchKernelGGL(slab_reduce_epi_kernel, dim3((unsigned)std::min<int64_t>(ceil_div(n, 256), 4096)), dim3(256),
@@ -1217,7 +1232,7 @@ using namespace grl;
 // x6-sized calls need W's planes; the others the fp32 path's slabs (at most kFp32SlabCap)
 extern "C" size_t grl_linear_fwd_ex_workspace_size(int64_t M, int32_t K, int32_t C, int64_t path_rows) {
   if (M <= 0 || K <= 0 || C <= 0) return 0;
-  return x6_path_ok(M, path_rows, C, K) ? x6_ws_bytes_p(M, path_rows, C, K) : small_ws_bytes(M, C, K);
+  return x6_path_ok(M, path_rows, C, K) ? x6_ws_bytes_p(M, path_rows, C, K) : small_ws_bytes(M, path_rows, C, K);
 }
 
 extern "C" size_t grl_linear_fwd_workspace_size(int64_t M, int32_t K, int32_t C) {
@@ -1440,7 +1455,7 @@ extern "C" int grl_graphconv_fwd_train(const GrlTypedCsr* g, const float* X, int
 
 extern "C" size_t grl_linear_bwd_data_workspace_size(int64_t M, int32_t K, int32_t C) {
   if (M <= 0 || K <= 0 || C <= 0) return 0;
-  return x6_shape_ok(M, K, C) ? x6_ws_bytes(M, K, C) : small_ws_bytes(M, K, C);
+  return x6_shape_ok(M, K, C) ? x6_ws_bytes(M, K, C) : small_ws_bytes(M, 0, K, C);
 }
 
 extern "C" int grl_linear_bwd_data(const float* g, const float* relu_out, const float* W, float* dZ, int64_t lddz,

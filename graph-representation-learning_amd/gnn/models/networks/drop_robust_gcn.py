@@ -19,7 +19,8 @@ import torch
 from torch import nn
 
 from gnn.models.base_network import BaseNetwork
-from gnn.models.networks.robust_gcn import GraphConv, NodeSelfAtten, apply_linear, make_linear_relu
+from gnn.models.networks.robust_gcn import (ROW_LINEAR_MIN_ROWS, GraphConv, NodeSelfAtten, apply_linear,
+                                            make_linear_relu)
 from grl import DropEdge, TypedGraph
 from grl.dist import ShardedGraph
 from grl.ops import bag_linear, feature_dropout
@@ -114,7 +115,10 @@ class FeatureDropout(nn.Dropout):
     per forward (torch's CUDA generator, so torch.manual_seed reproduces
     runs; broadcast from rank 0 on a sharded graph) and numbers that
     forward's calls from 0.  `stream` (data-parallel rank) keeps the ranks'
-    masks independent.  Host tensors get plain nn.Dropout."""
+    masks independent.  Host tensors, and graphs of at most
+    ROW_LINEAR_MIN_ROWS rows that are not a shard (document pages: too small
+    to shard, host-bound steps where one fused torch op beats two library
+    calls), get plain nn.Dropout."""
 
     STREAM_SHIFT = 32
     DOMAIN = 1 << 48  # call ids apart from EdgeDropout's (which may share the seed)
@@ -127,16 +131,20 @@ class FeatureDropout(nn.Dropout):
         self._calls = 0
         self._seed_t: Optional[torch.Tensor] = None
         self.row0 = 0
+        self._hash = True
 
     def reset_calls(self) -> None:
         self._calls = 0
 
-    def begin_forward(self, device, shard: Optional[ShardedGraph] = None) -> None:
-        """Per-forward state: the global row of this rank's first row, and
-        (device-drawn seeds) the forward's seed."""
+    def begin_forward(self, device, shard: Optional[ShardedGraph] = None, rows: Optional[int] = None) -> None:
+        """Per-forward state: the global row of this rank's first row, the
+        mask kind (the hash on shards and on graphs of more than
+        ROW_LINEAR_MIN_ROWS rows), and (device-drawn seeds) the forward's
+        seed."""
         self.row0 = shard.plan.row_begin if shard is not None else 0
+        self._hash = shard is not None or rows is None or rows > ROW_LINEAR_MIN_ROWS
         if self.seed_source is not None or self.seed is not None or not self.training or self.p == 0.0 \
-                or torch.device(device).type != "cuda":
+                or torch.device(device).type != "cuda" or not self._hash:
             return
         seed_t = torch.randint(0, 2**62, (1,), dtype=torch.int64, device=device)
         self._seed_t = shard.broadcast_seed(seed_t) if shard is not None else seed_t
@@ -164,7 +172,7 @@ class FeatureDropout(nn.Dropout):
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         if not self.training or self.p == 0.0:
             return x
-        if not x.is_cuda:
+        if not x.is_cuda or not self._hash:
             return super().forward(x)
         return feature_dropout(x.float(), self.record(x.device), self.row0)
 
@@ -222,7 +230,7 @@ class GraphCNNDropEdge(BaseNetwork):
         sharded = isinstance(graph, ShardedGraph)
         # row-local layers of a shard take the one-GPU model's GEMM path (bitwise its rows)
         pr = graph.global_rows if sharded else 0
-        self.dropout.begin_forward(V.device, graph if sharded else None)
+        self.dropout.begin_forward(V.device, graph if sharded else None, V.numel() // max(V.shape[-1], 1))
         embedding = self.dropout(self._embed(V))
         # efficient_mode=True: dropout covers the identity block of A_pre
         # (:69,:76); False: dropout hits raw A, identity added after (:72-74).

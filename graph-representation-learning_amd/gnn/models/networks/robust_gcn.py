@@ -165,14 +165,17 @@ class NodeSelfAtten(nn.Module):
         the softmax then runs over every node of the graph
         (grl.dist.sharded_node_attention)."""
         pr = shard.global_rows if shard is not None else 0
-        # f, g, h read the same V: one GEMM over their concatenated weights (2 x F/8 + F columns; a column's
-        # result does not depend on the others)
-        lins = (self.f[0], self.g[0], self.h[0])
-        W = torch.cat([m.weight for m in lins])
-        b = torch.cat([m.bias for m in lins])
-        fgh = linear_rows(V, W, b, True, pr)
-        dk = self.f[0].out_features
-        f, g, h = fgh[..., :dk], fgh[..., dk:2 * dk], fgh[..., 2 * dk:]
+        if _on_grl(V, pr):
+            # f, g, h read the same V: one GEMM over their concatenated weights (2 x F/8 + F columns; a
+            # column's result does not depend on the others)
+            lins = (self.f[0], self.g[0], self.h[0])
+            W = torch.cat([m.weight for m in lins])
+            b = torch.cat([m.bias for m in lins])
+            fgh = linear_rows(V, W, b, True, pr)
+            dk = self.f[0].out_features
+            f, g, h = fgh[..., :dk], fgh[..., dk:2 * dk], fgh[..., 2 * dk:]
+        else:  # small graphs: torch's three GEMMs, no concatenation or strided slices around them
+            f, g, h = self.f(V), self.g(V), self.h(V)
         if shard is not None:
             return sharded_node_attention(f, g, h, V, self.gamma, shard)
         return node_self_attention(f, g, h, V, self.gamma)

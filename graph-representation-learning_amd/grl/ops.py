@@ -720,7 +720,8 @@ def row_linear(X: torch.Tensor, W: torch.Tensor, b=None, relu: bool = False, pat
         raise _lib.GrlError("row_linear: float32 input and weight required")
     lead = X.shape[:-1]
     X2 = _rows_view(X)
-    out = _RowLinear.apply(X2, W, b, relu, int(path_rows))
+    # path_rows >= M: the M-invariant kernels only (never grl_linear_fwd's unpinned large-M tile)
+    out = _RowLinear.apply(X2, W, b, relu, int(max(path_rows, X2.shape[0])))
     return out.view(*lead, W.shape[0])
 
 

@@ -128,7 +128,7 @@ def main():
             return _orig(*a, **k)
         setattr(gdist, fn, wrap)
 
-    for N, net in ((3000, 64), (20000, 256)):  # two-kernel layers / one-kernel layers + p2p row blocks
+    for N, net in ((5000, 64), (20000, 256)):  # two-kernel layers / one-kernel layers + p2p row blocks
         g = TypedGraph.synthetic(N, 12.0, L, kind="er", seed=4, device=DEV)
         gen = torch.Generator().manual_seed(5)
         V = (torch.rand(N, FIN, generator=gen) < 0.1).float().to(DEV)

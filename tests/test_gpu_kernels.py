@@ -338,12 +338,15 @@ def test_small_m_split_k_deterministic(M, K, C):
 
     assert _lib.lib().grl_linear_fwd_workspace_size(M, K, C) > 0  # the split path is what runs
     # large M takes the x6 path: only W's bf16 planes (3 x 256-padded C x K); off the x6 shape the fp32
-    # path's chunk slabs, in row blocks of at most 256 MB
+    # GEMM in one pass (the call fills the chip: no slabs)
     big = _lib.lib().grl_linear_fwd_workspace_size(1_000_000, K, C)
     if K % 16 == 0:
         assert big == 3 * (-(-C // 256) * 256) * K * 2 + 256
     else:
-        assert 0 < big <= (256 << 20) + 256
+        assert big == 0
+    # below the x6 size and the one-pass tile count: the chunk slabs, in row blocks of at most 256 MB
+    mid = _lib.lib().grl_linear_fwd_workspace_size(20_000, 1280, 16)
+    assert 0 < mid <= (256 << 20) + 256
     rng = np.random.default_rng(M)
     Zw = to_dev(rng.standard_normal((M, K + 8)).astype(np.float32))
     Z = Zw[:, :K]

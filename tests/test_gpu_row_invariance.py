@@ -5,10 +5,12 @@ the hash-keyed feature dropout (verdict r4 item 3, drop_robust_gcn.py:64,
 
 A node-range shard computes its rows in calls with fewer rows than the
 one-GPU model's; every row-local op must give those rows the same bits:
-  * the fp32 GEMM sums K in fixed chunks added in chunk order, split over
-    workgroups (small M) or inside one (large M): the rows of an M-row call
-    equal the same rows of any other call, bitwise;
-  * path_rows makes a smaller call take the bigger call's path (x6 or fp32);
+  * the fp32 GEMM sums K in fixed chunks added in chunk order (slabs) for
+    calls of fewer than 256 output tiles and in one pass for larger ones:
+    the rows of an M-row call equal the same rows of any other call made
+    for M rows (path_rows), bitwise;
+  * path_rows makes a smaller call take the bigger call's path (x6, fp32
+    one pass or fp32 slabs);
   * NodeSelfAtten's key split depends on N only: a query range's rows equal
     the whole-range call's;
   * feature dropout's mask is the hash of (seed, call, global element id)."""
@@ -24,28 +26,50 @@ DEV = torch.device("cuda:0")
 
 
 @pytest.mark.parametrize("K,C", [(448, 64), (1792, 256), (512, 128), (128, 1280), (1280, 53), (100, 30)])
-def test_fp32_gemm_rows_do_not_depend_on_m(K, C):
-    """grl_linear_fwd on the fp32 path (below the x6 size floor): the rows
-    of calls of 74 .. 60000 rows (split-K slabs and the unsplit chunked
-    kernel) are bitwise the same rows of the largest call; within 1e-5 of
-    float64."""
+@pytest.mark.parametrize("M", [60000, 8000])
+def test_fp32_gemm_rows_do_not_depend_on_m(K, C, M):
+    """grl_linear_fwd_ex on the fp32 path (below the x6 size floor), the
+    path chosen for M rows (path_rows = M): the rows of calls of 74 .. M rows
+    are bitwise the same rows of the M-row call -- on the one-pass kernel
+    (M's calls of >= 256 output tiles) and on the chunk slabs (fewer tiles);
+    within 1e-5 of float64."""
+    from grl.ops import x6_rows_ok
+
     g = torch.Generator(device=DEV).manual_seed(K + C)
-    M = 60000
     X = torch.randn(M, K, generator=g, device=DEV)
     W = torch.randn(K, C, generator=g, device=DEV) / K ** 0.5
     b = torch.randn(C, generator=g, device=DEV)
-    from grl.ops import x6_rows_ok
-
-    full = linear_fwd(X, W, b, True)
     if x6_rows_ok(M, C, K):
-        M = 16384  # keep the reference call on the fp32 path too
-        full = linear_fwd(X[:M].contiguous(), W, b, True)
+        M = 8192  # keep the reference call on the fp32 path too
+        X = X[:M].contiguous()
         assert not x6_rows_ok(M, C, K)
-    ref = torch.relu(X[:M].double() @ W.double() + b.double())
+    full = linear_fwd_ex(X, W, 0, b, True, path_rows=M)
+    ref = torch.relu(X.double() @ W.double() + b.double())
     assert float((full.double() - ref).abs().max()) <= 1e-5 * max(1.0, float(ref.abs().max()))
     for r0, r1 in ((0, 74), (5, 301), (1000, 3500), (777, 8000), (0, M // 2), (M // 3, M)):
-        part = linear_fwd(X[r0:r1].contiguous(), W, b, True)
+        r1 = min(r1, M)
+        part = linear_fwd_ex(X[r0:r1].contiguous(), W, 0, b, True, path_rows=M)
         assert torch.equal(part, full[r0:r1]), (r0, r1, float((part - full[r0:r1]).abs().max()))
+    if -(-M // 128) * -(-C // 128) < 256:  # the slabs, whose rows do not depend on M even without path_rows
+        part = linear_fwd(X[5:301].contiguous(), W, b, True)
+        assert torch.equal(part, full[5:301])
+
+
+@pytest.mark.parametrize("M", [40_000, 3000])  # both widths below the x6 size: one pass, slabs
+@pytest.mark.parametrize("K,C", [(1280, 56), (128, 160), (100, 30)])
+def test_narrow_tiles_give_the_wide_tiles_bits(M, K, C):
+    """Outputs of C columns with C mod 128 in 1..64 run on 64-column tiles;
+    the same columns computed inside a 128-multiple-wide call (128-column
+    tiles) are bitwise equal: the tile width never changes an element's
+    accumulation (one pass and chunk slabs alike)."""
+    g = torch.Generator(device=DEV).manual_seed(K + C + M)
+    X = torch.randn(M, K, generator=g, device=DEV)
+    Cw = -(-C // 128) * 128
+    Ww = torch.randn(K, Cw, generator=g, device=DEV) / K ** 0.5
+    bw = torch.randn(Cw, generator=g, device=DEV)
+    wide = linear_fwd_ex(X, Ww, 0, bw, True, path_rows=M)
+    narrow = linear_fwd_ex(X, Ww[:, :C].contiguous(), 0, bw[:C].contiguous(), True, path_rows=M)
+    assert torch.equal(narrow, wide[:, :C])
 
 
 @pytest.mark.parametrize("K,C", [(512, 128), (1792, 256)])
