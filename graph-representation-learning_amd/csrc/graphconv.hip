@@ -707,7 +707,10 @@ __global__ __launch_bounds__(GRL_WS_DIAG_LB) void graphconv_ws_kernel(
                                                      (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)ra));
                       xv[q] = zero4();
                       if (col_ok) {
-                        const f32x4_t t = *(gvec4*)(rowp + col);
+                        // C > 256: streaming loads, so the gathered rows (no reuse to speak of in L2) evict
+                        // less of W's 11 MB of planes (1.3 % at F = C = 512, profiles/r05_ab_wide_ntx.txt)
+                        const f32x4_t t = PROD == 4 ? __builtin_nontemporal_load((gvec4*)(rowp + col))
+                                                    : *(gvec4*)(rowp + col);
                         xv[q] = make_float4(t[0], t[1], t[2], t[3]);
                       }
                     }

@@ -12,7 +12,7 @@ make -s -C "$CS" >/dev/null
 SRC=${3:-linear}
 SRCFILE=$CS/$SRC.hip
 if [ -f "$SRC" ]; then SRCFILE=$SRC; SRC=$(basename "$SRC" .hip); fi  # a file elsewhere (e.g. an older revision)
-for f in common spmm graph attention embed linear graphconv layout_graph; do cp "$ROOT/build/obj/$f.o" "$OBJ/"; done
+cp "$ROOT"/build/obj/*.o "$OBJ/"
 EXTRA=""
 [ "$SRC" = attention ] && EXTRA="-mllvm -amdgpu-mfma-vgpr-form -fno-slp-vectorize"  # as the Makefile builds it
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -I"$ROOT/include" -I"$CS" -Wno-unused-result $EXTRA $2 -c "$SRCFILE" -o "$OBJ/$SRC.o"

@@ -5,7 +5,8 @@
 # chained as with &&).  Usage: tools/gpu_session.sh STEP...
 #   steps: tests smoke bench bench_extras bench_drop bench_c5 bench_c5s prof_bench prof_fwd prof_bwd
 #          prof_linear prof_layer prof_attn prof_c1 pmc_fwd_fetch pmc_fwd_write pmc_list pmc_linear_mfma
-#          pmc_fwd_tlb pmc_c4_tlb; round 4: ab_attn_hu tests_r4 pmc_infer_l2 pmc_wide_mfma prof_wide
+#          pmc_fwd_tlb pmc_c4_tlb; round 4: ab_attn_hu tests_r4 pmc_infer_l2 pmc_wide_mfma prof_wide;
+#          round 5: pmc_wide_l2 pmc_wide_mfma5
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
 OUT=gpurun_out
@@ -151,6 +152,14 @@ for step in "$@"; do
                   unset PROBE_QUICK PROBE_SHAPES ;;
     prof_wide) export PROBE_SHAPES=512x256,512x512,1024x512; run prof_wide 400 rocprofv3 --kernel-trace --stats \
                   -d "$OUT/prof_wide" -o run --output-format csv -- python tools/probe_wide.py; unset PROBE_SHAPES ;;
+    pmc_wide_l2) export PROBE_QUICK=1 PROBE_SHAPES=${PROBE_SHAPES:-256x256,512x512}; run pmc_wide_l2 300 \
+                  timeout -s KILL 240 rocprofv3 --pmc TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum TCC_EA0_RDREQ_sum \
+                  GRBM_GUI_ACTIVE --kernel-trace -d "$OUT/pmc_wide_l2" -o run --output-format csv \
+                  -- python tools/probe_wide.py; unset PROBE_QUICK PROBE_SHAPES ;;
+    pmc_wide_mfma5) export PROBE_QUICK=1 PROBE_SHAPES=${PROBE_SHAPES:-256x256,512x512}; run pmc_wide_mfma5 300 \
+                  timeout -s KILL 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CU_CYCLES \
+                  SQ_INSTS_VALU SQ_INSTS_MFMA --kernel-trace -d "$OUT/pmc_wide_mfma5" -o run --output-format csv \
+                  -- python tools/probe_wide.py; unset PROBE_QUICK PROBE_SHAPES ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
