@@ -21,7 +21,7 @@ from torch import nn
 from gnn.models.base_network import BaseNetwork
 from gnn.models.networks.robust_gcn import (ROW_LINEAR_MIN_ROWS, GraphConv, NodeSelfAtten, apply_linear,
                                             make_linear_relu)
-from grl import DropEdge, TypedGraph
+from grl import DropEdge, TypedGraph, device_check
 from grl.dist import ShardedGraph
 from grl.ops import bag_linear, feature_dropout
 
@@ -255,4 +255,9 @@ class GraphCNNDropEdge(BaseNetwork):
         if self.use_attention:
             new_v = self.self_atten(new_v, shard=graph) if sharded else self.self_atten(new_v)
         new_v = self.dropout(apply_linear(self.w_rand.projection, new_v, relu=True, path_rows=pr))
-        return apply_linear(self.classifier, new_v, path_rows=pr)
+        logits = apply_linear(self.classifier, new_v, path_rows=pr)
+        if sharded and not torch.is_grad_enabled() and logits.is_cuda:
+            # sharded inference has no procedure around it to surface a persistent kernel's stream-ordered
+            # failure (grl_check): one check per forward (training: allreduce_gradients checks)
+            device_check(logits.device)
+        return logits

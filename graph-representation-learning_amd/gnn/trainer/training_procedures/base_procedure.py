@@ -89,7 +89,9 @@ class BaseProcedure:
         if self.distributed:
             from grl.dist import allreduce_gradients
 
-            allreduce_gradients(self.model.parameters(), average=True)
+            # check=False: the step may be a captured HIP graph (no host wait inside); the procedure checks
+            # after the step instead
+            allreduce_gradients(self.model.parameters(), average=True, check=False)
 
     @staticmethod
     def _resolve(module, section: Dict[str, Any], what: str):

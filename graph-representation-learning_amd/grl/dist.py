@@ -1007,7 +1007,8 @@ def broadcast_module(module: torch.nn.Module, src: int = 0, group=None) -> None:
             _c_broadcast(t.data, src_in_group, group)
 
 
-def allreduce_gradients(params, group=None, bucket_bytes: int = 64 << 20, average: bool = False) -> None:
+def allreduce_gradients(params, group=None, bucket_bytes: int = 64 << 20, average: bool = False,
+                        check: bool = True) -> None:
     """Sum the .grad of `params` over the ranks of `group` in place.
 
     With node-range shards every rank's weight gradient of a GraphConv
@@ -1017,7 +1018,10 @@ def allreduce_gradients(params, group=None, bucket_bytes: int = 64 << 20, averag
     (one RCCL call each; all of GraphCNNDropEdge's fit one bucket).
     average=True divides by the world size (data parallelism's mean).
     Without a process group nothing runs; a one-rank group runs the real
-    collectives (a sum over one rank: the gradients unchanged)."""
+    collectives (a sum over one rank: the gradients unchanged).
+    check: then surface a persistent kernel's stream-ordered failure of this
+    step (grl_check, which waits for the stream) before any optimizer step
+    reads the gradients: the sharded training step's sync point."""
     if not _comm_on(group):
         return
     grads = [p.grad for p in params if p.grad is not None]
@@ -1050,6 +1054,10 @@ def allreduce_gradients(params, group=None, bucket_bytes: int = 64 << 20, averag
         bucket.append(g)
         size += g.numel() * g.element_size()
     flush()
+    if check and grads and grads[0].is_cuda:
+        from .graph import device_check
+
+        device_check(grads[0].device)
 
 
 def edge_balanced_bounds(deg: torch.Tensor, world: int) -> List[int]:

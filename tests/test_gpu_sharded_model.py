@@ -325,3 +325,31 @@ def test_streamed_layer_chain_equals_one_gpu(mode, nb):
     import torch.multiprocessing as mp
 
     mp.spawn(_stream_chain_worker, args=(2, _free_port(), mode, nb), nprocs=2, join=True)
+
+
+def test_sharded_model_surfaces_a_poisoned_kernel(monkeypatch):
+    """Stream-ordered failures of the persistent GraphConv kernel reach the
+    caller of the sharded model with no procedure around it: the inference
+    forward checks once at its end, and allreduce_gradients (the training
+    step's sync point, before any optimizer step) checks the step's kernels
+    -- both raise GrlError naming the entry point instead of returning NaN."""
+    import grl
+    from grl import _lib
+    from grl.dist import LocalGroup, ShardedGraph, allreduce_gradients
+
+    g, bounds, V, y = _inputs(1, 20_000, "nodes")
+    sg = ShardedGraph.in_process(g, bounds, halo="dense", group=LocalGroup(1))[0]
+    m = _model(256)
+    grl.check()
+    monkeypatch.setenv("GRL_WS_SPIN", "1")
+    m.eval()
+    with torch.no_grad(), pytest.raises(_lib.GrlError, match="grl_graphconv"):
+        m.forward([V, sg])
+    m.train()
+    logits = m.forward([V, sg]).reshape(-1, OUT)
+    torch.nn.functional.cross_entropy(logits, y, reduction="sum").backward()
+    with pytest.raises(_lib.GrlError, match="grl_graphconv"):
+        allreduce_gradients([p for p in m.parameters() if p.requires_grad], group=sg.group)
+    monkeypatch.delenv("GRL_WS_SPIN")
+    torch.cuda.synchronize()
+    grl.check()
