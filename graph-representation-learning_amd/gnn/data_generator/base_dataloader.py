@@ -1,7 +1,8 @@
 """Dataset + collate -> torch DataLoader (the reference's BaseDataLoader,
 gnn/data_generator/base_dataloader.py:13-112): same config keys, the
 collate chain Compose[configured collates..., default_collate], DistributedSampler
-when config.distributed."""
+when config.distributed (not with graph_parallel: node_range, where every rank
+loads the same batches)."""
 from __future__ import annotations
 
 import logging
@@ -14,6 +15,7 @@ from torch.utils.data.distributed import DistributedSampler
 
 from gnn.data_generator import data_collate, datasets
 from gnn.data_generator.data_collate.numpy_padding import TypedEdgePadding
+from gnn.utils.config import node_range_parallel
 
 
 def _to_tensors(batch: Dict[str, Any]) -> Dict[str, Any]:
@@ -60,7 +62,9 @@ class BaseDataLoader:
                         **kwargs) -> DataLoader:
         try:
             collate = Compose(self._load_collate_processors(data_config.get("data_collate")))
-            distributed = bool(self.config.get("distributed"))
+            # graph_parallel node_range (additive): every rank loads the same batches and takes a node range
+            # of each batch's graph, so no document sampler
+            distributed = bool(self.config.get("distributed")) and not node_range_parallel(self.config)
             batch_size = data_config.get("batch_size", 1)
             sampler = None
             if distributed:

@@ -2,7 +2,9 @@
 gnn/inferencer/inference_procedures/kv_inference.py:13-118): one document at
 a time, softmax (inference_settings.activation), argmax class and score per
 text line, returned as the input boxes annotated with formal_key, key_type
-and confidence."""
+and confidence.  With `graph_parallel: node_range` every rank predicts its
+node range of the document's graph (grl.dist.ShardedGraph) and the logits
+are all-gathered, so every rank returns the whole document's boxes."""
 from __future__ import annotations
 
 from typing import Any, Dict, List
@@ -37,10 +39,24 @@ class KVInference(BaseProcedure):
         rowptr, colidx = edges_to_typed_csr(sample["typed_edges"], n)
         return TypedGraph.from_csr_host(rowptr, colidx, 6, self.device, num_cols=n, batch_shape=(1, n))
 
+    def _sharded_logits(self, V: torch.Tensor, g) -> torch.Tensor:
+        """The model's logits (1, N, C) from this rank's node range of the
+        document's graph, all-gathered (graph_parallel: node_range)."""
+        from grl.dist import ShardedGraph
+
+        if not isinstance(g, TypedGraph):
+            g = TypedGraph.from_dense(g, layout="bnln")
+        gp = self.config.get("graph_parallel_args") or {}
+        sg = ShardedGraph.from_graph(g, balance=gp.get("balance", "edges"), halo=gp.get("halo", "auto"))
+        rb, re = sg.plan.row_begin, sg.plan.row_end
+        rows = self.model([V.reshape(-1, V.shape[-1])[rb:re], sg])
+        return sg.gather_rows(rows.reshape(re - rb, -1)).unsqueeze(0)
+
     def step_process(self, sample: Dict[str, Any]) -> List[Dict[str, Any]]:
         raw = sample["label"]
         V = torch.tensor(sample["textline_encoding"], dtype=torch.float, device=self.device).unsqueeze(0)
-        logits = self.activator(self.model([V, self._graph(sample)]))
+        g = self._graph(sample)
+        logits = self.activator(self._sharded_logits(V, g) if self.graph_parallel else self.model([V, g]))
         scores, classes = logits.max(dim=-1)
         classes = classes.reshape(-1).cpu().tolist()
         scores = scores.reshape(-1).cpu().tolist()

@@ -12,7 +12,16 @@ replicas stay identical.  Only rank 0 writes checkpoints.  Every rank is
 seeded alike (cl_warper.py:36-40), so after the broadcast each rank's CUDA
 generator is re-seeded with seed + rank and its EdgeDropout modules get
 stream = rank: ranks draw independent feature-dropout and DropEdge masks
-instead of the same ones on different documents."""
+instead of the same ones on different documents.
+
+Node-range graph parallelism (additive `graph_parallel: node_range` with
+`distributed: true`; gnn.utils.config.node_range_parallel): every rank loads
+the same batches, takes a node range of each batch's graph
+(grl.dist.ShardedGraph) and runs the model on its rows; the loss is weighted
+so the ranks' losses add up to the one-process loss, and the gradients are
+SUMMED over ranks -- the one-process step's.  The ranks then draw the
+one-process masks (no per-rank dropout streams: the sharded model's masks
+are keyed on global rows / edges and rank 0's seeds)."""
 from __future__ import annotations
 
 import logging
@@ -24,6 +33,7 @@ import torch.nn as nn
 
 from gnn.trainer import losses, lr_schedulers, optimizers
 from gnn.utils.checkpoint_handler import CheckpointHandler
+from gnn.utils.config import node_range_parallel
 
 
 class NullWriter:
@@ -49,13 +59,15 @@ class BaseProcedure:
         self.distributed = bool(config.get("distributed")) and torch.distributed.is_available() \
             and torch.distributed.is_initialized()
         self.rank = torch.distributed.get_rank() if self.distributed else 0
+        self.graph_parallel = self.distributed and node_range_parallel(config)
         self.device, self.device_ids = self._prepare_device(config.get("num_gpus", 1))
         self.model = self._load_prev_checkpoint(model).to(self.device)
         if self.distributed:
             from grl.dist import broadcast_module
 
             broadcast_module(self.model, src=0)
-            self._independent_dropout_streams()
+            if not self.graph_parallel:
+                self._independent_dropout_streams()
         self.criterion = self._init_criterion()
         self.optimizer = self._init_optimizer()
         self.lr_scheduler = self._init_lr_scheduler()
@@ -85,13 +97,14 @@ class BaseProcedure:
             torch.cuda.manual_seed(torch.initial_seed() + self.rank)
 
     def _sync_gradients(self) -> None:
-        """DDP's gradient averaging, as one bucketed all-reduce per step."""
+        """DDP's gradient averaging, as one bucketed all-reduce per step; with
+        node-range shards the sum (each rank's gradient is its rows' part)."""
         if self.distributed:
             from grl.dist import allreduce_gradients
 
             # check=False: the step may be a captured HIP graph (no host wait inside); the procedure checks
             # after the step instead
-            allreduce_gradients(self.model.parameters(), average=True, check=False)
+            allreduce_gradients(self.model.parameters(), average=not self.graph_parallel, check=False)
 
     @staticmethod
     def _resolve(module, section: Dict[str, Any], what: str):

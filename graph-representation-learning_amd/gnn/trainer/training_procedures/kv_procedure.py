@@ -7,6 +7,11 @@ macro P/R/F1 over non-padding, non-"other" nodes; validation each epoch;
 checkpoint on best validation loss.  Additive: a batch produced by
 TypedEdgePadding carries "typed_edges" instead of a dense adjacency and is
 turned into a TypedGraph directly (O(E) host->device instead of O(N^2)).
+Additive: with `graph_parallel: node_range` and `distributed: true` each
+rank trains and validates on a node range of every batch's graph
+(_step_process_shard; base_procedure.py's docstring), for graphs too large
+for one GPU; the reference's multi-GPU mode (data parallelism over
+documents) stays the default.
 """
 from __future__ import annotations
 
@@ -89,6 +94,8 @@ class KVProcedure(BaseProcedure):
         from gnn.trainer.training_procedures.step_graph import StepGraph, as_mode
 
         mode = as_mode(config.get("capture_train_step", "capture" if self.device.type == "cuda" else None))
+        if self.graph_parallel:  # the sharded step exchanges halos through collectives: eager
+            mode = None
         self.step_graph = StepGraph(self, mode) if mode else None
 
     def _init_dataloaders(self):
@@ -114,6 +121,8 @@ class KVProcedure(BaseProcedure):
         return ({f"{item_name}_{k}": v for k, v in scores.items()}, {"pred": pred_names, "lbl": true_names})
 
     def _step_process(self, batch: Dict[str, Any], **kwargs):
+        if self.graph_parallel:
+            return self._step_process_shard(batch)
         V = batch["textline_encoding"].float().to(self.device)
         A = batch_graph(batch, self.device)
         targets = batch["node_label"].to(self.device)
@@ -124,6 +133,61 @@ class KVProcedure(BaseProcedure):
         scores["loss"] = loss.item()
         device_check(self.device)  # the step already synced: surface a kernel's stream-ordered failure
         return loss, scores, items
+
+    def _step_process_shard(self, batch: Dict[str, Any]):
+        """_step_process on this rank's node range of the batch's graph
+        (graph_parallel: node_range; batch_size 1: the model's attention is a
+        softmax over one graph); rank r runs the model on rows [b_r, b_{r+1})
+        (GraphCNNDropEdge.forward([V_rows, ShardedGraph]): halo exchanges
+        inside, softmax of the attention over every node).  The returned loss
+        is this rank's share -- the criterion on its rows, weighted by its
+        rows' share of the batch's weighted targets -- so the ranks' losses
+        (and, summed, their gradients) are the one-process step's.  Metrics
+        and the reported loss are those of the whole batch on every rank."""
+        from grl.dist import ShardedGraph, all_reduce_sum
+
+        V = batch["textline_encoding"].float().to(self.device)
+        A = batch_graph(batch, self.device)
+        if not isinstance(A, TypedGraph):  # the collate's dense (B, N, L, N) batch
+            A = TypedGraph.from_dense(A, layout="bnln")
+        targets = batch["node_label"].to(self.device)
+        B, N = targets.shape[0], targets.shape[1]
+        if B != 1:  # NodeSelfAtten's softmax runs per page; a shard's runs over its whole graph
+            raise ValueError(f"graph_parallel: node_range trains one graph per step (batch_size: 1), got {B}")
+        gp = self.config.get("graph_parallel_args") or {}
+        sg = ShardedGraph.from_graph(A, balance=gp.get("balance", "edges"), halo=gp.get("halo", "auto"))
+        rb, re = sg.plan.row_begin, sg.plan.row_end
+        logits = self.model.forward([V.reshape(B * N, -1)[rb:re], sg]).reshape(1, re - rb, -1)
+        t_rows = targets.reshape(1, -1)[:, rb:re]
+        loss = self._shard_loss(logits, t_rows, targets)
+        logits_all = sg.gather_rows(logits.detach().reshape(re - rb, -1)).reshape(B, N, -1)
+        predicts = self.activator(logits_all).argmax(dim=-1)
+        scores, items = self._get_metric_scores(predicts, targets, item_name="Node classification")
+        scores["loss"] = float(all_reduce_sum(loss.detach().clone().reshape(1)).item())
+        device_check(self.device)
+        return loss, scores, items
+
+    def _shard_loss(self, logits: torch.Tensor, t_rows: torch.Tensor, targets: torch.Tensor) -> torch.Tensor:
+        """This rank's share of a mean-reduced criterion: its rows' loss times
+        their share of the batch's target weight (valid targets, or their
+        class weights), so the shares add up to the whole batch's mean."""
+        inner = getattr(self.criterion, "criterion", self.criterion)
+        if getattr(inner, "reduction", "mean") != "mean":
+            return self.criterion(logits, t_rows)
+        ignore = getattr(inner, "ignore_index", None)
+        weight = getattr(inner, "weight", None)
+
+        def mass(t: torch.Tensor) -> torch.Tensor:
+            valid = t != ignore if ignore is not None else torch.ones_like(t, dtype=torch.bool)
+            if weight is None:
+                return valid.sum().to(torch.float32)
+            w = weight.to(t.device)[t.clamp(min=0)]
+            return torch.where(valid, w, torch.zeros((), device=t.device)).sum()
+
+        m_loc, m_all = mass(t_rows), mass(targets)
+        if float(m_loc) == 0.0:  # no labelled row here: a zero share that still reaches every parameter's graph
+            return logits.sum() * 0.0
+        return self.criterion(logits, t_rows) * (m_loc / m_all)
 
     def _run_train_step(self, batch: Dict[str, Any], **kwargs):
         if self.step_graph is not None:

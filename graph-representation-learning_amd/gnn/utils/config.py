@@ -64,3 +64,16 @@ def to_plain(v: Any) -> Any:
 def load_config(path: str) -> AttrDict:
     with open(path, encoding="utf-8-sig") as f:
         return AttrDict(yaml.safe_load(f) or {})
+
+
+def node_range_parallel(cfg) -> bool:
+    """Additive config key `graph_parallel`: "node_range" (with distributed:
+    true) trains and validates every batch's graph as node-range shards, one
+    per rank (grl.dist.ShardedGraph), instead of the reference's data
+    parallelism over documents; absent / "documents" keeps the latter."""
+    v = cfg.get("graph_parallel")
+    if v in (None, False, "", "none", "documents"):
+        return False
+    if v != "node_range":
+        raise ValueError(f"graph_parallel must be 'node_range' or 'documents', got {v!r}")
+    return bool(cfg.get("distributed"))

@@ -381,6 +381,20 @@ def all_gather_into(out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
         _c_all_gather_into_tensor(out, inp, group)
 
 
+def all_reduce_sum(t: torch.Tensor, group=None) -> torch.Tensor:
+    """t summed over the ranks of `group`, in place (host-staged on gloo);
+    returns t.  No group: t unchanged."""
+    if not _comm_on(group):
+        return t
+    if _host_staged(group) and t.is_cuda:
+        h = t.cpu()
+        _c_all_reduce(h, dist.ReduceOp.SUM, group)
+        t.copy_(h)
+    else:
+        _c_all_reduce(t, dist.ReduceOp.SUM, group)
+    return t
+
+
 def all_gather_list(t: torch.Tensor, group=None) -> List[torch.Tensor]:
     src = t.cpu() if _host_staged(group) else t
     outs = [torch.empty_like(src) for _ in range(_world(group))]

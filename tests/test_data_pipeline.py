@@ -215,3 +215,16 @@ def test_macro_report_equals_sklearn():
             continue
         ref = classification_report(tn, pn, output_dict=True, zero_division=0)["macro avg"]
         assert got == {k2: ref[k2] for k2 in ("precision", "recall", "f1-score", "support")}, (trial, got, ref)
+
+
+def test_graph_parallel_config_switch():
+    """graph_parallel: node_range needs distributed; anything else is refused
+    (gnn.utils.config.node_range_parallel)."""
+    from gnn.utils.config import node_range_parallel
+
+    assert not node_range_parallel({})
+    assert not node_range_parallel({"graph_parallel": "documents", "distributed": True})
+    assert not node_range_parallel({"graph_parallel": "node_range"})
+    assert node_range_parallel({"graph_parallel": "node_range", "distributed": True})
+    with pytest.raises(ValueError):
+        node_range_parallel({"graph_parallel": "edges", "distributed": True})
