@@ -158,7 +158,9 @@ def test_dropedge_mask_matches_oracle(p):
 
 
 @pytest.mark.parametrize("M,K,C", [(1, 8, 4), (74, 1792, 256), (300, 3584, 256), (129, 10, 5), (517, 36, 200),
-                                   (1000, 1792, 128)])
+                                   (1000, 1792, 128),
+                                   # one pass (>= 256 output tiles) on 64-column tiles: aligned, unaligned, 3 tiles
+                                   (40_000, 100, 56), (33_000, 64, 30), (20_000, 128, 160)])
 @pytest.mark.parametrize("relu,bias", [(False, True), (True, True), (False, False)])
 def test_linear_matches_fp64(M, K, C, relu, bias):
     rng = np.random.default_rng(M * 7 + K)
@@ -188,6 +190,12 @@ def test_linear_fragment_layout_exact():
     bi = rng.integers(-8, 9, C).astype(np.float32)
     out = linear_fwd(to_dev(Zi), to_dev(Wi), to_dev(bi), False).cpu().numpy()
     np.testing.assert_array_equal(out, Zi @ Wi + bi)
+    # the one-pass form (>= 256 output tiles) on 64-column tiles (136 = 128 + 8) and on 128-column ones
+    for Mb, Cb in ((33_000, 136), (33_000, 128)):
+        Zb = rng.integers(-8, 9, (Mb, K)).astype(np.float32)
+        Wb = rng.integers(-8, 9, (K, Cb)).astype(np.float32)
+        out = linear_fwd(to_dev(Zb), to_dev(Wb), None, False).cpu().numpy()
+        np.testing.assert_array_equal(out, Zb @ Wb)
 
 
 def test_errors_raise_not_fallback():
