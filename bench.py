@@ -402,7 +402,8 @@ def main():
             out["cpu_baseline"], out["parity"] = cpu_baseline_shard(args, g_step, pipe, Z, L, F, world)
     if world > 1:
         dist.barrier()  # the other ranks wait while rank 0 times the host baseline
-    if world == 1 and wname.startswith("C3"):
+    # C3 and C3-sized custom shapes (a second Z of a d = 512, 8M-node graph would not fit beside the first)
+    if world == 1 and wname.startswith("C3") and Z.numel() * 4 <= (64 << 30):
         out["dropedge_train_p0.3"] = dropedge_train(graph, X_loc, E_loc, 3)
         surface("dropedge_train_p0.3", dev)
         if args.c4_reference:

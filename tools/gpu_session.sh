@@ -33,8 +33,7 @@ for step in "$@"; do
     bench) run bench 600 python bench.py ;;
     bench_extras) run bench_extras 600 python bench.py --extras --cpu-seconds 0 ;;
     bench_drop) run bench_drop 600 python bench.py --p 0.3 --cpu-seconds 0 ;;
-    bench_c5) run bench_c5 900 python bench.py --graph rmat --nodes-per-gpu 8388608 --avg-deg 64 --dim 512 \
-                  --p 0.2 --steps 5 --warmup 2 ;;
+    bench_c5) run bench_c5 900 python bench.py --workload C5 --steps 5 --warmup 2 ;;
     bench_c5s) run bench_c5s 600 python bench.py --graph rmat --nodes-per-gpu 1048576 --avg-deg 64 --dim 512 \
                   --p 0.2 --steps 10 --warmup 3 ;;
     prof_bench) run prof_bench 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_bench" -o run --output-format csv \
