@@ -38,7 +38,7 @@ def timed(fn, iters=20):
 
 def main():
     out = {}
-    for M in (296, 100_000, 1_000_000):
+    for M in [int(x) for x in os.environ.get("PROBE_ROWS", "296,100000,1000000").split(",")]:
         for name, (K, C, bias, relu) in SHAPES.items():
             lin = torch.nn.Linear(K, C, bias=bias).to(DEV)
             X = torch.randn(M, K, device=DEV, requires_grad=True)
