@@ -228,3 +228,28 @@ def test_graph_parallel_config_switch():
     assert node_range_parallel({"graph_parallel": "node_range", "distributed": True})
     with pytest.raises(ValueError):
         node_range_parallel({"graph_parallel": "edges", "distributed": True})
+
+
+@pytest.mark.parametrize("weight", [None, [0.5 + 0.1 * i for i in range(5)]])
+def test_shard_loss_shares_add_up_to_the_batch_mean(weight):
+    """graph_parallel: node_range -- each rank's loss is its rows' criterion
+    times their share of the batch's (class-weighted) valid targets, so the
+    shares over any node-range split add up to the one-process mean
+    (KVProcedure._shard_loss; ignore_index -100 rows carry no weight), and a
+    rank with no labelled row contributes an exact zero."""
+    from gnn.trainer.losses import CrossEntropyLoss
+    from gnn.trainer.training_procedures.kv_procedure import KVProcedure
+
+    torch.manual_seed(0)
+    proc = KVProcedure.__new__(KVProcedure)
+    proc.criterion = CrossEntropyLoss(weight=weight)
+    N, C = 37, 5
+    logits = torch.randn(1, N, C, dtype=torch.float64)
+    t = torch.randint(0, C, (1, N))
+    t[0, 10:20] = -100
+    full = proc.criterion(logits.float(), t).double()
+    for bounds in ([0, 18, 37], [0, 5, 12, 30, 37], [0, 10, 20, 37]):
+        parts = [proc._shard_loss(logits[:, a:b].float(), t[:, a:b], t) for a, b in zip(bounds[:-1], bounds[1:])]
+        assert abs(float(sum(p.double() for p in parts)) - float(full)) <= 1e-6 * max(1.0, abs(float(full)))
+    empty = proc._shard_loss(logits[:, 10:20].float().requires_grad_(), t[:, 10:20], t)
+    assert float(empty) == 0.0 and empty.requires_grad
