@@ -186,6 +186,7 @@ def _thread_ranks(world, mode, net_size, n_per_rank, balance):
     (2, "sparse", 64, 3000, "edges"),
     (2, "dense", 256, 20_000, "nodes"),   # one-kernel forward / data gradient, p2p row blocks in the backward
     (3, "sparse", 256, 20_000, "nodes"),
+    (4, "sparse", 64, 2_000, "edges"),      # four ranks: every rank both sends and receives from three peers
 ])
 def test_sharded_model_equals_one_gpu(world, mode, net_size, n_per_rank, balance, tmp_path):
     import torch.multiprocessing as mp
