@@ -1028,14 +1028,16 @@ int pick_splits(int64_t M, int64_t N, int64_t K) {
 }
 
 // The output-stationary fp32 GEMM (forward, data gradient; the x6 path's
-// fallback) sums K in fixed chunks whose size depends on K alone -- at most
-// 16 chunks of whole K tiles -- one chunk per K split into fp32 slabs that a
-// second pass adds in chunk order with the bias / ReLU epilogue.  So every
-// element is the same fp32 operations whatever M is, and a node-range
-// shard's rows equal the whole graph's.  Small M gets the
-// chunks' parallelism (a lone workgroup walking all of K is bound by load
-// latency: a 74-node page is one 128-row tile); M whose slabs would exceed
-// kFp32SlabCap runs in row blocks that fit.  (Summing the chunks inside one
+// fallback) sums K in fixed chunks of whole K tiles -- their size chosen
+// from K and the WHOLE call's output tiles (path_rows), never from the rows
+// at hand: about kFp32WantBlocks workgroups, at most kFp32MaxChunks chunks --
+// one chunk per K split into fp32 slabs that a second pass adds in chunk
+// order with the bias / ReLU epilogue.  So every element is the same fp32
+// operations whatever M is, and a node-range shard's rows equal the whole
+// graph's.  Small calls get the chunks' parallelism (a lone
+// workgroup walking all of K is bound by load latency: a 74-node page is one
+// 128-row tile; its 1792-deep GraphConv GEMM runs as 56 one-tile chunks);
+// M whose slabs would exceed kFp32SlabCap runs in row blocks that fit.  (Summing the chunks inside one
 // workgroup instead -- a second accumulator set -- cost 1 wave per SIMD at
 // 225-251 VGPRs: the classifier's 100k rows ran 5x slower than hipBLASLt.)
 // Calls made for at least kFp32OnePassTiles output tiles -- counted on the
@@ -1043,33 +1045,40 @@ int pick_splits(int64_t M, int64_t N, int64_t K) {
 // decides alike -- fill the chip without the chunks and walk all of K in one
 // accumulator instead: the slabs of K = 512 at 100k rows were 16 chunks of
 // one K tile each, 1.6 GB of slab traffic for a 13 GFLOP GEMM.
-constexpr int64_t kFp32MaxChunks = 16;
+constexpr int64_t kFp32MaxChunks = 64;
+constexpr int64_t kFp32WantBlocks = 1024;  // ~4 workgroups per CU
 constexpr size_t kFp32SlabCap = (size_t)256 << 20;
 constexpr int64_t kFp32OnePassTiles = 256;
 
-int64_t fp32_chunk_tiles(int64_t K) {
-  const int64_t tiles = std::max<int64_t>(1, ceil_div(K, GEMM_BK));
-  return ceil_div(tiles, kFp32MaxChunks);
+int64_t path_rows_of(int64_t M, int64_t path_rows) { return std::max<int64_t>(M, path_rows); }
+
+// output tiles of the whole call (path_rows) the arithmetic is chosen for
+int64_t fp32_path_tiles(int64_t M, int64_t path_rows, int64_t N) {
+  return ceil_div(path_rows_of(M, path_rows), BM) * ceil_div(std::max<int64_t>(N, 1), BN);
 }
 
-int fp32_chunks(int64_t K) {
-  return (int)ceil_div(std::max<int64_t>(1, ceil_div(K, GEMM_BK)), fp32_chunk_tiles(K));
+int64_t fp32_chunk_tiles(int64_t tiles, int64_t K) {
+  const int64_t kt = std::max<int64_t>(1, ceil_div(K, GEMM_BK));
+  const int64_t want = std::max<int64_t>(1, ceil_div(kFp32WantBlocks, std::max<int64_t>(tiles, 1)));
+  return ceil_div(kt, std::min<int64_t>(std::min<int64_t>(want, kFp32MaxChunks), kt));
 }
 
-// rows per slab pass: all of M, or the BM-multiple whose slabs fit kFp32SlabCap
-int64_t fp32_block_rows(int64_t M, int64_t N, int64_t K) {
-  const int64_t per_row = (int64_t)fp32_chunks(K) * std::max<int64_t>(N, 1) * 4;
+int fp32_chunks(int64_t tiles, int64_t K) {
+  return (int)ceil_div(std::max<int64_t>(1, ceil_div(K, GEMM_BK)), fp32_chunk_tiles(tiles, K));
+}
+
+// rows per slab pass: all of M, or the BM-multiple whose `chunks` slabs fit kFp32SlabCap
+int64_t fp32_block_rows(int64_t M, int64_t N, int chunks) {
+  const int64_t per_row = (int64_t)chunks * std::max<int64_t>(N, 1) * 4;
   const int64_t cap = std::max<int64_t>(BM, (int64_t)kFp32SlabCap / per_row / BM * BM);
   return std::min<int64_t>(M, cap);
 }
 
-int64_t path_rows_of(int64_t M, int64_t path_rows) { return std::max<int64_t>(M, path_rows); }
-
 // K splits of the fp32 output GEMM: 1 (one pass, no slabs) for calls of
 // kFp32OnePassTiles tiles, else the chunk count
 int pick_splits_small(int64_t M, int64_t path_rows, int64_t N, int64_t K) {
-  if (ceil_div(path_rows_of(M, path_rows), BM) * ceil_div(std::max<int64_t>(N, 1), BN) >= kFp32OnePassTiles) return 1;
-  return fp32_chunks(K);
+  const int64_t tiles = fp32_path_tiles(M, path_rows, N);
+  return tiles >= kFp32OnePassTiles ? 1 : fp32_chunks(tiles, K);
 }
 
 // row blocks of the db column sum: ~64 rows each (>= 1 block, <= 1024)
@@ -1077,7 +1086,7 @@ int colsum_splits(int64_t M) { return (int)std::max<int64_t>(1, std::min<int64_t
 
 size_t small_ws_bytes(int64_t M, int64_t path_rows, int64_t N, int64_t K) {
   const int s = pick_splits_small(M, path_rows, N, K);
-  return s > 1 ? (size_t)s * (size_t)fp32_block_rows(M, N, K) * (size_t)N * 4 + 256 : 0;
+  return s > 1 ? (size_t)s * (size_t)fp32_block_rows(M, N, s) * (size_t)N * 4 + 256 : 0;
 }
 
 // Large-tile path selection (the fp32 fallback when the x6 path is off).
@@ -1201,12 +1210,12 @@ int run_output_gemm(GemmArgs a, bool aligned, const char* who, void* ws, size_t 
   const float* const A0 = a.A;
   const float* const Amask0 = a.Amask;
   const int64_t M = a.M;
-  const int64_t R = fp32_block_rows(M, a.N, a.K);
+  const int64_t R = fp32_block_rows(M, a.N, splits);
   a.C = static_cast<float*>(ws);
   a.ldc = a.N;
   a.bias = nullptr;
   a.relu = 0;
-  a.k_per_split = fp32_chunk_tiles(a.K) * GEMM_BK;  // one chunk per split
+  a.k_per_split = fp32_chunk_tiles(fp32_path_tiles(M, a.path_rows, a.N), a.K) * GEMM_BK;  // one chunk per split
   const int used = (int)ceil_div(a.K, a.k_per_split);
   for (int64_t r0 = 0; r0 < M; r0 += R) {  // row blocks: the same chunks, so the same bits, as one pass
     const int64_t rows = std::min<int64_t>(R, M - r0);

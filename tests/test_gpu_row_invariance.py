@@ -50,9 +50,6 @@ def test_fp32_gemm_rows_do_not_depend_on_m(K, C, M):
         r1 = min(r1, M)
         part = linear_fwd_ex(X[r0:r1].contiguous(), W, 0, b, True, path_rows=M)
         assert torch.equal(part, full[r0:r1]), (r0, r1, float((part - full[r0:r1]).abs().max()))
-    if -(-M // 128) * -(-C // 128) < 256:  # the slabs, whose rows do not depend on M even without path_rows
-        part = linear_fwd(X[5:301].contiguous(), W, b, True)
-        assert torch.equal(part, full[5:301])
 
 
 @pytest.mark.parametrize("M", [40_000, 3000])  # both widths below the x6 size: one pass, slabs
