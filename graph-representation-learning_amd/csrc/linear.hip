@@ -1023,7 +1023,7 @@ int pick_splits(int64_t M, int64_t N, int64_t K) {
   const int64_t tiles = ceil_div(M, BM) * ceil_div(N, BN);
   const int64_t want = (int64_t)device_cu_count() * 4;  // ~4 blocks per CU
   int64_t s = std::max<int64_t>(1, want / std::max<int64_t>(tiles, 1));
-  s = std::min<int64_t>(s, ceil_div(K, 4 * GEMM_BK));  // each split keeps >= 4 K tiles
+  s = std::min<int64_t>(s, ceil_div(K, GEMM_BK));  // each split keeps >= 1 K tile (a 296-row C1 batch: 10 splits)
   return (int)std::max<int64_t>(1, std::min<int64_t>(s, 256));
 }
 
@@ -1081,8 +1081,9 @@ int pick_splits_small(int64_t M, int64_t path_rows, int64_t N, int64_t K) {
   return tiles >= kFp32OnePassTiles ? 1 : fp32_chunks(tiles, K);
 }
 
-// row blocks of the db column sum: ~64 rows each (>= 1 block, <= 1024)
-int colsum_splits(int64_t M) { return (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(M, 64), 1024)); }
+// row blocks of the db column sum: ~16 rows each (>= 1 block, <= 1024); a block's rows are a chain of
+// dependent load rounds, so small M wants short blocks (a 296-row C1 batch: 19 blocks, 2 rounds each)
+int colsum_splits(int64_t M) { return (int)std::max<int64_t>(1, std::min<int64_t>(ceil_div(M, 16), 1024)); }
 
 size_t small_ws_bytes(int64_t M, int64_t path_rows, int64_t N, int64_t K) {
   const int s = pick_splits_small(M, path_rows, N, K);
