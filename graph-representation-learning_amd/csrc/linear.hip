@@ -1023,7 +1023,8 @@ int pick_splits(int64_t M, int64_t N, int64_t K) {
   const int64_t tiles = ceil_div(M, BM) * ceil_div(N, BN);
   const int64_t want = (int64_t)device_cu_count() * 4;  // ~4 blocks per CU
   int64_t s = std::max<int64_t>(1, want / std::max<int64_t>(tiles, 1));
-  s = std::min<int64_t>(s, ceil_div(K, GEMM_BK));  // each split keeps >= 1 K tile (a 296-row C1 batch: 10 splits)
+  // each split keeps >= 4 K tiles (1 or 2 measured the same on the C1 step, profiles/r05_ab_c1_dw_splits.txt)
+  s = std::min<int64_t>(s, ceil_div(K, 4 * GEMM_BK));
   return (int)std::max<int64_t>(1, std::min<int64_t>(s, 256));
 }
 
