@@ -42,12 +42,11 @@ class KVInference(BaseProcedure):
     def _sharded_logits(self, V: torch.Tensor, g) -> torch.Tensor:
         """The model's logits (1, N, C) from this rank's node range of the
         document's graph, all-gathered (graph_parallel: node_range)."""
-        from grl.dist import ShardedGraph
+        from gnn.trainer.training_procedures.kv_procedure import sharded_graph_cached
 
         if not isinstance(g, TypedGraph):
             g = TypedGraph.from_dense(g, layout="bnln")
-        gp = self.config.get("graph_parallel_args") or {}
-        sg = ShardedGraph.from_graph(g, balance=gp.get("balance", "edges"), halo=gp.get("halo", "auto"))
+        sg = sharded_graph_cached(self, g, self.config.get("graph_parallel_args") or {})
         rb, re = sg.plan.row_begin, sg.plan.row_end
         rows = self.model([V.reshape(-1, V.shape[-1])[rb:re], sg])
         return sg.gather_rows(rows.reshape(re - rb, -1)).unsqueeze(0)

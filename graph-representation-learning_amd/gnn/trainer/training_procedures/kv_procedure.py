@@ -42,6 +42,27 @@ def batch_graph(batch: Dict[str, Any], device: torch.device, num_types: int = 6)
     return batch["adjacency_matrix"].float().to(device)
 
 
+def sharded_graph_cached(owner, graph: TypedGraph, args: Dict[str, Any]):
+    """This rank's node-range shard of `graph` (graph_parallel: node_range),
+    from a small per-owner cache keyed on the graph's structure
+    (ShardedGraph.cache_key): a graph met again reuses its shard plan."""
+    from collections import OrderedDict
+
+    from grl.dist import ShardedGraph
+
+    kw = {"balance": args.get("balance", "edges"), "halo": args.get("halo", "auto")}
+    cache = owner.__dict__.setdefault("_shard_cache", OrderedDict())
+    key = ShardedGraph.cache_key(graph, **kw)
+    sg = cache.get(key)
+    if sg is None:
+        sg = ShardedGraph.from_graph(graph, **kw)
+        cache[key] = sg
+        while len(cache) > 4:
+            cache.popitem(last=False)
+    cache.move_to_end(key)
+    return sg
+
+
 def macro_report(y_true: np.ndarray, y_pred: np.ndarray, names) -> Dict[str, Any]:
     """sklearn's classification_report(true_names, pred_names, output_dict=True,
     zero_division=0)["macro avg"] (the reference's per-step metric,
@@ -144,7 +165,7 @@ class KVProcedure(BaseProcedure):
         rows' share of the batch's weighted targets -- so the ranks' losses
         (and, summed, their gradients) are the one-process step's.  Metrics
         and the reported loss are those of the whole batch on every rank."""
-        from grl.dist import ShardedGraph, all_reduce_sum
+        from grl.dist import all_reduce_sum
 
         V = batch["textline_encoding"].float().to(self.device)
         A = batch_graph(batch, self.device)
@@ -154,8 +175,7 @@ class KVProcedure(BaseProcedure):
         B, N = targets.shape[0], targets.shape[1]
         if B != 1:  # NodeSelfAtten's softmax runs per page; a shard's runs over its whole graph
             raise ValueError(f"graph_parallel: node_range trains one graph per step (batch_size: 1), got {B}")
-        gp = self.config.get("graph_parallel_args") or {}
-        sg = ShardedGraph.from_graph(A, balance=gp.get("balance", "edges"), halo=gp.get("halo", "auto"))
+        sg = sharded_graph_cached(self, A, self.config.get("graph_parallel_args") or {})
         rb, re = sg.plan.row_begin, sg.plan.row_end
         logits = self.model.forward([V.reshape(B * N, -1)[rb:re], sg]).reshape(1, re - rb, -1)
         t_rows = targets.reshape(1, -1)[:, rb:re]

@@ -1109,6 +1109,20 @@ class ShardedGraph:
         # one-GPU layer's (GrlTypedCsr.path_rows)
         self.graph.path_rows = self.global_rows
 
+    @staticmethod
+    def cache_key(graph: TypedGraph, **kw):
+        """A key identifying `graph`'s structure (rows, types, edges and a
+        checksum of its CSR arrays) plus the sharding options: every rank
+        computes the same key from the same graph, so a procedure that meets
+        one large graph step after step reuses its shard plan instead of
+        rebuilding it (from_graph exchanges index lists)."""
+        L = graph.num_types
+        idx = torch.arange(1, graph.colidx.numel() + 1, device=graph.colidx.device, dtype=torch.int64)
+        chk = torch.stack([(graph.colidx.to(torch.int64) * idx).sum(), graph.rowptr.to(torch.int64).sum(),
+                           (graph.vals.double().sum() * 1e6).to(torch.int64) if graph.vals is not None
+                           else torch.zeros((), dtype=torch.int64, device=graph.colidx.device)]).tolist()
+        return (graph.num_rows, L, int(graph.colidx.numel()), tuple(chk), tuple(sorted(kw.items())))
+
     @property
     def global_rows(self) -> int:
         """Rows of the whole graph this shard belongs to."""

@@ -90,6 +90,7 @@ def _worker(rank, world, port, cfg):
             v_gp, _ = gp._run_val_step(batch)
             v_one, _ = single._run_val_step(batch)
             assert abs(v_gp["loss"] - v_one["loss"]) <= 1e-4 * max(1.0, abs(v_one["loss"])), (step, v_gp, v_one)
+        assert len(gp._shard_cache) == STEPS  # each step's validation reused its training step's shard plan
         flat = torch.cat([p.detach().reshape(-1).cpu() for p in gp.model.parameters()])
         gathered = [torch.empty_like(flat) for _ in range(world)]
         dist.all_gather(gathered, flat)
