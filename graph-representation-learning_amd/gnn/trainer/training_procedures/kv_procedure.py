@@ -15,6 +15,7 @@ documents) stays the default.
 """
 from __future__ import annotations
 
+import functools
 import math
 from collections import defaultdict
 from typing import Any, Dict, List, Tuple
@@ -63,6 +64,17 @@ def sharded_graph_cached(owner, graph: TypedGraph, args: Dict[str, Any]):
     return sg
 
 
+@functools.lru_cache(maxsize=16)
+def _label_map(names: Tuple[str, ...]):
+    """class id -> label index in sorted-name order (sklearn works on the names: equal names are one
+    label), and the label count; built once per class list, not on every step."""
+    uniq = sorted(set(names))
+    pos = {nm: j for j, nm in enumerate(uniq)}
+    idmap = np.array([pos[nm] for nm in names], dtype=np.int64)
+    idmap.setflags(write=False)
+    return idmap, len(uniq)
+
+
 def macro_report(y_true: np.ndarray, y_pred: np.ndarray, names) -> Dict[str, Any]:
     """sklearn's classification_report(true_names, pred_names, output_dict=True,
     zero_division=0)["macro avg"] (the reference's per-step metric,
@@ -75,11 +87,8 @@ def macro_report(y_true: np.ndarray, y_pred: np.ndarray, names) -> Dict[str, Any
     its host time (it ran on every training step)."""
     if y_true.size == 0 and y_pred.size == 0:
         return {"precision": 0.0, "recall": 0.0, "f1-score": 0.0, "support": 0.0}
-    uniq = sorted(set(names))  # sklearn works on the names: equal names are one label
-    pos = {nm: j for j, nm in enumerate(uniq)}
-    idmap = np.array([pos[nm] for nm in names], dtype=np.int64)
+    idmap, U = _label_map(tuple(names))
     yt, yp = idmap[y_true], idmap[y_pred]
-    U = len(uniq)
     true_sum = np.bincount(yt, minlength=U)
     pred_sum = np.bincount(yp, minlength=U)
     tp_sum = np.bincount(yt[yt == yp], minlength=U)
@@ -130,8 +139,8 @@ class KVProcedure(BaseProcedure):
 
     def _get_metric_scores(self, preds: torch.Tensor, gts: torch.Tensor,
                            item_name: str = "item") -> Tuple[Dict[str, Any], Dict[str, Any]]:
-        y_pred = preds.reshape(-1).cpu().numpy()
-        y_true = gts.reshape(-1).cpu().numpy()
+        both = torch.stack([preds.reshape(-1), gts.reshape(-1).to(preds.dtype)]).cpu().numpy()  # one device sync
+        y_pred, y_true = both[0], both[1]
         args = self.config.data_config.dataset.get("args") or {}
         ignore = [args.get("node_label_padding_value", -100), args.get("other_class_index")]
         keep = np.isin(y_true, [v for v in ignore if v is not None], invert=True)
