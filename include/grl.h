@@ -281,15 +281,15 @@ int grl_typed_spmm_bwd_slice(const GrlTypedCsc* g, const float* dZ,
  * v_mfma_f32_32x32x16_bf16 (error at the fp32-rounding level, DESIGN.md
  * §4.2); W's bf16 planes go to `workspace`.  Environment GRL_GEMM_X6=0
  * (read per call) selects v_mfma_f32_32x32x2_f32 instead.
- * When the output tiles cannot fill the chip (small graphs: a 74-node page
- * is one 128-row tile) K is split over workgroups into fp32 slabs in
- * `workspace`, added in split order (deterministic) with bias/ReLU applied
- * once; larger M sums K in the same fixed chunks inside each workgroup, so
- * every element is the same fp32 operations whatever M is (a row of a
- * node-range shard equals the whole graph's row on the same path).
- * grl_linear_fwd_workspace_size() is 0 when neither applies (the
- * workspace may then be NULL), else the bytes the call requires; a large-M
- * call given less falls back to the fp32-MFMA kernel.                    */
+ * Otherwise, calls of >= 256 output tiles walk all of K in one pass; calls
+ * that cannot fill the chip (small graphs: a 74-node page is one 128-row
+ * tile) split K into chunks over workgroups -- sized from K and the call's
+ * tile count, at most 64 -- as fp32 slabs in `workspace`, added in chunk
+ * order (deterministic) with bias/ReLU applied once (slabs over 256 MB in
+ * row blocks).  Each form is M-invariant, and grl_linear_fwd_ex's path_rows
+ * makes every choice for the whole call's rows.
+ * grl_linear_fwd_workspace_size() is 0 when no workspace is needed (it may
+ * then be NULL), else the bytes the call requires.                        */
 size_t grl_linear_fwd_workspace_size(int64_t M, int32_t K, int32_t C);
 int grl_linear_fwd(const float* Z, int64_t ldz, const float* W,
                    const float* bias, float* out, int64_t M, int32_t K,
@@ -301,9 +301,10 @@ int grl_linear_fwd(const float* Z, int64_t ldz, const float* W,
  * row-major (nn.Linear.weight: out = Z W^T + bias, the row-local linears of
  * GraphCNNDropEdge -- emb2, NodeSelfAtten's f / g / h, the RanPAC projection,
  * the classifier -- drop_robust_gcn.py:36-58, robust_gcn.py:81-83).
- * path_rows: the row count the x6-vs-fp32 choice is made for (0 = M); a
- * node-range shard passes the whole graph's, so its rows are bitwise the
- * one-GPU call's.  Workspace: grl_linear_fwd_ex_workspace_size().          */
+ * path_rows: the row count every arithmetic choice is made for (x6 vs fp32,
+ * one pass vs chunk slabs and the chunk size; 0 = M); a node-range shard
+ * passes the whole graph's, so its rows are bitwise the one-GPU call's.
+ * Workspace: grl_linear_fwd_ex_workspace_size().                           */
 size_t grl_linear_fwd_ex_workspace_size(int64_t M, int32_t K, int32_t C,
                                         int64_t path_rows);
 int grl_linear_fwd_ex(const float* Z, int64_t ldz, const float* W,
