@@ -95,9 +95,11 @@ def test_spmm_strided_input_rows():
     assert_bitwise(Z.cpu().numpy(), Zref, "strided forward")
 
 
-def test_csc_matches_oracle():
-    N, L = 700, 6
-    rowptr, colidx, v = host_graph(N, L, 9.0, 77, hub=300, vals=True)
+@pytest.mark.parametrize("N,deg,hub", [(700, 9.0, 300),   # the radix-sort transpose
+                                       (120, 3.0, 40)])    # a page: the one-workgroup transpose
+def test_csc_matches_oracle(N, deg, hub):
+    L = 6
+    rowptr, colidx, v = host_graph(N, L, deg, 77, hub=hub, vals=True)
     g = TypedGraph.from_csr_host(rowptr, colidx, L, DEV, vals=v)
     c = g.csc()
     colptr, zrow, eid, cvals = c_oracle.csr_to_csc(rowptr, colidx, L, N, True, v)
@@ -109,10 +111,11 @@ def test_csc_matches_oracle():
 
 @pytest.mark.parametrize("layout", ["bnln", "bnnl", "pre"])
 @pytest.mark.parametrize("float_vals", [False, True])
-def test_dense_to_csr_matches_oracle(layout, float_vals):
+@pytest.mark.parametrize("B,N", [(3, 37), (4, 400)])  # one-workgroup rowptr scan; hipCUB's (> 8191 segments)
+def test_dense_to_csr_matches_oracle(layout, float_vals, B, N):
     import inputs as gi
 
-    B, N, L = 3, 37, 6
+    L = 6
     A = gi.random_adj_bnln(4, B, N, L, 5.0, float_vals=float_vals)
     if layout == "bnln":
         At = to_dev(A)
