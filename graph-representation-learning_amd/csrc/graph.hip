@@ -122,37 +122,42 @@ __global__ __launch_bounds__(SMALL_T) void small_rowptr_kernel(const int32_t* __
 }
 
 // keys_out / eid = colidx sorted by column, ties in edge order (what the
-// stable radix sort of (colidx, iota) gives): thread per column, its edges
-// counted, offsets scanned, then placed in ascending edge order
+// stable radix sort of (colidx, iota) gives): the packed keys col << 13 | e
+// are distinct, so a bitonic sort of them in LDS (padded to a power of two
+// with keys past every real one) is that stable order
+constexpr int SMALL_BITS = 13;  // SMALL_N = 2^13: column and edge id each fit
+static_assert(SMALL_N == 1 << SMALL_BITS, "packed (column, edge) keys");
 __global__ __launch_bounds__(SMALL_T) void small_csc_sort_kernel(const int32_t* __restrict__ colidx, int nnz,
-                                                                 int num_cols, int32_t* __restrict__ keys_out,
+                                                                 int32_t* __restrict__ keys_out,
                                                                  int32_t* __restrict__ eid) {
-  __shared__ int col_s[SMALL_N];
-  __shared__ int off[SMALL_N];
-  __shared__ int part[SMALL_T];
-  for (int e = threadIdx.x; e < nnz; e += SMALL_T) col_s[e] = colidx[e];
+  __shared__ uint32_t key[SMALL_N];
+  int n = 2;
+  while (n < nnz) n <<= 1;
+  for (int e = threadIdx.x; e < n; e += SMALL_T)
+    key[e] = e < nnz ? ((uint32_t)colidx[e] << SMALL_BITS) | (uint32_t)e : 0xffffffffu;
   __syncthreads();
-  for (int c = threadIdx.x; c < num_cols; c += SMALL_T) {
-    int k = 0;
-    for (int e = 0; e < nnz; ++e) k += col_s[e] == c ? 1 : 0;
-    off[c] = k;
-  }
-  __syncthreads();
-  block_exclusive_scan(off, num_cols, part);
-  for (int c = threadIdx.x; c < num_cols; c += SMALL_T) {
-    int p = off[c];
-    for (int e = 0; e < nnz; ++e)
-      if (col_s[e] == c) {
-        keys_out[p] = c;
-        eid[p] = e;
-        ++p;
+  for (int k = 2; k <= n; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < n; i += SMALL_T) {
+        const int l = i ^ j;
+        if (l > i) {
+          const uint32_t a = key[i], b = key[l];
+          if ((a > b) == ((i & k) == 0)) {
+            key[i] = b;
+            key[l] = a;
+          }
+        }
       }
+      __syncthreads();
+    }
+  }
+  for (int p = threadIdx.x; p < nnz; p += SMALL_T) {
+    keys_out[p] = (int32_t)(key[p] >> SMALL_BITS);
+    eid[p] = (int32_t)(key[p] & (SMALL_N - 1));
   }
 }
 
-bool small_csc(int64_t nnz, int64_t num_cols) {
-  return nnz <= SMALL_N && num_cols <= SMALL_N && nnz * num_cols <= (int64_t)1 << 21;
-}
+bool small_csc(int64_t nnz, int64_t num_cols) { return nnz <= SMALL_N && num_cols <= SMALL_N; }
 
 __global__ void iota_kernel(int32_t* __restrict__ v, int64_t n) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
@@ -427,8 +432,7 @@ extern "C" int grl_csr_to_csc(const GrlTypedCsr* g, int64_t num_cols, int32_t* c
   if (nnz > 0) {
     GRL_CHECK_ARG(g->colidx && zrow && eid, "grl_csr_to_csc: NULL pointer");
     if (small_csc(nnz, num_cols)) {  // a page: one workgroup, the same stable order
-      hipLaunchKernelGGL(small_csc_sort_kernel, dim3(1), dim3(SMALL_T), 0, st, g->colidx, (int)nnz, (int)num_cols,
-                         keys_out, eid);
+      hipLaunchKernelGGL(small_csc_sort_kernel, dim3(1), dim3(SMALL_T), 0, st, g->colidx, (int)nnz, keys_out, eid);
       GRL_LAUNCH_CHECK();
     } else {
       hipLaunchKernelGGL(iota_kernel, dim3(grid_for(nnz)), dim3(256), 0, st, vals_iota, nnz);

@@ -95,10 +95,10 @@ def test_spmm_strided_input_rows():
     assert_bitwise(Z.cpu().numpy(), Zref, "strided forward")
 
 
-@pytest.mark.parametrize("N,deg,hub", [(700, 9.0, 300),   # the radix-sort transpose
+@pytest.mark.parametrize("N,deg,hub", [(1500, 9.0, 300),  # > 8192 edges: the radix-sort transpose
                                        (120, 3.0, 40),     # a page: the one-workgroup transpose
                                        (64, 0.0, 0),       # no edges at all
-                                       (8192, 0.03, 0)])   # 8192 columns: the one-workgroup limit
+                                       (8192, 1.0, 0)])    # 8192 columns and edges: the one-workgroup limit
 def test_csc_matches_oracle(N, deg, hub):
     L = 6
     rowptr, colidx, v = host_graph(N, L, deg, 77, hub=hub, vals=True)
