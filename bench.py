@@ -119,6 +119,19 @@ def spmm_bytes(E, N, L, F, p, idx_bytes=4, ptr_bytes=4):
     return keep * E * F * 4 + idx_bytes * E + ptr_bytes * (N * L + 1) + keep * N * F * 4 + N * (L + 1) * F * 4
 
 
+def _grl_option(name):
+    from grl import get_option
+
+    return get_option(name)
+
+
+def _grl_options(**kw):
+    """grl.options: path options for a block (the chain forms the extras compare against)."""
+    from grl import options
+
+    return options(**kw)
+
+
 def _events(n):
     return [torch.cuda.Event(enable_timing=True) for _ in range(n)]
 
@@ -546,11 +559,11 @@ def traffic_key(wname, world, args, n_loc):
 
 def load_traffic(args, wname, n_loc, world, kernel):
     """HBM bytes per launch of `kernel` from a committed rocprofv3 PMC summary
-    of the same workload at the same world size (profiles/pmc_traffic.json,
-    written by tools/pmc_traffic.py), or None when no such record exists --
-    e.g. every N>1 line: a shard runs the slice kernels over its [own | halo]
-    table, which no PMC pass has measured (one GPU's whole-graph bytes are
-    not its traffic)."""
+    of the same workload at the same world size and shard shape, on the same
+    kernel family (profiles/pmc_traffic.json, written by tools/pmc_traffic.py
+    for one GPU and tools/pmc_rank_traffic.py for a rank's slice kernels over
+    its [own | halo] table), or None when no such record exists (one GPU's
+    whole-graph bytes are never a shard's traffic)."""
     path = os.path.join(HERE, "profiles", "pmc_traffic.json")
     if not os.path.exists(path):
         return None
@@ -558,7 +571,8 @@ def load_traffic(args, wname, n_loc, world, kernel):
         rec = json.load(open(path)).get(traffic_key(wname, world, args, n_loc))
     except (OSError, ValueError):  # unreadable summary: report traffic as unmeasured
         return None
-    if not rec or not str(kernel).startswith(rec.get("kernel", "").replace(" ", "").split("<")[0]):
+    family = rec.get("kernel", "").replace(" ", "").split("<")[0].split("(")[0] if rec else ""
+    if not family or not str(kernel).replace(" ", "").startswith(family):
         return None
     return rec.get("hbm_bytes_per_launch")
 
@@ -731,7 +745,7 @@ def extras(args, graph, X_full, L, F, dev, E_loc, n_loc):
     ms = _time(lambda: linear_fwd(Zd, W, b, True), iters)
     flops = 2.0 * Zd.shape[0] * Zd.shape[1] * F
     path = ("x6: fp32 split into 3 bf16 parts, 6 products on v_mfma_f32_32x32x16_bf16 (DESIGN 4.2)"
-            if os.environ.get("GRL_GEMM_X6", "1") != "0" else "fp32 MFMA v_mfma_f32_32x32x2_f32")
+            if _grl_option("gemm_x6") != 0 else "fp32 MFMA v_mfma_f32_32x32x2_f32")
     res["linear_mfma_fwd"] = {"ms": ms, "TFLOPs_fp32_equivalent": flops / (ms * 1e-3) / 1e12,
                               "vs_f32_mfma_peak": flops / (ms * 1e-3) / 1e12 / F32_MFMA_PEAK_TFS, "path": path}
     from grl.ops import linear_bwd_data, linear_bwd_weight, relu_grad
@@ -776,13 +790,10 @@ def extras(args, graph, X_full, L, F, dev, E_loc, n_loc):
                     max(3, iters // 2), warm=2),
         "path": "keeps X, not Z (7.2 GB less held): fwd one kernel without Z; bwd dX one kernel that also writes "
                 "G_s = A_s^T g, dW_s = X^T G_s (no re-aggregation)"}
-    os.environ["GRL_GRAPHCONV_FUSED_BWD"] = "0"
-    try:
+    with _grl_options(graphconv_fused_bwd=0):
         res["graphconv_layer_fwd_bwd_p0.3_chain_bwd"] = {
             "ms": _time(layer, max(3, iters // 2), warm=2),
             "path": "bwd dX as autograd's chain: dZ = g W^T (x6 GEMM), then the CSC gather"}
-    finally:
-        del os.environ["GRL_GRAPHCONV_FUSED_BWD"]
     res["graphconv_layer_fwd_bwd_p0.3_two_ops"] = {"ms": _time(layer_two_ops, max(3, iters // 2), warm=2)}
     from grl.ops import graph_conv_bwd_data, linear_bwd_data, spmm_backward
 
@@ -801,8 +812,7 @@ def extras(args, graph, X_full, L, F, dev, E_loc, n_loc):
     fused = graph_conv_infer(Xe, graph, W, b, True)
     res["graphconv_infer_fwd"] = {"ms": _time(lambda: graph_conv_infer(Xe, graph, W, b, True), iters, warm=2),
                                   "path": "one kernel (graphconv_ws_kernel): gather waves + MFMA waves, Z in LDS"}
-    os.environ["GRL_GRAPHCONV_FUSED"] = "0"
-    try:
+    with _grl_options(graphconv_fused=0):
         two = graph_conv_infer(Xe, graph, W, b, True)
         res["graphconv_infer_fwd_two_kernels"] = {
             "ms": _time(lambda: graph_conv_infer(Xe, graph, W, b, True), iters, warm=2),
@@ -810,8 +820,6 @@ def extras(args, graph, X_full, L, F, dev, E_loc, n_loc):
         res["graphconv_infer_fwd_two_kernels_z_chunks_1GiB"] = {
             "ms": _time(lambda: graph_conv_infer(Xe, graph, W, b, True, max_workspace_bytes=1 << 30), iters,
                         warm=2)}
-    finally:
-        del os.environ["GRL_GRAPHCONV_FUSED"]
     del fused, two, Xe, Xl, Wp, bp
     torch.cuda.empty_cache()
     res["graphconv_wide_layers"] = wide_layers(graph, dev, max(3, iters // 2))
@@ -824,7 +832,7 @@ def wide_layers(graph, dev, iters):
     2C = 512 from cat[g1, g2], drop_robust_gcn.py:84-85) and a d = 512 layer
     (C5's width; gcn1/gcn2 at F = C = 512).  Per shape: inference (one
     grl_graphconv_fwd call) and the layer fwd+bwd through graph_conv, one
-    kernel vs GRL_GRAPHCONV_FUSED=0 / GRL_GRAPHCONV_FUSED_BWD=0 (SpMM writing
+    kernel vs the graphconv_fused / graphconv_fused_bwd path options at 0 (SpMM writing
     Z + x6 GEMM; dZ GEMM + CSC gather); forward bitwise checked."""
     from grl import DropEdge
     from grl.ops import graph_conv, graph_conv_infer
@@ -847,14 +855,10 @@ def wide_layers(graph, dev, iters):
         one = graph_conv_infer(X, gl, W, b, True)
         r["infer_one_kernel_ms"] = _time(lambda: graph_conv_infer(X, gl, W, b, True), iters)
         r["layer_fwd_bwd_one_kernel_ms"] = _time(layer, iters, warm=2)
-        os.environ["GRL_GRAPHCONV_FUSED"] = "0"
-        os.environ["GRL_GRAPHCONV_FUSED_BWD"] = "0"
-        try:
+        with _grl_options(graphconv_fused=0, graphconv_fused_bwd=0):
             r["infer_bitwise_equal_to_chain"] = bool(torch.equal(graph_conv_infer(X, gl, W, b, True), one))
             r["infer_chain_ms"] = _time(lambda: graph_conv_infer(X, gl, W, b, True), iters)
             r["layer_fwd_bwd_chain_ms"] = _time(layer, iters, warm=1)
-        finally:
-            del os.environ["GRL_GRAPHCONV_FUSED"], os.environ["GRL_GRAPHCONV_FUSED_BWD"]
         r["kernel"] = ("graphconv_ws_kernel: two 256-column virtual segments per segment" +
                        (", 4 gather + 8 MFMA waves (C = 512)" if C > 256 else ", 8 gather + 4 MFMA waves"))
         out[name] = r

@@ -1806,35 +1806,20 @@ __global__ void attn_slab_sum_kernel(const float* __restrict__ slab, int64_t n, 
 
 enum AttnPass { PASS_FWD, PASS_BWD_Q, PASS_BWD_KV };
 
-// GRL_ATTN_X6=0 (read per call) keeps the fp32-MFMA kernels
-bool attn_x6_enabled() {
-  const char* e = getenv("GRL_ATTN_X6");
-  return !(e && e[0] == '0');
-}
+// path option attn_x6 = 0 keeps the fp32-MFMA kernels
+bool attn_x6_enabled() { return opt(OPT_ATTN_X6) != 0; }
 
-// GRL_ATTN_FWD8=0 (read per call) keeps the pipelined forward on 4-wave workgroups (A/B aid)
-bool attn_fwd8_enabled() {
-  const char* e = getenv("GRL_ATTN_FWD8");
-  return !(e && e[0] == '0');
-}
+// path option attn_fwd8 = 0 keeps the pipelined forward on 4-wave workgroups (A/B aid)
+bool attn_fwd8_enabled() { return opt(OPT_ATTN_FWD8) != 0; }
 
-// GRL_ATTN_DH8=0 (read per call) keeps dH on 4-wave workgroups (A/B aid)
-bool attn_dh8_enabled() {
-  const char* e = getenv("GRL_ATTN_DH8");
-  return !(e && e[0] == '0');
-}
+// path option attn_dh8 = 0 keeps dH on 4-wave workgroups (A/B aid)
+bool attn_dh8_enabled() { return opt(OPT_ATTN_DH8) != 0; }
 
-// GRL_ATTN_FUSED_DQ=0 (read per call) keeps the separate dQ kernel (A/B aid)
-bool attn_fused_dq_enabled() {
-  const char* e = getenv("GRL_ATTN_FUSED_DQ");
-  return !(e && e[0] == '0');
-}
+// path option attn_fused_dq = 0 keeps the separate dQ kernel (A/B aid)
+bool attn_fused_dq_enabled() { return opt(OPT_ATTN_FUSED_DQ) != 0; }
 
-// GRL_ATTN_PIPE=0 (read per call) keeps the unpipelined x6 forward (A/B aid)
-bool attn_pipe_enabled() {
-  const char* e = getenv("GRL_ATTN_PIPE");
-  return !(e && e[0] == '0');
-}
+// path option attn_pipe = 0 keeps the unpipelined x6 forward (A/B aid)
+bool attn_pipe_enabled() { return opt(OPT_ATTN_PIPE) != 0; }
 
 template <int DKP, int NT>
 int launch_attn(AttnPass pass, const AttnArgs& a0, int64_t B, int S, hipStream_t st) {
@@ -2063,8 +2048,8 @@ static size_t attn_qslab_x_bytes(int64_t B, int64_t N) {  // one key workgroup's
   return (size_t)B * (size_t)(ceil_div(N, 32) * 32) * 16 * 4;
 }
 static int64_t attn_qslab_chunk(int64_t B, int64_t N) {  // key workgroups per fused launch
-  const char* e = getenv("GRL_ATTN_QSLAB_MAX");  // test aid: a smaller chunk budget (bytes)
-  const size_t cap = e && atoll(e) > 0 ? (size_t)atoll(e) : kAttnQslabMax;
+  const int64_t o = opt(OPT_ATTN_QSLAB_MAX);  // test aid: a smaller chunk budget (bytes)
+  const size_t cap = o > 0 ? (size_t)o : kAttnQslabMax;
   const int64_t all = ceil_div(N, KQ_KEYS), fit = (int64_t)(cap / attn_qslab_x_bytes(B, N));
   if (fit >= all) return all;
   const int64_t cus = device_cu_count();  // one workgroup per CU: whole rounds of the grid

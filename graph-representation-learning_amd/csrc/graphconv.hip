@@ -10,7 +10,7 @@
 //  * graphconv_ws_kernel (default): persistent, one workgroup per CU, gather
 //    waves and MFMA waves specialised and coupled by an LDS ring of Z tiles
 //    (64 rows x 128 columns); see its comment below;
-//  * graphconv_fused_kernel (GRL_FG_WS=0): 32-row tiles, every wave
+//  * graphconv_fused_kernel (fg_ws = 0): 32-row tiles, every wave
 //    alternates gather and multiply phases, three workgroups per CU.
 // Shared pieces: the gather sums a wave's rows' segment-t neighbour rows
 // (one float4 per lane, one 1 KB row per wave-instruction, the rows' edge
@@ -28,6 +28,21 @@
 #include "grl_internal.h"
 
 #include <cstdlib>
+#include <mutex>
+#include <vector>
+
+// Diagnostic switches (GRL_WS_STAMP, GRL_WS_ONLY_ROLE, GRL_WS_DIAG_*, GRL_WS_NOIL,
+// GRL_WS_WHATIF below) are honoured only in diagnostic builds, which
+// tools/build_diag.sh and tools/ws_regs.sh make with -DGRL_DIAG; a product
+// build ignores them.
+#ifndef GRL_DIAG
+#undef GRL_WS_STAMP
+#undef GRL_WS_ONLY_ROLE
+#undef GRL_WS_DIAG_LB
+#undef GRL_WS_DIAG_ONE
+#undef GRL_WS_WHATIF
+#undef GRL_WS_NOIL
+#endif
 
 namespace grl {
 namespace {
@@ -438,7 +453,7 @@ constexpr int WS_NB = (140 * 1024) / (WS_SLOT * 4);  // ring slots that ~140 KB 
 #ifndef GRL_WS_U16
 #define GRL_WS_U16 12
 #endif
-constexpr int WS_SPIN = 1 << 24;           // bounded waits (~0.5 s of s_sleep 1); GRL_WS_SPIN overrides
+constexpr int WS_SPIN = 1 << 24;           // bounded waits (~0.5 s of s_sleep 1); the ws_spin path option overrides
 constexpr int WS_STATUS_TIMEOUT = 1;       // status bit: a bounded wait ran out (results invalid)
 
 // GRL_WS_STAMP=1 (diagnostic builds only): every wave adds up the cycles it
@@ -450,6 +465,13 @@ constexpr int WS_STATUS_TIMEOUT = 1;       // status bit: a bounded wait ran out
 // 1 = compile the gather role alone, 2 = the MFMA role alone
 #ifndef GRL_WS_ONLY_ROLE
 #define GRL_WS_ONLY_ROLE 0
+#endif
+// GRL_WS_WHATIF (timing-only diagnostic builds, wrong results): 1 = the MFMA
+// waves re-read two steps of W (L2-hot) instead of the stream, 2 = no A split,
+// 4 = the gather alone (MFMA waves only release slots), 8 = the MFMA side
+// alone (gather waves store zeros for the typed segments)
+#ifndef GRL_WS_WHATIF
+#define GRL_WS_WHATIF 0
 #endif
 #if GRL_WS_STAMP
 __device__ unsigned long long g_ws_dbg[1024 * 12 * 2];
@@ -655,6 +677,12 @@ __global__ __launch_bounds__(GRL_WS_DIAG_LB) void graphconv_ws_kernel(
               }
             }
           } else {
+#if GRL_WS_WHATIF & 8
+            // what-if: the MFMA side alone (typed segments are never gathered)
+            if (!claim()) return;
+            for (int r = 0; r < RW; ++r) flush(r, zero4());
+            if (false)
+#endif
 #pragma unroll 1
             for (int gi = 0; gi < NG; ++gi) {
               // the next list (next group; else the next segment's first, unless the next virtual part
@@ -759,6 +787,9 @@ __global__ __launch_bounds__(GRL_WS_DIAG_LB) void graphconv_ws_kernel(
     const uint16_t* wbase = Wf + (int64_t)(c * WS_CB) * 3 * FG_FRAG;
     const int loff = lane * 8;
     auto load_b = [&](bf16x8_t (&bb)[WS_CB][3], int gstep) {
+#if GRL_WS_WHATIF & 1
+      gstep = gstep & 1;  // what-if (timing only): a 2-step W stream that stays in L2
+#endif
       const uint16_t* w = wbase + (int64_t)gstep * WSTEP;
 #pragma unroll
       for (int j = 0; j < WS_CB; ++j)
@@ -791,6 +822,12 @@ __global__ __launch_bounds__(GRL_WS_DIAG_LB) void graphconv_ws_kernel(
       v1 = *reinterpret_cast<const float4*>(ar + 4);
     };
     auto split_a = [&](const float4& v0, const float4& v1, bf16x8_t (&a)[3]) {
+#if GRL_WS_WHATIF & 2
+      a[0] = __builtin_bit_cast(bf16x8_t, make_uint4(__float_as_uint(v0.x), __float_as_uint(v0.y), __float_as_uint(v1.x), __float_as_uint(v1.y)));
+      a[1] = __builtin_bit_cast(bf16x8_t, make_uint4(__float_as_uint(v0.z), __float_as_uint(v0.w), __float_as_uint(v1.z), __float_as_uint(v1.w)));
+      a[2] = a[0];  // what-if (timing only): no split VALU
+      return;
+#endif
       uint2 p0, p1, p2, r0, r1, r2;
       split3(v0, p0, p1, p2);
       split3(v1, r0, r1, r2);
@@ -800,6 +837,9 @@ __global__ __launch_bounds__(GRL_WS_DIAG_LB) void graphconv_ws_kernel(
     };
     // scheduling hint for the region just written: 2 MFMAs, then 3 VALU / 1 MFMA
     auto interleave = [&]() {
+#ifdef GRL_WS_NOIL
+      if (PROD == 4) return;  // A/B: no hand-placed interleave at C > 256 (two MFMA waves per SIMD)
+#endif
       __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
 #pragma unroll
       for (int q = 0; q < 10; ++q) {
@@ -817,6 +857,10 @@ __global__ __launch_bounds__(GRL_WS_DIAG_LB) void graphconv_ws_kernel(
         const int slot = u % WS_NB, g = u / WS_NB;
         const float* zs = ring + slot * WS_SLOT;
         if (!wait_ge(&produced[slot], PROD * (g + 1), &waited, spin_limit, status)) return;
+#if GRL_WS_WHATIF & 4
+        if (lane == 0) lds_add_rel(&consumed[slot], 1);  // what-if: the gather alone
+        continue;
+#endif
         // Software-pipelined by row block: the split of the next row block's
         // A fragments (VALU) is interleaved with the current row block's 12
         // MFMAs (an MFMA holds the SIMD's issue for 8 of its 32 cycles; the
@@ -908,17 +952,14 @@ extern "C" int grl_debug_ws_stats(unsigned long long* host, int64_t n) {
 }
 #endif
 
-// GRL_GRAPHCONV_FUSED=0 (read on every call) keeps grl_graphconv_fwd on the
+// The graphconv_fused path option 0 keeps grl_graphconv_fwd on the
 // two-kernel path (A/B aid and tests).
-bool graphconv_fused_enabled() {
-  const char* e = getenv("GRL_GRAPHCONV_FUSED");
-  return !(e && e[0] == '0');
-}
+bool graphconv_fused_enabled() { return opt(OPT_GRAPHCONV_FUSED) != 0; }
 
 // The gathered width F: one virtual segment (64, 128, 256) or 2 / 4 of 256
 // columns; the output width C <= 512 (C > 256: 4 gather + 8 MFMA waves); L
 // <= 7 (a gather wave's rowptr window holds RW L + 1 entries in 1 or 2
-// registers).  The phase-alternating kernel (GRL_FG_WS=0) takes F <= 256, C
+// registers).  The phase-alternating kernel (fg_ws = 0) takes F <= 256, C
 // <= 256 only; other shapes always run the persistent one.
 bool graphconv_fused_shape_ok(int F, int C, int L) {
   return (F == 64 || F == 128 || F == 256 || F == 512 || F == 1024) && C >= 1 && C <= 512 && L >= 1 && L <= 7;
@@ -935,9 +976,8 @@ static int* ws_status(void* ws, int64_t K, int C) {
 }
 
 static int ws_spin_limit() {
-  const char* e = getenv("GRL_WS_SPIN");  // test / diagnostic aid: a tiny bound forces the timeout path
-  const long v = e ? strtol(e, nullptr, 10) : 0;
-  return v > 0 && v < (1L << 30) ? (int)v : WS_SPIN;
+  const int64_t v = opt(OPT_WS_SPIN);  // test / diagnostic aid: a tiny bound forces the timeout path
+  return v > 0 ? (int)v : WS_SPIN;
 }
 
 // A persistent kernel whose bounded wait ran out left its outputs partly
@@ -945,7 +985,7 @@ static int ws_spin_limit() {
 // follow-up kernel fills the call's outputs with NaN when the call's status
 // word is set, and ORs the entry point's bit into the per-device sticky
 // word, which grl_check() reads and clears at the caller's next sync point.
-// GRL_WS_STATUS=sync (debug aid) makes an eager call wait for its kernel and
+// ws_status_sync = 1 (debug aid) makes an eager call wait for its kernel and
 // return GRL_E_TIMEOUT itself, as round 3's entry points did.
 __device__ int g_grl_sticky;  // WS_WHO_* bits of the calls whose outputs were poisoned
 
@@ -966,10 +1006,10 @@ static const char* who_name(int who) {
 }
 
 static int graphconv_status(const int* status, float* a, int64_t na, float* b, int64_t nb, hipStream_t st, int who) {
-  const char* mode = getenv("GRL_WS_STATUS");
+  const bool sync = opt(OPT_WS_STATUS_SYNC) != 0;
   hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (mode && strcmp(mode, "sync") == 0) GRL_HIP(hipStreamIsCapturing(st, &cs));
-  if (!(mode && strcmp(mode, "sync") == 0) || cs != hipStreamCaptureStatusNone) {
+  if (sync) GRL_HIP(hipStreamIsCapturing(st, &cs));
+  if (!sync || cs != hipStreamCaptureStatusNone) {
     hipLaunchKernelGGL(ws_poison_kernel, dim3(1024), dim3(256), 0, st, status, a, na, b, b ? nb : 0, who);
     GRL_LAUNCH_CHECK();
     return GRL_OK;
@@ -1040,9 +1080,8 @@ int graphconv_fused_fwd(const GrlTypedCsr* g, const float* X, int64_t ldx, int F
   GRL_CHECK_ARG(tiles < 2147483647LL, "grl_graphconv_fwd: too many row tiles");
   const DropDev d = to_dev(de);
   const bool v = g->vals != nullptr;
-  const char* wse = getenv("GRL_FG_WS");
   // the persistent kernel (Z out, wide shapes and row-range views: only it)
-  if (!(wse && wse[0] == '0') || Z || F > 256 || C > 256 || g->self_row0 != 0) {
+  if (opt(OPT_FG_WS) != 0 || Z || F > 256 || C > 256 || g->self_row0 != 0) {
     const int64_t ldz = K;
     const int64_t ws_tiles = ceil_div(M, WS_R);
     const int64_t grid = std::min<int64_t>(ws_tiles, (int64_t)device_cu_count());
@@ -1122,16 +1161,47 @@ __global__ void sticky_take_kernel(int* __restrict__ host_word) {
 }  // namespace
 }  // namespace grl
 
+namespace grl {
+namespace {
+// grl_check's pinned host words: one per host thread at a time (virtual ranks
+// check concurrently).  A thread takes a word from a process-wide free list
+// (allocating only when the list is empty) and gives it back when it exits,
+// so a session that starts fresh threads per run reuses the same few words
+// instead of leaking one per thread.  Portable + coherent: usable whichever
+// device a later check targets.
+std::mutex g_word_mu;
+std::vector<int*> g_free_words;
+struct CheckWord {
+  int* p = nullptr;
+  ~CheckWord() {
+    if (p) {
+      std::lock_guard<std::mutex> lk(g_word_mu);
+      g_free_words.push_back(p);
+    }
+  }
+};
+}  // namespace
+}  // namespace grl
+
 extern "C" int grl_check(grl_stream_t stream) {
   using namespace grl;
   hipStream_t st = as_stream(stream);
-  // one pinned word per host thread (virtual ranks check concurrently), allocated once
-  thread_local int* word = nullptr;
-  if (!word) {
-    void* p = nullptr;
-    GRL_HIP(hipHostMalloc(&p, sizeof(int), hipHostMallocCoherent));
-    word = static_cast<int*>(p);
+  thread_local CheckWord held;
+  if (!held.p) {
+    {
+      std::lock_guard<std::mutex> lk(g_word_mu);
+      if (!g_free_words.empty()) {
+        held.p = g_free_words.back();
+        g_free_words.pop_back();
+      }
+    }
+    if (!held.p) {
+      void* p = nullptr;
+      GRL_HIP(hipHostMalloc(&p, sizeof(int), hipHostMallocCoherent | hipHostMallocPortable));
+      held.p = static_cast<int*>(p);
+    }
   }
+  int* const word = held.p;
   *reinterpret_cast<volatile int*>(word) = 0;
   hipLaunchKernelGGL(sticky_take_kernel, dim3(1), dim3(64), 0, st, word);
   GRL_LAUNCH_CHECK();

@@ -139,4 +139,26 @@ struct TraceRange {
 // Number of CUs of the current device (cached per process).
 int device_cu_count();
 
+// Path options (grl_set_option / grl_get_option, include/grl.h): the test and
+// A/B hooks that select among kernel forms of one entry point.  Defaults are
+// the production choices; nothing in the library reads the environment.
+enum GrlOpt {
+  OPT_GEMM_X6,              // 1: split-bf16 (x6) GEMMs where sized for them; 0: fp32-MFMA kernels
+  OPT_GRAPHCONV_FUSED,      // 1: one-kernel GraphConv forward where eligible; 0: SpMM + GEMM
+  OPT_GRAPHCONV_FUSED_BWD,  // 1: one-kernel GraphConv data gradient (read by the host layer)
+  OPT_FG_WS,                // 1: persistent warp-specialized one-kernel form; 0: phase-alternating
+  OPT_SPMM_WIDE,            // -1: whole-row waves for tables > 12 GB; 1 / 0: always / never
+  OPT_SPMM_BLOCKS_PER_CU,   // SpMM workgroups per CU (24)
+  OPT_ATTN_X6,              // 1: x6 attention kernels; 0: fp32-MFMA kernels
+  OPT_ATTN_FWD8,            // 1: 8-wave pipelined forward; 0: 4-wave
+  OPT_ATTN_DH8,             // 1: 8-wave dH pass; 0: 4-wave
+  OPT_ATTN_FUSED_DQ,        // 1: dQ folded into the dK pass; 0: separate dQ kernel
+  OPT_ATTN_PIPE,            // 1: software-pipelined x6 forward; 0: unpipelined
+  OPT_ATTN_QSLAB_MAX,       // fused dK/dQ slab budget in bytes (0: 24 GiB)
+  OPT_WS_SPIN,              // persistent kernels' bounded-wait limit (0: 2^24 sleeps)
+  OPT_WS_STATUS_SYNC,       // 1: an eager one-kernel call checks its own status (debug)
+  OPT_COUNT
+};
+int64_t opt(GrlOpt o);
+
 }  // namespace grl

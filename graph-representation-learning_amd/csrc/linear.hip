@@ -1110,13 +1110,10 @@ int launch_gemm256p(GemmArgs a, int splits, hipStream_t st) {
   return GRL_OK;
 }
 
-// Split-bf16 ("x6") path selection.  GRL_GEMM_X6=0 keeps the fp32-MFMA
-// kernels (A/B aid and tests; read on every call, so a workspace query and
-// the call it sizes must see the same setting).
-bool x6_enabled() {
-  const char* e = getenv("GRL_GEMM_X6");
-  return !(e && e[0] == '0');
-}
+// Split-bf16 ("x6") path selection.  The gemm_x6 path option 0 keeps the
+// fp32-MFMA kernels (A/B aid and tests; a workspace query and the call it
+// sizes must see the same setting).
+bool x6_enabled() { return opt(OPT_GEMM_X6) != 0; }
 
 bool x6_shape_ok(int64_t M, int64_t N, int64_t K) {
   return x6_enabled() && K % X6_K == 0 && K > 0 && M >= 4 && N >= 4 &&

@@ -100,16 +100,9 @@ __device__ __forceinline__ void vstore(float* p, const float& v) {
 // 6.24 vs 6.41-6.67 ms, p=0.3 forward and CSC backward 2-3 % faster, C4
 // 28.3-28.9 vs 29.1-29.6 ms, C5 125.9 vs 130.3 ms; 20 and 26 are slower
 // than either (6.45-6.55 ms at C3), 22 and 28 close to 24.  The
-// GRL_SPMM_BLOCKS_PER_CU environment variable overrides it (tuning aid, e.g.
-// to leave room for a concurrent GEMM on another stream).
-int spmm_blocks_per_cu() {
-  static const int v = [] {
-    const char* e = getenv("GRL_SPMM_BLOCKS_PER_CU");
-    const int x = e ? atoi(e) : 0;
-    return x > 0 && x <= 64 ? x : 24;
-  }();
-  return v;
-}
+// spmm_blocks_per_cu path option overrides it (tuning aid, e.g. to leave
+// room for a concurrent GEMM on another stream).
+int spmm_blocks_per_cu() { return (int)opt(OPT_SPMM_BLOCKS_PER_CU); }
 
 // Device view of a split plan (all null / zero when the graph is not split).
 struct SplitDev {
@@ -555,12 +548,12 @@ struct LaunchShape {
 };
 
 // Gathered tables above 12 GB keep a whole row (up to 512 columns) in one
-// wave.  GRL_SPMM_WIDE=1/0 forces whole-row / 256-column waves (A/B aid and
-// tests; read on every launch).
+// wave.  The spmm_wide path option 1 / 0 forces whole-row / 256-column waves
+// (A/B aid and tests).
 int64_t wide_table_bytes() {
-  const char* e = getenv("GRL_SPMM_WIDE");
-  if (e && e[0] == '1') return 0;
-  if (e && e[0] == '0') return INT64_MAX;
+  const int64_t w = opt(OPT_SPMM_WIDE);
+  if (w == 1) return 0;
+  if (w == 0) return INT64_MAX;
   return (int64_t)12 << 30;
 }
 

@@ -78,6 +78,10 @@ class BaseDataLoader:
                 batch_size = max(1, batch_size // replicas)  # the reference can reach 0 here
                 sampler = DistributedSampler(dataset, num_replicas=replicas, rank=rank,
                                              shuffle=bool(data_config.get("shuffle")))
+            elif node_range_parallel(self.config) and bool(data_config.get("shuffle")):
+                # node_range: every rank must see the SAME batch each step, so the config's shuffle runs as
+                # one replica's sampler with a fixed seed on every rank (set_epoch reshuffles per epoch)
+                sampler = DistributedSampler(dataset, num_replicas=1, rank=0, shuffle=True, drop_last=False)
             return DataLoader(dataset, batch_size=batch_size, num_workers=data_config.get("num_workers", 0),
                               drop_last=bool(data_config.get("drop_last")),
                               pin_memory=bool(data_config.get("pin_memory")) and torch.cuda.is_available(),

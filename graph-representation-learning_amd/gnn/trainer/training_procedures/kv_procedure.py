@@ -45,8 +45,11 @@ def batch_graph(batch: Dict[str, Any], device: torch.device, num_types: int = 6)
 
 def sharded_graph_cached(owner, graph: TypedGraph, args: Dict[str, Any]):
     """This rank's node-range shard of `graph` (graph_parallel: node_range),
-    from a small per-owner cache keyed on the graph's structure
-    (ShardedGraph.cache_key): a graph met again reuses its shard plan."""
+    from a small per-owner cache bucketed on the graph's structure
+    (ShardedGraph.cache_key) and confirmed by exact equality of the CSR
+    arrays (ShardedGraph.same_graph): a graph met again reuses its shard
+    plan; a different graph whose key collides gets its own plan.  Every
+    rank holds the same graph, so every rank takes the same branch."""
     from collections import OrderedDict
 
     from grl.dist import ShardedGraph
@@ -54,10 +57,12 @@ def sharded_graph_cached(owner, graph: TypedGraph, args: Dict[str, Any]):
     kw = {"balance": args.get("balance", "edges"), "halo": args.get("halo", "auto")}
     cache = owner.__dict__.setdefault("_shard_cache", OrderedDict())
     key = ShardedGraph.cache_key(graph, **kw)
-    sg = cache.get(key)
-    if sg is None:
+    hit = cache.get(key)
+    if hit is not None and ShardedGraph.same_graph(hit[1], graph):
+        sg = hit[0]
+    else:
         sg = ShardedGraph.from_graph(graph, **kw)
-        cache[key] = sg
+        cache[key] = (sg, graph)
         while len(cache) > 4:
             cache.popitem(last=False)
     cache.move_to_end(key)
@@ -161,7 +166,10 @@ class KVProcedure(BaseProcedure):
         predicts = self.activator(logits).argmax(dim=-1)
         scores, items = self._get_metric_scores(predicts, targets, item_name="Node classification")
         scores["loss"] = loss.item()
-        device_check(self.device)  # the step already synced: surface a kernel's stream-ordered failure
+        if not torch.is_grad_enabled():
+            # validation: the step already synced, surface a kernel's stream-ordered failure here (a
+            # training step checks once, after backward: _run_train_step)
+            device_check(self.device)
         return loss, scores, items
 
     def _step_process_shard(self, batch: Dict[str, Any]):
@@ -193,7 +201,8 @@ class KVProcedure(BaseProcedure):
         predicts = self.activator(logits_all).argmax(dim=-1)
         scores, items = self._get_metric_scores(predicts, targets, item_name="Node classification")
         scores["loss"] = float(all_reduce_sum(loss.detach().clone().reshape(1)).item())
-        device_check(self.device)
+        if not torch.is_grad_enabled():  # as _step_process: training steps check after backward
+            device_check(self.device)
         return loss, scores, items
 
     def _shard_loss(self, logits: torch.Tensor, t_rows: torch.Tensor, targets: torch.Tensor) -> torch.Tensor:
@@ -226,6 +235,9 @@ class KVProcedure(BaseProcedure):
                 predicts = self.activator(logits).argmax(dim=-1)
                 scores, items = self._get_metric_scores(predicts, targets, item_name="Node classification")
                 scores["loss"] = loss.item()
+                # a captured step replays forward .. optimizer step as one graph: its stream-ordered
+                # failure report is read only here, AFTER the update (a poisoned step's weights are
+                # NaN by then; the error still stops training)
                 device_check(self.device)
                 return scores, items
         self.model.train()

@@ -128,6 +128,8 @@ SIGNATURES = {
     "grl_version": (ctypes.c_char_p, []),
     "grl_last_error": (ctypes.c_char_p, []),
     "grl_check": (_c_i32, [_c_vp]),
+    "grl_set_option": (_c_i32, [ctypes.c_char_p, _c_i64]),
+    "grl_get_option": (_c_i32, [ctypes.c_char_p, _P(_c_i64)]),
     "grl_trace_push": (None, [ctypes.c_char_p]),
     "grl_trace_pop": (None, []),
     "grl_dropedge_init": (_c_i32, [_P(GrlDropEdge), ctypes.c_float, _c_u64, _c_u64, _c_i32]),
@@ -227,6 +229,32 @@ def check(rc: int, what: str) -> None:
 
 def call(name: str, *args) -> None:
     check(getattr(lib(), name)(*args), name)
+
+
+def set_option(name: str, value: int) -> None:
+    """grl_set_option: one of the library's path options (test / A-B hooks
+    that pick among kernel forms; include/grl.h)."""
+    call("grl_set_option", name.encode(), int(value))
+
+
+def get_option(name: str) -> int:
+    v = _c_i64(0)
+    call("grl_get_option", name.encode(), ctypes.byref(v))
+    return int(v.value)
+
+
+@contextlib.contextmanager
+def options(**kw):
+    """Set path options for the duration of a block, then restore them:
+    `with grl.options(gemm_x6=0): ...`."""
+    saved = {k: get_option(k) for k in kw}
+    try:
+        for k, v in kw.items():
+            set_option(k, v)
+        yield
+    finally:
+        for k, v in saved.items():
+            set_option(k, v)
 
 
 @contextlib.contextmanager

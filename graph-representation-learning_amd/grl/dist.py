@@ -1111,17 +1111,35 @@ class ShardedGraph:
 
     @staticmethod
     def cache_key(graph: TypedGraph, **kw):
-        """A key identifying `graph`'s structure (rows, types, edges and a
-        checksum of its CSR arrays) plus the sharding options: every rank
-        computes the same key from the same graph, so a procedure that meets
-        one large graph step after step reuses its shard plan instead of
-        rebuilding it (from_graph exchanges index lists)."""
+        """A BUCKET key for `graph`'s structure (rows, types, edges and
+        position-weighted checksums of rowptr, colidx and the bits of vals)
+        plus the sharding options: every rank computes the same key from the
+        same graph, so a procedure that meets one large graph step after step
+        reuses its shard plan instead of rebuilding it (from_graph exchanges
+        index lists).  Two graphs can still share a key; a cache hit must be
+        confirmed with same_graph (sharded_graph_cached does)."""
         L = graph.num_types
-        idx = torch.arange(1, graph.colidx.numel() + 1, device=graph.colidx.device, dtype=torch.int64)
-        chk = torch.stack([(graph.colidx.to(torch.int64) * idx).sum(), graph.rowptr.to(torch.int64).sum(),
-                           (graph.vals.double().sum() * 1e6).to(torch.int64) if graph.vals is not None
-                           else torch.zeros((), dtype=torch.int64, device=graph.colidx.device)]).tolist()
-        return (graph.num_rows, L, int(graph.colidx.numel()), tuple(chk), tuple(sorted(kw.items())))
+        dev = graph.colidx.device
+
+        def wsum(t: torch.Tensor) -> int:  # sum_i t[i] * (2 i + 1) * golden, wrapped in int64
+            t = t.reshape(-1).to(torch.int64)
+            w = torch.arange(t.numel(), device=dev, dtype=torch.int64) * 2 + 1
+            return int((t * w * 0x9E3779B1).sum())
+
+        vbits = graph.vals.contiguous().view(torch.int32) if graph.vals is not None else None
+        chk = (wsum(graph.rowptr), wsum(graph.colidx), wsum(vbits) if vbits is not None else 0)
+        return (graph.num_rows, L, int(graph.colidx.numel()), chk, tuple(sorted(kw.items())))
+
+    @staticmethod
+    def same_graph(a: TypedGraph, b: TypedGraph) -> bool:
+        """Exact equality of two graphs' CSR arrays (the confirmation of a
+        cache_key hit: O(E) on the device, about the checksum's cost)."""
+        if (a.num_rows, a.num_types, a.colidx.numel()) != (b.num_rows, b.num_types, b.colidx.numel()):
+            return False
+        if (a.vals is None) != (b.vals is None):
+            return False
+        return bool(torch.equal(a.rowptr, b.rowptr) and torch.equal(a.colidx, b.colidx)
+                    and (a.vals is None or torch.equal(a.vals.view(torch.int32), b.vals.view(torch.int32))))
 
     @property
     def global_rows(self) -> int:
@@ -1656,7 +1674,7 @@ class ShardedGraph:
             return graph_conv(self.exchange(X_loc), self.graph.with_dropedge(dropedge), layer.h_weights, layer.bias,
                               relu=relu)
         Z = self.aggregate(X_loc, dropedge, chunks)
-        return graph_linear(Z, layer.h_weights, layer.bias, relu=relu)
+        return graph_linear(Z, layer.h_weights, layer.bias, relu=relu, path_rows=self.global_rows)
 
 
 class _ShardedNodeAttention(torch.autograd.Function):

@@ -11,7 +11,6 @@ mask from the graph's (p, seed, call) record, exactly like forward.
 from __future__ import annotations
 
 import ctypes
-import os
 
 import torch
 
@@ -247,10 +246,13 @@ class _GraphLinear(torch.autograd.Function):
     ReLU mask fused into the operand loads (no g*mask temporary)."""
 
     @staticmethod
-    def forward(ctx, Z: torch.Tensor, W: torch.Tensor, b, relu: bool):
+    def forward(ctx, Z: torch.Tensor, W: torch.Tensor, b, relu: bool, path_rows: int = 0):
         Z2 = _rows_view(Z)
         Wc = W.contiguous()
-        out = linear_fwd(Z2, Wc, b.contiguous() if b is not None else None, relu)
+        bc = b.contiguous() if b is not None else None
+        # path_rows > 0: the GEMM path chosen for that many rows (a node-range
+        # shard's whole graph), so the shard's rows are the one-GPU layer's bits
+        out = linear_fwd_ex(Z2, Wc, 0, bc, relu, path_rows) if path_rows > 0 else linear_fwd(Z2, Wc, bc, relu)
         ctx.relu = relu
         ctx.has_b = b is not None
         ctx.save_for_backward(Z2, Wc, out if relu else None)
@@ -268,7 +270,7 @@ class _GraphLinear(torch.autograd.Function):
             dW, db = linear_bwd_weight(Z2, g, mask, want_b and db_pre is None)
             if not ctx.needs_input_grad[1]:
                 dW = None
-        return dZ, dW, db_pre if db_pre is not None else db, None
+        return dZ, dW, db_pre if db_pre is not None else db, None, None
 
 
 # Widths of the one-kernel GraphConv (graphconv.hip): the gathered width (the
@@ -287,12 +289,12 @@ def x6_rows_ok(M: int, N: int, K: int, path_rows: int = 0) -> bool:
     row blocks of one layer match the whole call bitwise when both take the
     same path -- which path_rows (the whole call's rows) guarantees."""
     rows = max(M, path_rows)
-    return (os.environ.get("GRL_GEMM_X6", "1")[:1] != "0" and K > 0 and K % 16 == 0 and M >= 1 and rows >= 4
+    return (_lib.get_option("gemm_x6") != 0 and K > 0 and K % 16 == 0 and M >= 1 and rows >= 4
             and N >= 4 and 2.0 * rows * N * K >= 1.6e10)
 
 
 def _bwd_data_enabled() -> bool:
-    return os.environ.get("GRL_GRAPHCONV_FUSED_BWD", "1") != "0"
+    return _lib.get_option("graphconv_fused_bwd") != 0
 
 
 def graph_conv_bwd_data(g: torch.Tensor, graph: TypedGraph, W: torch.Tensor, F: int, relu_out=None,
@@ -303,8 +305,8 @@ def graph_conv_bwd_data(g: torch.Tensor, graph: TypedGraph, W: torch.Tensor, F: 
     when relu_out is given).  F > 512 (gcn3's 2C-wide input at C = 512) runs
     one call per <= 512-column block of dX (the gather repeats per block; dZ
     still never exists).  None when the shape is outside the one-kernel path (the caller
-    then runs dZ = g W^T and the CSC gather).  GRL_GRAPHCONV_FUSED_BWD=0
-    disables it.  want_aggregate: return (dX, G_agg, g_eff) with G_agg =
+    then runs dZ = g W^T and the CSC gather).  The graphconv_fused_bwd path
+    option 0 disables it.  want_aggregate: return (dX, G_agg, g_eff) with G_agg =
     [A_drop,s^T g_eff]_s ([num_cols, segments * C], written by the same
     kernel) and g_eff the gradient through the ReLU, for dW_s = X^T G_agg_s."""
     if not _bwd_data_enabled() or isinstance(graph, EdgeBlockedGraph) or not graph.transpose_ok:
@@ -611,10 +613,13 @@ def graph_conv(X: torch.Tensor, graph: TypedGraph, W: torch.Tensor, b=None, relu
     return _GraphConv.apply(X, graph, W, b, relu, bool(recompute))
 
 
-def graph_linear(Z: torch.Tensor, W: torch.Tensor, b=None, relu: bool = False) -> torch.Tensor:
-    """out = Z W + b (optionally ReLU) on MFMA; Z rows x (L+1)F."""
+def graph_linear(Z: torch.Tensor, W: torch.Tensor, b=None, relu: bool = False, path_rows: int = 0) -> torch.Tensor:
+    """out = Z W + b (optionally ReLU) on MFMA; Z rows x (L+1)F.  path_rows:
+    the row count the GEMM path is chosen for (0: Z's own rows; a node-range
+    shard passes the whole graph's, as graph_conv does through
+    GrlTypedCsr.path_rows)."""
     _require_device(Z, "aggregated features")
-    return _GraphLinear.apply(Z, W, b, relu)
+    return _GraphLinear.apply(Z, W, b, relu, int(path_rows))
 
 
 # -------------------------------------------------------- feature dropout

@@ -173,6 +173,19 @@ const char* grl_last_error(void);
  * capturable.                                                              */
 int grl_check(grl_stream_t stream);
 
+/* Path options: the test / A-B hooks that pick among the kernel forms of one
+ * entry point (e.g. "gemm_x6" 0 = the fp32-MFMA GEMMs, "graphconv_fused" 0 =
+ * SpMM + GEMM instead of the one-kernel layer, "attn_x6" 0 = the fp32-MFMA
+ * attention kernels, "ws_spin" = the persistent kernels' wait bound).  The
+ * defaults are the production paths; every form computes the same result
+ * within its documented tolerance.  Process-wide, read at each call (a
+ * workspace query and the call it sizes must see the same settings).  The
+ * names and ranges are listed in csrc/common.hip; an unknown name or an
+ * out-of-range value is GRL_E_INVALID.  Nothing in the library reads the
+ * environment.                                                             */
+int grl_set_option(const char* name, int64_t value);
+int grl_get_option(const char* name, int64_t* value);
+
 /* roctx ranges (rocprofv3 --marker-trace): the hot entry points push their
  * own; these let a host layer bracket its steps, e.g. the halo exchange of a
  * node-range shard (grl/dist.py).  Pop closes the innermost open range.   */
@@ -279,8 +292,8 @@ int grl_typed_spmm_bwd_slice(const GrlTypedCsc* g, const float* dZ,
  * Large M (>= 16 GFLOP, K % 16 == 0, 16-B aligned): fp32 values split
  * exactly into three bf16 parts, six partial products on
  * v_mfma_f32_32x32x16_bf16 (error at the fp32-rounding level, DESIGN.md
- * §4.2); W's bf16 planes go to `workspace`.  Environment GRL_GEMM_X6=0
- * (read per call) selects v_mfma_f32_32x32x2_f32 instead.
+ * §4.2); W's bf16 planes go to `workspace`.  The path option gemm_x6 = 0
+ * (grl_set_option) selects v_mfma_f32_32x32x2_f32 instead.
  * Otherwise, calls of >= 256 output tiles walk all of K in one pass; calls
  * that cannot fill the chip (small graphs: a 74-node page is one 128-row
  * tile) split K into chunks over workgroups -- sized from K and the call's
@@ -340,7 +353,7 @@ int grl_graphconv_fwd(const GrlTypedCsr* g, const float* X, int64_t ldx,
  * bf16 planes, MFMA against W's planes) and the workspace holds only W's
  * planes (2.75 MB at K = 1792, C = 256) -- bitwise the two-kernel result.
  * Otherwise this is grl_graphconv_fwd_workspace_size().
- * GRL_GRAPHCONV_FUSED=0 forces the two-kernel path.                      */
+ * graphconv_fused = 0 forces the two-kernel path.                      */
 size_t grl_graphconv_fwd_workspace_query(const GrlTypedCsr* g, const float* X,
                                          int64_t ldx, int32_t F,
                                          const float* W, int32_t C);
@@ -465,7 +478,7 @@ int grl_bag_linear_bwd_weight(const float* V, int64_t ldv, const float* g,
  * (= softmax(QK^T) H) and row_max/row_sum [B, N] (the softmax statistics);
  * NULL otherwise.
  * fp32-accurate on the bf16 matrix cores (each fp32 value split exactly into
- * three bf16 parts, six partial products; GRL_ATTN_X6=0 selects the
+ * three bf16 parts, six partial products; attn_x6 = 0 selects the
  * fp32-MFMA kernels).  `workspace` (grl_node_attention_workspace_size bytes,
  * or NULL) holds the once-per-call bf16 splits of K and H (backward: also Q
  * and dO); NULL or too small makes every workgroup split its own blocks.   */

@@ -38,3 +38,22 @@ def golden():
         return dict(np.load(os.path.join(GOLDEN, name), allow_pickle=False))
 
     return load
+
+
+@pytest.fixture
+def grl_option():
+    """Set a libgrl path option (grl_set_option: the kernel-form hooks, e.g.
+    grl_option("gemm_x6", 0)) for one test; every option it touched is
+    restored afterwards."""
+    from grl import _lib
+
+    saved = {}
+
+    def set_(name, value):
+        if name not in saved:
+            saved[name] = _lib.get_option(name)
+        _lib.set_option(name, value)
+
+    yield set_
+    for name, value in saved.items():
+        _lib.set_option(name, value)

@@ -70,3 +70,31 @@ def test_dropedge_init_matches_oracle(p):
 def test_dropedge_init_rejects_negative_p():
     de = _lib.GrlDropEdge()
     assert _lib.lib().grl_dropedge_init(ctypes.byref(de), -0.1, 0, 0, 1) == _lib.GRL_E_INVALID
+
+
+def test_path_options_round_trip_and_reject_unknown_names():
+    """grl_set_option / grl_get_option: the kernel-form hooks that replaced the
+    per-call environment variables (nothing in libgrl reads the environment):
+    defaults are the production paths, values round-trip, grl.options()
+    restores them, unknown names and out-of-range values are GRL_E_INVALID."""
+    import grl
+
+    defaults = {"gemm_x6": 1, "graphconv_fused": 1, "graphconv_fused_bwd": 1, "fg_ws": 1, "spmm_wide": -1,
+                "spmm_blocks_per_cu": 24, "attn_x6": 1, "attn_fwd8": 1, "attn_dh8": 1, "attn_fused_dq": 1,
+                "attn_pipe": 1, "attn_qslab_max": 0, "ws_spin": 0, "ws_status_sync": 0}
+    assert {k: grl.get_option(k) for k in defaults} == defaults
+    with grl.options(gemm_x6=0, ws_spin=7, spmm_wide=1):
+        assert (grl.get_option("gemm_x6"), grl.get_option("ws_spin"), grl.get_option("spmm_wide")) == (0, 7, 1)
+    assert {k: grl.get_option(k) for k in defaults} == defaults
+    with pytest.raises(grl.GrlError, match="unknown option"):
+        grl.set_option("GRL_GEMM_X6", 0)
+    with pytest.raises(grl.GrlError, match="outside"):
+        grl.set_option("gemm_x6", 2)
+    os.environ["GRL_GEMM_X6"] = "0"  # the round-5 variable: read by nothing now
+    try:
+        assert grl.get_option("gemm_x6") == 1
+        from grl.ops import x6_rows_ok
+
+        assert x6_rows_ok(1_000_000, 256, 1792)
+    finally:
+        del os.environ["GRL_GEMM_X6"]

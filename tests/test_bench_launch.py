@@ -42,9 +42,11 @@ def test_gpus_must_be_positive():
 
 def test_pmc_traffic_is_keyed_by_workload_world_and_kernel():
     """roofline.traffic comes only from a PMC record of the same workload, at
-    the same world size, on the same kernel family: the C3 one-GPU record is
-    found; a C4 shard (n_loc = 1M at P = 4, the shape that used to collide
-    with C3's key) and every N > 1 line get None (printed as traffic: null)."""
+    the same world size and shard shape, on the same kernel family: the C3
+    one-GPU record is found; C4's rank-0 shards at P = 2 / 4 / 8 find the
+    records tools/pmc_rank_traffic.py wrote for their slice kernels (n_loc =
+    1M at P = 4 is also C3's row count: the world size and kernel keep them
+    apart); any other shard shape or kernel gets None (traffic: null)."""
     import argparse
     import importlib.util
 
@@ -55,6 +57,9 @@ def test_pmc_traffic_is_keyed_by_workload_world_and_kernel():
     one = "spmm_kernel<4,1,8,false,false> (grl_typed_spmm_fwd)"
     shard = "spmm_kernel / spmm_pair_kernel (grl_typed_spmm_fwd_slice, 2 slices of 128 columns)"
     assert bench.load_traffic(a, "C3", 1_000_000, 1, one) > 3e10
-    assert bench.load_traffic(a, "C4", 1_000_000, 4, shard) is None
-    assert bench.load_traffic(a, "C4", 2_000_000, 2, shard) is None
+    c4 = {P: bench.load_traffic(a, "C4", 4_000_000 // P, P, shard) for P in (2, 4, 8)}
+    assert 7e10 < c4[2] < 9e10 and 3.5e10 < c4[4] < 4.5e10 and 1.7e10 < c4[8] < 2.3e10, c4
+    assert bench.load_traffic(a, "C4", 1_000_000, 4, one) is None  # the one-GPU kernel's string: not this record
+    assert bench.load_traffic(a, "C4", 1_500_000, 2, shard) is None  # another shard shape
+    assert bench.load_traffic(a, "C4", 1_000_000, 1, one) is None  # C4 has no one-GPU record
     assert bench.load_traffic(a, "C3", 1_000_000, 1, "gemm_x6_kernel") is None  # another kernel's bytes: never

@@ -253,3 +253,33 @@ def test_shard_loss_shares_add_up_to_the_batch_mean(weight):
         assert abs(float(sum(p.double() for p in parts)) - float(full)) <= 1e-6 * max(1.0, abs(float(full)))
     empty = proc._shard_loss(logits[:, 10:20].float().requires_grad_(), t[:, 10:20], t)
     assert float(empty) == 0.0 and empty.requires_grad
+
+
+def test_node_range_honours_shuffle_with_one_order_for_every_rank(tmp_path):
+    """graph_parallel: node_range with shuffle: true -- every rank must train
+    on the same batch each step, so the loader shuffles through a fixed-seed
+    one-replica sampler (the same order wherever it is built, a new order per
+    epoch through set_epoch) instead of ignoring shuffle."""
+    from torch.utils.data import DistributedSampler
+
+    cfg = make_config(str(tmp_path))
+    cfg.distributed = True
+    cfg.graph_parallel = "node_range"
+    orders = []
+    for _ in range(2):  # two "ranks": two independently built loaders
+        loader = BaseDataLoader(cfg)
+        ds = loader._load_dataset("DatapileDataset", cfg.data_config.training, data_type="training")
+        dl = loader._get_dataloader(ds, ds.data_config)
+        assert isinstance(dl.sampler, DistributedSampler) and dl.sampler.num_replicas == 1
+        per_epoch = []
+        for ep in range(3):
+            dl.sampler.set_epoch(ep)
+            per_epoch.append(list(iter(dl.sampler)))
+        orders.append(per_epoch)
+    assert orders[0] == orders[1]
+    assert sorted(orders[0][0]) == list(range(5))
+    assert len({tuple(o) for o in orders[0]}) > 1  # reshuffled across epochs
+    cfg.data_config.training.shuffle = False
+    loader = BaseDataLoader(cfg)
+    ds = loader._load_dataset("DatapileDataset", cfg.data_config.training, data_type="training")
+    assert not isinstance(loader._get_dataloader(ds, ds.data_config).sampler, DistributedSampler)

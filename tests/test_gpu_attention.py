@@ -6,6 +6,7 @@ import numpy as np
 import pytest
 import torch
 
+import grl
 from grl import _lib
 from grl.ops import node_attention_forward, node_self_attention
 
@@ -39,21 +40,21 @@ SHAPES = [(1, 74, 16, 128), (4, 74, 16, 128), (2, 33, 4, 32), (1, 1, 2, 16), (3,
 MODES = ["x6", "x6-no-workspace", "f32"]
 
 
-def _set_mode(mode, monkeypatch):
+def _set_mode(mode, monkeypatch, grl_option):
     """x6: split-bf16 kernels with the once-per-call operand planes (default);
     x6-no-workspace: the same kernels splitting every block themselves;
-    f32: the fp32-MFMA kernels (GRL_ATTN_X6=0)."""
+    f32: the fp32-MFMA kernels (attn_x6 = 0)."""
     import grl.ops
 
-    monkeypatch.setenv("GRL_ATTN_X6", "0" if mode == "f32" else "1")
+    grl_option("attn_x6", int("0" if mode == "f32" else "1"))
     if mode == "x6-no-workspace":
         monkeypatch.setattr(grl.ops, "_attn_workspace", lambda *a, **k: (None, 0))
 
 
 @pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("B,N,dk,dv", SHAPES)
-def test_forward_matches_fp64(B, N, dk, dv, mode, monkeypatch):
-    _set_mode(mode, monkeypatch)
+def test_forward_matches_fp64(B, N, dk, dv, mode, monkeypatch, grl_option):
+    _set_mode(mode, monkeypatch, grl_option)
     Q, K, H, V, gamma = _inputs(B, N, dk, dv, seed=N + dk)
     out = node_attention_forward(Q, K, H, V, gamma)
     ref = _ref(*(t.double() for t in (Q, K, H, V, gamma)))
@@ -62,8 +63,8 @@ def test_forward_matches_fp64(B, N, dk, dv, mode, monkeypatch):
 
 @pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("B,N,dk,dv", SHAPES)
-def test_backward_matches_fp64(B, N, dk, dv, mode, monkeypatch):
-    _set_mode(mode, monkeypatch)
+def test_backward_matches_fp64(B, N, dk, dv, mode, monkeypatch, grl_option):
+    _set_mode(mode, monkeypatch, grl_option)
     Q, K, H, V, gamma = _inputs(B, N, dk, dv, seed=7 * N + dv)
     leaves = [t.clone().requires_grad_(True) for t in (Q, K, H, V, gamma)]
     out = node_self_attention(*leaves)
@@ -120,9 +121,9 @@ def test_bad_widths_raise():
 
 @pytest.mark.parametrize("B,N,dk,dv", [(1, 74, 16, 128), (4, 1100, 16, 128), (64, 1024, 16, 128), (2, 300, 32, 256),
                                        (1, 2048, 16, 128), (2, 1000, 5, 100), (3, 4099, 16, 64), (2, 4127, 32, 32)])
-def test_pipelined_forward_same_bits(B, N, dk, dv, monkeypatch):
+def test_pipelined_forward_same_bits(B, N, dk, dv, monkeypatch, grl_option):
     """attn_fwd_x6p_kernel (block k+1's softmax inside block k's P.H MFMAs)
-    against the unpipelined x6 forward (GRL_ATTN_PIPE=0): same products, same
+    against the unpipelined x6 forward (attn_pipe = 0): same products, same
     order of every sum -- out and the saved row stats bitwise, with key
     splits, partial last blocks and every value width."""
     from grl.ops import node_self_attention
@@ -130,7 +131,7 @@ def test_pipelined_forward_same_bits(B, N, dk, dv, monkeypatch):
     Q, K, H, V, gamma = _inputs(B, N, dk, dv, seed=7 * N + dk)
     res = {}
     for pipe in ("1", "0"):
-        monkeypatch.setenv("GRL_ATTN_PIPE", pipe)
+        grl_option("attn_pipe", int(pipe))
         out = node_attention_forward(Q, K, H, V, gamma)
         leaves = [t.clone().requires_grad_(True) for t in (Q, K, H, V, gamma)]
         node_self_attention(*leaves).square().sum().backward()
@@ -142,10 +143,10 @@ def test_pipelined_forward_same_bits(B, N, dk, dv, monkeypatch):
 
 @pytest.mark.parametrize("B,N,dk,dv", [(1, 8192, 16, 128), (2, 5000, 16, 100), (3, 4099, 9, 128), (1, 6000, 1, 97),
                                        (200, 24, 16, 128)])  # many pages shorter than one query block
-def test_fused_dq_backward(B, N, dk, dv, monkeypatch):
+def test_fused_dq_backward(B, N, dk, dv, monkeypatch, grl_option):
     """dQ folded into the key-stationary dK kernel (attn_bwd_kq_x6_kernel:
     exact MFMA transpose of dS, per-workgroup slabs added in order) against
-    fp64 and against the separate dQ kernel (GRL_ATTN_FUSED_DQ=0); dK / dH
+    fp64 and against the separate dQ kernel (attn_fused_dq = 0); dK / dH
     within the same tolerance, deterministic run to run."""
     lib = _lib.lib()
     assert lib.grl_node_attention_bwd_workspace_size(B, N, dk, dv) > lib.grl_node_attention_workspace_size(B, N, dk, dv)
@@ -153,7 +154,7 @@ def test_fused_dq_backward(B, N, dk, dv, monkeypatch):
     dout = torch.randn(B, N, dv, generator=torch.Generator().manual_seed(4)).to(DEV)
     grads = {}
     for fused in ("1", "0", "1"):
-        monkeypatch.setenv("GRL_ATTN_FUSED_DQ", fused)
+        grl_option("attn_fused_dq", int(fused))
         leaves = [t.clone().requires_grad_(True) for t in (Q, K, H, V, gamma)]
         node_self_attention(*leaves).backward(dout)
         g = [t.grad for t in leaves]
@@ -170,15 +171,15 @@ def test_fused_dq_backward(B, N, dk, dv, monkeypatch):
 
 
 @pytest.mark.parametrize("B,N,dk,dv", [(1, 8192, 16, 128), (3, 4099, 9, 100), (2, 5000, 32, 128)])
-def test_eight_wave_workgroups_same_bits(B, N, dk, dv, monkeypatch):
+def test_eight_wave_workgroups_same_bits(B, N, dk, dv, monkeypatch, grl_option):
     """The forward and dH kernels on 8-wave (256-row) workgroups compute every
-    row exactly as on 4-wave ones (GRL_ATTN_FWD8 / GRL_ATTN_DH8 = 0): out and
+    row exactly as on 4-wave ones (attn_fwd8 / attn_dh8 = 0): out and
     every gradient bitwise, partial last blocks and splits included."""
     Q, K, H, V, gamma = _inputs(B, N, dk, dv, seed=N + dv)
     res = {}
     for v in ("1", "0"):
-        monkeypatch.setenv("GRL_ATTN_FWD8", v)
-        monkeypatch.setenv("GRL_ATTN_DH8", v)
+        grl_option("attn_fwd8", int(v))
+        grl_option("attn_dh8", int(v))
         leaves = [t.clone().requires_grad_(True) for t in (Q, K, H, V, gamma)]
         out = node_self_attention(*leaves)
         out.square().sum().backward()
@@ -193,7 +194,7 @@ RANGED = [(1, 20_000, 16, 128, (0, 7000, 13_003, 20_000)), (2, 3000, 16, 100, (0
 
 @pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("B,N,dk,dv,cuts", RANGED)
-def test_query_ranges_partition_the_attention(B, N, dk, dv, cuts, mode, monkeypatch):
+def test_query_ranges_partition_the_attention(B, N, dk, dv, cuts, mode, monkeypatch, grl_option):
     """grl_node_attention_fwd_rows / _bwd_rows (a node-range shard's queries
     against every key, grl.dist sharded_node_attention): over a partition of
     the queries, each range's output rows match the float64 attention (the
@@ -204,7 +205,7 @@ def test_query_ranges_partition_the_attention(B, N, dk, dv, cuts, mode, monkeypa
     rounding of the sum).  Rows outside a range stay zero."""
     from grl.ops import node_attention_backward
 
-    _set_mode(mode, monkeypatch)
+    _set_mode(mode, monkeypatch, grl_option)
     Q, K, H, V, gamma = _inputs(B, N, dk, dv, seed=N + 7)
     dout = torch.randn(B, N, dv, generator=torch.Generator().manual_seed(3)).to(DEV)
     Qd, Kd, Hd, Vd, gd = (t.double().requires_grad_(True) for t in (Q, K, H, V, gamma))
@@ -231,9 +232,9 @@ def test_query_ranges_partition_the_attention(B, N, dk, dv, cuts, mode, monkeypa
 
 
 @pytest.mark.parametrize("B,N,budget_x", [(1, 20_000, 23), (2, 9000, 7), (1, 4500, 1)])
-def test_fused_dq_key_chunks_are_bitwise(B, N, budget_x, monkeypatch):
+def test_fused_dq_key_chunks_are_bitwise(B, N, budget_x, monkeypatch, grl_option):
     """The fused dK/dQ pass in key chunks (the dQ slabs of budget_x key
-    workgroups per launch, GRL_ATTN_QSLAB_MAX), each chunk's slabs added onto
+    workgroups per launch, the attn_qslab_max option), each chunk's slabs added onto
     dQ in order: dQ, dK, dH bitwise the one-launch pass's."""
     from grl.ops import node_attention_backward
 
@@ -242,7 +243,7 @@ def test_fused_dq_key_chunks_are_bitwise(B, N, budget_x, monkeypatch):
     out, onorm, rmax, rsum = node_attention_forward(Q, K, H, V, gamma, stats=True)
     whole = node_attention_backward(Q, K, H, gamma, onorm, rmax, rsum, dout)
     npad = -(-N // 32) * 32
-    monkeypatch.setenv("GRL_ATTN_QSLAB_MAX", str(budget_x * B * npad * 16 * 4))
+    grl_option("attn_qslab_max", budget_x * B * npad * 16 * 4)
     chunked = node_attention_backward(Q, K, H, gamma, onorm, rmax, rsum, dout)
     for a, b in zip(whole, chunked):
         assert torch.equal(a, b)
@@ -274,10 +275,7 @@ def test_half_million_nodes_forward_backward():
     D = (dO * o).sum(-1, keepdim=True)
     dQ_ref = (p * (dP - D)) @ Kd
     torch.testing.assert_close(dQ[0, rows].double(), dQ_ref, rtol=1e-4, atol=1e-4 * float(dQ_ref.abs().max()))
-    os.environ["GRL_ATTN_FUSED_DQ"] = "0"
-    try:
+    with grl.options(attn_fused_dq=0):
         _, dK2, dH2 = node_attention_backward(Q, K, H, gamma, onorm, rmax, rsum, dout)
-    finally:
-        del os.environ["GRL_ATTN_FUSED_DQ"]
     for a, b in ((dK, dK2), (dH, dH2)):
         assert float((a - b).abs().max()) <= 1e-5 * max(1.0, float(b.abs().max()))

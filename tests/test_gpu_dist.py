@@ -169,7 +169,10 @@ def _shard_worker(rank, world, port, mode, kind):
         grads = [t.grad.clone() for t in (layer.h_weights, layer.bias)]
         layer.zero_grad()
         X_a, X_b = X[rb:re].clone().requires_grad_(True), X[rb:re].clone().requires_grad_(True)
-        (sg.graphconv(X_a, layer, de, relu=True, chunks=2) * R[rb:re]).sum().backward()
+        out_c = sg.graphconv(X_a, layer, de, relu=True, chunks=2)
+        # the chunked layer's linear takes the whole graph's GEMM path (path_rows): the same rows' bits
+        assert torch.equal(out_c, out_loc)
+        (out_c * R[rb:re]).sum().backward()
         allreduce_gradients(layer.parameters())
         assert all(torch.equal(t.grad, g0) for t, g0 in zip((layer.h_weights, layer.bias), grads))
         (sg.graphconv(X_b, layer, de, relu=True) * R[rb:re]).sum().backward()
@@ -296,11 +299,10 @@ def _fused_shard_worker(rank, world, port, mode):
         full = graph_conv_infer(X, g.with_dropedge(de), W, b, True)
         out = graph_conv_infer(X_ext, local, W, b, True)
         assert torch.equal(out, full[rb:re])
-        os.environ["GRL_GRAPHCONV_FUSED"] = "0"
-        try:
+        import grl
+
+        with grl.options(graphconv_fused=0):
             assert torch.equal(graph_conv_infer(X_ext, local, W, b, True), out)
-        finally:
-            del os.environ["GRL_GRAPHCONV_FUSED"]
     finally:
         dist.destroy_process_group()
 

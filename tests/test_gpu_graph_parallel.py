@@ -165,3 +165,40 @@ def test_graph_parallel_predict_equals_single_process(tmp_path):
     with open(os.path.join(str(tmp_path), "classes26.json"), "w") as f:
         json.dump({"classes": [f"c{i}" for i in range(26)]}, f)
     mp.spawn(_predict_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+
+
+def test_shard_cache_confirms_a_key_hit(monkeypatch):
+    """A cache_key collision (forced here: every graph gets one key) must not
+    hand a graph another graph's shard plan: the hit is confirmed by exact
+    equality of the CSR arrays (ShardedGraph.same_graph), so a different
+    graph gets its own plan and the same graph met again reuses its plan."""
+    from grl import TypedGraph
+    from grl.dist import ShardedGraph
+    from gnn.trainer.training_procedures.kv_procedure import sharded_graph_cached
+
+    dev = torch.device("cuda")
+    rng = np.random.default_rng(3)
+
+    def graph():
+        A = (rng.random((1, 40, L, 40)) < 0.05).astype(np.float32)
+        return TypedGraph.from_dense(torch.from_numpy(A).to(dev), layout="bnln")
+
+    g1, g2 = graph(), graph()
+    assert not ShardedGraph.same_graph(g1, g2)
+    monkeypatch.setattr(ShardedGraph, "cache_key", staticmethod(lambda g, **kw: ("collide",)))
+
+    class Owner:
+        pass
+
+    o = Owner()
+    s1 = sharded_graph_cached(o, g1, {})
+    s2 = sharded_graph_cached(o, g2, {})
+    assert s2 is not s1
+    assert torch.equal(s2.graph.colidx, ShardedGraph.from_graph(g2).graph.colidx)
+    g2_again = TypedGraph(g2.rowptr.clone(), g2.colidx.clone(), L, has_self=True, num_cols=g2.num_cols)
+    assert sharded_graph_cached(o, g2_again, {}) is s2
+    # vals compared by their bits: the same structure with other weights is another graph
+    g3 = TypedGraph(g2.rowptr.clone(), g2.colidx.clone(), L, has_self=True, num_cols=g2.num_cols,
+                    vals=torch.rand(g2.colidx.numel(), device=dev))
+    assert not ShardedGraph.same_graph(g2, g3)
+    assert sharded_graph_cached(o, g3, {}) is not s2

@@ -54,12 +54,12 @@ def test_graphconv_small_matches_two_ops_and_oracle(N, L, deg, F, C, has_self, r
 
 
 @pytest.mark.parametrize("di,strided", [(0, False), (1, False), (2, True)])
-def test_graphconv_row_chunks_bitwise(di, strided, monkeypatch):
+def test_graphconv_row_chunks_bitwise(di, strided, monkeypatch, grl_option):
     """Bounded workspace on the two-kernel path: rows in chunks (here 12
     chunks, the last partial) give the whole-graph bits, which are the
     two-op bits (also with X a column slice of a wider matrix, and DropEdge
     sparing the self loops)."""
-    monkeypatch.setenv("GRL_GRAPHCONV_FUSED", "0")
+    grl_option("graphconv_fused", 0)
     N, L, F, C = 100_003, 6, 256, 256
     de = [None, DropEdge(0.3, 2, 0, True), DropEdge(0.2, 5, 3, False)][di]
     g = TypedGraph.synthetic(N, 16.0, L, seed=0, device=DEV).with_dropedge(de)
@@ -154,13 +154,13 @@ def _ws_query(X, g, W, C):
                                                   (18_001, 7, 512, 500, True, 14.0), (40_003, 3, 512, 260, False, 9.0)])
 @pytest.mark.parametrize("variant", ["plain", "drop_bias_relu", "drop_spare_self", "strided_relu"])
 @pytest.mark.parametrize("kernel", ["ws", "phases"])
-def test_fused_graphconv_bitwise_equals_two_kernels(N, L, F, C, has_self, deg, variant, kernel, monkeypatch):
+def test_fused_graphconv_bitwise_equals_two_kernels(N, L, F, C, has_self, deg, variant, kernel, monkeypatch, grl_option):
     """The one-kernel GraphConv (graphconv.hip; both kernels: the
-    warp-specialized default and the phase-alternating GRL_FG_WS=0 one)
+    warp-specialized default and the phase-alternating fg_ws = 0 one)
     gives the two-kernel bits (typed SpMM, then the x6 GEMM): the same fmaf
     chain per Z element, the same split, K order and product order; and it
     runs in a workspace of only W's planes (Z never reaches HBM)."""
-    monkeypatch.setenv("GRL_FG_WS", "1" if kernel == "ws" else "0")
+    grl_option("fg_ws", int("1" if kernel == "ws" else "0"))
     de = {"plain": None, "drop_bias_relu": DropEdge(0.3, 3, 2, True), "drop_spare_self": DropEdge(0.25, 9, 0, False),
           "strided_relu": None}[variant]
     bias = variant == "drop_bias_relu"
@@ -182,7 +182,7 @@ def test_fused_graphconv_bitwise_equals_two_kernels(N, L, F, C, has_self, deg, v
     out = graph_conv_infer(X, g, W, b, relu)
     ref = _two_op(X, g, W, b, relu)
     assert torch.equal(out, ref)
-    monkeypatch.setenv("GRL_GRAPHCONV_FUSED", "0")
+    grl_option("graphconv_fused", 0)
     assert _ws_query(X, g, W, C) >= N * K * 4
     assert torch.equal(graph_conv_infer(X, g, W, b, relu), out)
 
@@ -215,11 +215,11 @@ def test_fused_graphconv_edge_values_and_oracle():
 
 @pytest.mark.parametrize("de", [None, DropEdge(0.3, 4, 2, True)])
 @pytest.mark.parametrize("recompute", [False, True])
-def test_training_forward_one_kernel_same_bits(de, recompute, monkeypatch):
+def test_training_forward_one_kernel_same_bits(de, recompute, monkeypatch, grl_option):
     """The training GraphConv (graph_conv with gradients) runs its forward as
     one kernel that also writes Z for the backward (grl_graphconv_fwd_train),
     or -- recompute=True -- as the inference kernel; out, Z and every
-    gradient are bitwise those of the two-kernel path (GRL_GRAPHCONV_FUSED=0)."""
+    gradient are bitwise those of the two-kernel path (graphconv_fused = 0)."""
     from grl.ops import graph_conv_fwd_train, spmm_forward
 
     N, L, F, C = 20_011, 6, 256, 256
@@ -231,10 +231,10 @@ def test_training_forward_one_kernel_same_bits(de, recompute, monkeypatch):
     R = torch.randn(N, C, device=DEV, generator=gen)
     out_f, Z_f = graph_conv_fwd_train(X0, g, W0, b0, True)
     assert torch.equal(Z_f, spmm_forward(X0, g))
-    monkeypatch.setenv("GRL_GRAPHCONV_FUSED_BWD", "0")  # dX by the chain (the reassociated one: test below)
+    grl_option("graphconv_fused_bwd", 0)  # dX by the chain (the reassociated one: test below)
     res = {}
     for fused in ("1", "0"):
-        monkeypatch.setenv("GRL_GRAPHCONV_FUSED", fused)
+        grl_option("graphconv_fused", int(fused))
         X, W, b = (t.clone().requires_grad_(True) for t in (X0, W0, b0))
         out = graph_conv(X, g, W, b, relu=True, recompute=recompute)
         (out * R).sum().backward()
@@ -274,7 +274,7 @@ def test_wide_training_forward_one_kernel_same_bits(F, C, de):
                                                   (20_011, 6, 512, 512, True, 10.0), (20_011, 6, 256, 512, True, 10.0),
                                                   (10_007, 6, 1024, 512, True, 8.0), (18_001, 7, 384, 512, True, 12.0)])
 @pytest.mark.parametrize("variant", ["plain", "drop_self", "drop_spare_self_vals"])
-def test_bwd_data_one_kernel(N, L, F, C, has_self, deg, variant, monkeypatch):
+def test_bwd_data_one_kernel(N, L, F, C, has_self, deg, variant, monkeypatch, grl_option):
     """grl_graphconv_bwd_data: dX = sum_s (A_drop,s^T G) W_s^T in one kernel
     over the typed transpose (DropEdge ids through eid, so the forward's
     mask) against the autograd chain dZ = G W^T, dX = A_drop^T dZ: within
@@ -308,12 +308,12 @@ def test_bwd_data_one_kernel(N, L, F, C, has_self, deg, variant, monkeypatch):
     b0 = torch.randn(C, device=DEV, generator=gen)
     res = {}
     for fb in ("1", "0"):
-        monkeypatch.setenv("GRL_GRAPHCONV_FUSED_BWD", fb)
+        grl_option("graphconv_fused_bwd", int(fb))
         X, Wp, b = (t.clone().requires_grad_(True) for t in (X0, W, b0))
         out = graph_conv(X, g, Wp, b, relu=True)
         (out * G).sum().backward()
         res[fb] = (out.detach(), X.grad, Wp.grad, b.grad)
-    monkeypatch.setenv("GRL_GRAPHCONV_FUSED_BWD", "1")
+    grl_option("graphconv_fused_bwd", 1)
     assert torch.equal(res["1"][1], graph_conv_bwd_data(G, g, W, F, res["1"][0]))
     assert torch.equal(res["1"][0], res["0"][0]) and torch.equal(res["1"][2], res["0"][2])
     assert torch.equal(res["1"][3], res["0"][3])
@@ -379,15 +379,15 @@ def test_recompute_takes_weight_gradient_from_the_aggregate(de):
     assert bool(((res[True][3] - res[False][3]).abs() <= 1e-5 * bound_b + 1e-6).all())
 
 
-def test_persistent_kernel_timeout_is_an_error(monkeypatch):
+def test_persistent_kernel_timeout_is_an_error(monkeypatch, grl_option):
     """graphconv_ws_kernel's bounded waits: with a one-sleep bound
-    (GRL_WS_SPIN=1) the MFMA waves give up before the gather waves fill the
+    (ws_spin = 1) the MFMA waves give up before the gather waves fill the
     ring.  The calls stay stream-ordered (no host sync): a follow-up kernel
     fills each failed call's outputs with NaN and records the entry point in
     the sticky device word, and grl.check() -- at the caller's next sync
     point -- raises GrlError(GRL_E_TIMEOUT) naming every failed entry point,
     then clears the word.  Replays of a captured call fail the same way.
-    GRL_WS_STATUS=sync keeps the per-call check (the call itself raises).
+    ws_status_sync = 1 keeps the per-call check (the call itself raises).
     With the normal bound the next call is correct again."""
     import grl
     from grl.ops import graph_conv_bwd_data
@@ -404,7 +404,7 @@ def test_persistent_kernel_timeout_is_an_error(monkeypatch):
     dX_ref = graph_conv_bwd_data(G, g, W, F)
     assert dX_ref is not None
     grl.check()  # nothing pending
-    monkeypatch.setenv("GRL_WS_SPIN", "1")
+    grl_option("ws_spin", 1)
     out = graph_conv_infer(X, g, W, b, True)  # no raise, no sync: the failure is stream-ordered
     with pytest.raises(_lib.GrlError, match=r"grl_graphconv_fwd: a wave .* gave up waiting"):
         grl.check()
@@ -416,10 +416,10 @@ def test_persistent_kernel_timeout_is_an_error(monkeypatch):
     with pytest.raises(_lib.GrlError, match="grl_graphconv_fwd_train, grl_graphconv_bwd_data"):
         grl.check()
     assert bool(torch.isnan(out_t).all()) and bool(torch.isnan(dX).all())
-    monkeypatch.setenv("GRL_WS_STATUS", "sync")  # debug aid: every eager call checks itself
+    grl_option("ws_status_sync", 1)  # debug aid: every eager call checks itself
     with pytest.raises(_lib.GrlError, match="gave up waiting"):
         graph_conv_infer(X, g, W, b, True)
-    monkeypatch.delenv("GRL_WS_STATUS")
+    grl_option("ws_status_sync", 0)
     # inside a capture: the replay's outputs are NaN and grl.check() reports it
     hg = torch.cuda.CUDAGraph()
     with torch.cuda.graph(hg):
@@ -428,7 +428,7 @@ def test_persistent_kernel_timeout_is_an_error(monkeypatch):
     with pytest.raises(_lib.GrlError, match="grl_graphconv_fwd"):
         grl.check()
     assert bool(torch.isnan(out_c).all())
-    monkeypatch.delenv("GRL_WS_SPIN")
+    grl_option("ws_spin", 0)
     assert torch.equal(graph_conv_infer(X, g, W, b, True), ref)
     assert torch.equal(graph_conv_bwd_data(G, g, W, F), dX_ref)
     grl.check()
@@ -439,7 +439,7 @@ def test_persistent_kernel_timeout_is_an_error(monkeypatch):
         grl.check()
 
 
-def test_timeout_report_is_never_lost_between_checks(monkeypatch):
+def test_timeout_report_is_never_lost_between_checks(monkeypatch, grl_option):
     """grl_check takes the sticky word with ONE atomic exchange (its old value
     written to a pinned host word): a poisoned call on another stream that
     lands while checks run on this stream is reported by exactly one check
@@ -454,7 +454,7 @@ def test_timeout_report_is_never_lost_between_checks(monkeypatch):
     b = torch.randn(C, device=DEV, generator=gen)
     graph_conv_infer(X, g, W, b, True)
     grl.check()
-    monkeypatch.setenv("GRL_WS_SPIN", "1")
+    grl_option("ws_spin", 1)
     reports = 0
     for delay in (0, 2_000_000, 20_000_000):  # the poison lands before, during, after the checks below
         side = torch.cuda.Stream(DEV)
@@ -475,11 +475,11 @@ def test_timeout_report_is_never_lost_between_checks(monkeypatch):
             reports += 1
         assert bool(torch.isnan(out).all())
     assert reports == 3  # one per poisoned call
-    monkeypatch.delenv("GRL_WS_SPIN")
+    grl_option("ws_spin", 0)
     grl.check()
 
 
-def test_bench_surfaces_a_poisoned_timed_region(monkeypatch):
+def test_bench_surfaces_a_poisoned_timed_region(monkeypatch, grl_option):
     """bench.py checks after every timed region (bench.surface): a poisoned
     run exits non-zero naming the section and the entry point instead of
     being reported as a timing."""
@@ -490,11 +490,11 @@ def test_bench_surfaces_a_poisoned_timed_region(monkeypatch):
     X = torch.randn(N, F, device=DEV)
     W = torch.randn(7 * F, C, device=DEV) / 40
     bench.surface("clean", DEV)
-    monkeypatch.setenv("GRL_WS_SPIN", "1")
+    grl_option("ws_spin", 1)
     graph_conv_infer(X, g, W, None, True)
     with pytest.raises(SystemExit, match=r"bench.py: extras \(layers\): .*grl_graphconv_fwd"):
         bench.surface("extras (layers)", DEV)
-    monkeypatch.delenv("GRL_WS_SPIN")
+    grl_option("ws_spin", 0)
     bench.surface("clean again", DEV)
 
 

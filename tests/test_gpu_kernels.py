@@ -378,7 +378,7 @@ def test_small_m_split_k_deterministic(M, K, C):
 @pytest.mark.parametrize("x6", ["1", "0"])
 @pytest.mark.parametrize("M,K,C", [(300_000, 1792, 256), (70_003, 3584, 256), (131_072, 512, 128), (65_600, 256, 1792),
                                    (45_001, 1792, 200)])
-def test_large_tile_gemms_match_fp64(M, K, C, x6, monkeypatch):
+def test_large_tile_gemms_match_fp64(M, K, C, x6, monkeypatch, grl_option):
     """Shapes that take the large-M paths (>= 16 GFLOP, aligned, K % 16 == 0):
     x6 = "1" the split-bf16 kernel (gemm_x6_kernel), "0" the fp32 256x256
     LDS-DMA tile (gemm256p_kernel).  Forward with bias+ReLU, dZ and dW/db
@@ -386,7 +386,7 @@ def test_large_tile_gemms_match_fp64(M, K, C, x6, monkeypatch):
     tails and a C that is not a multiple of the 256-column tile included."""
     from grl.ops import linear_bwd_data, linear_bwd_weight
 
-    monkeypatch.setenv("GRL_GEMM_X6", x6)
+    grl_option("gemm_x6", int(x6))
 
     gen = torch.Generator(device=DEV).manual_seed(M % 1000)
     Z = torch.randn(M, K, device=DEV, generator=gen)
@@ -411,14 +411,14 @@ def test_large_tile_gemms_match_fp64(M, K, C, x6, monkeypatch):
     assert torch.equal(linear_fwd(Z, W, b, True), out)  # deterministic
 
 
-def test_x6_split_is_exact_on_wide_dynamic_range(monkeypatch):
+def test_x6_split_is_exact_on_wide_dynamic_range(monkeypatch, grl_option):
     """The x6 GEMM splits every fp32 value into three bf16 parts exactly: rows
     of Z scaled over 2^-60 .. 2^60 and W columns over 2^-30 .. 2^30 keep the
     per-element error at the fp32 level (<= 1e-6 of sum |terms|), the same
     bound the fp32-MFMA kernel meets; integer data is exact."""
     from grl.ops import linear_bwd_data
 
-    monkeypatch.setenv("GRL_GEMM_X6", "1")
+    grl_option("gemm_x6", 1)
     M, K, C = 40_000, 1792, 256
     gen = torch.Generator(device=DEV).manual_seed(7)
     rs = torch.pow(2.0, torch.randint(-60, 61, (M, 1), device=DEV, generator=gen).float())
@@ -438,21 +438,21 @@ def test_x6_split_is_exact_on_wide_dynamic_range(monkeypatch):
 
 
 @pytest.mark.parametrize("wide", ["1", "0"])
-def test_spmm_wide_rows_bitwise(wide, monkeypatch):
-    """F in (256, 512]: one wave per whole row (GRL_SPMM_WIDE=1, the choice for
+def test_spmm_wide_rows_bitwise(wide, monkeypatch, grl_option):
+    """F in (256, 512]: one wave per whole row (spmm_wide = 1, the choice for
     gathered tables above 12 GB) or 256-column waves along grid.y ("0"); both
     bitwise equal to the oracle, forward and backward, with DropEdge, float
     edge values and split heavy rows."""
-    monkeypatch.setenv("GRL_SPMM_WIDE", wide)
+    grl_option("spmm_wide", int(wide))
     test_spmm_fwd_bwd_bitwise((300, 6, 16.0, 512, 0, True, True), 1)
     test_spmm_fwd_bwd_bitwise((200, 6, 8.0, 384, 0, False, True), 2)
     test_split_rows_bitwise_rmat((300, 128), 1, 512, True)
 
 
-def test_x6_strided_z_matches_contiguous(monkeypatch):
+def test_x6_strided_z_matches_contiguous(monkeypatch, grl_option):
     """The x6 forward reads Z through its row stride (ldz > K, as a column
     slice of a wider buffer gives): bitwise the same as on a contiguous copy."""
-    monkeypatch.setenv("GRL_GEMM_X6", "1")
+    grl_option("gemm_x6", 1)
     M, K, C = 40_000, 1792, 256
     gen = torch.Generator(device=DEV).manual_seed(11)
     big = torch.randn(M, K + 32, device=DEV, generator=gen)

@@ -328,7 +328,7 @@ def test_streamed_layer_chain_equals_one_gpu(mode, nb):
     mp.spawn(_stream_chain_worker, args=(2, _free_port(), mode, nb), nprocs=2, join=True)
 
 
-def test_sharded_model_surfaces_a_poisoned_kernel(monkeypatch):
+def test_sharded_model_surfaces_a_poisoned_kernel(monkeypatch, grl_option):
     """Stream-ordered failures of the persistent GraphConv kernel reach the
     caller of the sharded model with no procedure around it: the inference
     forward checks once at its end, and allreduce_gradients (the training
@@ -342,7 +342,7 @@ def test_sharded_model_surfaces_a_poisoned_kernel(monkeypatch):
     sg = ShardedGraph.in_process(g, bounds, halo="dense", group=LocalGroup(1))[0]
     m = _model(256)
     grl.check()
-    monkeypatch.setenv("GRL_WS_SPIN", "1")
+    grl_option("ws_spin", 1)
     m.eval()
     with torch.no_grad(), pytest.raises(_lib.GrlError, match="grl_graphconv"):
         m.forward([V, sg])
@@ -351,6 +351,6 @@ def test_sharded_model_surfaces_a_poisoned_kernel(monkeypatch):
     torch.nn.functional.cross_entropy(logits, y, reduction="sum").backward()
     with pytest.raises(_lib.GrlError, match="grl_graphconv"):
         allreduce_gradients([p for p in m.parameters() if p.requires_grad], group=sg.group)
-    monkeypatch.delenv("GRL_WS_SPIN")
+    grl_option("ws_spin", 0)
     torch.cuda.synchronize()
     grl.check()

@@ -15,6 +15,6 @@ if [ -f "$SRC" ]; then SRCFILE=$SRC; SRC=$(basename "$SRC" .hip); fi  # a file e
 cp "$ROOT"/build/obj/*.o "$OBJ/"
 EXTRA=""
 [ "$SRC" = attention ] && EXTRA="-mllvm -amdgpu-mfma-vgpr-form -fno-slp-vectorize"  # as the Makefile builds it
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -I"$ROOT/include" -I"$CS" -Wno-unused-result $EXTRA $2 -c "$SRCFILE" -o "$OBJ/$SRC.o"
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -I"$ROOT/include" -I"$CS" -Wno-unused-result -DGRL_DIAG $EXTRA $2 -c "$SRCFILE" -o "$OBJ/$SRC.o"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$OUT/libgrl_$1.so" "$OBJ"/*.o -L/opt/rocm/lib -lrocprofiler-sdk-roctx
 echo "$OUT/libgrl_$1.so"

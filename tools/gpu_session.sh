@@ -6,7 +6,7 @@
 #   steps: tests smoke bench bench_extras bench_drop bench_c5 bench_c5s prof_bench prof_fwd prof_bwd
 #          prof_linear prof_layer prof_attn prof_c1 pmc_fwd_fetch pmc_fwd_write pmc_list pmc_linear_mfma
 #          pmc_fwd_tlb pmc_c4_tlb; round 4: ab_attn_hu tests_r4 pmc_infer_l2 pmc_wide_mfma prof_wide;
-#          round 5: pmc_wide_l2 pmc_wide_mfma5
+#          round 5: pmc_wide_l2 pmc_wide_mfma5; round 6: rank2 rank4 rank8 tests_r6a
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 export TMPDIR=/tmp
 OUT=gpurun_out
@@ -159,6 +159,17 @@ for step in "$@"; do
                   timeout -s KILL 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CU_CYCLES \
                   SQ_INSTS_VALU SQ_INSTS_MFMA --kernel-trace -d "$OUT/pmc_wide_mfma5" -o run --output-format csv \
                   -- python tools/probe_wide.py; unset PROBE_QUICK PROBE_SHAPES ;;
+    rank2|rank4|rank8) P=${step#rank}
+                  run probe_rank$P 300 python tools/probe_rank_shard.py --world $P --json "$OUT/rank$P.json"
+                  run prof_rank$P 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_rank$P" -o run \
+                    --output-format csv -- python tools/probe_rank_shard.py --world $P --no-parity
+                  run pmcf_rank$P 300 timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-trace \
+                    -d "$OUT/pmcf_rank$P" -o run --output-format csv -- python tools/probe_rank_shard.py --world $P --no-parity
+                  run pmcw_rank$P 300 timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-trace \
+                    -d "$OUT/pmcw_rank$P" -o run --output-format csv -- python tools/probe_rank_shard.py --world $P --no-parity ;;
+    tests_r6a) run pytest_gpu_r6a 600 python -u -m pytest tests/test_gpu_graph_parallel.py tests/test_gpu_dist.py \
+                  -m gpu -v -rf --timeout 300 --timeout-method thread ;;
+    ab_wide) rm -f gpurun_out/ab_wide.log; run ab_wide 900 tools/ab_wide.sh ${AB_LIBS} ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -3,7 +3,7 @@
 #   tools/ws_regs.sh FV PROD [extra -D flags]
 cd "$(dirname "$0")/../graph-representation-learning_amd/csrc" || exit 1
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -fPIC -std=c++17 -I../../include -Wall -Wno-unused-result \
-  -DGRL_WS_DIAG_ONE -DGRL_WS_DIAG_FV=$1 -DGRL_WS_DIAG_PROD=$2 "${@:3}" -c graphconv.hip -o /tmp/gcd.o \
+  -DGRL_DIAG -DGRL_WS_DIAG_ONE -DGRL_WS_DIAG_FV=$1 -DGRL_WS_DIAG_PROD=$2 "${@:3}" -c graphconv.hip -o /tmp/gcd.o \
   -Rpass-analysis=kernel-resource-usage 2>&1 | python3 -c "
 import re,sys
 txt=sys.stdin.read()
