@@ -479,6 +479,35 @@ __device__ __forceinline__ void asplit8(float4 lo, float4 hi, abf16x8_t& a0, abf
   a2 = __builtin_bit_cast(abf16x8_t, make_uint4(l2.x, l2.y, h2.x, h2.y));
 }
 
+#if defined(GRL_DIAG) && defined(GRL_ATTN_WI16)
+// what-if (diagnostic builds only; timing, wrong results): every 32x32x16
+// product as two v_mfma_f32_16x16x32_bf16 on the same operand registers into
+// two quarters of the accumulator -- the same FLOPs and pipe cycles in the
+// 16x16x32 shape, to price its clock against the 32x32x16 kernels
+typedef float af32x4_t __attribute__((ext_vector_type(4)));
+#define WI16(q0, q1, a, b)                                                   \
+  do {                                                                      \
+    q0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, q0, 0, 0, 0);        \
+    q1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, a, q1, 0, 0, 0);        \
+  } while (0)
+#define MFMA6(acc, a0, a1, a2, b0, b1, b2)                                  \
+  do {                                                                      \
+    af32x4_t q0_ = {acc[0], acc[1], acc[2], acc[3]}, q1_ = {acc[4], acc[5], acc[6], acc[7]};       \
+    af32x4_t q2_ = {acc[8], acc[9], acc[10], acc[11]}, q3_ = {acc[12], acc[13], acc[14], acc[15]}; \
+    WI16(q0_, q1_, a2, b0);                                                 \
+    WI16(q2_, q3_, a1, b1);                                                 \
+    WI16(q0_, q1_, a0, b2);                                                 \
+    WI16(q2_, q3_, a1, b0);                                                 \
+    WI16(q0_, q1_, a0, b1);                                                 \
+    WI16(q2_, q3_, a0, b0);                                                 \
+    for (int r_ = 0; r_ < 4; ++r_) {                                        \
+      acc[r_] = q0_[r_];                                                    \
+      acc[4 + r_] = q1_[r_];                                                \
+      acc[8 + r_] = q2_[r_];                                                \
+      acc[12 + r_] = q3_[r_];                                               \
+    }                                                                       \
+  } while (0)
+#else
 #define MFMA6(acc, a0, a1, a2, b0, b1, b2)                                  \
   do {                                                                      \
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, b0, acc, 0, 0, 0);   \
@@ -488,6 +517,7 @@ __device__ __forceinline__ void asplit8(float4 lo, float4 hi, abf16x8_t& a0, abf
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b1, acc, 0, 0, 0);   \
     acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, b0, acc, 0, 0, 0);   \
   } while (0)
+#endif
 
 template <int W>
 __device__ __forceinline__ int hswz(int key, int col) {  // H plane element offset

@@ -72,92 +72,6 @@ __global__ __launch_bounds__(256) void dense_fill_kernel(const float* __restrict
 
 __global__ void set_tail_zero(int32_t* p) { *p = 0; }
 
-// ---------------------------------------------------------------------------
-// CSR -> CSC
-// ---------------------------------------------------------------------------
-// Page-sized graphs (a 74-node document page: 1,777 rowptr entries, 216
-// edges) in one workgroup each, instead of hipCUB's multi-launch scan and
-// radix sort: the captured training step of the reference's workload
-// converts its dense A every step, where launches, not bytes, are the cost.
-// Same integers out (exclusive sums; the stable sort by column).
-constexpr int SMALL_T = 1024, SMALL_IT = 8, SMALL_N = SMALL_T * SMALL_IT;  // <= 8192 entries
-
-// exclusive prefix sum of v[0..n) in place in LDS (n <= SMALL_N), by one 1024-thread workgroup
-__device__ void block_exclusive_scan(int* v, int n, int* part) {
-  const int t = threadIdx.x;
-  int loc[SMALL_IT], sum = 0;
-#pragma unroll
-  for (int i = 0; i < SMALL_IT; ++i) {
-    const int j = t * SMALL_IT + i;
-    loc[i] = j < n ? v[j] : 0;
-    sum += loc[i];
-  }
-  part[t] = sum;
-  __syncthreads();
-  for (int d = 1; d < SMALL_T; d <<= 1) {  // inclusive scan of the threads' sums
-    const int x = t >= d ? part[t - d] : 0;
-    __syncthreads();
-    part[t] += x;
-    __syncthreads();
-  }
-  int run = t ? part[t - 1] : 0;
-#pragma unroll
-  for (int i = 0; i < SMALL_IT; ++i) {
-    const int j = t * SMALL_IT + i;
-    if (j < n) v[j] = run;
-    run += loc[i];
-  }
-  __syncthreads();
-}
-
-// rowptr[0..n_in] = exclusive sums of counts[0..n_in) (rowptr[n_in] = the total)
-__global__ __launch_bounds__(SMALL_T) void small_rowptr_kernel(const int32_t* __restrict__ counts, int n_in,
-                                                               int32_t* __restrict__ rowptr) {
-  __shared__ int v[SMALL_N];
-  __shared__ int part[SMALL_T];
-  for (int j = threadIdx.x; j <= n_in; j += SMALL_T) v[j] = j < n_in ? counts[j] : 0;
-  __syncthreads();
-  block_exclusive_scan(v, n_in + 1, part);
-  for (int j = threadIdx.x; j <= n_in; j += SMALL_T) rowptr[j] = v[j];
-}
-
-// keys_out / eid = colidx sorted by column, ties in edge order (what the
-// stable radix sort of (colidx, iota) gives): the packed keys col << 13 | e
-// are distinct, so a bitonic sort of them in LDS (padded to a power of two
-// with keys past every real one) is that stable order
-constexpr int SMALL_BITS = 13;  // SMALL_N = 2^13: column and edge id each fit
-static_assert(SMALL_N == 1 << SMALL_BITS, "packed (column, edge) keys");
-__global__ __launch_bounds__(SMALL_T) void small_csc_sort_kernel(const int32_t* __restrict__ colidx, int nnz,
-                                                                 int32_t* __restrict__ keys_out,
-                                                                 int32_t* __restrict__ eid) {
-  __shared__ uint32_t key[SMALL_N];
-  int n = 2;
-  while (n < nnz) n <<= 1;
-  for (int e = threadIdx.x; e < n; e += SMALL_T)
-    key[e] = e < nnz ? ((uint32_t)colidx[e] << SMALL_BITS) | (uint32_t)e : 0xffffffffu;
-  __syncthreads();
-  for (int k = 2; k <= n; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = threadIdx.x; i < n; i += SMALL_T) {
-        const int l = i ^ j;
-        if (l > i) {
-          const uint32_t a = key[i], b = key[l];
-          if ((a > b) == ((i & k) == 0)) {
-            key[i] = b;
-            key[l] = a;
-          }
-        }
-      }
-      __syncthreads();
-    }
-  }
-  for (int p = threadIdx.x; p < nnz; p += SMALL_T) {
-    keys_out[p] = (int32_t)(key[p] >> SMALL_BITS);
-    eid[p] = (int32_t)(key[p] & (SMALL_N - 1));
-  }
-}
-
-bool small_csc(int64_t nnz, int64_t num_cols) { return nnz <= SMALL_N && num_cols <= SMALL_N; }
 
 __global__ void iota_kernel(int32_t* __restrict__ v, int64_t n) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
@@ -378,11 +292,6 @@ extern "C" int grl_dense_to_csr_rowptr(const float* A, int64_t B, int64_t N, int
                        strides[1], strides[2], strides[3], counts);
     GRL_LAUNCH_CHECK();
   }
-  if (rows + 1 <= SMALL_N) {  // a page: one workgroup
-    hipLaunchKernelGGL(small_rowptr_kernel, dim3(1), dim3(SMALL_T), 0, st, counts, (int)rows, rowptr);
-    GRL_LAUNCH_CHECK();
-    return GRL_OK;
-  }
   hipLaunchKernelGGL(set_tail_zero, dim3(1), dim3(1), 0, st, counts + rows);
   GRL_LAUNCH_CHECK();
   GRL_HIP(hipcub::DeviceScan::ExclusiveSum(temp, temp_bytes, counts, rowptr, (int)(rows + 1), st));
@@ -431,15 +340,10 @@ extern "C" int grl_csr_to_csc(const GrlTypedCsr* g, int64_t num_cols, int32_t* c
   size_t temp_bytes = workspace_bytes - 2 * align_up((size_t)nn * 4);
   if (nnz > 0) {
     GRL_CHECK_ARG(g->colidx && zrow && eid, "grl_csr_to_csc: NULL pointer");
-    if (small_csc(nnz, num_cols)) {  // a page: one workgroup, the same stable order
-      hipLaunchKernelGGL(small_csc_sort_kernel, dim3(1), dim3(SMALL_T), 0, st, g->colidx, (int)nnz, keys_out, eid);
-      GRL_LAUNCH_CHECK();
-    } else {
-      hipLaunchKernelGGL(iota_kernel, dim3(grid_for(nnz)), dim3(256), 0, st, vals_iota, nnz);
-      GRL_LAUNCH_CHECK();
-      GRL_HIP(hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, g->colidx, keys_out, vals_iota, eid, (int)nnz, 0,
-                                                 bits_for((uint64_t)std::max<int64_t>(num_cols - 1, 1)), st));
-    }
+    hipLaunchKernelGGL(iota_kernel, dim3(grid_for(nnz)), dim3(256), 0, st, vals_iota, nnz);
+    GRL_LAUNCH_CHECK();
+    GRL_HIP(hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, g->colidx, keys_out, vals_iota, eid, (int)nnz, 0,
+                                               bits_for((uint64_t)std::max<int64_t>(num_cols - 1, 1)), st));
     const int hs = g->has_self ? 1 : 0;
     hipLaunchKernelGGL(csc_gather_kernel, dim3(grid_for(nnz)), dim3(256), 0, st, g->rowptr,
                        g->num_rows * g->num_types, g->num_types, hs, eid, g->vals, nnz, zrow,

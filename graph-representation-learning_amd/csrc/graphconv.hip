@@ -31,7 +31,7 @@
 #include <mutex>
 #include <vector>
 
-// Diagnostic switches (GRL_WS_STAMP, GRL_WS_ONLY_ROLE, GRL_WS_DIAG_*, GRL_WS_NOIL,
+// Diagnostic switches (GRL_WS_STAMP, GRL_WS_ONLY_ROLE, GRL_WS_DIAG_*,
 // GRL_WS_WHATIF below) are honoured only in diagnostic builds, which
 // tools/build_diag.sh and tools/ws_regs.sh make with -DGRL_DIAG; a product
 // build ignores them.
@@ -41,7 +41,6 @@
 #undef GRL_WS_DIAG_LB
 #undef GRL_WS_DIAG_ONE
 #undef GRL_WS_WHATIF
-#undef GRL_WS_NOIL
 #endif
 
 namespace grl {
@@ -837,9 +836,6 @@ __global__ __launch_bounds__(GRL_WS_DIAG_LB) void graphconv_ws_kernel(
     };
     // scheduling hint for the region just written: 2 MFMAs, then 3 VALU / 1 MFMA
     auto interleave = [&]() {
-#ifdef GRL_WS_NOIL
-      if (PROD == 4) return;  // A/B: no hand-placed interleave at C > 256 (two MFMA waves per SIMD)
-#endif
       __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
 #pragma unroll
       for (int q = 0; q < 10; ++q) {

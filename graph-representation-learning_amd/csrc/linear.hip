@@ -22,6 +22,22 @@
 
 #include <cstdlib>
 
+// GRL_X6T_WHATIF (diagnostic builds with -DGRL_DIAG only; timing, wrong
+// results): the dW GEMM without its split VALU (1), without its operand
+// stream after two steps (2), without its per-step barrier (4)
+#if !defined(GRL_DIAG) || !defined(GRL_X6T_WHATIF)
+#undef GRL_X6T_WHATIF
+#define GRL_X6T_WHATIF 0
+#endif
+// register sets of the dW GEMM's staged rows: 1, the loads one K16 step ahead
+// of their LDS stash; 2 (diagnostic builds: -DGRL_DIAG -DGRL_X6T_NR=2), two
+// steps -- measured neutral (profiles/r06_ab_dw_nr2.txt): the operand stream
+// costs the kernel power, not latency
+#if !defined(GRL_DIAG) || !defined(GRL_X6T_NR)
+#undef GRL_X6T_NR
+#define GRL_X6T_NR 1
+#endif
+
 namespace grl {
 namespace {
 
@@ -872,42 +888,55 @@ __global__ __launch_bounds__(512) void gemm_x6t_kernel(GemmArgs p) {
   const float* __restrict__ b_base = p.B + bn;
   const int st_off0 = kr0 * 256 + (col ^ ((kr0 & 3) << 5));
   const int st_off1 = kr1 * 256 + (col ^ ((kr1 & 3) << 5));
-  float4 ra0, ra1, rb0, rb1;
-  bool in0 = true, in1 = true;  // the staged rows lie inside this split's K range
+  // register sets of staged rows: set j holds step t's rows for t = j (mod NR); NR = 2 puts the loads
+  // two K16 steps ahead of their LDS stash (one step of MFMAs would leave an HBM miss's latency exposed)
+  constexpr int NR = GRL_X6T_NR;
+  float4 ra0[NR], ra1[NR], rb0[NR], rb1[NR];
+  bool in0[NR], in1[NR];  // the staged rows lie inside this split's K range
   const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
   // Rows past the split's end are loaded clamped (from kbeg) and zeroed only
   // when stashed, after the next step's MFMAs: zeroing right after the loads
   // made hipcc branch on the loaded registers and wait vmcnt(0) for them
   // there, exposing the whole load latency on every K16 step
   // (cdna_hip_programming.md, "register or load" selects).
-#define X6T_LOAD(t)                                                                                       \
+#define X6T_LOAD(t, j)                                                                                    \
   do {                                                                                                    \
     const int64_t k_ = kbeg + (t) * X6_K;                                                                 \
-    in0 = k_ + kr0 < kend;                                                                                \
-    in1 = k_ + kr1 < kend;                                                                                \
-    const int64_t r0_ = in0 ? k_ + kr0 : kbeg;                                                            \
-    const int64_t r1_ = in1 ? k_ + kr1 : kbeg;                                                            \
-    ra0 = *reinterpret_cast<const float4*>(a_base + r0_ * p.lda);                                         \
-    ra1 = *reinterpret_cast<const float4*>(a_base + r1_ * p.lda);                                         \
-    rb0 = *reinterpret_cast<const float4*>(b_base + r0_ * p.ldb);                                         \
-    rb1 = *reinterpret_cast<const float4*>(b_base + r1_ * p.ldb);                                         \
+    in0[j] = k_ + kr0 < kend;                                                                             \
+    in1[j] = k_ + kr1 < kend;                                                                             \
+    const int64_t r0_ = in0[j] ? k_ + kr0 : kbeg;                                                         \
+    const int64_t r1_ = in1[j] ? k_ + kr1 : kbeg;                                                         \
+    ra0[j] = *reinterpret_cast<const float4*>(a_base + r0_ * p.lda);                                      \
+    ra1[j] = *reinterpret_cast<const float4*>(a_base + r1_ * p.lda);                                      \
+    rb0[j] = *reinterpret_cast<const float4*>(b_base + r0_ * p.ldb);                                      \
+    rb1[j] = *reinterpret_cast<const float4*>(b_base + r1_ * p.ldb);                                      \
   } while (0)
+#if GRL_X6T_WHATIF & 1  /* what-if (timing only): no split VALU, the raw bits as planes */
+#define X6T_SPLIT3(v, q0_, q1_, q2_)                                                                      \
+  do {                                                                                                    \
+    q0_ = make_uint2(__float_as_uint((v).x), __float_as_uint((v).y));                                     \
+    q1_ = make_uint2(__float_as_uint((v).z), __float_as_uint((v).w));                                     \
+    q2_ = q0_;                                                                                            \
+  } while (0)
+#else
+#define X6T_SPLIT3(v, q0_, q1_, q2_) split3(v, q0_, q1_, q2_)
+#endif
 #define X6T_SPLIT(v, base, off)                                                                           \
   do {                                                                                                    \
     uint2 q0_, q1_, q2_;                                                                                  \
-    split3(v, q0_, q1_, q2_);                                                                             \
+    X6T_SPLIT3(v, q0_, q1_, q2_);                                                                         \
     *reinterpret_cast<uint2*>((base) + (off)) = q0_;                                                      \
     *reinterpret_cast<uint2*>((base) + X6_PLANE + (off)) = q1_;                                           \
     *reinterpret_cast<uint2*>((base) + 2 * X6_PLANE + (off)) = q2_;                                       \
   } while (0)
-#define X6T_STASH(st)                                                                                     \
+#define X6T_STASH(st, j)                                                                                  \
   do {                                                                                                    \
-    if (!in0) ra0 = rb0 = zero4; /* wave-uniform: only a split's last K16 step branches */                \
-    if (!in1) ra1 = rb1 = zero4;                                                                          \
-    X6T_SPLIT(ra0, (st), st_off0);                                                                        \
-    X6T_SPLIT(ra1, (st), st_off1);                                                                        \
-    X6T_SPLIT(rb0, (st) + 3 * X6_PLANE, st_off0);                                                         \
-    X6T_SPLIT(rb1, (st) + 3 * X6_PLANE, st_off1);                                                         \
+    if (!in0[j]) ra0[j] = rb0[j] = zero4; /* wave-uniform: only a split's last K16 step branches */       \
+    if (!in1[j]) ra1[j] = rb1[j] = zero4;                                                                 \
+    X6T_SPLIT(ra0[j], (st), st_off0);                                                                     \
+    X6T_SPLIT(ra1[j], (st), st_off1);                                                                     \
+    X6T_SPLIT(rb0[j], (st) + 3 * X6_PLANE, st_off0);                                                      \
+    X6T_SPLIT(rb1[j], (st) + 3 * X6_PLANE, st_off1);                                                      \
   } while (0)
 
   // this lane's transposed-read coordinates: k = 8h + ((lane & 15) >> 2),
@@ -924,9 +953,11 @@ __global__ __launch_bounds__(512) void gemm_x6t_kernel(GemmArgs p) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.0f;
 
   if (nk > 0) {
-    X6T_LOAD(0);
-    X6T_STASH(smem);
-    if (nk > 1) X6T_LOAD(1);
+    X6T_LOAD(0, 0);
+    X6T_STASH(smem, 0);
+#pragma unroll
+    for (int j = 1; j <= NR; ++j)
+      if (nk > j) X6T_LOAD(j, j % NR);
   }
   __syncthreads();
   {
@@ -937,8 +968,11 @@ __global__ __launch_bounds__(512) void gemm_x6t_kernel(GemmArgs p) {
     for (int i = 0; i < 4; ++i) oa[i] = tk * 256 + ((wm * 128 + i * 32 + tc) ^ sx);
 #pragma unroll
     for (int j = 0; j < 2; ++j) ob[j] = tk * 256 + ((wn * 64 + j * 32 + tc) ^ sx);
-    auto step = [&](int64_t t, auto stage) {
+    // step t reads LDS stage S = t & 1 and stashes register set J = (t + 1) % NR into the other stage:
+    // both constants of the body (the loop is unrolled by two, and NR is 1 or 2)
+    auto step = [&](int64_t t, auto stage, auto rset) {
       constexpr int S = decltype(stage)::value;
+      constexpr int J = decltype(rset)::value;  // (t + 1) % NR
       const lds_u16* cur = s3 + S * X6_STAGE;
       bf16x8_t a_[4][3], b_[2][3];
 #pragma unroll
@@ -961,17 +995,35 @@ __global__ __launch_bounds__(512) void gemm_x6t_kernel(GemmArgs p) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a_[i][0], b_[j][0], acc[i][j], 0, 0, 0);
         }
       if (t + 1 < nk) {
-        X6T_STASH(smem + (S ^ 1) * X6_STAGE);  // the other stage: last read in step t-1
-        if (t + 2 < nk) X6T_LOAD(t + 2);
+        X6T_STASH(smem + (S ^ 1) * X6_STAGE, J);  // the other stage: last read in step t-1
+#if GRL_X6T_WHATIF & 2
+        if (t + 1 + NR < nk && t < 2) X6T_LOAD(t + 1 + NR, J);  // what-if: no Z / g stream after the first steps
+#else
+        if (t + 1 + NR < nk) X6T_LOAD(t + 1 + NR, J);
+#endif
       }
+#if GRL_X6T_WHATIF & 4
+      __builtin_amdgcn_s_waitcnt(0);  // what-if: no barrier (races; timing only)
+#else
       __syncthreads();
+#endif
     };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
     int64_t t = 0;
-    for (; t + 1 < nk; t += 2) {
-      step(t, std::integral_constant<int, 0>{});
-      step(t + 1, std::integral_constant<int, 1>{});
+    if constexpr (NR == 1) {
+      for (; t + 1 < nk; t += 2) {
+        step(t, I0{}, I0{});
+        step(t + 1, I1{}, I0{});
+      }
+      if (t < nk) step(t, I0{}, I0{});
+    } else {  // NR == 2: the register set to stash is (t + 1) & 1 = the other LDS stage's parity
+      for (; t + 1 < nk; t += 2) {
+        step(t, I0{}, I1{});
+        step(t + 1, I1{}, I0{});
+      }
+      if (t < nk) step(t, I0{}, I1{});
     }
-    if (t < nk) step(t, std::integral_constant<int, 0>{});
   }
 #undef X6T_LOAD
 #undef X6T_SPLIT

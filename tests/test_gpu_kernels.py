@@ -96,9 +96,9 @@ def test_spmm_strided_input_rows():
 
 
 @pytest.mark.parametrize("N,deg,hub", [(1500, 9.0, 300),  # > 8192 edges: the radix-sort transpose
-                                       (120, 3.0, 40),     # a page: the one-workgroup transpose
+                                       (120, 3.0, 40),     # a page
                                        (64, 0.0, 0),       # no edges at all
-                                       (8192, 1.0, 0)])    # 8192 columns and edges: the one-workgroup limit
+                                       (8192, 1.0, 0)])    # 8192 columns and edges
 def test_csc_matches_oracle(N, deg, hub):
     L = 6
     rowptr, colidx, v = host_graph(N, L, deg, 77, hub=hub, vals=True)
@@ -113,7 +113,7 @@ def test_csc_matches_oracle(N, deg, hub):
 
 @pytest.mark.parametrize("layout", ["bnln", "bnnl", "pre"])
 @pytest.mark.parametrize("float_vals", [False, True])
-@pytest.mark.parametrize("B,N", [(3, 37), (4, 400)])  # one-workgroup rowptr scan; hipCUB's (> 8191 segments)
+@pytest.mark.parametrize("B,N", [(3, 37), (4, 400)])  # a page and > 8191 row segments
 def test_dense_to_csr_matches_oracle(layout, float_vals, B, N):
     import inputs as gi
 
