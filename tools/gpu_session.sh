@@ -170,6 +170,14 @@ for step in "$@"; do
     tests_r6a) run pytest_gpu_r6a 600 python -u -m pytest tests/test_gpu_graph_parallel.py tests/test_gpu_dist.py \
                   -m gpu -v -rf --timeout 300 --timeout-method thread ;;
     ab_wide) rm -f gpurun_out/ab_wide.log; run ab_wide 900 tools/ab_wide.sh ${AB_LIBS} ;;
+    pmc_wide_roles) for lib in libgrl.so diag/libgrl_wi4.so diag/libgrl_wi8.so; do n=$(basename $lib .so)
+                  GRL_LIB_PATH=graph-representation-learning_amd/grl/$lib PROBE_QUICK=1 PROBE_SHAPES=512x512,256x256 \
+                  run pmc_roles_$n 300 timeout -s KILL 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE \
+                  SQ_BUSY_CU_CYCLES SQ_INSTS_VALU SQ_INSTS_MFMA --kernel-trace -d "$OUT/pmc_roles_$n" -o run \
+                  --output-format csv -- python tools/probe_wide.py; done ;;
+    rehearse_p2) run rehearse_p2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+                  --master-addr 127.0.0.1 --master-port 29613 bench.py --gpus 2 --dist-backend gloo --steps 3 \
+                  --warmup 1 --cpu-seconds 5 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
