@@ -55,6 +55,8 @@ WORKLOADS = {  # name: (graph, nodes_total (None: per GPU), avg_deg, d, dropedge
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--option", action="append", default=[], metavar="NAME=VALUE",
+                    help="a libgrl path option (grl_set_option) for this run, e.g. spmm_blocks_per_cu=16 (A/B aid)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--workload", choices=["auto"] + list(WORKLOADS), default="auto",
@@ -226,6 +228,12 @@ def main():
     elif int(os.environ["WORLD_SIZE"]) != args.gpus:
         raise SystemExit(f"bench.py: WORLD_SIZE={os.environ['WORLD_SIZE']} from the launcher but --gpus {args.gpus}: "
                          "launch one rank per GPU with --gpus equal to the number of ranks")
+    if args.option:  # (each rank, after the spawn) before any kernel: a workspace query and its call see the same
+        from grl import set_option
+
+        for kv in args.option:
+            name, _, value = kv.partition("=")
+            set_option(name.strip(), int(value))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

@@ -59,9 +59,9 @@ for step in "$@"; do
     pmc_linear_mfma) run pmc_linear_mfma 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CU_CYCLES \
                   --kernel-trace -d "$OUT/pmc_linear_mfma" -o run --output-format csv \
                   -- python bench.py --only linear --steps 5 --warmup 1 ;;
-    pmc_linear_mfma_f32) export GRL_GEMM_X6=0; run pmc_linear_mfma_f32 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES \
+    pmc_linear_mfma_f32) run pmc_linear_mfma_f32 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES \
                   GRBM_GUI_ACTIVE SQ_BUSY_CU_CYCLES --kernel-trace -d "$OUT/pmc_linear_mfma_f32" -o run \
-                  --output-format csv -- python bench.py --only linear --steps 5 --warmup 1; unset GRL_GEMM_X6 ;;
+                  --output-format csv -- python bench.py --only linear --steps 5 --warmup 1 --option gemm_x6=0 ;;
     pmc_fwd_tlb) run pmc_fwd_tlb 300 rocprofv3 --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum \
                   --kernel-trace -d "$OUT/pmc_fwd_tlb" -o run --output-format csv \
                   -- python bench.py --only fwd --steps 5 --warmup 1 ;;
@@ -109,11 +109,8 @@ for step in "$@"; do
     prof_c5b) run prof_c5b 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_c5b" -o run --output-format csv \
                   -- python bench.py --workload C5 --only fwd --steps 5 --warmup 1 ;;
     probe_contig) run probe_contig 300 python tools/probe_contig.py ;;
-    ab_ws_status) run ab_ws_status 900 tools/ab_ws_status.sh r2gc ;;
     tests_warper) run pytest_gpu_warper 600 python -u -m pytest tests/test_gpu_warper.py tests/test_gpu_graph_capture.py \
                   -m gpu -v -rf --timeout 300 --timeout-method thread ;;
-    ab_noslp) export ATTN_N="100000 131072"; run ab_attn_noslp 900 tools/ab_attn_lib.sh attn_noslp && \
-              run ab_gc_noslp 900 tools/ab_ws_status.sh gc_noslp && run ab_lin_noslp 900 tools/ab_gemm_lib.sh lin_noslp ;;
     tests_attn) run pytest_gpu_attn 600 python -u -m pytest tests/test_gpu_attention.py tests/test_gpu_model.py -m gpu -q -rf \
                   --timeout 300 --timeout-method thread ;;
     ab_attn) export ATTN_N="100000 131072"; run ab_attn 900 tools/ab_attn_lib.sh ${AB_LIBS:-attn_prev} ;;
@@ -135,7 +132,6 @@ for step in "$@"; do
     pmc_layer_mfma) run pmc_layer_mfma 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CU_CYCLES \
                   SQ_INSTS_VALU SQ_INSTS_MFMA --kernel-trace -d "$OUT/pmc_layer_mfma" -o run --output-format csv \
                   -- python bench.py --only layer --steps 3 --warmup 1 ;;
-    ab_fused_dq) rm -f gpurun_out/ab_fused_dq.log; run ab_fused_dq 900 tools/ab_fused_dq.sh ;;
     prof_attn_fused) run prof_attn_fused 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_attn_fused" -o run \
                   --output-format csv -- python tools/probe_attn.py 100000 ;;
     ab_attn_hu) export ATTN_N="100000"; rm -f gpurun_out/ab_attn_lib.log; run ab_attn_hu 500 tools/ab_attn_lib.sh attn_b20 attn_pin0 attn_hu0 attn_r3 ;;
@@ -178,6 +174,7 @@ for step in "$@"; do
     rehearse_p2) run rehearse_p2 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
                   --master-addr 127.0.0.1 --master-port 29613 bench.py --gpus 2 --dist-backend gloo --steps 3 \
                   --warmup 1 --cpu-seconds 5 ;;
+    ab_fused) rm -f gpurun_out/ab_fused_lib.log; run ab_fused 900 tools/ab_fused_lib.sh ${AB_LIBS} ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

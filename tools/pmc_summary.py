@@ -42,7 +42,7 @@ def main():
              "SQ_VALU_MFMA_BUSY_CYCLES = 32 x number of 32x32x16 bf16 MFMAs (6 per fp32 32x32x16 block: 168M "
              "per launch); TFLOP/s = fp32-equivalent flops (2MKC) over wall time"),
             ("linear_fwd_C3_f32mfma", "pmc_linear_mfma_f32", "gemm256p_kernel<true, false, 0, 3>",
-             "gemm256p_kernel<KC,RC,STORE,3> (grl_linear_fwd with GRL_GEMM_X6=0)",
+             "gemm256p_kernel<KC,RC,STORE,3> (grl_linear_fwd with gemm_x6 = 0)",
              "SQ_VALU_MFMA_BUSY_CYCLES = 64 x number of 32x32x2 f32 MFMAs (224M per launch)")):
         if not os.path.isdir(os.path.join(root, d)):
             continue

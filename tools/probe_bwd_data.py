@@ -11,7 +11,7 @@ import time
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "graph-representation-learning_amd"))
 import torch  # noqa: E402
 
-from grl import DropEdge, TypedGraph  # noqa: E402
+from grl import DropEdge, TypedGraph, set_option  # noqa: E402
 from grl.ops import graph_conv, graph_conv_bwd_data, linear_bwd_data, spmm_backward  # noqa: E402
 
 
@@ -60,10 +60,10 @@ def main():
             (graph_conv(X, g, Wp, b, relu=True) * G).sum().backward()
 
         for fb in ("1", "0"):
-            os.environ["GRL_GRAPHCONV_FUSED_BWD"] = fb
+            set_option("graphconv_fused_bwd", int(fb))
             print(f"p={p}: layer fwd+bwd (dX {'one kernel' if fb == '1' else 'chain'}) "
                   f"{timeit(layer, 5):.3f} ms", flush=True)
-        os.environ.pop("GRL_GRAPHCONV_FUSED_BWD")
+        set_option("graphconv_fused_bwd", 1)
         del X, Wp, b, X0, b0
 
 

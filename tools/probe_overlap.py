@@ -1,6 +1,6 @@
 """Diagnostic: can the HBM-bound typed SpMM and the MFMA-bound GraphConv GEMM
 run concurrently on two HIP streams (C3 shapes)?  Times each alone and both
-together; run under GRL_SPMM_BLOCKS_PER_CU=16/8/4 to vary the SpMM's
+together; run with grl.set_option("spmm_blocks_per_cu", 16 / 8 / 4) to vary the SpMM's
 persistent-grid footprint."""
 import os
 import sys

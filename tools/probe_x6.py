@@ -1,5 +1,5 @@
 """Diagnostic: split-bf16 ("x6") vs fp32-MFMA GEMMs at the C3 layer shape.
-Runs itself twice (GRL_GEMM_X6=1 / 0, the switch is read once per process)
+Runs itself twice (path option gemm_x6 = 1 / 0, one child process each)
 and prints time, TFLOP/s and the error vs fp64 on sampled rows, relative to
 sum |terms| per element (the test suite's criterion)."""
 import json
@@ -12,7 +12,10 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 
 def child():
     import torch
+    from grl import set_option
     from grl.ops import linear_bwd_data, linear_fwd
+
+    set_option("gemm_x6", int(sys.argv[2]))
 
     def t(fn, n=10):
         fn()
@@ -58,8 +61,7 @@ if __name__ == "__main__":
         child()
     else:
         for v in ("1", "0"):
-            env = dict(os.environ, GRL_GEMM_X6=v)
-            r = subprocess.run([sys.executable, __file__, "child"], env=env, capture_output=True, text=True)
+            r = subprocess.run([sys.executable, __file__, "child", v], capture_output=True, text=True)
             line = [x for x in r.stdout.splitlines() if x.startswith("RESULT ")]
             print(line[0] if line else f"x6={v} failed rc={r.returncode}: {r.stderr[-2000:]}", flush=True)
             if r.returncode:
