@@ -1139,7 +1139,8 @@ class ShardedGraph:
         if (a.vals is None) != (b.vals is None):
             return False
         return bool(torch.equal(a.rowptr, b.rowptr) and torch.equal(a.colidx, b.colidx)
-                    and (a.vals is None or torch.equal(a.vals.view(torch.int32), b.vals.view(torch.int32))))
+                    and (a.vals is None or torch.equal(a.vals.contiguous().view(torch.int32),
+                                                  b.vals.contiguous().view(torch.int32))))
 
     @property
     def global_rows(self) -> int:

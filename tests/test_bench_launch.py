@@ -63,3 +63,12 @@ def test_pmc_traffic_is_keyed_by_workload_world_and_kernel():
     assert bench.load_traffic(a, "C4", 1_500_000, 2, shard) is None  # another shard shape
     assert bench.load_traffic(a, "C4", 1_000_000, 1, one) is None  # C4 has no one-GPU record
     assert bench.load_traffic(a, "C3", 1_000_000, 1, "gemm_x6_kernel") is None  # another kernel's bytes: never
+
+
+def test_unknown_path_option_is_refused_before_any_work():
+    """bench.py --option NAME=VALUE sets a libgrl path option (grl_set_option)
+    for the run; an unknown name fails at once, naming it, with no JSON line."""
+    r = _bench(["--option", "no_such_option=1", "--cpu-seconds", "0"])
+    assert r.returncode != 0
+    assert "unknown option 'no_such_option'" in r.stderr
+    assert not any(ln.startswith("{") for ln in r.stdout.splitlines())
