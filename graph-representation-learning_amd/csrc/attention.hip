@@ -1548,6 +1548,176 @@ __global__ __launch_bounds__(64 * NW, 8 / NW) void attn_bwd_kv_x6_kernel(AttnArg
 }
 
 
+// ---------------------------------------------------------------------------
+// dH on v_mfma_f32_16x16x32_bf16 (dk <= 16, PRE staging, 8 waves of 32 keys):
+// the work of attn_bwd_kv_x6_kernel<16, true, true, *, 8> in 16 x 16 tiles.
+//  * S = Q K^T, 4 tiles (2 query x 2 key) of 3 MFMAs: the six x6 products of
+//    the dk = 16 contraction paired along K = 32 -- lanes 0..31 carry the
+//    first product's 16 k, lanes 32..63 the second's: [Q_hi | Q_hi] [K_hi |
+//    K_mid], [Q_mid | Q_lo] [K_hi | K_hi], [Q_mid | Q_hi] [K_mid | K_lo].
+//    The keys' planes (B) are split once into registers; the query rows (A)
+//    come from the staged Q planes, row c of query tile t being query
+//    8 (c >> 2) + 4 t + (c & 3), so that the tile rows a lane group g holds
+//    after the MFMA are queries 8 g .. 8 g + 7 -- its K slice of the P.dO
+//    product, in natural order;
+//  * P = 2^(s - lse2) (8 distinct queries per lane), split into planes, is
+//    the B operand of dH^T += dO^T P as it lies; dO^T's fragments are two
+//    ds_read_b64_tr_b16 per plane (rows 8 g .. 8 g + 3 and 8 g + 4 ..
+//    8 g + 7: the two 16-lane groups of a half read blocks 8 rows apart, the
+//    conflict-free case of the swizzled 256-B rows);
+//  * 16 f32x4 accumulators (8 feature x 2 key tiles), x6 product order.
+// The same products as the 32x32x16 kernel with the two plane products of
+// S summed inside one MFMA: results equal within fp32 rounding (tested vs
+// float64).  Staging, stats and the query split are the 32x32x16 kernel's.
+typedef float af32x4_t __attribute__((ext_vector_type(4)));
+#define MFMA16(acc, a, b) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16((a), (b), (acc), 0, 0, 0)
+template <bool SPLIT>
+__global__ __launch_bounds__(512, 1) void attn_bwd_h16_kernel(AttnArgs a) {
+  constexpr int NW = 8, FT = 8;  // 128 value columns = 8 tiles of 16
+  __shared__ __attribute__((aligned(16))) uint16_t Qp_s[2 * 3 * 32 * 32];
+  __shared__ __attribute__((aligned(16))) uint16_t Op_s[2 * 3 * 32 * 128];
+  __shared__ __attribute__((aligned(16))) float Ms_s[2 * 32];  // lse2 per query
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int c16 = lane & 15, g = lane >> 4;
+  const int64_t N = a.N, b = blockIdx.y;
+  const int64_t key0 = (int64_t)blockIdx.x * (32 * NW) + wave * 32;  // this wave's 32 keys
+  const int64_t q_lo = SPLIT ? (int64_t)blockIdx.z * a.kr : a.q0, q_hi = SPLIT ? min<int64_t>(N, q_lo + a.kr) : a.q1;
+  // B operands of S: key 16 kt + c16, k = 8 (g & 1) .. + 7, plane by MFMA m and lane half
+  abf16x8_t kb[2][3];
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt) {
+    const int64_t key = key0 + 16 * kt + c16;
+    const bool kv = key < N;
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int d = 8 * (g & 1) + j;
+      v[j] = (kv && d < a.dk) ? a.K[(b * N + key) * a.dk + d] * ALOG2E : 0.0f;  // base-2 scores
+    }
+    abf16x8_t p0, p1, p2;
+    asplit8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]), p0, p1, p2);
+    kb[kt][0] = g < 2 ? p0 : p1;  // [K_hi | K_mid]
+    kb[kt][1] = p0;               // [K_hi | K_hi]
+    kb[kt][2] = g < 2 ? p1 : p2;  // [K_mid | K_lo]
+  }
+  af32x4_t acc[FT][2];
+#pragma unroll
+  for (int ft = 0; ft < FT; ++ft)
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) acc[ft][kt] = af32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+  const int64_t qps = (int64_t)gridDim.y * N * 32, ops = (int64_t)gridDim.y * N * 128;
+  DmaRows<32, PL_PLAIN, NW> qd;
+  DmaRows<128, PL_SWZ128, NW> od;
+  qd.init(a.Qpl + b * N * 32, qps, wave, lane);
+  od.init(a.Opl + b * N * 128, ops, wave, lane);
+  qd.issue(q_lo, N, Qp_s, wave, lane);
+  od.issue(q_lo, N, Op_s, wave, lane);
+  float pm = 0.0f;
+  auto fetch_stats = [&](int64_t q0) {
+    if (tid < 32) {
+      const int64_t qq = q0 + tid;
+      // lse2 = +inf => P = 0 for padded queries
+      pm = qq < q_hi ? fmaf(a.smax[b * N + qq], ALOG2E, alog2(a.ssum[b * N + qq])) : INFINITY;
+    }
+  };
+  fetch_stats(q_lo);
+  // A-operand planes of S per MFMA m for this lane's half: [hi | hi], [mid | lo], [mid | hi]
+  const int qa0 = 0, qa1 = g < 2 ? 1 : 2, qa2 = g < 2 ? 1 : 0;
+  const int qrow0 = 8 * (c16 >> 2) + (c16 & 3);  // query tile 0's row; tile 1: + 4
+  const int qcol = 8 * (g & 1);
+  const int q4 = c16 >> 2, p4 = c16 & 3;  // transposed reads: row q4 of a 4-row block, 8-B piece p4
+
+  auto block = [&](int64_t q0, auto stc) {
+    constexpr int SC = decltype(stc)::value;
+    const int stg = SC >= 0 ? SC : (int)(((q0 - q_lo) >> 5) & 1);
+    const lds_u16* Op3 = (const lds_u16*)Op_s + stg * 3 * 4096;
+    float* Ms = Ms_s + stg * 32;
+    if (tid < 32) Ms[tid] = pm;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (q0 + 32 < q_hi) {
+      qd.issue(q0 + 32, N, Qp_s + (stg ^ 1) * 3 * 1024, wave, lane);
+      od.issue(q0 + 32, N, Op_s + (stg ^ 1) * 3 * 4096, wave, lane);
+      fetch_stats(q0 + 32);
+    }
+    // S tiles [qt][kt]: rows (queries 8 g + 4 qt + i) in registers, keys 16 kt + c16 on lanes
+    af32x4_t st[2][2];
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      const uint16_t* qr = Qp_s + stg * 3 * 1024 + (qrow0 + 4 * qt) * 32 + qcol;
+      abf16x8_t qa[3];
+      qa[0] = *reinterpret_cast<const abf16x8_t*>(qr + qa0 * 1024);
+      qa[1] = *reinterpret_cast<const abf16x8_t*>(qr + qa1 * 1024);
+      qa[2] = *reinterpret_cast<const abf16x8_t*>(qr + qa2 * 1024);
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        af32x4_t sacc = {0.0f, 0.0f, 0.0f, 0.0f};
+        MFMA16(sacc, qa[0], kb[kt][0]);
+        MFMA16(sacc, qa[1], kb[kt][1]);
+        MFMA16(sacc, qa[2], kb[kt][2]);
+        st[qt][kt] = sacc;
+      }
+    }
+    // P = 2^(s - lse2) for queries 8 g .. 8 g + 7 (a padded key's column is never stored)
+    const float4 m0 = *reinterpret_cast<const float4*>(Ms + 8 * g);
+    const float4 m1 = *reinterpret_cast<const float4*>(Ms + 8 * g + 4);
+    abf16x8_t pb[2][3];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      const float4 lo = make_float4(aexp2(st[0][kt][0] - m0.x), aexp2(st[0][kt][1] - m0.y),
+                                    aexp2(st[0][kt][2] - m0.z), aexp2(st[0][kt][3] - m0.w));
+      const float4 hi = make_float4(aexp2(st[1][kt][0] - m1.x), aexp2(st[1][kt][1] - m1.y),
+                                    aexp2(st[1][kt][2] - m1.z), aexp2(st[1][kt][3] - m1.w));
+      asplit8(lo, hi, pb[kt][0], pb[kt][1], pb[kt][2]);
+    }
+    // dH^T[feature][key] += dO^T[feature][query] P[query][key]
+#pragma unroll
+    for (int ft = 0; ft < FT; ++ft) {
+      abf16x8_t oa[3];
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        oa[pl] = tr8s(Op3 + pl * 4096 + swz128(8 * g + q4, 16 * ft + 4 * p4),
+                      Op3 + pl * 4096 + swz128(8 * g + 4 + q4, 16 * ft + 4 * p4));
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {  // gemm_x6_kernel's product order
+        MFMA16(acc[ft][kt], oa[2], pb[kt][0]);
+        MFMA16(acc[ft][kt], oa[1], pb[kt][1]);
+        MFMA16(acc[ft][kt], oa[0], pb[kt][2]);
+        MFMA16(acc[ft][kt], oa[1], pb[kt][0]);
+        MFMA16(acc[ft][kt], oa[0], pb[kt][1]);
+        MFMA16(acc[ft][kt], oa[0], pb[kt][0]);
+      }
+    }
+  };
+  int64_t q0 = q_lo;
+  for (; q0 + 32 < q_hi; q0 += 64) {
+    block(q0, std::integral_constant<int, 0>{});
+    block(q0 + 32, std::integral_constant<int, 1>{});
+  }
+  if (q0 < q_hi) block(q0, std::integral_constant<int, 0>{});
+  // query split: partial dH into slab blockIdx.z (summed in split order afterwards)
+  const int64_t rows = (int64_t)gridDim.y * N;
+  float* dst = SPLIT ? a.part + (int64_t)blockIdx.z * rows * a.dv : a.dH;
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt) {
+    const int64_t key = key0 + 16 * kt + c16;
+    if (key >= N) continue;
+    float* row = dst + (b * N + key) * a.dv;
+#pragma unroll
+    for (int ft = 0; ft < FT; ++ft) {
+      const int f = 16 * ft + 4 * g;
+      if (f + 3 < a.dv) {
+        *reinterpret_cast<float4*>(row + f) = make_float4(acc[ft][kt][0], acc[ft][kt][1], acc[ft][kt][2], acc[ft][kt][3]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          if (f + i < a.dv) row[f + i] = acc[ft][kt][i];
+      }
+    }
+  }
+}
+#undef MFMA16
+
 // Key-stationary dK with dQ folded in (dk <= 16, PRE staging): what the
 // query-stationary attn_bwd_q_x6_kernel computes, without recomputing S and
 // dP = dO H^T for it -- 66 MFMAs per 32 x 32 block pair there, 18 more here.
@@ -1848,6 +2018,9 @@ bool attn_dh8_enabled() { return opt(OPT_ATTN_DH8) != 0; }
 // path option attn_fused_dq = 0 keeps the separate dQ kernel (A/B aid)
 bool attn_fused_dq_enabled() { return opt(OPT_ATTN_FUSED_DQ) != 0; }
 
+// path option attn_dh16 = 0 keeps dH on the 32x32x16 kernel
+bool attn_dh16_enabled() { return opt(OPT_ATTN_DH16) != 0; }
+
 // path option attn_pipe = 0 keeps the unpipelined x6 forward (A/B aid)
 bool attn_pipe_enabled() { return opt(OPT_ATTN_PIPE) != 0; }
 
@@ -1916,7 +2089,13 @@ int launch_attn(AttnPass pass, const AttnArgs& a0, int64_t B, int S, hipStream_t
       }
     } else {
       if (S > 1) a.part2 = a.part + (int64_t)S * rows * a.dv;
-      if (pre && attn_dh8_enabled()) {  // dH on 256-key workgroups
+      if (pre && attn_dh8_enabled() && DKP == 16 && attn_dh16_enabled()) {  // dH in 16 x 16 tiles
+        const dim3 g8((unsigned)ceil_div(a.N, 256), (unsigned)B, (unsigned)S);
+        if (S > 1)
+          hipLaunchKernelGGL((attn_bwd_h16_kernel<true>), g8, dim3(512), 0, st, a);
+        else
+          hipLaunchKernelGGL((attn_bwd_h16_kernel<false>), g8, dim3(512), 0, st, a);
+      } else if (pre && attn_dh8_enabled()) {  // dH on 256-key workgroups
         const dim3 g8((unsigned)ceil_div(a.N, 256), (unsigned)B, (unsigned)S);
         if (S > 1)
           hipLaunchKernelGGL((attn_bwd_kv_x6_kernel<DKP, true, true, true, 8>), g8, dim3(512), 0, st, a);

@@ -177,6 +177,7 @@ def test_eight_wave_workgroups_same_bits(B, N, dk, dv, monkeypatch, grl_option):
     every gradient bitwise, partial last blocks and splits included."""
     Q, K, H, V, gamma = _inputs(B, N, dk, dv, seed=N + dv)
     res = {}
+    grl_option("attn_dh16", 0)  # the 32x32x16 dH on both workgroup sizes
     for v in ("1", "0"):
         grl_option("attn_fwd8", int(v))
         grl_option("attn_dh8", int(v))
@@ -186,6 +187,31 @@ def test_eight_wave_workgroups_same_bits(B, N, dk, dv, monkeypatch, grl_option):
         res[v] = [out.detach()] + [t.grad for t in leaves]
     for a, b in zip(res["1"], res["0"]):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("B,N,dk,dv", [(1, 8192, 16, 128), (3, 4099, 9, 100), (64, 1024, 16, 128), (4, 1100, 16, 128),
+                                       (1, 20_000, 16, 128), (2, 4127, 16, 32)])
+def test_dh_on_16x16x32_matches_fp64(B, N, dk, dv, grl_option):
+    """attn_bwd_h16_kernel (dH in 16 x 16 tiles on v_mfma_f32_16x16x32_bf16,
+    the six x6 products of S paired along K = 32): every gradient against
+    float64, and dH within fp32 rounding of the 32x32x16 kernel -- unsplit
+    and query-split grids (N = 1100 x 4, 20k), partial blocks, dk = 9,
+    dv = 100 (zero-padded planes) and dv = 32 (its own 32-wide planes: the
+    32x32x16 kernel runs)."""
+    Q, K, H, V, gamma = _inputs(B, N, dk, dv, seed=5 * N + dk)
+    dout = torch.randn(B, N, dv, generator=torch.Generator().manual_seed(4)).to(DEV)
+    grads = {}
+    for v in (1, 0):
+        grl_option("attn_dh16", v)
+        leaves = [t.clone().requires_grad_(True) for t in (Q, K, H, V, gamma)]
+        node_self_attention(*leaves).backward(dout)
+        grads[v] = [t.grad for t in leaves]
+    ref_leaves = [t.double().clone().requires_grad_(True) for t in (Q, K, H, V, gamma)]
+    _ref(*ref_leaves).backward(dout.double())
+    for name, a, c, r in zip("QKHVg", grads[1], grads[0], ref_leaves):
+        scale = r.grad.abs().max().item() + 1.0
+        torch.testing.assert_close(a.double(), r.grad, rtol=1e-4, atol=2e-5 * scale, msg=f"dh16 d{name}")
+        torch.testing.assert_close(a.double(), c.double(), rtol=1e-5, atol=1e-6 * scale, msg=f"dh16 vs 32x32 d{name}")
 
 
 RANGED = [(1, 20_000, 16, 128, (0, 7000, 13_003, 20_000)), (2, 3000, 16, 100, (0, 0, 1, 1500, 3000)),

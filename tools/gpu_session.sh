@@ -175,6 +175,9 @@ for step in "$@"; do
                   --master-addr 127.0.0.1 --master-port 29613 bench.py --gpus 2 --dist-backend gloo --steps 3 \
                   --warmup 1 --cpu-seconds 5 ;;
     ab_fused) rm -f gpurun_out/ab_fused_lib.log; run ab_fused 900 tools/ab_fused_lib.sh ${AB_LIBS} ;;
+    ab_attn_opt) rm -f gpurun_out/ab_attn_opt.log; run ab_attn_opt 900 tools/ab_attn_opt.sh ${AB_OPTS} ;;
+    tests_dh16) run pytest_gpu_dh16 600 python -u -m pytest tests/test_gpu_attention.py -m gpu -v -rf --timeout 300 \
+                  --timeout-method thread -k "dh_on_16 or eight_wave or backward_matches" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

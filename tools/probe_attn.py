@@ -22,7 +22,14 @@ def timeit(fn, n=5):
 
 
 dev = torch.device("cuda:0")
-for N in ([int(x) for x in sys.argv[1:]] or (2048, 16384, 65536, 131072)):
+# arguments: N values, and NAME=VALUE path options (grl.set_option) for the whole run
+_opts = [a for a in sys.argv[1:] if "=" in a]
+if _opts:
+    from grl import set_option
+
+    for kv in _opts:
+        set_option(kv.split("=")[0], int(kv.split("=")[1]))
+for N in ([int(x) for x in sys.argv[1:] if "=" not in x] or (2048, 16384, 65536, 131072)):
     dk, dv = 16, 128
     torch.manual_seed(N)  # the same inputs in every library's run (AB_SAVE bit check)
     Q, K = torch.relu(torch.randn(1, N, dk, device=dev)), torch.relu(torch.randn(1, N, dk, device=dev))
@@ -46,5 +53,5 @@ for N in ([int(x) for x in sys.argv[1:]] or (2048, 16384, 65536, 131072)):
             same = bool(torch.equal(torch.load(path, weights_only=True), got))
         else:
             torch.save(got, path)
-    print(f"N={N:7d} fwd {ms:9.3f} ms {flops / ms / 1e9:7.1f} TFLOP/s | fwd+bwd {ms_fb:9.3f} ms "
+    print(f"{' '.join(_opts)} N={N:7d} fwd {ms:9.3f} ms {flops / ms / 1e9:7.1f} TFLOP/s | fwd+bwd {ms_fb:9.3f} ms "
           f"{(flops + bflops) / ms_fb / 1e9:7.1f} TFLOP/s bitwise_vs_first={same}", flush=True)
