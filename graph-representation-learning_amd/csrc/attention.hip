@@ -1651,10 +1651,10 @@ __global__ __launch_bounds__(512, 1) void attn_bwd_h16_kernel(AttnArgs a) {
       qa[2] = *reinterpret_cast<const abf16x8_t*>(qr + qa2 * 1024);
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) {
-        af32x4_t sacc = {0.0f, 0.0f, 0.0f, 0.0f};
-        MFMA16(sacc, qa[0], kb[kt][0]);
-        MFMA16(sacc, qa[1], kb[kt][1]);
+        af32x4_t sacc = {0.0f, 0.0f, 0.0f, 0.0f};  // small products first, hi.hi last: one rounding at |s|
         MFMA16(sacc, qa[2], kb[kt][2]);
+        MFMA16(sacc, qa[1], kb[kt][1]);
+        MFMA16(sacc, qa[0], kb[kt][0]);
         st[qt][kt] = sacc;
       }
     }
@@ -1937,6 +1937,257 @@ __global__ __launch_bounds__(64 * KQ_WAVES, 1) void attn_bwd_kq_x6_kernel(AttnAr
   }
 }
 
+// ---------------------------------------------------------------------------
+// The fused dK / dQ pass on v_mfma_f32_16x16x32_bf16 (dk <= 16, PRE staging,
+// 8 waves of 32 keys, one workgroup per CU): attn_bwd_kq_x6_kernel's work in
+// 16 x 16 tiles.  Per query block of 32:
+//  * S = Q K^T as in attn_bwd_h16_kernel (the six x6 products of the dk = 16
+//    contraction paired along K = 32; K at natural scale, as dQ needs it, so
+//    P = 2^(fma(s, log2 e, -lse2))) and dP = dO H^T (4 feature chunks of 32,
+//    6 products each) in the same 2 x 2 tiles: lane group g holds queries
+//    8 g .. 8 g + 7 of both, keys on lanes;
+//  * dS = P (dP - D), split into planes, is the B operand of
+//    dK^T[d][key] += Q^T dS as it lies (Q^T: transposed reads of the staged
+//    16-wide planes); the 32x32x16 kernel's dK and dQ tiles were half
+//    padding (dk = 16 of 32 rows), these have none;
+//  * the same registers are dS^T as an A operand: an MFMA against a 0/1
+//    selection of 16 queries transposes each plane exactly (one nonzero
+//    product per element), giving dS with queries on lanes and keys
+//    4 g .. 4 g + 3, 16 + 4 g .. 16 + 4 g + 3 in registers -- dQ's A operand,
+//    with K's planes (split once, registers) in that key order as B;
+//  * dQ partials go through the LDS slots and per-workgroup slabs exactly as
+//    in attn_bwd_kq_x6_kernel, so attn_qslab_sum_kernel is unchanged.
+// Per block and wave 144 MFMAs of 16x16x32 = 72 of 32x32x16 (84 there).
+// The same products in the same order per output; the pairing of S's
+// products inside one MFMA changes rounding only (tested vs float64).
+#define MFMA16(acc, a, b) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16((a), (b), (acc), 0, 0, 0)
+#define X6_16(acc, A, B)    \
+  do {                      \
+    MFMA16(acc, A[2], B[0]); \
+    MFMA16(acc, A[1], B[1]); \
+    MFMA16(acc, A[0], B[2]); \
+    MFMA16(acc, A[1], B[0]); \
+    MFMA16(acc, A[0], B[1]); \
+    MFMA16(acc, A[0], B[0]); \
+  } while (0)
+template <bool SPLIT>
+__global__ __launch_bounds__(64 * KQ_WAVES, 1) void attn_bwd_kq16_kernel(AttnArgs a) {
+  constexpr int FC = 4, NW = KQ_WAVES, KW = KQ_KEYS;  // 128 value columns = 4 chunks of 32
+  constexpr int RP = 36;                              // partial row pitch (floats), as attn_bwd_kq_x6_kernel
+  constexpr int RSLOT = NW * 16 * RP;
+  __shared__ __attribute__((aligned(16))) uint16_t Qp_s[2 * 3 * 32 * 16];  // 2 stages, 16-wide planes
+  __shared__ __attribute__((aligned(16))) uint16_t Op_s[2 * 3 * 32 * 128];
+  __shared__ __attribute__((aligned(16))) uint16_t Kt_s[3 * KW * 16];  // the workgroup's K rows, planes [key][16]
+  __shared__ __attribute__((aligned(16))) float Red_s[2 * RSLOT];  // 2 slots x the waves' partials [w][d][RP]
+  __shared__ __attribute__((aligned(16))) float Ms_s[2 * 32], Ds_s[2 * 32];  // lse2, D per query
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int c16 = lane & 15, g = lane >> 4;
+  const int64_t N = a.N, b = blockIdx.y;
+  const int64_t key0 = a.k0 + (int64_t)blockIdx.x * KW + wave * 32;  // this wave's 32 keys
+  const int64_t q_lo = SPLIT ? (int64_t)blockIdx.z * a.kr : a.q0, q_hi = SPLIT ? min<int64_t>(N, q_lo + a.kr) : a.q1;
+  // this wave's K rows, natural scale, as planes [key][16] in LDS (S's B operand; zero for padded
+  // keys), and dP's B operand H[key 16 kt + c16][32 fc + 8 g + j] in registers
+  {
+    const int64_t key = key0 + (lane >> 1);
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int d = 8 * (lane & 1) + j;
+      v[j] = (key < N && d < a.dk) ? a.K[(b * N + key) * a.dk + d] : 0.0f;
+    }
+    abf16x8_t p[3];
+    asplit8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]), p[0], p[1], p[2]);
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+      *reinterpret_cast<abf16x8_t*>(&Kt_s[pl * KW * 16 + (wave * 32 + (lane >> 1)) * 16 + 8 * (lane & 1)]) = p[pl];
+  }
+  abf16x8_t hb[2][FC][3];
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt) {
+    const int64_t key = key0 + 16 * kt + c16;
+    const bool kv = key < N;
+    float v[8];
+#pragma unroll
+    for (int fc = 0; fc < FC; ++fc) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int f = 32 * fc + 8 * g + j;
+        v[j] = (kv && f < a.dv) ? a.H[(b * N + key) * a.dv + f] : 0.0f;
+      }
+      asplit8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]), hb[kt][fc][0], hb[kt][fc][1],
+              hb[kt][fc][2]);
+    }
+  }
+  // B operand of dQ: K[key pi(g, j)][d c16] with pi(g, j) = 4 g + j (j < 4), 12 + 4 g + j (j >= 4):
+  // the key order of the transposed dS
+  abf16x8_t kq[3];
+  {
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int64_t key = key0 + (j < 4 ? 4 * g + j : 12 + 4 * g + j);
+      v[j] = (key < N && c16 < a.dk) ? a.K[(b * N + key) * a.dk + c16] : 0.0f;
+    }
+    asplit8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]), kq[0], kq[1], kq[2]);
+  }
+  // 0/1 selections of queries 16 nt .. 16 nt + 15: B[k = 8 g + j][n = c16] = 1 iff k == 16 nt + n
+  abf16x8_t sel[2];
+#pragma unroll
+  for (int nt = 0; nt < 2; ++nt) {
+    ai16x8_t s;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[j] = (8 * g + j == 16 * nt + c16) ? (short)0x3F80 : (short)0;
+    sel[nt] = __builtin_bit_cast(abf16x8_t, s);
+  }
+  af32x4_t acck[2] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
+  const int64_t qps = (int64_t)gridDim.y * N * 16, ops = (int64_t)gridDim.y * N * 128;
+  const uint16_t* Qpb = a.Qpl16 + b * N * 16;
+  const uint16_t* Opb = a.Opl + b * N * 128;
+  const int64_t npad = (N + 31) & ~(int64_t)31;  // slab rows padded to whole query blocks
+  float* slab = a.qslab + ((int64_t)b * gridDim.x + blockIdx.x) * 16 * npad;  // [d][npad]
+  float pm = 0.0f, pd = 0.0f;
+  auto fetch_stats = [&](int64_t q0) {
+    if (tid < 32) {
+      const int64_t qq = q0 + tid;
+      const bool v = qq < q_hi;
+      pm = v ? fmaf(a.smax[b * N + qq], ALOG2E, alog2(a.ssum[b * N + qq])) : INFINITY;  // P = 0 when padded
+      pd = v ? a.Drow[b * N + qq] : 0.0f;
+    }
+  };
+  auto reduce = [&](int64_t qb) {  // as attn_bwd_kq_x6_kernel: wave w adds queries [4w, 4w + 4) x 16 d
+    const float* src = Red_s + (int)(((qb - q_lo) >> 5) & 1) * RSLOT;
+    const int q = 4 * wave + (lane >> 4), d = lane & 15;
+    float x = src[d * RP + q];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) x += src[w * 16 * RP + d * RP + q];
+    slab[d * npad + qb + q] = x;
+  };
+  dma_block<16, PL_PLAIN, NW>(Qpb, qps, q_lo, N, Qp_s, wave, lane);
+  dma_block<128, PL_SWZ128, NW>(Opb, ops, q_lo, N, Op_s, wave, lane);
+  fetch_stats(q_lo);
+  const int qa1 = g < 2 ? 1 : 2, qa2 = g < 2 ? 1 : 0;  // S's A planes per MFMA: [hi|hi], [mid|lo], [mid|hi]
+  const int kb0 = g < 2 ? 0 : 1, kb2 = g < 2 ? 1 : 2;  // and B planes: [hi|mid], [hi|hi], [mid|lo]
+  const int qrow0 = 8 * (c16 >> 2) + (c16 & 3);        // query tile 0's row c16; tile 1: + 4
+  const int q4 = c16 >> 2, p4 = c16 & 3;               // transposed reads: row q4 of a 4-row block, piece p4
+
+  for (int64_t q0 = q_lo; q0 < q_hi; q0 += 32) {
+    const int stg = (int)(((q0 - q_lo) >> 5) & 1);
+    const uint16_t* Qp = Qp_s + stg * 3 * 512;
+    const lds_u16* Qt = (const lds_u16*)Qp_s + stg * 3 * 512;
+    const uint16_t* Op = Op_s + stg * 3 * 4096;
+    float* Ms = Ms_s + stg * 32;
+    float* Ds = Ds_s + stg * 32;
+    if (tid < 32) {
+      Ms[tid] = pm;
+      Ds[tid] = pd;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (q0 + 32 < q_hi) {
+      dma_block<16, PL_PLAIN, NW>(Qpb, qps, q0 + 32, N, Qp_s + (stg ^ 1) * 3 * 512, wave, lane);
+      dma_block<128, PL_SWZ128, NW>(Opb, ops, q0 + 32, N, Op_s + (stg ^ 1) * 3 * 4096, wave, lane);
+      fetch_stats(q0 + 32);
+    }
+    if (q0 > q_lo) reduce(q0 - 32);
+    // S and dP tiles [qt][kt]: rows (queries 8 g + 4 qt + i) in registers, keys 16 kt + c16 on lanes
+    af32x4_t st[2][2], dp[2][2];
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      const uint16_t* qr = Qp + (qrow0 + 4 * qt) * 16 + 8 * (g & 1);
+      abf16x8_t qa[3];
+      qa[0] = *reinterpret_cast<const abf16x8_t*>(qr);
+      qa[1] = *reinterpret_cast<const abf16x8_t*>(qr + qa1 * 512);
+      qa[2] = *reinterpret_cast<const abf16x8_t*>(qr + qa2 * 512);
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        const uint16_t* kr = Kt_s + (wave * 32 + 16 * kt + c16) * 16 + 8 * (g & 1);
+        af32x4_t s = {0.0f, 0.0f, 0.0f, 0.0f};  // small products first, hi.hi last: one rounding at |s|
+        MFMA16(s, qa[2], *reinterpret_cast<const abf16x8_t*>(kr + kb2 * KW * 16));
+        MFMA16(s, qa[1], *reinterpret_cast<const abf16x8_t*>(kr));
+        MFMA16(s, qa[0], *reinterpret_cast<const abf16x8_t*>(kr + kb0 * KW * 16));
+        st[qt][kt] = s;
+        dp[qt][kt] = af32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+      }
+    }
+#pragma unroll
+    for (int fc = 0; fc < FC; ++fc)
+#pragma unroll
+      for (int qt = 0; qt < 2; ++qt) {
+        const int off = swz128(qrow0 + 4 * qt, 32 * fc + 8 * g);  // conflict-free in the b128 lane groups
+        abf16x8_t oa[3];
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl) oa[pl] = *reinterpret_cast<const abf16x8_t*>(&Op[pl * 4096 + off]);
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) X6_16(dp[qt][kt], oa, hb[kt][fc]);
+      }
+    // dS = P (dP - D) for queries 8 g .. 8 g + 7, split into planes: dS[q][key] as B (k = q)
+    const float4 m0 = *reinterpret_cast<const float4*>(Ms + 8 * g), m1 = *reinterpret_cast<const float4*>(Ms + 8 * g + 4);
+    const float4 e0 = *reinterpret_cast<const float4*>(Ds + 8 * g), e1 = *reinterpret_cast<const float4*>(Ds + 8 * g + 4);
+    abf16x8_t dsp[2][3];
+#pragma unroll
+    for (int kt = 0; kt < 2; ++kt) {
+      const float4 lo = make_float4(aexp2(fmaf(st[0][kt][0], ALOG2E, -m0.x)) * (dp[0][kt][0] - e0.x),
+                                    aexp2(fmaf(st[0][kt][1], ALOG2E, -m0.y)) * (dp[0][kt][1] - e0.y),
+                                    aexp2(fmaf(st[0][kt][2], ALOG2E, -m0.z)) * (dp[0][kt][2] - e0.z),
+                                    aexp2(fmaf(st[0][kt][3], ALOG2E, -m0.w)) * (dp[0][kt][3] - e0.w));
+      const float4 hi = make_float4(aexp2(fmaf(st[1][kt][0], ALOG2E, -m1.x)) * (dp[1][kt][0] - e1.x),
+                                    aexp2(fmaf(st[1][kt][1], ALOG2E, -m1.y)) * (dp[1][kt][1] - e1.y),
+                                    aexp2(fmaf(st[1][kt][2], ALOG2E, -m1.z)) * (dp[1][kt][2] - e1.z),
+                                    aexp2(fmaf(st[1][kt][3], ALOG2E, -m1.w)) * (dp[1][kt][3] - e1.w));
+      asplit8(lo, hi, dsp[kt][0], dsp[kt][1], dsp[kt][2]);
+    }
+    {  // dK^T[d][key] += Q^T[d][q] dS[q][key]; Q^T rows 8 g .. 8 g + 7 by transposed reads
+      abf16x8_t qT[3];
+#pragma unroll
+      for (int pl = 0; pl < 3; ++pl)
+        qT[pl] = tr8s(Qt + pl * 512 + (8 * g + q4) * 16 + 4 * p4, Qt + pl * 512 + (8 * g + 4 + q4) * 16 + 4 * p4);
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) X6_16(acck[kt], qT, dsp[kt]);
+    }
+    // dS^T plane by plane against the selections: tile (kt, nt) holds dS[q 16 nt + c16][key 16 kt + 4 g + i];
+    // each element is one plane value times 1, so it packs back to that bf16 exactly
+    abf16x8_t dt[2][3];
+#pragma unroll
+    for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+      for (int nt = 0; nt < 2; ++nt) {
+        af32x4_t t0 = {0.0f, 0.0f, 0.0f, 0.0f}, t1 = {0.0f, 0.0f, 0.0f, 0.0f};
+        MFMA16(t0, dsp[0][pl], sel[nt]);
+        MFMA16(t1, dsp[1][pl], sel[nt]);
+        dt[nt][pl] = __builtin_bit_cast(abf16x8_t, make_uint4(apack(t0[0], t0[1]), apack(t0[2], t0[3]),
+                                                              apack(t1[0], t1[1]), apack(t1[2], t1[3])));
+      }
+    // dQ_blk[q 16 nt + 4 g + i][d c16] over this wave's 32 keys -> this block's slot, row d of the wave's partial
+    float* dst = Red_s + stg * RSLOT + wave * 16 * RP + c16 * RP + 4 * g;
+#pragma unroll
+    for (int nt = 0; nt < 2; ++nt) {
+      af32x4_t dq = {0.0f, 0.0f, 0.0f, 0.0f};
+      X6_16(dq, dt[nt], kq);
+      *reinterpret_cast<float4*>(dst + 16 * nt) = make_float4(dq[0], dq[1], dq[2], dq[3]);
+    }
+  }
+  __syncthreads();
+  if (q_hi > q_lo) reduce(q_lo + ((q_hi - q_lo - 1) >> 5 << 5));  // the last block's partials
+  // dK[key 16 kt + c16][d 4 g + i]; query split: partial dK into slab blockIdx.z
+  const int64_t rows = (int64_t)gridDim.y * N;
+  float* dkd = SPLIT ? a.part2 + (int64_t)blockIdx.z * rows * a.dk : a.dK;
+#pragma unroll
+  for (int kt = 0; kt < 2; ++kt) {
+    const int64_t key = key0 + 16 * kt + c16;
+    if (key >= N) continue;
+    float* row = dkd + (b * N + key) * a.dk;
+    if (a.dk == 16) {
+      *reinterpret_cast<float4*>(row + 4 * g) = make_float4(acck[kt][0], acck[kt][1], acck[kt][2], acck[kt][3]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        if (4 * g + i < a.dk) row[4 * g + i] = acck[kt][i];
+    }
+  }
+}
+#undef X6_16
+#undef MFMA16
+
 // dQ[b][q][d] = sum over key workgroups x of qslab[b][x][q][d], in x order;
 // accumulate: start from dQ (a later key chunk: the same chain of fp32 adds
 // as one pass over every chunk's slabs)
@@ -2020,6 +2271,9 @@ bool attn_fused_dq_enabled() { return opt(OPT_ATTN_FUSED_DQ) != 0; }
 
 // path option attn_dh16 = 0 keeps dH on the 32x32x16 kernel
 bool attn_dh16_enabled() { return opt(OPT_ATTN_DH16) != 0; }
+
+// path option attn_kq16 = 0 keeps the fused dK / dQ pass on the 32x32x16 kernel
+bool attn_kq16_enabled() { return opt(OPT_ATTN_KQ16) != 0; }
 
 // path option attn_pipe = 0 keeps the unpipelined x6 forward (A/B aid)
 bool attn_pipe_enabled() { return opt(OPT_ATTN_PIPE) != 0; }
@@ -2115,7 +2369,11 @@ int launch_attn(AttnPass pass, const AttnArgs& a0, int64_t B, int S, hipStream_t
             AttnArgs ac = a;
             ac.k0 = x0 * KQ_KEYS;
             const dim3 gkq((unsigned)std::min<int64_t>(xc, xall - x0), (unsigned)B, (unsigned)S);
-            if (S > 1)
+            if (attn_kq16_enabled() && S > 1)
+              hipLaunchKernelGGL((attn_bwd_kq16_kernel<true>), gkq, dim3(64 * KQ_WAVES), 0, st, ac);
+            else if (attn_kq16_enabled())
+              hipLaunchKernelGGL((attn_bwd_kq16_kernel<false>), gkq, dim3(64 * KQ_WAVES), 0, st, ac);
+            else if (S > 1)
               hipLaunchKernelGGL((attn_bwd_kq_x6_kernel<true>), gkq, dim3(64 * KQ_WAVES), 0, st, ac);
             else
               hipLaunchKernelGGL((attn_bwd_kq_x6_kernel<false>), gkq, dim3(64 * KQ_WAVES), 0, st, ac);

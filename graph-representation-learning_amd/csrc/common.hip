@@ -53,6 +53,7 @@ constexpr OptDef kOpts[OPT_COUNT] = {
     {"attn_fused_dq", 1, 0, 1},
     {"attn_pipe", 1, 0, 1},
     {"attn_dh16", 1, 0, 1},
+    {"attn_kq16", 1, 0, 1},
     {"attn_qslab_max", 0, 0, INT64_MAX},
     {"ws_spin", 0, 0, (int64_t)1 << 30},
     {"ws_status_sync", 0, 0, 1},
@@ -61,8 +62,9 @@ std::atomic<int64_t> g_opt[OPT_COUNT] = {
     {kOpts[0].def},  {kOpts[1].def},  {kOpts[2].def},  {kOpts[3].def},  {kOpts[4].def},
     {kOpts[5].def},  {kOpts[6].def},  {kOpts[7].def},  {kOpts[8].def},  {kOpts[9].def},
     {kOpts[10].def}, {kOpts[11].def}, {kOpts[12].def}, {kOpts[13].def}, {kOpts[14].def},
+    {kOpts[15].def},
 };
-static_assert(OPT_COUNT == 15, "one default per option");
+static_assert(OPT_COUNT == 16, "one default per option");
 
 int find_opt(const char* name) {
   for (int i = 0; name && i < OPT_COUNT; ++i)

@@ -155,6 +155,7 @@ enum GrlOpt {
   OPT_ATTN_FUSED_DQ,        // 1: dQ folded into the dK pass; 0: separate dQ kernel
   OPT_ATTN_PIPE,            // 1: software-pipelined x6 forward; 0: unpipelined
   OPT_ATTN_DH16,            // 1: dH pass on 16x16x32 MFMAs (dk <= 16; default); 0: the 32x32x16 kernel
+  OPT_ATTN_KQ16,            // 1: fused dK/dQ pass on 16x16x32 MFMAs (dk <= 16; default); 0: the 32x32x16 kernel
   OPT_ATTN_QSLAB_MAX,       // fused dK/dQ slab budget in bytes (0: 24 GiB)
   OPT_WS_SPIN,              // persistent kernels' bounded-wait limit (0: 2^24 sleeps)
   OPT_WS_STATUS_SYNC,       // 1: an eager one-kernel call checks its own status (debug)

@@ -81,7 +81,7 @@ def test_path_options_round_trip_and_reject_unknown_names():
 
     defaults = {"gemm_x6": 1, "graphconv_fused": 1, "graphconv_fused_bwd": 1, "fg_ws": 1, "spmm_wide": -1,
                 "spmm_blocks_per_cu": 24, "attn_x6": 1, "attn_fwd8": 1, "attn_dh8": 1, "attn_fused_dq": 1,
-                "attn_pipe": 1, "attn_dh16": 1, "attn_qslab_max": 0, "ws_spin": 0, "ws_status_sync": 0}
+                "attn_pipe": 1, "attn_dh16": 1, "attn_kq16": 1, "attn_qslab_max": 0, "ws_spin": 0, "ws_status_sync": 0}
     assert {k: grl.get_option(k) for k in defaults} == defaults
     with grl.options(gemm_x6=0, ws_spin=7, spmm_wide=1):
         assert (grl.get_option("gemm_x6"), grl.get_option("ws_spin"), grl.get_option("spmm_wide")) == (0, 7, 1)

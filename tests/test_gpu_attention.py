@@ -210,8 +210,44 @@ def test_dh_on_16x16x32_matches_fp64(B, N, dk, dv, grl_option):
     _ref(*ref_leaves).backward(dout.double())
     for name, a, c, r in zip("QKHVg", grads[1], grads[0], ref_leaves):
         scale = r.grad.abs().max().item() + 1.0
+        print(f"d{name}: scale {scale:.3e} err vs fp64 {float((a.double() - r.grad).abs().max()):.3e} "
+              f"(32x32x16: {float((c.double() - r.grad).abs().max()):.3e})")
         torch.testing.assert_close(a.double(), r.grad, rtol=1e-4, atol=2e-5 * scale, msg=f"dh16 d{name}")
         torch.testing.assert_close(a.double(), c.double(), rtol=1e-5, atol=1e-6 * scale, msg=f"dh16 vs 32x32 d{name}")
+
+
+@pytest.mark.parametrize("B,N,dk,dv", [(1, 8192, 16, 128), (3, 4099, 9, 100), (64, 1024, 16, 128), (4, 1100, 16, 128),
+                                       (1, 20_000, 16, 128), (1, 6000, 1, 97), (200, 24, 16, 128)])
+def test_kq_on_16x16x32_matches_fp64(B, N, dk, dv, grl_option):
+    """attn_bwd_kq16_kernel (the fused dK / dQ pass in 16 x 16 tiles on
+    v_mfma_f32_16x16x32_bf16: S's products paired along K = 32, dS^T by
+    exact MFMA selection, dQ with keys in the transposed order): every
+    gradient against float64 and within fp32 rounding of the 32x32x16 kernel
+    -- unsplit and query-split grids, partial blocks, pages shorter than a
+    query block, dk = 1 / 9, dv = 97 / 100; deterministic run to run."""
+    Q, K, H, V, gamma = _inputs(B, N, dk, dv, seed=7 * N + dk)
+    dout = torch.randn(B, N, dv, generator=torch.Generator().manual_seed(6)).to(DEV)
+    grads = {}
+    for v in (1, 0, 1):
+        grl_option("attn_kq16", v)
+        leaves = [t.clone().requires_grad_(True) for t in (Q, K, H, V, gamma)]
+        node_self_attention(*leaves).backward(dout)
+        g = [t.grad for t in leaves]
+        if v in grads:
+            for a, b in zip(grads[v], g):
+                assert torch.equal(a, b)
+        grads[v] = g
+    ref_leaves = [t.double().clone().requires_grad_(True) for t in (Q, K, H, V, gamma)]
+    _ref(*ref_leaves).backward(dout.double())
+    for name, a, c, r in zip("QKHVg", grads[1], grads[0], ref_leaves):
+        scale = r.grad.abs().max().item() + 1.0
+        e16, e32 = float((a.double() - r.grad).abs().max()), float((c.double() - r.grad).abs().max())
+        print(f"d{name}: scale {scale:.3e} err vs fp64 {e16:.3e} (32x32x16: {e32:.3e}) "
+              f"apart {float((a - c).abs().max()):.3e}")
+        torch.testing.assert_close(a.double(), r.grad, rtol=1e-4, atol=2e-5 * scale, msg=f"kq16 d{name}")
+        # dQ sums dS over every key with cancellation (the keys' dS add to ~0 per query), so the two
+        # kernels' roundings differ by more than dH's; the bar is the 32x32x16 kernel's own error
+        assert e16 <= 2.0 * e32 + 1e-6 * scale, f"kq16 d{name}: {e16} vs {e32}"
 
 
 RANGED = [(1, 20_000, 16, 128, (0, 7000, 13_003, 20_000)), (2, 3000, 16, 100, (0, 0, 1, 1500, 3000)),
@@ -257,13 +293,15 @@ def test_query_ranges_partition_the_attention(B, N, dk, dv, cuts, mode, monkeypa
         torch.testing.assert_close(got.double(), want, rtol=1e-4, atol=per * scale * ranges)
 
 
+@pytest.mark.parametrize("kq16", [0, 1])
 @pytest.mark.parametrize("B,N,budget_x", [(1, 20_000, 23), (2, 9000, 7), (1, 4500, 1)])
-def test_fused_dq_key_chunks_are_bitwise(B, N, budget_x, monkeypatch, grl_option):
+def test_fused_dq_key_chunks_are_bitwise(B, N, budget_x, kq16, monkeypatch, grl_option):
     """The fused dK/dQ pass in key chunks (the dQ slabs of budget_x key
     workgroups per launch, the attn_qslab_max option), each chunk's slabs added onto
-    dQ in order: dQ, dK, dH bitwise the one-launch pass's."""
+    dQ in order: dQ, dK, dH bitwise the one-launch pass's (both kernels)."""
     from grl.ops import node_attention_backward
 
+    grl_option("attn_kq16", kq16)
     Q, K, H, V, gamma = _inputs(B, N, 16, 128, seed=N)
     dout = torch.randn(B, N, 128, generator=torch.Generator().manual_seed(4)).to(DEV)
     out, onorm, rmax, rsum = node_attention_forward(Q, K, H, V, gamma, stats=True)

@@ -178,6 +178,8 @@ for step in "$@"; do
     ab_attn_opt) rm -f gpurun_out/ab_attn_opt.log; run ab_attn_opt 900 tools/ab_attn_opt.sh ${AB_OPTS} ;;
     tests_dh16) run pytest_gpu_dh16 600 python -u -m pytest tests/test_gpu_attention.py -m gpu -v -rf --timeout 300 \
                   --timeout-method thread -k "dh_on_16 or eight_wave or backward_matches" ;;
+    tests_kq16) run pytest_gpu_kq16 600 python -u -m pytest tests/test_gpu_attention.py -m gpu -v -s -rf --timeout 300 \
+                  --timeout-method thread -k "kq_on_16 or dh_on_16 or key_chunks or fused_dq_backward or backward_matches" ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
