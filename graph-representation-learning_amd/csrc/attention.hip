@@ -1950,14 +1950,15 @@ __global__ __launch_bounds__(64 * KQ_WAVES, 1) void attn_bwd_kq_x6_kernel(AttnAr
 //    dK^T[d][key] += Q^T dS as it lies (Q^T: transposed reads of the staged
 //    16-wide planes); the 32x32x16 kernel's dK and dQ tiles were half
 //    padding (dk = 16 of 32 rows), these have none;
-//  * the same registers are dS^T as an A operand: an MFMA against a 0/1
-//    selection of 16 queries transposes each plane exactly (one nonzero
-//    product per element), giving dS with queries on lanes and keys
-//    4 g .. 4 g + 3, 16 + 4 g .. 16 + 4 g + 3 in registers -- dQ's A operand,
-//    with K's planes (split once, registers) in that key order as B;
+//  * dS transposed through the wave's LDS slots: each plane's registers are
+//    written as [key][q] rows and read back by ds_read_b64_tr_b16 with
+//    queries on lanes and keys 8 g .. 8 g + 7 in registers -- dQ's A
+//    operand, with K's planes (split once, registers) as B (an exact
+//    selection-MFMA transposition, 12 more MFMAs and 12 packs per block,
+//    measured 0.3-1.4 % slower end to end);
 //  * dQ partials go through the LDS slots and per-workgroup slabs exactly as
 //    in attn_bwd_kq_x6_kernel, so attn_qslab_sum_kernel is unchanged.
-// Per block and wave 144 MFMAs of 16x16x32 = 72 of 32x32x16 (84 there).
+// Per block and wave 132 MFMAs of 16x16x32 = 66 of 32x32x16 (84 there).
 // The same products in the same order per output; the pairing of S's
 // products inside one MFMA changes rounding only (tested vs float64).
 #define MFMA16(acc, a, b) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16((a), (b), (acc), 0, 0, 0)
@@ -1980,6 +1981,7 @@ __global__ __launch_bounds__(64 * KQ_WAVES, 1) void attn_bwd_kq16_kernel(AttnArg
   __shared__ __attribute__((aligned(16))) uint16_t Kt_s[3 * KW * 16];  // the workgroup's K rows, planes [key][16]
   __shared__ __attribute__((aligned(16))) float Red_s[2 * RSLOT];  // 2 slots x the waves' partials [w][d][RP]
   __shared__ __attribute__((aligned(16))) float Ms_s[2 * 32], Ds_s[2 * 32];  // lse2, D per query
+  __shared__ __attribute__((aligned(16))) uint16_t Dt_s[NW * 2 * 1024];  // each wave's two 32 x 32 bf16 dS slots
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int c16 = lane & 15, g = lane >> 4;
   const int64_t N = a.N, b = blockIdx.y;
@@ -2018,26 +2020,16 @@ __global__ __launch_bounds__(64 * KQ_WAVES, 1) void attn_bwd_kq16_kernel(AttnArg
               hb[kt][fc][2]);
     }
   }
-  // B operand of dQ: K[key pi(g, j)][d c16] with pi(g, j) = 4 g + j (j < 4), 12 + 4 g + j (j >= 4):
-  // the key order of the transposed dS
+  // B operand of dQ: K[key 8 g + j][d c16], the key order of the transposed dS
   abf16x8_t kq[3];
   {
     float v[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int64_t key = key0 + (j < 4 ? 4 * g + j : 12 + 4 * g + j);
+      const int64_t key = key0 + 8 * g + j;
       v[j] = (key < N && c16 < a.dk) ? a.K[(b * N + key) * a.dk + c16] : 0.0f;
     }
     asplit8(make_float4(v[0], v[1], v[2], v[3]), make_float4(v[4], v[5], v[6], v[7]), kq[0], kq[1], kq[2]);
-  }
-  // 0/1 selections of queries 16 nt .. 16 nt + 15: B[k = 8 g + j][n = c16] = 1 iff k == 16 nt + n
-  abf16x8_t sel[2];
-#pragma unroll
-  for (int nt = 0; nt < 2; ++nt) {
-    ai16x8_t s;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) s[j] = (8 * g + j == 16 * nt + c16) ? (short)0x3F80 : (short)0;
-    sel[nt] = __builtin_bit_cast(abf16x8_t, s);
   }
   af32x4_t acck[2] = {{0.0f, 0.0f, 0.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
   const int64_t qps = (int64_t)gridDim.y * N * 16, ops = (int64_t)gridDim.y * N * 128;
@@ -2144,19 +2136,30 @@ __global__ __launch_bounds__(64 * KQ_WAVES, 1) void attn_bwd_kq16_kernel(AttnArg
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt) X6_16(acck[kt], qT, dsp[kt]);
     }
-    // dS^T plane by plane against the selections: tile (kt, nt) holds dS[q 16 nt + c16][key 16 kt + 4 g + i];
-    // each element is one plane value times 1, so it packs back to that bf16 exactly
     abf16x8_t dt[2][3];
+    {
+      // dS^T through this wave's LDS slots: plane pl's [key][q] rows (16-B chunk c of row k at
+      // c ^ ((k >> 2) & 3): conflict-free row writes and transposed reads), read back by
+      // ds_read_b64_tr_b16 as tile nt = dS[q 16 nt + c16][keys 8 g .. 8 g + 7]; plane 2 reuses slot 0
+      // (a wave's LDS instructions execute in order, so its reads of plane 0 precede the rewrite)
 #pragma unroll
-    for (int pl = 0; pl < 3; ++pl)
+      for (int pl = 0; pl < 3; ++pl) {
+        uint16_t* slot = Dt_s + (wave * 2 + (pl & 1)) * 1024;
 #pragma unroll
-      for (int nt = 0; nt < 2; ++nt) {
-        af32x4_t t0 = {0.0f, 0.0f, 0.0f, 0.0f}, t1 = {0.0f, 0.0f, 0.0f, 0.0f};
-        MFMA16(t0, dsp[0][pl], sel[nt]);
-        MFMA16(t1, dsp[1][pl], sel[nt]);
-        dt[nt][pl] = __builtin_bit_cast(abf16x8_t, make_uint4(apack(t0[0], t0[1]), apack(t0[2], t0[3]),
-                                                              apack(t1[0], t1[1]), apack(t1[2], t1[3])));
+        for (int kt = 0; kt < 2; ++kt) {
+          const int k = 16 * kt + c16;
+          *reinterpret_cast<abf16x8_t*>(slot + k * 32 + ((g ^ ((k >> 2) & 3)) << 3)) = dsp[kt][pl];
+        }
+        const lds_u16* sl = (const lds_u16*)Dt_s + (wave * 2 + (pl & 1)) * 1024;
+        const int k0 = 8 * g + q4, k1 = 8 * g + 4 + q4;
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+          const int ch = 2 * nt + (p4 >> 1), w = 4 * (p4 & 1);
+          dt[nt][pl] = tr8s(sl + k0 * 32 + ((ch ^ ((k0 >> 2) & 3)) << 3) + w,
+                            sl + k1 * 32 + ((ch ^ ((k1 >> 2) & 3)) << 3) + w);
+        }
       }
+    }
     // dQ_blk[q 16 nt + 4 g + i][d c16] over this wave's 32 keys -> this block's slot, row d of the wave's partial
     float* dst = Red_s + stg * RSLOT + wave * 16 * RP + c16 * RP + 4 * g;
 #pragma unroll

@@ -221,7 +221,7 @@ def test_dh_on_16x16x32_matches_fp64(B, N, dk, dv, grl_option):
 def test_kq_on_16x16x32_matches_fp64(B, N, dk, dv, grl_option):
     """attn_bwd_kq16_kernel (the fused dK / dQ pass in 16 x 16 tiles on
     v_mfma_f32_16x16x32_bf16: S's products paired along K = 32, dS^T by
-    exact MFMA selection, dQ with keys in the transposed order): every
+    a round trip through the wave's LDS slots, dQ over the wave's keys): every
     gradient against float64 and within fp32 rounding of the 32x32x16 kernel
     -- unsplit and query-split grids, partial blocks, pages shorter than a
     query block, dk = 1 / 9, dv = 97 / 100; deterministic run to run."""
