@@ -1,0 +1,195 @@
+"""Property tests over random shapes (SURVEY.md §4 build-test plan item 2):
+hypothesis draws B, N, L, F, C, density (including no edges at all), binary
+or float edge values, self edges present or not, N = 1, and the DropEdge rate.
+
+CPU half (no GPU, no libgrl compute): the typed-CSR restatement
+(oracle/grl_oracle.c: dense -> CSR, fused-DropEdge SpMM, CSC transpose and
+the backward gather) against the dense restatement of robust_gcn.py:45-72
+(oracle/dense_ref.py, itself pinned to the reference by tests/golden), and
+the index invariants of the conversions.  GPU half (``-m gpu``): libgrl's
+typed SpMM forward / backward, its dense -> CSR conversion and its CSC
+transpose against the C oracle on the same draws -- bitwise, as the fixed
+cases of test_gpu_kernels.py require.  derandomize=True: the same examples
+on every run."""
+import numpy as np
+import pytest
+from hypothesis import HealthCheck, given, settings
+from hypothesis import strategies as st
+
+import inputs as gi
+from oracle import c_oracle, dense_ref
+
+CPU_SETTINGS = settings(max_examples=60, deadline=None, derandomize=True,
+                        suppress_health_check=[HealthCheck.too_slow])
+GPU_SETTINGS = settings(max_examples=30, deadline=None, derandomize=True,
+                        suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
+
+
+@st.composite
+def dense_cases(draw):
+    B = draw(st.integers(1, 3))
+    N = draw(st.integers(1, 24))
+    L = draw(st.integers(1, 7))
+    F = draw(st.integers(1, 20))
+    C = draw(st.integers(1, 9))
+    epn = draw(st.sampled_from([0.0, 0.5, 2.0, 6.0, 40.0]))  # 40: every entry present at small N
+    float_vals = draw(st.booleans())
+    self_edges = draw(st.booleans())
+    p = draw(st.sampled_from([0.0, 0.3, 0.5]))
+    seed = draw(st.integers(0, 2 ** 20))
+    return B, N, L, F, C, epn, float_vals, self_edges, p, seed
+
+
+def _scale_close(got, want, tol, what):
+    got = np.asarray(got, dtype=np.float64)
+    want = np.asarray(want, dtype=np.float64)
+    scale = max(1.0, float(np.abs(want).max()) if want.size else 1.0)
+    err = float(np.abs(got - want).max()) if want.size else 0.0
+    assert err <= tol * scale, f"{what}: max|d| {err:.3e} > {tol:.0e} x {scale:.3g}"
+
+
+@CPU_SETTINGS
+@given(dense_cases())
+def test_csr_restatement_equals_dense_reference(case):
+    """GraphConv forward and data gradient through the typed CSR / CSC
+    (the engine's algorithm) equal the dense A_pre math within 1e-5, with
+    and without the fused DropEdge mask (the same hash draws on both sides)."""
+    B, N, L, F, C, epn, float_vals, self_edges, p, seed = case
+    A = gi.random_adj_bnln(seed, B, N, L, epn, float_vals=float_vals, self_edges=self_edges)
+    V = gi.features(seed + 1, B, N, F)
+    W, b = gi.graphconv_params(seed + 2, F, C, L)
+    dout = gi.features(seed + 3, B, N, C)
+    call = seed % 7
+    A_pre = dense_ref.preprocess_adj(np.transpose(A, (0, 1, 3, 2)).astype(np.float64))
+    d = None
+    if p > 0:
+        mult = dense_ref.dropedge_weights_pre(A, p, seed, call)
+        A_pre = dense_ref.apply_dropedge(A_pre, mult).astype(np.float64)
+        d = c_oracle.drop(p, seed, call, True)
+    out, Z = dense_ref.graphconv_forward(V.astype(np.float64), A_pre, W.astype(np.float64), b.astype(np.float64))
+    dV, _, _ = dense_ref.graphconv_backward(V.astype(np.float64), A_pre, W.astype(np.float64), Z,
+                                            dout.astype(np.float64))
+
+    rowptr, colidx, vals = c_oracle.dense_to_csr(A, [N * L * N, L * N, N, 1], B, N, L)
+    Zc = c_oracle.spmm_fwd(rowptr, colidx, V.reshape(B * N, F), L, True, vals=vals, d=d)
+    _scale_close(Zc.reshape(Z.shape), Z, 1e-5, "aggregation Z")
+    outc = Zc.astype(np.float64) @ W.astype(np.float64) + b
+    _scale_close(outc.reshape(out.shape), out, 1e-5, "GraphConv out")
+    dZ = (dout.reshape(B * N, C).astype(np.float64) @ W.T.astype(np.float64)).astype(np.float32)
+    colptr, zrow, eid, cvals = c_oracle.csr_to_csc(rowptr, colidx, L, B * N, True, vals)
+    dVc = c_oracle.spmm_bwd(colptr, zrow, eid, dZ, L, F, B * N, True, cvals, d=d, self_base=int(rowptr[-1]))
+    _scale_close(dVc.reshape(dV.shape), dV, 1e-5, "data gradient dV")
+
+
+@CPU_SETTINGS
+@given(dense_cases())
+def test_conversions_keep_every_edge_once(case):
+    """dense -> typed CSR: rowptr non-decreasing over B N L segments, each
+    segment's columns strictly increasing (no duplicates), exactly A's
+    nonzeros with their values; CSR -> CSC: a permutation of the edges
+    (eid) whose columns are non-decreasing and whose rows are the CSR rows."""
+    B, N, L, F, C, epn, float_vals, self_edges, p, seed = case
+    A = gi.random_adj_bnln(seed, B, N, L, epn, float_vals=float_vals, self_edges=self_edges)
+    rowptr, colidx, vals = c_oracle.dense_to_csr(A, [N * L * N, L * N, N, 1], B, N, L)
+    assert rowptr.size == B * N * L + 1 and rowptr[0] == 0
+    assert np.all(np.diff(rowptr) >= 0)
+    E = int(rowptr[-1])
+    assert E == int(np.count_nonzero(A))
+    for s in range(B * N * L):  # segment s = (b, n, l): b's column block holds b N .. b N + N - 1
+        b, n, l = s // (N * L), (s // L) % N, s % L
+        cols = colidx[rowptr[s]:rowptr[s + 1]]
+        assert np.all(np.diff(cols) > 0)
+        want = np.nonzero(A[b, n, l])[0] + b * N
+        np.testing.assert_array_equal(cols, want)
+        if vals is not None:
+            np.testing.assert_array_equal(vals[rowptr[s]:rowptr[s + 1]], A[b, n, l][A[b, n, l] != 0])
+    colptr, zrow, eid, cvals = c_oracle.csr_to_csc(rowptr, colidx, L, B * N, True, vals)
+    assert colptr.size == B * N + 1 and colptr[-1] == E and np.all(np.diff(colptr) >= 0)
+    np.testing.assert_array_equal(np.sort(eid[:E]), np.arange(E))
+    seg = np.repeat(np.arange(B * N * L), np.diff(rowptr))  # CSR segment of each edge
+    for c in range(B * N):
+        es = eid[colptr[c]:colptr[c + 1]]
+        assert np.all(np.diff(es) > 0)  # stable: CSR order within a column
+        assert np.all(colidx[es] == c)
+        # Z row of the edge's (node, type) segment, after the node's self block
+        np.testing.assert_array_equal(zrow[colptr[c]:colptr[c + 1]], (seg[es] // L) * (L + 1) + 1 + seg[es] % L)
+        if vals is not None:
+            np.testing.assert_array_equal(cvals[colptr[c]:colptr[c + 1]], vals[es])
+
+
+# ---------------------------------------------------------------------------
+# GPU half: libgrl against the C oracle on the same kind of draws (bitwise)
+
+@st.composite
+def csr_cases(draw):
+    N = draw(st.integers(1, 400))
+    L = draw(st.integers(1, 7))
+    deg = draw(st.sampled_from([0.0, 1.0, 4.0, 17.0]))
+    F = draw(st.sampled_from([1, 3, 4, 16, 33, 64, 128, 250, 256, 300, 512]))
+    vals = draw(st.booleans())
+    has_self = draw(st.booleans())
+    p = draw(st.sampled_from([0.0, 0.2, 0.3, 1.0]))
+    seed = draw(st.integers(0, 2 ** 20))
+    return N, L, deg, F, vals, has_self, p, seed
+
+
+@pytest.mark.gpu
+@GPU_SETTINGS
+@given(csr_cases())
+def test_gpu_spmm_random_shapes_bitwise(case):
+    """grl_typed_spmm_fwd / _bwd over random typed graphs (empty rows and
+    types, N = 1, widths off the float4 grid, p = 1 drops everything):
+    bitwise the oracle's CSR-order fmaf chains."""
+    import torch
+
+    from grl import DropEdge, TypedGraph
+    from grl.ops import typed_aggregate
+    from oracle import hash as ohash
+
+    dev = torch.device("cuda:0")
+    N, L, deg, F, vals, has_self, p, seed = case
+    rowptr, colidx = ohash.synth_csr(0, L, N, int(N * deg), seed)
+    v = np.random.default_rng(seed + 2).uniform(0.1, 2.0, colidx.size).astype(np.float32) if vals else None
+    X = np.random.default_rng(seed + 3).standard_normal((N, F)).astype(np.float32)
+    de = DropEdge(p, seed, seed % 5, True) if p > 0 else None
+    ebase, sbase = 77 + seed, 10 ** 9 + seed
+    g = TypedGraph.from_csr_host(rowptr, colidx, L, dev, vals=v, has_self=has_self, edge_id_base=ebase,
+                                 self_id_base=sbase).with_dropedge(de)
+    Xt = torch.from_numpy(X).to(dev).requires_grad_(True)
+    Z = typed_aggregate(Xt, g)
+    d = None if de is None else c_oracle.drop(de.p, de.seed, de.call, de.drop_self)
+    Zref = c_oracle.spmm_fwd(rowptr, colidx, X, L, has_self, vals=v, d=d, edge_base=ebase, self_base=sbase)
+    np.testing.assert_array_equal(Z.detach().cpu().numpy(), Zref)
+    dZ = np.random.default_rng(seed + 4).standard_normal(Zref.shape).astype(np.float32)
+    Z.backward(torch.from_numpy(dZ).to(dev))
+    colptr, zrow, eid, cvals = c_oracle.csr_to_csc(rowptr, colidx, L, N, has_self, v)
+    dXref = c_oracle.spmm_bwd(colptr, zrow, eid, dZ, L, F, N, has_self, cvals, d=d, edge_base=ebase,
+                              self_base=sbase)
+    np.testing.assert_array_equal(Xt.grad.cpu().numpy(), dXref)
+
+
+@pytest.mark.gpu
+@GPU_SETTINGS
+@given(dense_cases())
+def test_gpu_dense_to_csr_and_csc_random_shapes(case):
+    """grl_dense_to_csr_* (the collate layout A (B, N, L, N), as
+    preprocess_adj's input) and the device CSC transpose: the oracle's
+    integers and values exactly, N = 1 and edgeless pages included."""
+    import torch
+
+    from grl import TypedGraph
+
+    dev = torch.device("cuda:0")
+    B, N, L, F, C, epn, float_vals, self_edges, p, seed = case
+    A = gi.random_adj_bnln(seed, B, N, L, epn, float_vals=float_vals, self_edges=self_edges)
+    g = TypedGraph.from_dense(torch.from_numpy(A).to(dev), layout="bnln")
+    rp, ci, va = c_oracle.dense_to_csr(A, [N * L * N, L * N, N, 1], B, N, L)
+    np.testing.assert_array_equal(g.rowptr.cpu().numpy(), rp)
+    np.testing.assert_array_equal(g.colidx.cpu().numpy()[:ci.size], ci)
+    if float_vals:
+        np.testing.assert_array_equal(g.vals.cpu().numpy()[:ci.size], va)
+    c = g.csc()
+    colptr, zrow, eid, cvals = c_oracle.csr_to_csc(rp, ci, L, B * N, True, va if float_vals else None)
+    np.testing.assert_array_equal(c["colptr"].cpu().numpy(), colptr)
+    np.testing.assert_array_equal(c["zrow"].cpu().numpy()[:ci.size], zrow)
+    np.testing.assert_array_equal(c["eid"].cpu().numpy()[:ci.size], eid)
