@@ -193,3 +193,128 @@ def test_gpu_dense_to_csr_and_csc_random_shapes(case):
     np.testing.assert_array_equal(c["colptr"].cpu().numpy(), colptr)
     np.testing.assert_array_equal(c["zrow"].cpu().numpy()[:ci.size], zrow)
     np.testing.assert_array_equal(c["eid"].cpu().numpy()[:ci.size], eid)
+
+
+@st.composite
+def layer_cases(draw):
+    N = draw(st.integers(1, 3000))
+    L = draw(st.integers(1, 7))
+    deg = draw(st.sampled_from([0.0, 2.0, 9.0, 30.0]))
+    F = draw(st.sampled_from([1, 16, 64, 100, 128, 256, 512]))
+    C = draw(st.sampled_from([1, 7, 64, 128, 200, 256, 512]))
+    has_self = draw(st.booleans())
+    relu = draw(st.booleans())
+    bias = draw(st.booleans())
+    p = draw(st.sampled_from([0.0, 0.3]))
+    seed = draw(st.integers(0, 2 ** 20))
+    return N, L, deg, F, C, has_self, relu, bias, p, seed
+
+
+@pytest.mark.gpu
+@GPU_SETTINGS
+@given(layer_cases())
+def test_gpu_graphconv_random_shapes(case):
+    """One GraphConv layer (robust_gcn.py:45-51 + the ReLU of
+    drop_robust_gcn.py:76) over random shapes: the inference call is bitwise
+    the two-op chain (typed SpMM, then the linear) on whichever kernel it
+    picks; out and the gradients of X, W, b within 1e-5 of float64 products of
+    the oracle's aggregation (relative to the sum of |terms|)."""
+    import torch
+
+    from grl import DropEdge, TypedGraph
+    from grl.ops import graph_conv, graph_conv_infer, linear_fwd, typed_aggregate
+    from oracle import hash as ohash
+
+    dev = torch.device("cuda:0")
+    N, L, deg, F, C, has_self, relu, bias, p, seed = case
+    rowptr, colidx = ohash.synth_csr(0, L, N, int(N * deg), seed)
+    de = DropEdge(p, seed, 3, True) if p > 0 else None
+    g = TypedGraph.from_csr_host(rowptr, colidx, L, dev, has_self=has_self).with_dropedge(de)
+    rng = np.random.default_rng(seed)
+    K = (L + (1 if has_self else 0)) * F
+    X = rng.standard_normal((N, F)).astype(np.float32)
+    W = (rng.standard_normal((K, C)) / np.sqrt(K)).astype(np.float32)
+    b = rng.standard_normal(C).astype(np.float32) if bias else None
+    Xt, Wt = torch.from_numpy(X).to(dev), torch.from_numpy(W).to(dev)
+    bt = torch.from_numpy(b).to(dev) if bias else None
+    out = graph_conv_infer(Xt, g, Wt, bt, relu)
+    assert torch.equal(out, linear_fwd(typed_aggregate(Xt, g), Wt, bt, relu))
+
+    d = None if de is None else c_oracle.drop(de.p, de.seed, de.call, de.drop_self)
+    Z = c_oracle.spmm_fwd(rowptr, colidx, X, L, has_self, d=d).astype(np.float64)
+    W64 = W.astype(np.float64)
+    pre = Z @ W64 + (b.astype(np.float64) if bias else 0.0)
+    o = np.maximum(pre, 0.0) if relu else pre
+    scale = np.abs(Z) @ np.abs(W64) + (np.abs(b.astype(np.float64)) if bias else 0.0)
+    assert np.all(np.abs(out.cpu().numpy() - o) <= 1e-5 * scale + 1e-6)
+
+    # training: gradients of X, W, b for a fixed upstream gradient
+    gout = rng.standard_normal((N, C)).astype(np.float32)
+    Xg, Wg = Xt.clone().requires_grad_(True), Wt.clone().requires_grad_(True)
+    bg = bt.clone().requires_grad_(True) if bias else None
+    y = graph_conv(Xg, g, Wg, bg, relu)
+    assert torch.equal(y.detach(), out)
+    y.backward(torch.from_numpy(gout).to(dev))
+    # the ReLU's gradient through the layer's own output mask (a float64 pre-activation within rounding of 0
+    # may fall on either side; out itself is checked above)
+    gz = gout.astype(np.float64) * ((y.detach().cpu().numpy() > 0) if relu else 1.0)
+    dW = Z.T @ gz
+    dZ = gz @ W64.T
+    colptr, zrow, eid, _ = c_oracle.csr_to_csc(rowptr, colidx, L, N, has_self, None)
+    sb = int(rowptr[-1])  # the self loops' DropEdge ids follow the typed edges' (TypedGraph's default)
+    dX = c_oracle.spmm_bwd(colptr, zrow, eid, dZ.astype(np.float32), L, F, N, has_self, None, d=d,
+                           self_base=sb).astype(np.float64)
+    sW = np.abs(Z.T) @ np.abs(gz) + 1e-6
+    assert np.all(np.abs(Wg.grad.cpu().numpy() - dW) <= 1e-5 * sW + 1e-6), "dW"
+    if bias:
+        assert np.all(np.abs(bg.grad.cpu().numpy() - gz.sum(0)) <= 1e-5 * np.abs(gz).sum(0) + 1e-6), "db"
+    # dX: the oracle gathers fp32-rounded dZ rows, the engine its own fp32 dZ: compare at the scale of |dZ| terms
+    sdZ = np.abs(gz) @ np.abs(W64.T)
+    sX = c_oracle.spmm_bwd(colptr, zrow, eid, sdZ.astype(np.float32), L, F, N, has_self, None, d=d, self_base=sb)
+    assert np.all(np.abs(Xg.grad.cpu().numpy() - dX) <= 2e-5 * sX + 1e-6), "dX"
+
+
+@st.composite
+def attention_cases(draw):
+    B = draw(st.integers(1, 4))
+    N = draw(st.integers(1, 1500))
+    dk = draw(st.sampled_from([0, 1, 5, 16, 32, 40, 64]))
+    dv = draw(st.sampled_from([1, 4, 32, 100, 128, 256, 300]))
+    seed = draw(st.integers(0, 2 ** 20))
+    return B, N, dk, dv, seed
+
+
+@pytest.mark.gpu
+@GPU_SETTINGS
+@given(attention_cases())
+def test_gpu_node_attention_random_shapes(case):
+    """NodeSelfAtten (robust_gcn.py:90-96: softmax(Q K^T) H, gamma, residual)
+    forward and every gradient over random B, N, dk (0 = uniform
+    attention), dv (beyond one call's width: column blocks) against float64."""
+    import torch
+
+    from grl.ops import node_self_attention
+
+    dev = torch.device("cuda:0")
+    B, N, dk, dv, seed = case
+    gen = torch.Generator().manual_seed(seed)
+    Q = torch.relu(torch.randn(B, N, dk, generator=gen))
+    K = torch.relu(torch.randn(B, N, dk, generator=gen))
+    H = torch.relu(torch.randn(B, N, dv, generator=gen))
+    V = torch.randn(B, N, dv, generator=gen)
+    gamma = torch.randn(dv, generator=gen)
+    dout = torch.randn(B, N, dv, generator=gen)
+    leaves = [t.to(dev).requires_grad_(True) for t in (Q, K, H, V, gamma)]
+    out = node_self_attention(*leaves)
+    out.backward(dout.to(dev))
+    ref = [t.double().requires_grad_(True) for t in (Q, K, H, V, gamma)]
+    r = ref[4] * torch.matmul(torch.softmax(torch.matmul(ref[0], ref[1].transpose(1, 2)), -1), ref[2]) + ref[3]
+    r.backward(dout.double())
+    tol = 1e-4 if N > 1000 else 1e-5
+    torch.testing.assert_close(out.detach().cpu().double(), r.detach(), rtol=tol, atol=tol)
+    for name, a, w in zip("QKHVg", leaves, ref):
+        if w.numel() == 0:  # dk = 0: Q and K have no entries
+            assert a.grad is None or a.grad.numel() == 0
+            continue
+        scale = w.grad.abs().max().item() + 1.0
+        torch.testing.assert_close(a.grad.cpu().double(), w.grad, rtol=1e-4, atol=2e-5 * scale, msg=f"d{name}")
