@@ -9,8 +9,8 @@ the backward gather) against the dense restatement of robust_gcn.py:45-72
 the index invariants of the conversions.  GPU half (``-m gpu``): libgrl's
 typed SpMM forward / backward, its dense -> CSR conversion and its CSC
 transpose against the C oracle on the same draws -- bitwise, as the fixed
-cases of test_gpu_kernels.py require.  derandomize=True: the same examples
-on every run."""
+cases of test_gpu_kernels.py require.  derandomize=True and no example
+database: the same examples on every run and every machine."""
 import numpy as np
 import pytest
 from hypothesis import HealthCheck, given, settings
@@ -19,9 +19,9 @@ from hypothesis import strategies as st
 import inputs as gi
 from oracle import c_oracle, dense_ref
 
-CPU_SETTINGS = settings(max_examples=60, deadline=None, derandomize=True,
+CPU_SETTINGS = settings(max_examples=60, deadline=None, derandomize=True, database=None,
                         suppress_health_check=[HealthCheck.too_slow])
-GPU_SETTINGS = settings(max_examples=30, deadline=None, derandomize=True,
+GPU_SETTINGS = settings(max_examples=30, deadline=None, derandomize=True, database=None,
                         suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
 
 
@@ -186,7 +186,7 @@ def test_gpu_dense_to_csr_and_csc_random_shapes(case):
     rp, ci, va = c_oracle.dense_to_csr(A, [N * L * N, L * N, N, 1], B, N, L)
     np.testing.assert_array_equal(g.rowptr.cpu().numpy(), rp)
     np.testing.assert_array_equal(g.colidx.cpu().numpy()[:ci.size], ci)
-    if float_vals:
+    if float_vals and ci.size:  # (no edges: no values to keep, g.vals is None)
         np.testing.assert_array_equal(g.vals.cpu().numpy()[:ci.size], va)
     c = g.csc()
     colptr, zrow, eid, cvals = c_oracle.csr_to_csc(rp, ci, L, B * N, True, va if float_vals else None)
