@@ -802,7 +802,10 @@ static int spmm_bwd_entry(const char* who, const GrlTypedCsc* g, const float* dZ
   GRL_CHECK_ARG(col0 >= 0 && (int64_t)col0 + F <= F_total, "%s: columns [%d, %d) outside the %d-column segments",
                 who, col0, col0 + F, F_total);
   if (g->num_rows == 0) return GRL_OK;
-  GRL_CHECK_ARG(dZ && dX && g->colptr && (g->nnz == 0 || (g->zrow && g->eid)), "%s: NULL pointer", who);
+  // dZ is never read when no entry and no self term points into it (a node-range shard without own
+  // rows or edges: its halo rows' dX is zero, and its empty dZ has no storage)
+  GRL_CHECK_ARG((dZ || (g->nnz == 0 && g->self_rows == 0)) && dX && g->colptr && (g->nnz == 0 || (g->zrow && g->eid)),
+                "%s: NULL pointer", who);
   const int hs = g->has_self ? 1 : 0;
   return launch_spmm<true>(g->num_rows, g->self_rows, g->num_types, hs, g->colptr, g->zrow, g->eid, g->vals,
                            g->edge_id_base, g->self_id_base, dZ + col0, (int64_t)F_total, F, dX, lddx, to_dev(de),

@@ -318,3 +318,89 @@ def test_gpu_node_attention_random_shapes(case):
             continue
         scale = w.grad.abs().max().item() + 1.0
         torch.testing.assert_close(a.grad.cpu().double(), w.grad, rtol=1e-4, atol=2e-5 * scale, msg=f"d{name}")
+
+
+@st.composite
+def shard_cases(draw):
+    N = draw(st.integers(1, 2500))
+    L = draw(st.integers(1, 7))
+    deg = draw(st.sampled_from([0.0, 1.0, 6.0, 20.0]))
+    F = draw(st.sampled_from([4, 16, 64, 128, 256]))
+    world = draw(st.integers(1, 5))
+    cuts = sorted(draw(st.lists(st.integers(0, N), min_size=world - 1, max_size=world - 1)))  # empty shards too
+    mode = draw(st.sampled_from(["sparse", "dense"]))
+    chunks = draw(st.sampled_from([None, 1, 2]))
+    p = draw(st.sampled_from([0.0, 0.3]))
+    seed = draw(st.integers(0, 2 ** 20))
+    return N, L, deg, F, [0] + cuts + [N], mode, chunks, p, seed
+
+
+@pytest.mark.gpu
+@GPU_SETTINGS
+@given(shard_cases())
+def test_gpu_sharded_aggregation_random_partitions(case):
+    """Node-range shards over random partitions -- 1 to 5
+    ranks, empty shards, sparse or dense halo, column-slice pipelining or
+    not, DropEdge on global edge ids -- as threads over a LocalGroup (the
+    in-process stand-in whose collectives are pinned to RCCL's by
+    tests/test_gpu_rccl.py): every shard's Z rows are bitwise the one-GPU
+    aggregation's; its dX rows after the reverse exchange add the peers'
+    partials in peer order after the own rows' sum (a different fp32 order
+    than one CSC pass), so they match within test_gpu_dist.py's bound."""
+    import threading
+
+    import torch
+
+    from grl import DropEdge, TypedGraph
+    from grl.dist import LocalGroup, ShardedGraph
+    from grl.ops import typed_aggregate
+    from oracle import hash as ohash
+
+    dev = torch.device("cuda:0")
+    N, L, deg, F, bounds, mode, chunks, p, seed = case
+    world = len(bounds) - 1
+    rowptr, colidx = ohash.synth_csr(0, L, N, int(N * deg), seed)
+    g = TypedGraph.from_csr_host(rowptr, colidx, L, dev)
+    de = DropEdge(p, seed, 2, True) if p > 0 else None
+    gen = torch.Generator(device=dev).manual_seed(seed)
+    X = torch.randn(N, F, device=dev, generator=gen)
+    Xr = X.clone().requires_grad_(True)
+    Z = typed_aggregate(Xr, g.with_dropedge(de))
+    dZ = torch.randn(Z.shape, device=dev, generator=gen)
+    Z.backward(dZ)
+
+    grp = LocalGroup(world)
+    shards = ShardedGraph.in_process(g, bounds, halo=mode, group=grp)
+    got, errs = [None] * world, [None] * world
+
+    def body(r):
+        try:
+            torch.cuda.set_device(dev)
+            rb, re = bounds[r], bounds[r + 1]
+            with torch.autograd.set_multithreading_enabled(False), torch.cuda.stream(torch.cuda.Stream(dev)):
+                Xl = X[rb:re].clone().requires_grad_(True)
+                Zl = shards[r].aggregate(Xl, de, chunks=chunks)
+                Zl.backward(dZ[rb:re])
+                torch.cuda.current_stream().synchronize()
+                got[r] = (Zl.detach(), Xl.grad)
+        except BaseException as e:  # a failed rank must not hang the others
+            errs[r] = e
+            grp.abort()
+
+    ts = [threading.Thread(target=body, args=(r,)) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(120)
+        assert not t.is_alive(), "virtual rank hung"
+    for e in errs:
+        if e is not None and not isinstance(e, threading.BrokenBarrierError):
+            raise e
+    for e in errs:
+        if e is not None:
+            raise e
+    for r in range(world):
+        rb, re = bounds[r], bounds[r + 1]
+        assert torch.equal(got[r][0], Z.detach()[rb:re]), f"Z rows of rank {r}"
+        gx = got[r][1] if got[r][1] is not None else torch.zeros(re - rb, F, device=dev)
+        torch.testing.assert_close(gx, Xr.grad[rb:re], rtol=1e-5, atol=1e-4, msg=f"dX rows of rank {r}")
