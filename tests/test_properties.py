@@ -404,3 +404,99 @@ def test_gpu_sharded_aggregation_random_partitions(case):
         assert torch.equal(got[r][0], Z.detach()[rb:re]), f"Z rows of rank {r}"
         gx = got[r][1] if got[r][1] is not None else torch.zeros(re - rb, F, device=dev)
         torch.testing.assert_close(gx, Xr.grad[rb:re], rtol=1e-5, atol=1e-4, msg=f"dX rows of rank {r}")
+
+
+@st.composite
+def sharded_layer_cases(draw):
+    N = draw(st.integers(1, 12000))
+    L = draw(st.integers(1, 6))
+    deg = draw(st.sampled_from([0.0, 2.0, 12.0]))
+    F = draw(st.sampled_from([16, 64, 256]))
+    C = draw(st.sampled_from([8, 48, 256]))
+    world = draw(st.integers(1, 4))
+    cuts = sorted(draw(st.lists(st.integers(0, N), min_size=world - 1, max_size=world - 1)))
+    mode = draw(st.sampled_from(["sparse", "dense"]))
+    form = draw(st.sampled_from(["plain", "chunks", "rows"]))
+    p = draw(st.sampled_from([0.0, 0.3]))
+    seed = draw(st.integers(0, 2 ** 20))
+    return N, L, deg, F, C, [0] + cuts + [N], mode, form, p, seed
+
+
+@pytest.mark.gpu
+@settings(max_examples=20, deadline=None, derandomize=True, database=None,
+          suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
+@given(sharded_layer_cases())
+def test_gpu_sharded_graphconv_random_partitions(case):
+    """A whole GraphConv layer (robust_gcn.py:45-51, ReLU) on node-range
+    shards over random partitions (1-4 LocalGroup ranks, empty shards,
+    sparse / dense halo; unpipelined, column-slice pipelined, or the
+    row-block pipelined one-kernel form): every shard's output rows bitwise
+    the one-GPU layer's; dX rows, and dW / db summed over the ranks by
+    allreduce_gradients, within the sharded tests' fp32 bounds."""
+    import copy
+    import threading
+
+    import torch
+
+    from gnn.models import GraphConv
+    from grl import DropEdge, TypedGraph
+    from grl.dist import LocalGroup, ShardedGraph, allreduce_gradients
+    from oracle import hash as ohash
+
+    dev = torch.device("cuda:0")
+    N, L, deg, F, C, bounds, mode, form, p, seed = case
+    world = len(bounds) - 1
+    rowptr, colidx = ohash.synth_csr(0, L, N, int(N * deg), seed)
+    g = TypedGraph.from_csr_host(rowptr, colidx, L, dev)
+    de = DropEdge(p, seed, 1, True) if p > 0 else None
+    gen = torch.Generator(device=dev).manual_seed(seed)
+    X = torch.randn(N, F, device=dev, generator=gen)
+    R = torch.randn(N, C, device=dev, generator=gen)
+    torch.manual_seed(seed)
+    base = GraphConv(F, C, L).to(dev)
+    one = copy.deepcopy(base)
+    Xg = X.clone().requires_grad_(True)
+    ref = one.propagate(Xg[None], g.with_dropedge(de), relu=True)[0]
+    (ref * R).sum().backward()
+
+    grp = LocalGroup(world)
+    shards = ShardedGraph.in_process(g, bounds, halo=mode, group=grp)
+    layers = [copy.deepcopy(base) for _ in range(world)]
+    got, errs = [None] * world, [None] * world
+    kw = {"plain": {}, "chunks": {"chunks": 2}, "rows": {"pipeline": "rows"}}[form]
+
+    def body(r):
+        try:
+            torch.cuda.set_device(dev)
+            rb, re = bounds[r], bounds[r + 1]
+            with torch.autograd.set_multithreading_enabled(False), torch.cuda.stream(torch.cuda.Stream(dev)):
+                Xl = X[rb:re].clone().requires_grad_(True)
+                out = shards[r].graphconv(Xl, layers[r], de, relu=True, **kw)
+                (out * R[rb:re]).sum().backward()
+                allreduce_gradients(layers[r].parameters(), group=shards[r].group)
+                torch.cuda.current_stream().synchronize()
+                got[r] = (out.detach(), Xl.grad, layers[r].h_weights.grad, layers[r].bias.grad)
+        except BaseException as e:  # a failed rank must not hang the others
+            errs[r] = e
+            grp.abort()
+
+    ts = [threading.Thread(target=body, args=(r,)) for r in range(world)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(240)
+        assert not t.is_alive(), "virtual rank hung"
+    for e in errs:
+        if e is not None and not isinstance(e, threading.BrokenBarrierError):
+            raise e
+    for e in errs:
+        if e is not None:
+            raise e
+    for r in range(world):
+        rb, re = bounds[r], bounds[r + 1]
+        out, gx, gw, gb = got[r]
+        assert torch.equal(out, ref.detach()[rb:re]), f"out rows of rank {r}"
+        gx = gx if gx is not None else torch.zeros(re - rb, F, device=dev)
+        torch.testing.assert_close(gx, Xg.grad[rb:re], rtol=1e-5, atol=1e-4, msg=f"dX rows of rank {r}")
+        torch.testing.assert_close(gw, one.h_weights.grad, rtol=1e-4, atol=1e-4, msg=f"dW on rank {r}")
+        torch.testing.assert_close(gb, one.bias.grad, rtol=1e-4, atol=1e-4, msg=f"db on rank {r}")
