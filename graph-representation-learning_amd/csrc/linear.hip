@@ -1475,7 +1475,8 @@ extern "C" int grl_graphconv_bwd_data(const GrlTypedCsr* gt, const int32_t* eid,
   GRL_CHECK_ARG(C > 0 && ldg >= C && F > 0 && g_rows >= 0 && g_rows <= gt->num_rows,
                 "grl_graphconv_bwd_data: need C > 0, ldg >= C, F > 0, 0 <= g_rows <= num_rows");
   if (gt->num_rows == 0) return GRL_OK;
-  GRL_CHECK_ARG(G && W && dX && gt->rowptr && (gt->nnz == 0 || (gt->colidx && eid)),
+  // (an empty node-range shard: no G rows and no entries, so its empty G is never read)
+  GRL_CHECK_ARG((G || (g_rows == 0 && gt->nnz == 0)) && W && dX && gt->rowptr && (gt->nnz == 0 || (gt->colidx && eid)),
                 "grl_graphconv_bwd_data: NULL pointer");
   if (!bwd_data_path(gt, G, ldg, C, W, F))
     GRL_FAIL(GRL_E_UNSUPPORTED, "grl_graphconv_bwd_data: shape outside the one-kernel path (C %d, F %d, L %d, rows "
@@ -1587,6 +1588,11 @@ extern "C" int grl_relu_grad(const float* g, const float* relu_out, float* g_eff
   TraceRange trace_("grl_relu_grad");
   GRL_CHECK_ARG(M >= 0 && C >= 0, "grl_relu_grad: bad sizes");
   if (C == 0) return GRL_OK;
+  if (M == 0) {  // no rows (an empty node-range shard): nothing to mask, db = 0
+    if (db && hipMemsetAsync(db, 0, (size_t)C * sizeof(float), as_stream(stream)) != hipSuccess)
+      GRL_FAIL(GRL_E_HIP, "grl_relu_grad: hipMemsetAsync failed");
+    return GRL_OK;
+  }
   GRL_CHECK_ARG(g && relu_out && g_eff, "grl_relu_grad: NULL pointer");
   const size_t need = grl_relu_grad_workspace_size(M, C);
   if (db && (!workspace || workspace_bytes < need))
@@ -1613,6 +1619,14 @@ extern "C" int grl_linear_bwd_weight(const float* Z, int64_t ldz, const float* g
   TraceRange trace_("grl_linear_bwd_weight");
   GRL_CHECK_ARG(M >= 0 && K >= 0 && C >= 0 && ldz >= K, "grl_linear_bwd_weight: bad sizes");
   if (K == 0 || C == 0) return GRL_OK;
+  if (M == 0) {  // no rows (an empty node-range shard): dW = 0, db = 0
+    GRL_CHECK_ARG(dW, "grl_linear_bwd_weight: NULL pointer");
+    hipStream_t st = as_stream(stream);
+    if (hipMemsetAsync(dW, 0, (size_t)K * C * sizeof(float), st) != hipSuccess ||
+        (db && hipMemsetAsync(db, 0, (size_t)C * sizeof(float), st) != hipSuccess))
+      GRL_FAIL(GRL_E_HIP, "grl_linear_bwd_weight: hipMemsetAsync failed");
+    return GRL_OK;
+  }
   GRL_CHECK_ARG(Z && g && dW, "grl_linear_bwd_weight: NULL pointer");
   const size_t need = grl_linear_bwd_weight_workspace_size(M, K, C);
   if (!workspace || workspace_bytes < need)
