@@ -24,6 +24,11 @@
  *    wait) reads and clears that word and returns GRL_E_TIMEOUT.
  *  - Return value 0 = success, negative GRL_E_* = failure; grl_last_error()
  *    returns a thread-local message for the last failure on this thread.
+ *  - Empty operands: an operand with no rows (an empty torch tensor, whose
+ *    data pointer is NULL) may be NULL whenever the call reads none of it --
+ *    e.g. a node-range shard with no own rows: its typed-SpMM backward,
+ *    ReLU/bias gradient (db = 0), weight gradient (dW = 0, db = 0) and
+ *    one-kernel data gradient succeed and write zeros where they write.
  *  - fp32 features, int32 indices.  Sums over a row's edges run in CSR order
  *    with one fmaf per edge, so results are bitwise reproducible run to run
  *    (no float atomics anywhere).
