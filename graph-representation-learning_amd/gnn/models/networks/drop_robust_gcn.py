@@ -228,6 +228,11 @@ class GraphCNNDropEdge(BaseNetwork):
         V, A = inputs
         graph = self.to_graph(A)
         sharded = isinstance(graph, ShardedGraph)
+        if sharded and any(b1 <= b0 for b0, b1 in zip(graph.plan.bounds[:-1], graph.plan.bounds[1:])):
+            # every rank holds the same bounds, so every rank raises here (none is left waiting in a
+            # collective): the streamed layers and the attention's row gathers assume each rank owns rows
+            raise ValueError(f"GraphCNNDropEdge over node-range shards needs every shard to own at least one "
+                             f"node (bounds {list(graph.plan.bounds)}): use fewer ranks than nodes")
         # row-local layers of a shard take the one-GPU model's GEMM path (bitwise its rows)
         pr = graph.global_rows if sharded else 0
         self.dropout.begin_forward(V.device, graph if sharded else None, V.numel() // max(V.shape[-1], 1))
